@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""bench.py — Mrays/s + frame ms of the MI355X render path (BASELINE.json metric).
+
+Workload (configs[1], "C2"): scenes/14-01-acceleration-tree/scene1 at 1920x1080,
+default RendererSettings (depth 3), one frame per step.  At HEAD the reference
+traces exactly one ray per pixel on this scene (its shadow-ray loop is dead code,
+crt_renderer.cpp:29-44), so rays = traversals = 2,073,600 per frame; the count
+is re-measured by the instrumented kernel, not assumed.
+
+N=1: the frame is rendered into HBM (scene + image resident; no PCIe in the
+timed region).  N>1 (one process per GPU, torchrun): the reference's bucket
+grid is dealt round-robin to ranks, each rank renders its buckets packed, and
+the tiles are gathered to rank 0 over RCCL (torch.distributed "nccl") and
+unpacked there — one frame per step, strong scaling.
+
+Also reported: the roofline of the render kernel (algorithmic bytes per launch
+÷ measured kernel time vs 8 TB/s HBM) and the CPU oracle (restatement of the
+reference, same threads-over-buckets structure) timed on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "chaos-ray-tracing-course-2025_amd"))
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (import before libcrt_hip so both share torch's HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+from crt_amd import native as N  # noqa: E402
+from crt_amd.scene_npz import load_npz  # noqa: E402
+
+SCENE_NPZ = ROOT / "tests" / "golden" / "scenes" / "14-01-acceleration-tree__scene1.npz"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+NODE_BYTES, TRI_BYTES, PIXEL_BYTES = 32, 52, 12   # SURVEY §8(d) algorithmic bytes
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (wall s)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
+                   help="per-launch HBM bytes measured by rocprofv3 --pmc (profiles/), if present")
+    return p.parse_args()
+
+
+def cpu_baseline(scene, settings, seconds: float) -> dict:
+    from oracle import pyoracle
+    from crt_amd.native import WorkCounts
+    threads = min(16, os.cpu_count() or 1)
+    orc = pyoracle.OracleScene(scene)
+    frames, rays = 0, 0
+    t0 = time.perf_counter()
+    while True:
+        wc = WorkCounts()
+        orc.render(settings, nthreads=threads, counts=wc)
+        frames += 1
+        rays += wc.traversals
+        el = time.perf_counter() - t0
+        if el >= seconds or frames >= 200:
+            break
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": rays / el / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{frames} full frames of the same workload, oracle/crt_oracle.cpp render_image "
+                      f"(bucket queue, {threads} threads, g++ -O3 no FMA) on {model or 'host CPU'}, "
+                      f"{el:.1f} s wall"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    scene = load_npz(SCENE_NPZ).set_resolution(a.width, a.height)
+    settings = N.RendererSettings.default()
+    gpu = N.HipScene(scene, device=local)
+    W, H = a.width, a.height
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+
+    frame = torch.empty(W * H * 3, dtype=torch.float32, device="cuda")
+    if world > 1:
+        stride = gpu.shard_stride(world)
+        packed = torch.empty(stride, dtype=torch.float32, device="cuda")
+        gathered = [torch.empty(stride, dtype=torch.float32, device="cuda") for _ in range(world)] \
+            if rank == 0 else None
+        gathered_flat = torch.empty(stride * world, dtype=torch.float32, device="cuda") if rank == 0 else None
+
+    def step():
+        if world == 1:
+            gpu.render_device(settings, frame.data_ptr(), sptr)
+            return
+        gpu.render_shard(settings, rank, world, packed.data_ptr(), sptr)
+        dist.gather(packed, gathered, dst=0)
+        if rank == 0:
+            torch.cat(gathered, out=gathered_flat)
+            gpu.unpack_shards(world, gathered_flat.data_ptr(), frame.data_ptr(), sptr)
+
+    # work counters of one full frame (outside the timed region)
+    counts = gpu.count_work(settings)
+    rays_per_frame = counts["traversals"]
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # kernel duration: event pairs around each render launch on the launch stream
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        ev[i][0].record(stream)
+        if world == 1:
+            gpu.render_device(settings, frame.data_ptr(), sptr)
+            ev[i][1].record(stream)
+        else:
+            gpu.render_shard(settings, rank, world, packed.data_ptr(), sptr)
+            ev[i][1].record(stream)
+            dist.gather(packed, gathered, dst=0)
+            if rank == 0:
+                torch.cat(gathered, out=gathered_flat)
+                gpu.unpack_shards(world, gathered_flat.data_ptr(), frame.data_ptr(), sptr)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    ms_per_step = elapsed / a.steps * 1e3
+    mrays = rays_per_frame * a.steps / elapsed / 1e6
+
+    # roofline of the render kernel: algorithmic bytes of one launch / its duration
+    shard_frac = 1.0 / world
+    alg_bytes = (NODE_BYTES * counts["node_tests"] + TRI_BYTES * counts["triangle_tests"]
+                 + PIXEL_BYTES * W * H) * shard_frac
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    try:
+        tj = json.loads(Path(a.traffic_json).read_text())
+        if tj.get("workload") == f"14-01/scene1 {W}x{H}" and world == 1:
+            traffic = tj.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not a.no_cpu_baseline:
+            cpu = cpu_baseline(scene, settings, a.cpu_seconds)
+        out = {
+            "metric": "Mrays/sec + frame ms, 1920x1080 scene 14-01",
+            "value": round(mrays, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "scene file scenes/14-01-acceleration-tree/scene1.crtscene (parsed fixture tests/golden/scenes)",
+            "config": {"workload": f"14-01-acceleration-tree/scene1 {W}x{H}, RendererSettings defaults "
+                                   f"(max_ray_depth 3), primary rays (HEAD traces no shadow rays)",
+                       "rays_per_frame": rays_per_frame, "node_tests_per_frame": counts["node_tests"],
+                       "triangle_tests_per_frame": counts["triangle_tests"],
+                       "parallelism": f"bucket-shard{world}" if world > 1 else "single-gpu",
+                       "frame_ms": round(ms_per_step, 5), "kernel_ms": round(kern_ms, 5)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

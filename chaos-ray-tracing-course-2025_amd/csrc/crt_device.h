@@ -1,0 +1,211 @@
+/*
+ * crt_device.h — per-ray math of the hot path for gfx950, written in the
+ * reference's exact fp32 operation order so results are bit-identical
+ * (build with -ffp-contract=off; fp32 '/' and sqrtf stay correctly rounded,
+ * HIP's default).  Reference lines are cited per function.
+ */
+#pragma once
+#include <stdint.h>
+
+#include "crt_layout.h"
+
+#if defined(__HIPCC__)
+#define CRT_HD __host__ __device__ __forceinline__
+#else
+#define CRT_HD inline
+#endif
+
+namespace crt_amd {
+
+struct Vec { float x, y, z; };
+
+CRT_HD Vec vec(float x, float y, float z) { Vec r; r.x = x; r.y = y; r.z = z; return r; }
+CRT_HD Vec vadd(Vec a, Vec b) { return vec(a.x + b.x, a.y + b.y, a.z + b.z); }
+CRT_HD Vec vsub(Vec a, Vec b) { return vec(a.x - b.x, a.y - b.y, a.z - b.z); }
+CRT_HD Vec vneg(Vec a) { return vec(-a.x, -a.y, -a.z); }
+CRT_HD Vec vscale(Vec a, float s) { return vec(a.x * s, a.y * s, a.z * s); }
+CRT_HD Vec vdiv(Vec a, float s) { return vec(a.x / s, a.y / s, a.z / s); }
+/* crt_vector.h:76-78: Vector*Vector multiplies the y component twice. */
+CRT_HD Vec vmul_quirk(Vec a, Vec b) { return vec(a.x * b.x, a.y * b.y * a.y, a.z * b.z); }
+CRT_HD float vdot(Vec a, Vec b) { return a.x * b.x + a.y * b.y + a.z * b.z; }          /* crt_vector.h:115-117 */
+CRT_HD Vec vcross(Vec a, Vec b) {                                                        /* crt_vector.h:107-113 */
+    return vec(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+CRT_HD float vlen_sq(Vec a) { return a.x * a.x + a.y * a.y + a.z * a.z; }               /* crt_vector.h:13-15 */
+CRT_HD float vlen(Vec a) { return sqrtf(vlen_sq(a)); }                                   /* crt_vector.cpp:7-9 */
+CRT_HD Vec vnormalize(Vec a) { return vdiv(a, vlen(a)); }                                /* crt_vector.h:98-101 */
+
+/* crt_matrix.h:66-74: row vector times row-major 3x3, each column summed from 0.0f. */
+CRT_HD Vec vec_mat(Vec v, const float m[9]) {
+    float r0 = 0.0f, r1 = 0.0f, r2 = 0.0f;
+    r0 += v.x * m[0]; r0 += v.y * m[3]; r0 += v.z * m[6];
+    r1 += v.x * m[1]; r1 += v.y * m[4]; r1 += v.z * m[7];
+    r2 += v.x * m[2]; r2 += v.y * m[5]; r2 += v.z * m[8];
+    return vec(r0, r1, r2);
+}
+
+/* Camera::generate_ray (crt_camera.cpp:7-35). aspect and tan_half_fov are the
+ * per-frame constants float(W)/H and std::tan(fov*0.5f), computed on the host. */
+CRT_HD void camera_ray(const DeviceScene &s, int x, int y, Vec &o, Vec &d) {
+    float dx = x + 0.5f, dy = y + 0.5f;
+    dx /= (float)s.width;
+    dy /= (float)s.height;
+    dx = (2.0f * dx) - 1.0f;
+    dy = 1.0f - (2.0f * dy);
+    dx *= s.aspect;
+    dx *= s.tan_half_fov;
+    dy *= s.tan_half_fov;
+    o = vec(s.cam_loc[0], s.cam_loc[1], s.cam_loc[2]);
+    d = vnormalize(vec_mat(vec(dx, dy, -1.0f), s.cam_rot));
+}
+
+/* ray_intersect_aabb_p (crt_intersection.cpp:14-45): for extent ∈ {min,max},
+ * axis ∈ {x,y,z}: skip near-parallel axes and faces behind the origin, else
+ * the hit point must lie in the face's other two slabs (inclusive).  The
+ * function is a pure OR over the six faces, so evaluation order is free.
+ *
+ * t = (plane - o) / d is negative iff the two operands have opposite signs and
+ * the quotient does not underflow to -0; for a nonzero numerator that needs
+ * |d| >= 2 (the smallest denormal halved ties to zero), so while |d| < 2 the
+ * sign test decides "behind" exactly and only faces in front pay the
+ * correctly-rounded divide. */
+CRT_HD bool opposite_signs(float a, float b) { return (a < 0.0f && b > 0.0f) || (a > 0.0f && b < 0.0f); }
+
+CRT_HD bool box_face(float plane, float o_a, float d_a, float o_u, float d_u, float o_w, float d_w,
+                     float lo_u, float hi_u, float lo_w, float hi_w) {
+    if (fabsf(d_a) < 1e-6f) return false;
+    const float num = plane - o_a;
+    if (opposite_signs(num, d_a) && fabsf(d_a) < 2.0f) return false;
+    const float t = num / d_a;
+    if (t < 0.0f) return false;
+    const float pu = o_u + d_u * t;
+    const float pw = o_w + d_w * t;
+    return pu >= lo_u && pu <= hi_u && pw >= lo_w && pw <= hi_w;
+}
+
+CRT_HD bool box_hit(Vec o, Vec d, const DNode &n) {
+    /* faces min.x, min.y, min.z, max.x, max.y, max.z; (u,v) = (1,2),(2,0),(0,1) */
+    return box_face(n.lo_x, o.x, d.x, o.y, d.y, o.z, d.z, n.lo_y, n.hi_y, n.lo_z, n.hi_z) ||
+           box_face(n.lo_y, o.y, d.y, o.z, d.z, o.x, d.x, n.lo_z, n.hi_z, n.lo_x, n.hi_x) ||
+           box_face(n.lo_z, o.z, d.z, o.x, d.x, o.y, d.y, n.lo_x, n.hi_x, n.lo_y, n.hi_y) ||
+           box_face(n.hi_x, o.x, d.x, o.y, d.y, o.z, d.z, n.lo_y, n.hi_y, n.lo_z, n.hi_z) ||
+           box_face(n.hi_y, o.y, d.y, o.z, d.z, o.x, d.x, n.lo_z, n.hi_z, n.lo_x, n.hi_x) ||
+           box_face(n.hi_z, o.z, d.z, o.x, d.x, o.y, d.y, n.lo_x, n.hi_x, n.lo_y, n.hi_y);
+}
+
+/* ray_intersect_triangle (crt_intersection.cpp:47-93), distance only.  The
+ * back_face_culling flag is read (from *cull) only for back-facing candidates. */
+CRT_HD bool tri_hit(Vec o, Vec d, const DTriGeo &g, const uint8_t *cull, float &t_out) {
+    const Vec N = vec(g.nx, g.ny, g.nz);
+    const float rn = vdot(N, d);
+    if (fabsf(rn) < 1e-6f) return false;
+    const Vec v0 = vec(g.v0x, g.v0y, g.v0z);
+    const float op = vdot(N, vsub(v0, o));
+    if (!(op < 0.0f) && *cull) return false;
+    if (opposite_signs(op, rn) && fabsf(rn) < 2.0f) return false;
+    const float t = op / rn;
+    if (t < 0.0f) return false;
+    const Vec v1 = vec(g.v1x, g.v1y, g.v1z), v2 = vec(g.v2x, g.v2y, g.v2z);
+    const Vec e0 = vsub(v1, v0), e1 = vsub(v2, v1), e2 = vsub(v0, v2);
+    const Vec p = vadd(o, vscale(d, t));
+    const Vec v0p = vsub(p, v0), v1p = vsub(p, v1), v2p = vsub(p, v2);
+    if (vdot(N, vcross(e0, v0p)) >= 0.0f && vdot(N, vcross(e1, v1p)) >= 0.0f &&
+        vdot(N, vcross(e2, v2p)) >= 0.0f) {
+        t_out = t;
+        return true;
+    }
+    return false;
+}
+
+/* Full Intersection record of the winning triangle (crt_intersection.cpp:71-88):
+ * recomputed from (ray, triangle, t) with the same operations, so it equals the
+ * record the reference built when it first found this hit. */
+struct HitRec {
+    float t;
+    Vec p, n, uv;
+    float bu, bv;
+    int32_t mat;
+};
+
+CRT_HD void hit_record(Vec o, Vec d, float t, const DTriGeo &g, const DTriAttr &at, const DVec4 &n0,
+                       const DVec4 &n1, const DVec4 &n2, const DVec4 &t0, const DVec4 &t1, const DVec4 &t2,
+                       HitRec &h) {
+    const Vec v0 = vec(g.v0x, g.v0y, g.v0z), v1 = vec(g.v1x, g.v1y, g.v1z), v2 = vec(g.v2x, g.v2y, g.v2z);
+    const Vec e0 = vsub(v1, v0), e2 = vsub(v0, v2);
+    const Vec p = vadd(o, vscale(d, t));
+    const Vec v0p = vsub(p, v0);
+    const Vec v0v1 = e0, v0v2 = vneg(e2);
+    const float bu = vlen(vcross(v0p, v0v2)) / vlen(vcross(v0v1, v0v2));
+    const float bv = vlen(vcross(v0v1, v0p)) / vlen(vcross(v0v1, v0v2));
+    h.t = t;
+    h.p = p;
+    if (at.mat_flags < 0) {   /* smooth shading bit */
+        const Vec a = vscale(vec(n1.x, n1.y, n1.z), bu);
+        const Vec b = vscale(vec(n2.x, n2.y, n2.z), bv);
+        const Vec c = vscale(vec(n0.x, n0.y, n0.z), 1 - bu - bv);
+        h.n = vadd(vadd(a, b), c);
+    } else {
+        h.n = vec(g.nx, g.ny, g.nz);
+    }
+    h.uv = vadd(vadd(vscale(vec(t1.x, t1.y, t1.z), bu), vscale(vec(t2.x, t2.y, t2.z), bv)),
+                vscale(vec(t0.x, t0.y, t0.z), 1.0f - bu - bv));
+    h.bu = bu;
+    h.bv = bv;
+    h.mat = at.mat_flags & 0x7fffffff;
+}
+
+/* PCG32 (crt_random.h:10-43) */
+struct Pcg32 {
+    uint64_t state, inc;
+    CRT_HD uint32_t next() {
+        const uint64_t old = state;
+        state = old * 6364136223846793005ULL + inc;
+        const uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        const uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((0u - rot) & 31u));
+    }
+};
+CRT_HD Pcg32 make_pcg(uint32_t x, uint32_t y) {
+    const uint64_t seed = ((uint64_t)x << 32) | y;
+    Pcg32 g;
+    g.state = 0;
+    g.inc = (seed << 1) | 1;
+    (void)g.next();
+    g.state += seed;
+    (void)g.next();
+    return g;
+}
+/* uniform() = bits(0x3f800000 | r>>9) - 1.0f = (r>>9) * 2^-23 exactly: the
+ * mantissa index m = r >> 9 addresses the host-computed sin/cos tables. */
+
+/* x86 cvttss2si semantics for the reference's static_cast<int>(float)
+ * (out of range / NaN → INT_MIN) */
+CRT_HD int trunc_x86(float f) {
+    if (f >= -2147483648.0f && f < 2147483648.0f) return (int)f;
+    return (int)0x80000000;
+}
+
+/* Texture::sample (crt_texture.cpp:9-49) */
+CRT_HD Vec sample_texture(const DTexture &tx, const DVec4 *texels, Vec uv, float bu, float bv) {
+    switch (tx.type) {
+    case 0: return vec(tx.c0x, tx.c0y, tx.c0z);
+    case 1:
+        if (bu <= tx.scalar || bv <= tx.scalar || (1.0f - bu - bv) <= tx.scalar) return vec(tx.c0x, tx.c0y, tx.c0z);
+        return vec(tx.c1x, tx.c1y, tx.c1z);
+    case 2: {
+        const int row = trunc_x86(uv.x / tx.scalar);
+        const int col = trunc_x86(uv.y / tx.scalar);
+        return ((row + col) & 1) ? vec(tx.c1x, tx.c1y, tx.c1z) : vec(tx.c0x, tx.c0y, tx.c0z);
+    }
+    default: {
+        int rx = trunc_x86(uv.x * tx.w) % tx.w;
+        int ry = trunc_x86((1.0f - uv.y) * tx.h) % tx.h;
+        if (rx < 0) rx += tx.w;   /* the reference indexes out of bounds here (UB) */
+        if (ry < 0) ry += tx.h;
+        const DVec4 t = texels[tx.texel_offset + (int64_t)ry * tx.w + rx];
+        return vec(t.x, t.y, t.z);
+    }
+    }
+}
+
+}  // namespace crt_amd

@@ -1,0 +1,89 @@
+/*
+ * crt_host.h — host-side (C++) scene preparation shared by the C-ABI layer.
+ */
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/crt_hip.h"
+#include "crt_layout.h"
+
+namespace crt_amd {
+
+/* Thread-local error channel behind crt_hip_last_error(). Returns `code`. */
+int set_error(int code, const std::string &msg);
+
+/* Owned storage behind a crt_scene_file (the parsed .crtscene). */
+struct SceneFile {
+    crt_scene_desc desc;
+    struct Mesh {
+        std::vector<float> positions, uvs;
+        bool has_uvs = false;
+        std::vector<int32_t> indices;
+        int32_t material_index = 0;
+    };
+    std::vector<Mesh> meshes_storage;
+    std::vector<crt_mesh_desc> meshes;
+    std::vector<crt_material_desc> materials;
+    std::vector<crt_texture_desc> textures;
+    std::vector<crt_light_desc> lights;
+    std::string warning;
+    void relink();
+};
+
+int parse_scene_json(const char *text, size_t len, const char *asset_root, SceneFile &out);
+
+/* The scene after mesh prep and tree build, in device layout (crt_layout.h). */
+struct HostScene {
+    /* camera / settings */
+    float background[3];
+    float cam_loc[3];
+    float cam_rot[9];
+    int32_t width = 0, height = 0;
+    float fov_radians = 0.f;
+    float aspect = 0.f, tan_half_fov = 0.f;
+    int32_t bucket_size = 24;
+    bool gi_on = false, reflections_on = true, refractions_on = true;
+
+    /* geometry (global ids: vertex/triangle order of crt_mesh.cpp) */
+    std::vector<float> vpos;            /* 3 per vertex */
+    std::vector<DVec4> vnormal, vuv;
+    std::vector<DTriAttr> tri_attr;
+    std::vector<float> face_normal;     /* 3 per triangle */
+    std::vector<uint8_t> tri_cull;
+
+    /* tree, reference numbering (preorder, child0 subtree first) */
+    std::vector<float> ref_bounds;      /* 6 per node */
+    std::vector<int32_t> ref_children;  /* 2 per node */
+    std::vector<int64_t> ref_leaf_off;  /* n+1 */
+    std::vector<int32_t> ref_leaf_tris;
+    std::vector<int32_t> ref_depth;
+
+    /* tree, device layout (traversal order) */
+    std::vector<DNode> nodes;
+    std::vector<DTriGeo> slots;
+    std::vector<int32_t> slot_tri;
+    std::vector<uint8_t> slot_cull;
+
+    /* shading */
+    std::vector<DMaterial> materials;
+    std::vector<DTexture> textures;
+    std::vector<DVec4> texels;
+    std::vector<DLight> lights;
+
+    /* stats */
+    int64_t leaf_count = 0;
+    int32_t max_depth = 0;
+    int32_t max_leaf_size = 0;
+};
+
+int prepare_scene(const crt_scene_desc *desc, HostScene &out);
+
+/* The reference bucket grid (crt_renderer.cpp:160-174) dealt round-robin to
+ * shard_count shards; returns the buckets of `shard` with packed offsets and
+ * the shard's packed pixel count. */
+std::vector<DBucket> shard_buckets(int32_t width, int32_t height, int32_t bucket_size, int shard,
+                                   int shard_count, int64_t *packed_pixels);
+
+}  // namespace crt_amd

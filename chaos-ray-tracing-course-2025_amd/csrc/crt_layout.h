@@ -1,0 +1,121 @@
+/*
+ * crt_layout.h — the scene as it lives in HBM (shared by host prep and kernels).
+ *
+ * Reference data structures being replaced:
+ *   AccelerationTreeNode { vector<Triangle> triangles; AABB bounds; int children[2]; int parent; }
+ *       64 B + heap-allocated Triangle copies (crt_acceleration_tree.h:15-24)
+ *   Triangle { const Vertex *v0,*v1,*v2; Vector face_normal; int material; flags }
+ *       48 B with pointers into an AoS Vertex array (crt_triangle.h:19-23)
+ *
+ * Device layout:
+ *   DNode[n]   32 B, in TRAVERSAL order = the order the reference's LIFO walk
+ *              (crt_intersection.cpp:116-133: push child0, push child1, pop)
+ *              visits nodes, i.e. preorder with child1 before child0.  A node
+ *              whose box test passes continues at i+1 (its first visited
+ *              child); a failed node or a leaf continues at `skip` — so the
+ *              walk needs no stack and visits exactly the reference's node
+ *              sequence.
+ *   DTriGeo[m] 48 B per LEAF SLOT: every triangle copy a leaf holds
+ *              (the reference's duplicated Triangle copies) stored contiguously
+ *              in leaf order, so a leaf is one contiguous run of 48-B records.
+ *   slot_tri[m] int32 global triangle id of each slot (final-hit attributes).
+ *   slot_cull[m] uint8 back_face_culling flag (read only for back-face hits).
+ *   DTriAttr[t] 16 B per triangle: vertex ids + material + smooth flag.
+ *   vertex normals / uvs as float4 (16-B aligned loads).
+ */
+#pragma once
+#include <stdint.h>
+
+namespace crt_amd {
+
+struct alignas(16) DNode {
+    float lo_x, lo_y, lo_z, hi_x;
+    float hi_y, hi_z;
+    int32_t a;   /* interior: skip index (first node after the subtree) | leaf: slot count   */
+    int32_t b;   /* interior: -1                                         | leaf: first slot  */
+};
+static_assert(sizeof(DNode) == 32, "DNode must be 32 B");
+
+struct alignas(16) DTriGeo {
+    float v0x, v0y, v0z, v1x;
+    float v1y, v1z, v2x, v2y;
+    float v2z, nx, ny, nz;
+};
+static_assert(sizeof(DTriGeo) == 48, "DTriGeo must be 48 B");
+
+struct alignas(16) DTriAttr {
+    int32_t i0, i1, i2;
+    int32_t mat_flags;   /* material index | (smooth_shading << 31) */
+};
+
+struct alignas(16) DVec4 { float x, y, z, w; };
+
+struct DMaterial {
+    int32_t type;
+    int32_t tex;
+    float ior;
+    int32_t pad;
+};
+
+struct DTexture {
+    int32_t type;
+    float c0x, c0y, c0z;
+    float c1x, c1y, c1z;
+    float scalar;
+    int32_t w, h;
+    int64_t texel_offset;   /* into the texel pool (float4 per texel), bitmap only */
+};
+
+struct DLight {
+    float intensity;
+    float px, py, pz;
+};
+
+/* Everything a render kernel needs, passed by value. */
+struct DeviceScene {
+    const DNode *nodes;
+    int32_t node_count;
+    const DTriGeo *slots;
+    const int32_t *slot_tri;
+    const uint8_t *slot_cull;
+    const DTriAttr *tri_attr;
+    const DVec4 *vnormal;
+    const DVec4 *vuv;
+    const DMaterial *materials;
+    const DTexture *textures;
+    const DVec4 *texels;
+    const DLight *lights;
+    int32_t light_count;
+    /* GI angle tables (cosf/sinf of pi*u and 2*pi*u for the 2^23 values of u) */
+    const float *gi_cos_pi;
+    const float *gi_sin_pi;
+    const float *gi_cos_2pi;
+    const float *gi_sin_2pi;
+    /* camera (crt_camera.cpp:7-35), per-frame constants precomputed on host */
+    float cam_loc[3];
+    float cam_rot[9];
+    int32_t width, height;
+    float inv_dummy;        /* keeps the struct 16-B friendly */
+    float aspect;           /* float(width) / height            (crt_camera.cpp:23) */
+    float tan_half_fov;     /* std::tan(fov_radians * 0.5f)     (crt_camera.cpp:26-27) */
+    float background[3];
+    int32_t gi_on, reflections_on, refractions_on;
+};
+
+/* Renderer settings as the kernels see them (crt_renderer.h:18-25). */
+struct DSettings {
+    uint32_t max_ray_depth;
+    uint32_t diffuse_reflection_ray_count;
+    float shadow_bias;
+    float reflection_bias;
+    float diffuse_reflection_bias;
+    float refraction_bias;
+};
+
+/* A bucket of the reference grid (crt_renderer.cpp:160-174). */
+struct DBucket {
+    int32_t x, y, w, h;
+    int64_t packed_offset;   /* pixel offset of this bucket inside its shard's packed buffer */
+};
+
+}  // namespace crt_amd

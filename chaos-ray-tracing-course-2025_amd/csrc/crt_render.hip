@@ -1,0 +1,825 @@
+/*
+ * crt_render.hip — gfx950 kernels + the C-ABI device layer (include/crt_hip.h).
+ *
+ * Replaces crt::render_image (src/core/crt_renderer.cpp:157-199) and the
+ * per-ray hot path beneath it (crt_intersection.cpp:14-136).
+ *
+ * Kernel structure (one launch per frame):
+ *   - one lane = one pixel; one wave = one 8x8 pixel tile (ray coherence inside
+ *     the wave), 4 waves per 256-thread workgroup; the tile list covers the
+ *     whole frame or one shard's buckets (multi-GPU);
+ *   - primary ray generated in-kernel (Camera::generate_ray, crt_camera.cpp:7-35);
+ *   - stackless tree walk over the traversal-ordered node array (crt_layout.h):
+ *     exactly the reference's node visit sequence, no per-lane stack;
+ *   - leaf triangles are contiguous 48-B records (no index indirection);
+ *   - only the winning triangle's Intersection record is built (bary, smooth
+ *     normal, uv), with the reference's arithmetic, after the walk;
+ *   - shading (crt_renderer.cpp:46-145) runs in the same kernel: recursion
+ *     becomes a per-lane LIFO of continuation frames, so the PCG draws happen in
+ *     the reference's depth-first order and rays never leave the GPU.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "crt_device.h"
+#include "crt_host.h"
+
+namespace crt_amd {
+
+constexpr float kPi = 3.14159265358979323846f;   /* std::numbers::pi_v<float> */
+
+struct alignas(16) Tile {
+    int32_t x, y, w, h;        /* pixel rectangle, w,h <= 8 */
+    int64_t out_base;          /* output pixel index of (x, y) */
+    int32_t out_stride;        /* output pixels per row */
+    int32_t pad;
+};
+
+struct alignas(16) UnpackBucket {
+    int32_t x, y, w, h;
+    int64_t src;               /* float offset of the bucket inside the gathered buffer */
+    int64_t pad;
+};
+
+enum FrameKind : int32_t { kDiffuseGI = 0, kReflect = 1, kRefractA = 2, kRefractB = 3 };
+
+/* A pending shade_ray activation (crt_renderer.cpp:46-145) waiting for a child. */
+struct Frame {
+    int32_t kind, depth, i, has_refr;
+    Vec acc;    /* diffuse: GI sum | reflect: albedo | refract: reflection colour */
+    Vec p, n;   /* diffuse: hit point and shading normal                         */
+    Vec a, b;   /* diffuse: right, forward basis | refract: refraction ray o, d   */
+    Vec alb;    /* diffuse: albedo sample | refract: .x = fresnel                */
+};
+
+struct LaneCounts { uint32_t traversals, nodes, tris, hits; };
+
+/* ---------------------------------------------------------------------- */
+/* ray_intersect_acceleration_tree (crt_intersection.cpp:109-136)           */
+/* ---------------------------------------------------------------------- */
+template <bool COUNT>
+__device__ __forceinline__ int trace_closest(const DeviceScene &s, Vec o, Vec d, float &best_t, LaneCounts &c) {
+    int best = -1;
+    best_t = 0.0f;
+    int i = 0;
+    const int n = s.node_count;
+    if (COUNT) ++c.traversals;
+    while (i < n) {
+        const DNode nd = s.nodes[i];
+        const bool pass = box_hit(o, d, nd);
+        if (COUNT) ++c.nodes;
+        if (nd.b < 0) {               /* interior: descend on pass, else skip the subtree */
+            i = pass ? i + 1 : nd.a;
+            continue;
+        }
+        if (pass) {                    /* leaf: ray_intersect_triangle_span, strict '<' keeps the first */
+            for (int k = 0; k < nd.a; ++k) {
+                const int slot = nd.b + k;
+                float t;
+                if (COUNT) ++c.tris;
+                if (tri_hit(o, d, s.slots[slot], s.slot_cull + slot, t) && (best < 0 || t < best_t)) {
+                    best_t = t;
+                    best = slot;
+                }
+            }
+        }
+        ++i;
+    }
+    if (COUNT && best >= 0) ++c.hits;
+    return best;
+}
+
+__device__ __forceinline__ void make_hit(const DeviceScene &s, Vec o, Vec d, float t, int slot, HitRec &h,
+                                         int32_t *tri_out = nullptr) {
+    const DTriGeo g = s.slots[slot];
+    const int32_t tri = s.slot_tri[slot];
+    const DTriAttr at = s.tri_attr[tri];
+    const DVec4 zero = {0.f, 0.f, 0.f, 0.f};
+    DVec4 n0 = zero, n1 = zero, n2 = zero;
+    if (at.mat_flags < 0) {
+        n0 = s.vnormal[at.i0];
+        n1 = s.vnormal[at.i1];
+        n2 = s.vnormal[at.i2];
+    }
+    hit_record(o, d, t, g, at, n0, n1, n2, s.vuv[at.i0], s.vuv[at.i1], s.vuv[at.i2], h);
+    if (tri_out) *tri_out = tri;
+}
+
+/* Diffuse direct term + normalisation (crt_renderer.cpp:81-99).  The shadow
+ * ray's trace_ray_with_refractions never enters its loop (:29-44), so every
+ * light is taken as unoccluded, as in the reference. */
+__device__ __forceinline__ Vec diffuse_finish(const DeviceScene &s, const DSettings &st, Vec acc, Vec p, Vec n, Vec alb) {
+    for (int l = 0; l < s.light_count; ++l) {
+        const DLight L = s.lights[l];
+        Vec ld = vsub(vec(L.px, L.py, L.pz), p);
+        const float r2 = vlen_sq(ld);
+        ld = vnormalize(ld);
+        const float dn = vdot(ld, n);
+        const float cos_law = (0.0f < dn) ? dn : 0.0f;          /* std::max(0.0f, dn) */
+        const float area = 4 * kPi * r2;
+        acc = vadd(acc, vscale(vdiv(vscale(alb, L.intensity), area), cos_law));
+    }
+    return vdiv(acc, (float)(st.diffuse_reflection_ray_count + 1));
+}
+
+/* One GI sample direction (crt_renderer.cpp:61-77).  rng.uniform() is
+ * m * 2^-23 with m = next() >> 9, so cosf/sinf of pi*u and 2pi*u are table
+ * lookups computed by the host's libm — bit-identical to the reference. */
+__device__ __forceinline__ void gi_ray(const DeviceScene &s, const DSettings &st, const Frame &f, Pcg32 &rng, Vec &o,
+                                       Vec &d) {
+    const uint32_t m1 = rng.next() >> 9;
+    Vec dir = vec(s.gi_cos_pi[m1], s.gi_sin_pi[m1], 0.0f);
+    const uint32_t m2 = rng.next() >> 9;
+    const float c = s.gi_cos_2pi[m2], sn = s.gi_sin_2pi[m2];
+    const float roty[9] = {c, 0.0f, -sn, 0.0f, 1.0f, 0.0f, sn, 0.0f, c};      /* crt_matrix.cpp:14-20 */
+    dir = vec_mat(dir, roty);
+    const float basis[9] = {f.a.x, f.a.y, f.a.z, f.n.x, f.n.y, f.n.z, f.b.x, f.b.y, f.b.z};   /* from_axes */
+    dir = vec_mat(dir, basis);
+    o = vadd(f.p, vscale(f.n, st.diffuse_reflection_bias));
+    d = dir;
+}
+
+/* powf(x, 5.0f) (crt_renderer.cpp:130): x^5 in double, rounded once. */
+__device__ __forceinline__ float pow5(float x) {
+    const double xd = x;
+    double r = xd * xd;
+    r = r * r;
+    r = r * xd;
+    return (float)r;
+}
+
+/* shade_ray for one camera ray (crt_renderer.cpp:46-155).
+ * FULL=false: scenes whose materials are only diffuse/constant with GI off —
+ * no recursion, no frame stack.  FULL=true: GI + reflective + refractive with
+ * a per-lane frame stack of MAXF entries (≥ max_ray_depth + 1, host-checked). */
+template <bool FULL, int MAXF, bool COUNT>
+__device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt) {
+    Vec o, d;
+    camera_ray(s, x, y, o, d);
+    uint32_t depth = 0;
+    Pcg32 rng;
+    if (FULL) rng = make_pcg((uint32_t)x, (uint32_t)y);
+    Frame stack[MAXF > 0 ? MAXF : 1];
+    int sp = 0;
+    Vec col;
+    for (;;) {
+        /* ---- enter shade_ray(ray) ---- */
+        bool called = false;
+        if (depth > st.max_ray_depth) {
+            col = vec(0.f, 0.f, 0.f);
+        } else {
+            float t;
+            const int slot = trace_closest<COUNT>(s, o, d, t, cnt);
+            if (slot < 0) {
+                col = vec(s.background[0], s.background[1], s.background[2]);
+            } else {
+                HitRec h;
+                make_hit(s, o, d, t, slot, h);
+                const DMaterial m = s.materials[h.mat];
+                if (m.type == CRT_MATERIAL_DIFFUSE) {
+                    const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+                    if (FULL && s.gi_on && st.diffuse_reflection_ray_count > 0) {
+                        Frame &f = stack[sp++];
+                        f.kind = kDiffuseGI;
+                        f.depth = (int32_t)depth;
+                        f.i = 0;
+                        f.acc = vec(0.f, 0.f, 0.f);
+                        f.p = h.p;
+                        f.n = h.n;
+                        f.a = vnormalize(vcross(d, h.n));       /* right   */
+                        f.b = vcross(f.a, h.n);                  /* forward */
+                        f.alb = alb;
+                        gi_ray(s, st, f, rng, o, d);
+                        depth = depth + 1;
+                        called = true;
+                    } else {
+                        col = diffuse_finish(s, st, vec(0.f, 0.f, 0.f), h.p, h.n, alb);
+                    }
+                } else if (FULL && m.type == CRT_MATERIAL_REFLECTIVE) {          /* :103-107 */
+                    const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+                    if (s.reflections_on) {
+                        Frame &f = stack[sp++];
+                        f.kind = kReflect;
+                        f.depth = (int32_t)depth;
+                        f.acc = alb;
+                        o = vadd(h.p, vscale(h.n, st.reflection_bias));
+                        d = vsub(d, vscale(vscale(h.n, 2.0f), vdot(d, h.n)));
+                        depth = depth + 1;
+                        called = true;
+                    } else {
+                        col = alb;
+                    }
+                } else if (FULL && m.type == CRT_MATERIAL_REFRACTIVE) {          /* :109-135 */
+                    if (!s.refractions_on) {
+                        col = vec(0.f, 0.f, 0.f);
+                    } else {
+                        Vec n = h.n;
+                        float n_out = 1.0f, n_in = m.ior;
+                        if (vdot(d, n) > 0.0f) {
+                            n = vneg(n);
+                            const float tmp = n_in; n_in = n_out; n_out = tmp;
+                        }
+                        Frame &f = stack[sp++];
+                        f.kind = kRefractA;
+                        f.depth = (int32_t)depth;
+                        f.has_refr = 0;
+                        {   /* Vector::refract (crt_vector.cpp:11-27) */
+                            Vec rd = d;
+                            const float ca = -vdot(rd, n);
+                            const float sa = sqrtf(1.0f - ca * ca);
+                            if (!(sa > n_in / n_out)) {
+                                const float sb = sa * n_out / n_in;
+                                const float cb = sqrtf(1.0f - sb * sb);
+                                rd = vadd(rd, vscale(n, ca));
+                                rd = vnormalize(rd);
+                                rd = vscale(rd, sb);
+                                rd = vadd(rd, vscale(vneg(n), cb));
+                                f.has_refr = 1;
+                            }
+                            /* refracted_at → refract_at with its default 1e-2f bias (crt_ray.h:30-50) */
+                            f.a = vadd(h.p, vscale(vneg(n), 1e-2f));
+                            f.b = rd;
+                        }
+                        f.alb.x = 0.5f * pow5(1.0f + vdot(d, n));
+                        o = vadd(h.p, vscale(n, st.reflection_bias));
+                        d = vsub(d, vscale(vscale(n, 2.0f), vdot(d, n)));
+                        depth = depth + 1;
+                        called = true;
+                    }
+                } else {                                                          /* Constant :137-139 */
+                    col = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+                }
+            }
+        }
+        if (called) continue;
+        if (!FULL) break;
+        /* ---- return col to the pending activations ---- */
+        while (sp > 0) {
+            Frame &f = stack[sp - 1];
+            if (f.kind == kDiffuseGI) {
+                f.acc = vadd(f.acc, col);
+                f.i += 1;
+                if ((uint32_t)f.i < st.diffuse_reflection_ray_count) {
+                    gi_ray(s, st, f, rng, o, d);
+                    depth = (uint32_t)f.depth + 1;
+                    called = true;
+                    break;
+                }
+                --sp;
+                col = diffuse_finish(s, st, f.acc, f.p, f.n, f.alb);
+            } else if (f.kind == kReflect) {
+                --sp;
+                col = vmul_quirk(f.acc, col);
+            } else if (f.kind == kRefractA) {
+                if (f.has_refr) {
+                    f.kind = kRefractB;
+                    f.acc = col;
+                    o = f.a;
+                    d = f.b;
+                    depth = (uint32_t)f.depth + 1;
+                    called = true;
+                    break;
+                }
+                --sp;   /* total internal reflection: the reflection colour is the result */
+            } else {
+                --sp;
+                const float fr = f.alb.x;
+                col = vadd(vscale(f.acc, fr), vscale(col, 1.0f - fr));
+            }
+        }
+        if (!called) break;
+    }
+    return col;
+}
+
+template <bool FULL, int MAXF, bool COUNT>
+__global__ __launch_bounds__(256) void k_render_tiles(DeviceScene s, DSettings st, const Tile *__restrict__ tiles,
+                                                      int ntiles, float *__restrict__ out,
+                                                      unsigned long long *__restrict__ counters) {
+    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int lane = (int)(threadIdx.x & 63);
+    if (wave >= ntiles) return;
+    const Tile tl = tiles[wave];
+    const int lx = lane & 7, ly = lane >> 3;
+    if (lx >= tl.w || ly >= tl.h) return;
+    LaneCounts cnt = {0u, 0u, 0u, 0u};
+    const Vec c = shade_pixel<FULL, MAXF, COUNT>(s, st, tl.x + lx, tl.y + ly, cnt);
+    float *px = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
+    px[0] = c.x;
+    px[1] = c.y;
+    px[2] = c.z;
+    if (COUNT) {
+        atomicAdd(&counters[0], (unsigned long long)cnt.traversals);
+        atomicAdd(&counters[1], (unsigned long long)cnt.nodes);
+        atomicAdd(&counters[2], (unsigned long long)cnt.tris);
+        atomicAdd(&counters[3], (unsigned long long)cnt.hits);
+    }
+}
+
+/* crt_hip_trace_batch: closest hit of arbitrary rays (a1–a4 KATs). */
+__global__ __launch_bounds__(256) void k_trace_rays(DeviceScene s, const float *__restrict__ rays, int64_t n,
+                                                    crt_hit *__restrict__ hits) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Vec o = vec(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+    const Vec d = vec(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+    LaneCounts cnt;
+    float t;
+    const int slot = trace_closest<false>(s, o, d, t, cnt);
+    crt_hit r;
+    r.distance = 0.f;
+    r.point[0] = r.point[1] = r.point[2] = 0.f;
+    r.normal[0] = r.normal[1] = r.normal[2] = 0.f;
+    r.uv[0] = r.uv[1] = r.uv[2] = 0.f;
+    r.bary_u = r.bary_v = 0.f;
+    r.material_index = 0;
+    r.hit = 0;
+    r.triangle_index = -1;
+    if (slot >= 0) {
+        HitRec h;
+        int32_t tri;
+        make_hit(s, o, d, t, slot, h, &tri);
+        r.distance = h.t;
+        r.point[0] = h.p.x; r.point[1] = h.p.y; r.point[2] = h.p.z;
+        r.normal[0] = h.n.x; r.normal[1] = h.n.y; r.normal[2] = h.n.z;
+        r.uv[0] = h.uv.x; r.uv[1] = h.uv.y; r.uv[2] = h.uv.z;
+        r.bary_u = h.bu; r.bary_v = h.bv;
+        r.material_index = h.mat;
+        r.hit = 1;
+        r.triangle_index = tri;
+    }
+    hits[i] = r;
+}
+
+/* Scatter gathered shard buffers back into the row-major frame. */
+__global__ __launch_bounds__(256) void k_unpack(const UnpackBucket *__restrict__ buckets, const float *__restrict__ src,
+                                                float *__restrict__ dst, int width) {
+    const UnpackBucket b = buckets[blockIdx.x];
+    const int npx = b.w * b.h;
+    for (int p = (int)threadIdx.x; p < npx; p += (int)blockDim.x) {
+        const int lx = p % b.w, ly = p / b.w;
+        const float *s = src + b.src + 3 * (int64_t)p;
+        float *d = dst + 3 * ((int64_t)(b.y + ly) * width + (b.x + lx));
+        d[0] = s[0];
+        d[1] = s[1];
+        d[2] = s[2];
+    }
+}
+
+}  // namespace crt_amd
+
+/* ====================================================================== */
+/*  C-ABI                                                                  */
+/* ====================================================================== */
+using namespace crt_amd;
+
+namespace {
+
+#define HIP_TRY(expr)                                                                            \
+    do {                                                                                         \
+        const hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                                    \
+            return set_error(CRT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));      \
+    } while (0)
+
+struct ShardPlan {
+    Tile *d_tiles = nullptr;
+    int ntiles = 0;
+    int64_t packed_pixels = 0;
+};
+
+struct GiTables { float *d = nullptr; };   /* 4 * 2^23 floats on one device */
+
+std::mutex g_gi_mu;
+std::map<int, GiTables> g_gi;              /* per device, process lifetime */
+std::vector<float> g_gi_host;
+
+constexpr int64_t kGiN = int64_t(1) << 23;
+
+void build_gi_host_tables() {
+    if (!g_gi_host.empty()) return;
+    g_gi_host.resize((size_t)(4 * kGiN));
+    float *cpi = g_gi_host.data(), *spi = cpi + kGiN, *c2 = spi + kGiN, *s2 = c2 + kGiN;
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> pool;
+    for (unsigned w = 0; w < nt; ++w) {
+        pool.emplace_back([=]() {
+            for (int64_t m = w; m < kGiN; m += nt) {
+                const float u = (float)m * (1.0f / 8388608.0f);          /* = uniform() exactly */
+                const float a = kPi * u;                                  /* crt_renderer.cpp:68 */
+                const float b = 2.0f * kPi * u;                           /* crt_renderer.cpp:71 */
+                cpi[m] = std::cos(a);
+                spi[m] = std::sin(a);
+                c2[m] = std::cos(b);
+                s2[m] = std::sin(b);
+            }
+        });
+    }
+    for (auto &t : pool) t.join();
+}
+
+}  // namespace
+
+struct crt_hip_scene {
+    int device = 0;
+    crt_scene_info info{};
+    bool has_secondary = false;    /* any reflective / refractive material */
+    bool has_diffuse = false;
+    DeviceScene ds{};
+    std::vector<void *> allocs;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    ShardPlan full;
+    std::map<std::pair<int, int>, ShardPlan> shard_plans;
+    std::map<int, std::pair<UnpackBucket *, int>> unpack_plans;
+    float *d_out = nullptr;
+    unsigned long long *d_counters = nullptr;
+    bool grid_empty = false;
+};
+
+namespace {
+
+template <class T>
+int upload(crt_hip_scene *sc, const std::vector<T> &v, const T **dst) {
+    *dst = nullptr;
+    if (v.empty()) return CRT_OK;
+    void *p = nullptr;
+    HIP_TRY(hipMalloc(&p, v.size() * sizeof(T)));
+    sc->allocs.push_back(p);
+    HIP_TRY(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    sc->info.device_bytes += (int64_t)(v.size() * sizeof(T));
+    *dst = static_cast<const T *>(p);
+    return CRT_OK;
+}
+
+int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool full_frame, ShardPlan &plan) {
+    std::vector<Tile> tiles;
+    const int W = sc->info.width;
+    if (full_frame) {
+        for (int y = 0; y < sc->info.height; y += 8)
+            for (int x = 0; x < W; x += 8)
+                tiles.push_back(Tile{x, y, std::min(8, W - x), std::min(8, sc->info.height - y),
+                                     (int64_t)y * W + x, W, 0});
+        plan.packed_pixels = (int64_t)W * sc->info.height;
+    } else {
+        int64_t total = 0;
+        for (const DBucket &b : buckets) {
+            for (int ty = 0; ty < b.h; ty += 8)
+                for (int tx = 0; tx < b.w; tx += 8)
+                    tiles.push_back(Tile{b.x + tx, b.y + ty, std::min(8, b.w - tx), std::min(8, b.h - ty),
+                                         b.packed_offset + (int64_t)ty * b.w + tx, b.w, 0});
+            total += (int64_t)b.w * b.h;
+        }
+        plan.packed_pixels = total;
+    }
+    plan.ntiles = (int)tiles.size();
+    if (!tiles.empty()) {
+        void *p = nullptr;
+        HIP_TRY(hipMalloc(&p, tiles.size() * sizeof(Tile)));
+        HIP_TRY(hipMemcpy(p, tiles.data(), tiles.size() * sizeof(Tile), hipMemcpyHostToDevice));
+        sc->allocs.push_back(p);
+        plan.d_tiles = static_cast<Tile *>(p);
+    }
+    return CRT_OK;
+}
+
+int ensure_gi_tables(crt_hip_scene *sc) {
+    if (sc->ds.gi_cos_pi) return CRT_OK;
+    std::lock_guard<std::mutex> g(g_gi_mu);
+    GiTables &t = g_gi[sc->device];
+    if (!t.d) {
+        build_gi_host_tables();
+        void *p = nullptr;
+        HIP_TRY(hipMalloc(&p, (size_t)(4 * kGiN) * sizeof(float)));
+        HIP_TRY(hipMemcpy(p, g_gi_host.data(), (size_t)(4 * kGiN) * sizeof(float), hipMemcpyHostToDevice));
+        t.d = static_cast<float *>(p);
+    }
+    sc->ds.gi_cos_pi = t.d;
+    sc->ds.gi_sin_pi = t.d + kGiN;
+    sc->ds.gi_cos_2pi = t.d + 2 * kGiN;
+    sc->ds.gi_sin_2pi = t.d + 3 * kGiN;
+    return CRT_OK;
+}
+
+int check_settings(const crt_renderer_settings *st) {
+    if (!st) return set_error(CRT_E_INVALID, "null settings");
+    return CRT_OK;
+}
+
+DSettings to_dsettings(const crt_renderer_settings *st) {
+    DSettings d;
+    d.max_ray_depth = st->max_ray_depth;
+    d.diffuse_reflection_ray_count = st->diffuse_reflection_ray_count;
+    d.shadow_bias = st->shadow_bias;
+    d.reflection_bias = st->reflection_bias;
+    d.diffuse_reflection_bias = st->diffuse_reflection_bias;
+    d.refraction_bias = st->refraction_bias;
+    return d;
+}
+
+/* Pick and launch the kernel variant for this scene + settings. */
+int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const ShardPlan &plan, float *d_out,
+                  hipStream_t stream, bool count) {
+    const bool gi = sc->info.gi_on && sc->has_diffuse && st->diffuse_reflection_ray_count > 0;
+    const bool full = gi || sc->has_secondary;
+    if (gi) {
+        const int rc = ensure_gi_tables(sc);
+        if (rc != CRT_OK) return rc;
+    }
+    if (plan.ntiles == 0) return CRT_OK;
+    const DSettings ds = to_dsettings(st);
+    const int blocks = (plan.ntiles + 3) / 4;
+    const uint64_t frames = (uint64_t)st->max_ray_depth + 1;
+    unsigned long long *cnt = sc->d_counters;
+#define CRT_LAUNCH(FULL, MAXF, COUNT)                                                                    \
+    hipLaunchKernelGGL((k_render_tiles<FULL, MAXF, COUNT>), dim3(blocks), dim3(256), 0, stream, sc->ds, ds, \
+                       plan.d_tiles, plan.ntiles, d_out, cnt)
+    if (!full) {
+        if (count) CRT_LAUNCH(false, 0, true); else CRT_LAUNCH(false, 0, false);
+    } else if (frames <= 4) {
+        if (count) CRT_LAUNCH(true, 4, true); else CRT_LAUNCH(true, 4, false);
+    } else if (frames <= 16) {
+        if (count) CRT_LAUNCH(true, 16, true); else CRT_LAUNCH(true, 16, false);
+    } else if (frames <= 64) {
+        if (count) CRT_LAUNCH(true, 64, true); else CRT_LAUNCH(true, 64, false);
+    } else {
+        return set_error(CRT_E_UNSUPPORTED, "max_ray_depth > 63 with recursive materials is not supported");
+    }
+#undef CRT_LAUNCH
+    HIP_TRY(hipGetLastError());
+    return CRT_OK;
+}
+
+int render_into(crt_hip_scene *sc, const crt_renderer_settings *st, float *d_rgb, hipStream_t stream, bool count) {
+    if (sc->grid_empty) {
+        /* bucket grid rounds to zero buckets: the reference renders nothing and
+         * returns the zero-initialised image (crt_renderer.cpp:158-174) */
+        HIP_TRY(hipMemsetAsync(d_rgb, 0, (size_t)sc->info.width * sc->info.height * 3 * sizeof(float), stream));
+        return CRT_OK;
+    }
+    HIP_TRY(hipEventRecord(sc->ev_start, stream));
+    int rc = launch_render(sc, st, sc->full, d_rgb, stream, count);
+    if (rc != CRT_OK) return rc;
+    HIP_TRY(hipEventRecord(sc->ev_stop, stream));
+    return CRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **out) {
+    if (!h || !out) return set_error(CRT_E_INVALID, "null argument");
+    *out = nullptr;
+    const HostScene &hs = *reinterpret_cast<const HostScene *>(h);
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return set_error(CRT_E_INVALID, "no such HIP device");
+    HIP_TRY(hipSetDevice(device));
+    std::unique_ptr<crt_hip_scene> sc(new crt_hip_scene());
+    sc->device = device;
+    crt_host_scene_info(h, &sc->info);
+    sc->info.device_bytes = 0;
+    for (const DMaterial &m : hs.materials) {
+        if (m.type == CRT_MATERIAL_REFLECTIVE || m.type == CRT_MATERIAL_REFRACTIVE) sc->has_secondary = true;
+        if (m.type == CRT_MATERIAL_DIFFUSE) sc->has_diffuse = true;
+    }
+    DeviceScene &ds = sc->ds;
+    int rc;
+    if ((rc = upload(sc.get(), hs.nodes, &ds.nodes)) != CRT_OK) return rc;
+    ds.node_count = (int32_t)hs.nodes.size();
+    if ((rc = upload(sc.get(), hs.slots, &ds.slots)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.slot_tri, &ds.slot_tri)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.slot_cull, &ds.slot_cull)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.tri_attr, &ds.tri_attr)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.vnormal, &ds.vnormal)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.vuv, &ds.vuv)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.materials, &ds.materials)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.textures, &ds.textures)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.texels, &ds.texels)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.lights, &ds.lights)) != CRT_OK) return rc;
+    ds.light_count = (int32_t)hs.lights.size();
+    std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
+    std::memcpy(ds.cam_rot, hs.cam_rot, sizeof ds.cam_rot);
+    ds.width = hs.width;
+    ds.height = hs.height;
+    ds.aspect = hs.aspect;
+    ds.tan_half_fov = hs.tan_half_fov;
+    std::memcpy(ds.background, hs.background, sizeof ds.background);
+    ds.gi_on = hs.gi_on;
+    ds.reflections_on = hs.reflections_on;
+    ds.refractions_on = hs.refractions_on;
+
+    HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&sc->ev_start));
+    HIP_TRY(hipEventCreate(&sc->ev_stop));
+    void *p = nullptr;
+    HIP_TRY(hipMalloc(&p, 4 * sizeof(unsigned long long)));
+    sc->allocs.push_back(p);
+    sc->d_counters = static_cast<unsigned long long *>(p);
+
+    int64_t px = 0;
+    const std::vector<DBucket> all = shard_buckets(hs.width, hs.height, hs.bucket_size, 0, 1, &px);
+    sc->grid_empty = all.empty();
+    if ((rc = make_tile_plan(sc.get(), all, true, sc->full)) != CRT_OK) return rc;
+    *out = sc.release();
+    return CRT_OK;
+}
+
+int crt_hip_scene_create(const crt_scene_desc *desc, int device, crt_hip_scene **out) {
+    crt_host_scene *h = nullptr;
+    int rc = crt_host_scene_create(desc, &h);
+    if (rc != CRT_OK) return rc;
+    rc = crt_hip_scene_upload(h, device, out);
+    crt_host_scene_destroy(h);
+    return rc;
+}
+
+int crt_hip_scene_info(const crt_hip_scene *sc, crt_scene_info *out) {
+    if (!sc || !out) return set_error(CRT_E_INVALID, "null argument");
+    *out = sc->info;
+    return CRT_OK;
+}
+
+void crt_hip_scene_destroy(crt_hip_scene *sc) {
+    if (!sc) return;
+    (void)hipSetDevice(sc->device);
+    if (sc->stream) (void)hipStreamSynchronize(sc->stream);
+    for (void *p : sc->allocs) (void)hipFree(p);
+    if (sc->d_out) (void)hipFree(sc->d_out);
+    for (auto &kv : sc->unpack_plans) (void)hipFree(kv.second.first);
+    if (sc->ev_start) (void)hipEventDestroy(sc->ev_start);
+    if (sc->ev_stop) (void)hipEventDestroy(sc->ev_stop);
+    if (sc->stream) (void)hipStreamDestroy(sc->stream);
+    delete sc;
+}
+
+int crt_hip_render_device(crt_hip_scene *sc, const crt_renderer_settings *st, float *d_rgb, void *stream) {
+    if (!sc || !d_rgb) return set_error(CRT_E_INVALID, "null argument");
+    int rc = check_settings(st);
+    if (rc != CRT_OK) return rc;
+    HIP_TRY(hipSetDevice(sc->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : sc->stream;
+    return render_into(sc, st, d_rgb, s, false);
+}
+
+int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rgb_out, crt_render_stats *stats) {
+    if (!sc || !rgb_out) return set_error(CRT_E_INVALID, "null argument");
+    int rc = check_settings(st);
+    if (rc != CRT_OK) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipSetDevice(sc->device));
+    const size_t nfl = (size_t)sc->info.width * sc->info.height * 3;
+    if (!sc->d_out) HIP_TRY(hipMalloc(&sc->d_out, nfl * sizeof(float)));
+    rc = render_into(sc, st, sc->d_out, sc->stream, false);
+    if (rc != CRT_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(rgb_out, sc->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
+    HIP_TRY(hipStreamSynchronize(sc->stream));
+    if (stats) {
+        std::memset(stats, 0, sizeof *stats);
+        float ms = 0.f;
+        if (!sc->grid_empty && sc->full.ntiles > 0) HIP_TRY(hipEventElapsedTime(&ms, sc->ev_start, sc->ev_stop));
+        stats->kernel_ms = ms;
+        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        stats->width = sc->info.width;
+        stats->height = sc->info.height;
+    }
+    return CRT_OK;
+}
+
+int crt_hip_last_kernel_ms(crt_hip_scene *sc, double *ms) {
+    if (!sc || !ms) return set_error(CRT_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(sc->device));
+    HIP_TRY(hipEventSynchronize(sc->ev_stop));
+    float f = 0.f;
+    HIP_TRY(hipEventElapsedTime(&f, sc->ev_start, sc->ev_stop));
+    *ms = f;
+    return CRT_OK;
+}
+
+int64_t crt_hip_shard_floats(const crt_hip_scene *sc, int shard, int shard_count) {
+    if (!sc || shard_count <= 0 || shard < 0 || shard >= shard_count) return set_error(CRT_E_INVALID, "bad shard");
+    int64_t px = 0;
+    shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size, shard, shard_count, &px);
+    return 3 * px;
+}
+
+int64_t crt_hip_shard_stride(const crt_hip_scene *sc, int shard_count) {
+    if (!sc || shard_count <= 0) return set_error(CRT_E_INVALID, "bad shard count");
+    int64_t m = 0;
+    for (int s = 0; s < shard_count; ++s) m = std::max(m, crt_hip_shard_floats(sc, s, shard_count));
+    return (m + 63) / 64 * 64;
+}
+
+int crt_hip_render_shard(crt_hip_scene *sc, const crt_renderer_settings *st, int shard, int shard_count,
+                         float *d_packed, void *stream) {
+    if (!sc || !d_packed) return set_error(CRT_E_INVALID, "null argument");
+    if (shard_count <= 0 || shard < 0 || shard >= shard_count) return set_error(CRT_E_INVALID, "bad shard");
+    int rc = check_settings(st);
+    if (rc != CRT_OK) return rc;
+    HIP_TRY(hipSetDevice(sc->device));
+    auto key = std::make_pair(shard, shard_count);
+    auto it = sc->shard_plans.find(key);
+    if (it == sc->shard_plans.end()) {
+        int64_t px = 0;
+        const std::vector<DBucket> b = shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size, shard,
+                                                     shard_count, &px);
+        ShardPlan plan;
+        if ((rc = make_tile_plan(sc, b, false, plan)) != CRT_OK) return rc;
+        it = sc->shard_plans.emplace(key, plan).first;
+    }
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : sc->stream;
+    HIP_TRY(hipEventRecord(sc->ev_start, s));
+    rc = launch_render(sc, st, it->second, d_packed, s, false);
+    if (rc != CRT_OK) return rc;
+    HIP_TRY(hipEventRecord(sc->ev_stop, s));
+    return CRT_OK;
+}
+
+int crt_hip_unpack_shards(crt_hip_scene *sc, int shard_count, const float *d_gathered, float *d_rgb, void *stream) {
+    if (!sc || !d_gathered || !d_rgb || shard_count <= 0) return set_error(CRT_E_INVALID, "bad argument");
+    HIP_TRY(hipSetDevice(sc->device));
+    auto it = sc->unpack_plans.find(shard_count);
+    if (it == sc->unpack_plans.end()) {
+        const int64_t stride = crt_hip_shard_stride(sc, shard_count);
+        std::vector<UnpackBucket> ub;
+        for (int s = 0; s < shard_count; ++s) {
+            int64_t px = 0;
+            for (const DBucket &b : shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size, s,
+                                                  shard_count, &px))
+                ub.push_back(UnpackBucket{b.x, b.y, b.w, b.h, s * stride + 3 * b.packed_offset, 0});
+        }
+        UnpackBucket *d = nullptr;
+        if (!ub.empty()) {
+            HIP_TRY(hipMalloc(&d, ub.size() * sizeof(UnpackBucket)));
+            HIP_TRY(hipMemcpy(d, ub.data(), ub.size() * sizeof(UnpackBucket), hipMemcpyHostToDevice));
+        }
+        it = sc->unpack_plans.emplace(shard_count, std::make_pair(d, (int)ub.size())).first;
+    }
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : sc->stream;
+    if (sc->grid_empty)
+        HIP_TRY(hipMemsetAsync(d_rgb, 0, (size_t)sc->info.width * sc->info.height * 3 * sizeof(float), s));
+    if (it->second.second > 0) {
+        hipLaunchKernelGGL(k_unpack, dim3(it->second.second), dim3(256), 0, s, it->second.first, d_gathered, d_rgb,
+                           sc->info.width);
+        HIP_TRY(hipGetLastError());
+    }
+    return CRT_OK;
+}
+
+int crt_hip_trace_batch(crt_hip_scene *sc, const float *rays, int64_t n, crt_hit *hits_out) {
+    if (!sc || (n > 0 && (!rays || !hits_out)) || n < 0) return set_error(CRT_E_INVALID, "bad argument");
+    if (n == 0) return CRT_OK;
+    HIP_TRY(hipSetDevice(sc->device));
+    float *d_rays = nullptr;
+    crt_hit *d_hits = nullptr;
+    HIP_TRY(hipMalloc(&d_rays, (size_t)n * 6 * sizeof(float)));
+    hipError_t e = hipMalloc(&d_hits, (size_t)n * sizeof(crt_hit));
+    if (e != hipSuccess) { (void)hipFree(d_rays); return set_error(CRT_E_HIP, hipGetErrorString(e)); }
+    e = hipMemcpy(d_rays, rays, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_trace_rays, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, sc->stream, sc->ds, d_rays,
+                           n, d_hits);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(sc->stream);
+    if (e == hipSuccess) e = hipMemcpy(hits_out, d_hits, (size_t)n * sizeof(crt_hit), hipMemcpyDeviceToHost);
+    (void)hipFree(d_rays);
+    (void)hipFree(d_hits);
+    if (e != hipSuccess) return set_error(CRT_E_HIP, hipGetErrorString(e));
+    return CRT_OK;
+}
+
+int crt_hip_count_work(crt_hip_scene *sc, const crt_renderer_settings *st, crt_work_counts *out) {
+    if (!sc || !out) return set_error(CRT_E_INVALID, "null argument");
+    int rc = check_settings(st);
+    if (rc != CRT_OK) return rc;
+    HIP_TRY(hipSetDevice(sc->device));
+    std::memset(out, 0, sizeof *out);
+    if (sc->grid_empty) return CRT_OK;
+    const size_t nfl = (size_t)sc->info.width * sc->info.height * 3;
+    if (!sc->d_out) HIP_TRY(hipMalloc(&sc->d_out, nfl * sizeof(float)));
+    HIP_TRY(hipMemsetAsync(sc->d_counters, 0, 4 * sizeof(unsigned long long), sc->stream));
+    rc = launch_render(sc, st, sc->full, sc->d_out, sc->stream, true);
+    if (rc != CRT_OK) return rc;
+    unsigned long long c[4];
+    HIP_TRY(hipMemcpyAsync(c, sc->d_counters, sizeof c, hipMemcpyDeviceToHost, sc->stream));
+    HIP_TRY(hipStreamSynchronize(sc->stream));
+    out->traversals = c[0];
+    out->node_tests = c[1];
+    out->triangle_tests = c[2];
+    out->hits = c[3];
+    return CRT_OK;
+}
+
+}  // extern "C"

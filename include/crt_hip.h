@@ -1,0 +1,246 @@
+/*
+ * crt_hip.h — C-ABI drop-in boundary for the MI355X (gfx950) render path.
+ *
+ * Replaces (reference = bvpav/chaos-ray-tracing-course-2025):
+ *   crt::Image crt::render_image(const crt::Scene&, const crt::RendererSettings&)
+ *       src/core/crt_renderer.h:27, defined at src/core/crt_renderer.cpp:157-199
+ *   and, below it, the per-ray hot path
+ *       crt::intersection::ray_intersect_acceleration_tree   src/core/crt_intersection.cpp:109-136
+ *       crt::intersection::ray_intersect_aabb_p              src/core/crt_intersection.cpp:14-45
+ *       crt::intersection::ray_intersect_triangle(_span)     src/core/crt_intersection.cpp:47-107
+ *
+ * Plain C: pointers + sizes, no C++/torch types.  Every entry point returns 0 on
+ * success or a negative CRT_E_* status; crt_hip_last_error() then holds a
+ * thread-local message.  The reference's render_image cannot fail; its callers
+ * (CLI main.cpp:22-26, _crt py_crt_module.cpp:91-94) map failures to exit code
+ * 1 / ValueError, and the shims in this repo do the same.
+ */
+#ifndef CRT_HIP_H
+#define CRT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRT_HIP_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------- */
+#define CRT_OK              0
+#define CRT_E_INVALID     (-1)   /* bad argument / malformed scene            */
+#define CRT_E_PARSE       (-2)   /* scene JSON rejected (crt_json.cpp:541-647) */
+#define CRT_E_UNSUPPORTED (-3)   /* feature outside this build's scope        */
+#define CRT_E_HIP         (-4)   /* HIP runtime error                         */
+#define CRT_E_NOMEM       (-5)
+#define CRT_E_IO          (-6)
+
+/* ---- scene description (the reference's crt::Scene inputs, flat) ---- */
+typedef struct crt_vec3 { float x, y, z; } crt_vec3;
+
+/* crt_material.h:5-10 */
+enum { CRT_MATERIAL_DIFFUSE = 0, CRT_MATERIAL_REFLECTIVE = 1,
+       CRT_MATERIAL_REFRACTIVE = 2, CRT_MATERIAL_CONSTANT = 3 };
+/* crt_texture.h:8-13 */
+enum { CRT_TEXTURE_ALBEDO = 0, CRT_TEXTURE_EDGES = 1,
+       CRT_TEXTURE_CHECKER = 2, CRT_TEXTURE_BITMAP = 3 };
+
+/* crt_texture.h:15-51 (tagged union flattened) */
+typedef struct crt_texture_desc {
+    int32_t  type;
+    crt_vec3 color0;          /* Albedo: albedo | Edges: edge_color | Checker: color_A */
+    crt_vec3 color1;          /* Edges: inner_color | Checker: color_B                 */
+    float    scalar;          /* Edges: edge_width  | Checker: square_size             */
+    int32_t  bitmap_width;    /* Bitmap: decoded texels, rgb fp32, top row first      */
+    int32_t  bitmap_height;
+    const float *bitmap_rgb;
+} crt_texture_desc;
+
+/* crt_material.h:12-16 + per-material TriangleFlags (crt_json.cpp:535) */
+typedef struct crt_material_desc {
+    int32_t type;
+    int32_t albedo_texture_index;   /* -1 for refractive (crt_json.cpp:493) */
+    float   ior;
+    int32_t smooth_shading;
+    int32_t back_face_culling;
+} crt_material_desc;
+
+/* one scene "object" (crt_json.cpp:150-218 → vertex_array_extend, crt_mesh.cpp:32-73) */
+typedef struct crt_mesh_desc {
+    const float   *positions;     /* vertex_count * 3                      */
+    const float   *uvs;           /* vertex_count * 3, or NULL (uv = 0)   */
+    int64_t        vertex_count;
+    const int32_t *indices;       /* index_count, multiple of 3, mesh-local */
+    int64_t        index_count;
+    int32_t        material_index;
+} crt_mesh_desc;
+
+/* crt_light.h:10-16 */
+typedef struct crt_light_desc { float intensity; crt_vec3 position; } crt_light_desc;
+
+/* crt_camera.h:13-25 + crt_transform.h:8-10 */
+typedef struct crt_camera_desc {
+    crt_vec3 location;
+    float    rotation[9];         /* row-major 3x3, ray_dir = v * R (crt_matrix.h:66-74) */
+    int32_t  width, height;
+    float    fov_degrees;         /* 90 when the scene file has none (crt_camera.h:13-15) */
+} crt_camera_desc;
+
+/* crt_scene.h:18-30 */
+typedef struct crt_scene_desc {
+    crt_vec3 background_color;
+    crt_camera_desc camera;
+    int32_t  bucket_size;                         /* default 24 (crt_scene.h:16) */
+    int32_t  gi_on, reflections_on, refractions_on;
+    const crt_mesh_desc     *meshes;    int32_t mesh_count;
+    const crt_material_desc *materials; int32_t material_count;
+    const crt_texture_desc  *textures;  int32_t texture_count;
+    const crt_light_desc    *lights;    int32_t light_count;
+} crt_scene_desc;
+
+/* crt_renderer.h:18-25 (same six fields, same defaults) */
+typedef struct crt_renderer_settings {
+    uint32_t max_ray_depth;                 /* 3    */
+    uint32_t diffuse_reflection_ray_count;  /* 4    */
+    float    shadow_bias;                   /* 1e-2 */
+    float    reflection_bias;               /* 1e-2 */
+    float    diffuse_reflection_bias;       /* 1e-2 */
+    float    refraction_bias;               /* 1e-2 */
+} crt_renderer_settings;
+
+/* crt_intersection.h:13-20 plus hit flag / triangle id (test hook only) */
+typedef struct crt_hit {
+    float   distance;
+    float   point[3];
+    float   normal[3];
+    float   uv[3];
+    float   bary_u, bary_v;
+    int32_t material_index;
+    int32_t hit;              /* 0 = std::nullopt */
+    int32_t triangle_index;   /* scene-global triangle id, -1 on miss */
+} crt_hit;
+
+typedef struct crt_scene_info {
+    int64_t triangle_count;
+    int64_t vertex_count;
+    int64_t node_count;        /* crt_acceleration_tree.cpp:87-106 node count */
+    int64_t leaf_count;
+    int64_t leaf_ref_count;    /* triangle copies held by leaves              */
+    int32_t max_depth;
+    int32_t max_leaf_size;
+    int64_t device_bytes;      /* bytes resident in HBM for this scene        */
+    int32_t width, height;
+    int32_t bucket_size;
+    int32_t gi_on, reflections_on, refractions_on;
+} crt_scene_info;
+
+typedef struct crt_render_stats {
+    double   kernel_ms;        /* device time of the render kernel(s)      */
+    double   total_ms;         /* host wall time of the whole call         */
+    int32_t  width, height;
+} crt_render_stats;
+
+/* Work counters of one frame (instrumented kernel, §8(d) algorithmic bytes). */
+typedef struct crt_work_counts {
+    uint64_t traversals;       /* calls of ray_intersect_acceleration_tree */
+    uint64_t node_tests;       /* ray_intersect_aabb_p calls               */
+    uint64_t triangle_tests;   /* ray_intersect_triangle calls             */
+    uint64_t hits;             /* traversals returning an intersection     */
+} crt_work_counts;
+
+/* ---- host: scene file loader (crt_json.cpp:541-647) ------------------ */
+typedef struct crt_scene_file crt_scene_file;
+/* Parse .crtscene JSON text. Same accept/reject rules and defaults as the
+ * reference loader; bitmap textures need a JPEG/PNG decoder (stb, absent) and
+ * make texture parsing fail exactly as a failed read_stb would. */
+int  crt_scene_file_parse(const char *json_text, size_t len, const char *asset_root,
+                          crt_scene_file **out);
+int  crt_scene_file_load(const char *path, crt_scene_file **out);
+const crt_scene_desc *crt_scene_file_desc(const crt_scene_file *f);
+/* Override image size (the reference CLI has no flags; BASELINE configs need it). */
+int  crt_scene_file_set_resolution(crt_scene_file *f, int32_t width, int32_t height);
+void crt_scene_file_destroy(crt_scene_file *f);
+
+/* ---- host: scene preparation (no GPU needed) ------------------------- */
+typedef struct crt_host_scene crt_host_scene;
+
+/* Mesh prep (vertex_array_extend, crt_mesh.cpp:10-73) and the exact
+ * acceleration-tree build (crt_acceleration_tree.cpp:13-106), flattened into
+ * the device layout.  The caller keeps ownership of every array in `desc`. */
+int  crt_host_scene_create(const crt_scene_desc *desc, crt_host_scene **out);
+int  crt_host_scene_info(const crt_host_scene *hs, crt_scene_info *out);
+/* Tree in the reference's own preorder numbering: bounds n*6 (min xyz, max xyz),
+ * children n*2 (-1 = none), leaf_offsets n+1, leaf_tris (global triangle ids,
+ * leaf order).  Any pointer may be NULL. */
+int  crt_host_scene_tree(const crt_host_scene *hs, float *bounds, int32_t *children,
+                         int64_t *leaf_offsets, int32_t *leaf_tris);
+int  crt_host_scene_vertex_normals(const crt_host_scene *hs, float *out);   /* 3 per vertex */
+int  crt_host_scene_face_normals(const crt_host_scene *hs, float *out);     /* 3 per triangle */
+void crt_host_scene_destroy(crt_host_scene *hs);
+
+/* ---- device scene ---------------------------------------------------- */
+typedef struct crt_hip_scene crt_hip_scene;
+
+/* crt_host_scene_create + crt_hip_scene_upload. */
+int  crt_hip_scene_create(const crt_scene_desc *desc, int device, crt_hip_scene **out);
+/* Copy a prepared scene into HBM of `device` (the host scene may be destroyed after). */
+int  crt_hip_scene_upload(const crt_host_scene *hs, int device, crt_hip_scene **out);
+int  crt_hip_scene_info(const crt_hip_scene *scene, crt_scene_info *out);
+void crt_hip_scene_destroy(crt_hip_scene *scene);
+
+/* Blocking drop-in for render_image: rgb_out is caller-allocated W*H*3 fp32,
+ * row-major, top row first, unclamped (crt_image.h:11-27). */
+int  crt_hip_render(crt_hip_scene *scene, const crt_renderer_settings *settings,
+                    float *rgb_out, crt_render_stats *stats);
+
+/* Asynchronous: render the whole frame into device memory d_rgb (W*H*3 fp32)
+ * on `stream` (a hipStream_t, NULL = the scene's own stream). */
+int  crt_hip_render_device(crt_hip_scene *scene, const crt_renderer_settings *settings,
+                           float *d_rgb, void *stream);
+
+/* Multi-GPU: the reference bucket grid (crt_renderer.cpp:160-174) is dealt
+ * to shards round-robin (bucket k → shard k % shard_count).  A shard renders
+ * its buckets packed, bucket after bucket, each bucket row-major.
+ * crt_hip_shard_floats gives the packed size (floats) of one shard;
+ * crt_hip_shard_stride the size every shard's slot is padded to for gathers. */
+int64_t crt_hip_shard_floats(const crt_hip_scene *scene, int shard, int shard_count);
+int64_t crt_hip_shard_stride(const crt_hip_scene *scene, int shard_count);
+int  crt_hip_render_shard(crt_hip_scene *scene, const crt_renderer_settings *settings,
+                          int shard, int shard_count, float *d_packed, void *stream);
+/* Host-side plan of one shard (no GPU): writes up to `cap` buckets as 6 int64
+ * each {x, y, w, h, packed_pixel_offset, bucket_index}; returns the number of
+ * buckets of the shard (or a negative status). */
+int64_t crt_shard_plan(int32_t width, int32_t height, int32_t bucket_size, int shard, int shard_count,
+                       int64_t *buckets_out, int64_t cap);
+/* d_gathered holds shard_count slots of crt_hip_shard_stride floats each. */
+int  crt_hip_unpack_shards(crt_hip_scene *scene, int shard_count, const float *d_gathered,
+                           float *d_rgb, void *stream);
+
+/* Test hook for the a1–a4 known-answer tests: closest hit of n rays
+ * (rays = n * 6 floats: origin xyz, direction xyz), host buffers. */
+int  crt_hip_trace_batch(crt_hip_scene *scene, const float *rays, int64_t n, crt_hit *hits_out);
+
+/* Work counters of one frame (instrumented variant of the render kernel). */
+int  crt_hip_count_work(crt_hip_scene *scene, const crt_renderer_settings *settings,
+                        crt_work_counts *out);
+
+/* Device-side stats of the last crt_hip_render_device launch on `scene`:
+ * device time in ms between the launch's start/stop events (blocks). */
+int  crt_hip_last_kernel_ms(crt_hip_scene *scene, double *ms);
+
+/* Defaults of crt_renderer.h:10-16. */
+void crt_renderer_settings_default(crt_renderer_settings *out);
+
+/* ---- host output (crt_image_ppm.cpp:9-23) ---------------------------- */
+int  crt_write_ppm(const char *path, const float *rgb, int32_t width, int32_t height,
+                   int32_t max_color_component);
+
+const char *crt_hip_last_error(void);
+int  crt_hip_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CRT_HIP_H */
