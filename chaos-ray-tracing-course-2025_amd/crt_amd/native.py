@@ -210,7 +210,9 @@ class SceneFile:
         return self._h
 
     def desc(self) -> SceneDesc:
-        return lib().crt_scene_file_desc(self._h).contents
+        d = lib().crt_scene_file_desc(self._h).contents
+        d._owner = self          # the struct views memory this object owns
+        return d
 
     def desc_ptr(self):
         return lib().crt_scene_file_desc(self._h)

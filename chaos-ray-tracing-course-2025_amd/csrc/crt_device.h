@@ -93,6 +93,27 @@ CRT_HD bool box_hit(Vec o, Vec d, const DNode &n) {
            box_face(n.hi_z, o.z, d.z, o.x, d.x, o.y, d.y, n.lo_x, n.hi_x, n.lo_y, n.hi_y);
 }
 
+/* Branch-free form of the same predicate: all six faces evaluated, OR-ed
+ * without short-circuit (no exec-mask branches; more VALU, no SALU). */
+CRT_HD int box_face_bf(float plane, float o_a, float d_a, float o_u, float d_u, float o_w, float d_w,
+                        float lo_u, float hi_u, float lo_w, float hi_w) {
+    const float num = plane - o_a;
+    const float t = num / d_a;
+    const float pu = o_u + d_u * t;
+    const float pw = o_w + d_w * t;
+    return (int)!(fabsf(d_a) < 1e-6f) & (int)!(t < 0.0f) & (int)(pu >= lo_u) & (int)(pu <= hi_u) &
+           (int)(pw >= lo_w) & (int)(pw <= hi_w);
+}
+
+CRT_HD bool box_hit_bf(Vec o, Vec d, const DNode &n) {
+    return 0 != (box_face_bf(n.lo_x, o.x, d.x, o.y, d.y, o.z, d.z, n.lo_y, n.hi_y, n.lo_z, n.hi_z) |
+           box_face_bf(n.lo_y, o.y, d.y, o.z, d.z, o.x, d.x, n.lo_z, n.hi_z, n.lo_x, n.hi_x) |
+           box_face_bf(n.lo_z, o.z, d.z, o.x, d.x, o.y, d.y, n.lo_x, n.hi_x, n.lo_y, n.hi_y) |
+           box_face_bf(n.hi_x, o.x, d.x, o.y, d.y, o.z, d.z, n.lo_y, n.hi_y, n.lo_z, n.hi_z) |
+           box_face_bf(n.hi_y, o.y, d.y, o.z, d.z, o.x, d.x, n.lo_z, n.hi_z, n.lo_x, n.hi_x) |
+           box_face_bf(n.hi_z, o.z, d.z, o.x, d.x, o.y, d.y, n.lo_x, n.hi_x, n.lo_y, n.hi_y));
+}
+
 /* ray_intersect_triangle (crt_intersection.cpp:47-93), distance only.  The
  * back_face_culling flag is read (from *cull) only for back-facing candidates. */
 CRT_HD bool tri_hit(Vec o, Vec d, const DTriGeo &g, const uint8_t *cull, float &t_out) {

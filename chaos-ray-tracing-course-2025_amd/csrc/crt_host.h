@@ -80,6 +80,11 @@ struct HostScene {
 
 int prepare_scene(const crt_scene_desc *desc, HostScene &out);
 
+/* Screen-space work estimate: every leaf cell is projected through the camera
+ * and its triangle count added to the 8x8 tiles its image overlaps.  Used only
+ * to dispatch expensive tiles first (results do not depend on it). */
+std::vector<float> tile_work_estimate(const HostScene &hs, int tiles_x, int tiles_y);
+
 /* The reference bucket grid (crt_renderer.cpp:160-174) dealt round-robin to
  * shard_count shards; returns the buckets of `shard` with packed offsets and
  * the shard's packed pixel count. */

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -99,6 +100,456 @@ __device__ __forceinline__ int trace_closest(const DeviceScene &s, Vec o, Vec d,
     return best;
 }
 
+/* Same walk, "while-while" form (after Aila & Laine 2009, adapted to the
+ * stackless order): a lane that reaches a passing leaf records it and keeps
+ * walking speculatively while other lanes of the wave still search; the wave
+ * then runs the triangle loop for every lane's pending leaf at once.  A lane
+ * holds one pending leaf, so leaves are still tested in visit order and the
+ * strict '<' keeps the reference's first-found winner.  A lane that meets a
+ * second passing leaf parks on it (`parked`) and takes it without re-testing
+ * its box in the next round. */
+template <bool COUNT>
+__device__ __forceinline__ int trace_closest_ww(const DeviceScene &s, Vec o, Vec d, float &best_t, LaneCounts &c) {
+    int best = -1;
+    best_t = 0.0f;
+    int i = 0;
+    const int n = s.node_count;
+    int lf = 0, lc = 0;          /* pending leaf: first slot, count */
+    bool parked = false;         /* node i is a passing leaf already counted */
+    if (COUNT) ++c.traversals;
+    for (;;) {
+        /* ---- traversal phase ---- */
+        while (i < n) {
+            const DNode nd = s.nodes[i];
+            bool pass;
+            if (parked) {
+                pass = true;
+                parked = false;
+            } else {
+                pass = box_hit(o, d, nd);
+                if (COUNT) ++c.nodes;
+            }
+            if (nd.b < 0) {
+                i = pass ? i + 1 : nd.a;
+            } else if (!pass) {
+                ++i;
+            } else if (lc == 0) {
+                lf = nd.b;
+                lc = nd.a;
+                ++i;
+            } else {
+                parked = true;   /* second leaf: wait here */
+                break;
+            }
+            if (__all(lc > 0 || i >= n)) break;
+        }
+        /* ---- intersection phase ---- */
+        for (int k = 0; k < lc; ++k) {
+            const int slot = lf + k;
+            float t;
+            if (COUNT) ++c.tris;
+            if (tri_hit(o, d, s.slots[slot], s.slot_cull + slot, t) && (best < 0 || t < best_t)) {
+                best_t = t;
+                best = slot;
+            }
+        }
+        lc = 0;
+        if (!__any(i < n)) break;
+    }
+    if (COUNT && best >= 0) ++c.hits;
+    return best;
+}
+
+/* While-while walk with software prefetch: while node i is tested, both
+ * possible successors (i+1, and the skip target of an interior node) are
+ * already in flight, and the next triangle record loads while the current one
+ * is tested.  BF selects the branch-free box predicate. */
+template <bool COUNT, bool BF>
+__device__ __forceinline__ int trace_closest_wwp(const DeviceScene &s, Vec o, Vec d, float &best_t, LaneCounts &c) {
+    int best = -1;
+    best_t = 0.0f;
+    int i = 0;
+    const int n = s.node_count;
+    const int last = n - 1;
+    int lf = 0, lc = 0;
+    bool parked = false;
+    if (COUNT) ++c.traversals;
+    DNode nd = s.nodes[0];
+    for (;;) {
+        while (i < n) {
+            const int i1 = i + 1 < n ? i + 1 : last;
+            const int alt = nd.b < 0 ? (nd.a < n ? nd.a : last) : i1;
+            const DNode n1 = s.nodes[i1];
+            const DNode n2 = s.nodes[alt];
+            bool pass;
+            if (parked) {
+                pass = true;
+                parked = false;
+            } else {
+                pass = BF ? box_hit_bf(o, d, nd) : box_hit(o, d, nd);
+                if (COUNT) ++c.nodes;
+            }
+            if (nd.b < 0) {
+                if (pass) { i = i + 1; nd = n1; } else { i = nd.a; nd = n2; }
+            } else if (!pass) {
+                ++i;
+                nd = n1;
+            } else if (lc == 0) {
+                lf = nd.b;
+                lc = nd.a;
+                ++i;
+                nd = n1;
+            } else {
+                parked = true;
+                break;
+            }
+            if (__all(lc > 0 || i >= n)) break;
+        }
+        if (lc > 0) {
+            DTriGeo g = s.slots[lf];
+            for (int k = 0; k < lc; ++k) {
+                const int slot = lf + k;
+                const DTriGeo gn = s.slots[k + 1 < lc ? slot + 1 : slot];
+                float t;
+                if (COUNT) ++c.tris;
+                if (tri_hit(o, d, g, s.slot_cull + slot, t) && (best < 0 || t < best_t)) {
+                    best_t = t;
+                    best = slot;
+                }
+                g = gn;
+            }
+        }
+        lc = 0;
+        if (!__any(i < n)) break;
+    }
+    if (COUNT && best >= 0) ++c.hits;
+    return best;
+}
+
+/* ---------------------------------------------------------------------- */
+/* Wave-cooperative walk (TRAV 4)                                           */
+/* ---------------------------------------------------------------------- */
+/* In the traversal-ordered layout every subtree is a contiguous node range
+ * and a range made of whole subtrees can be walked stacklessly on its own.
+ * So the reference's walk of one ray (the range [0, n)) can be cut into
+ * pieces at any passing interior node i: [i+1, skip(i+1)) stays with the lane
+ * (child1's subtree), [skip(i+1), end) is donated to the wave.  Idle lanes —
+ * lanes whose own ray is done or cheap — pop donated pieces, so a ray that
+ * crosses hundreds of nodes no longer serialises its whole wave.
+ *
+ * Exactness: the pieces partition exactly the node sequence the reference
+ * visits (same box test per node, same leaves, same triangles), and the
+ * winner is merged with a 64-bit key (t, slot): slots are numbered in the
+ * reference's visit order, so the smallest key is the reference's first-found
+ * closest hit (t >= 0; -0 and +0 are both mapped to 0, as '<' treats them). */
+constexpr int kCoopStack = 448;   /* donated pieces per wave */
+
+struct alignas(16) CoopLds {
+    float ray[64][6];                       /* o, d of each lane's ray */
+    unsigned long long key[64];             /* (t bits << 32) | slot, per ray */
+    unsigned long long stack[kCoopStack];   /* ray(6) | start(29) | end(29) */
+    int sp;                                 /* banked pieces (TRAV 5) */
+    int pad[3];
+};
+
+__device__ __forceinline__ unsigned long long coop_key(float t, int slot) {
+    const unsigned tb = t == 0.0f ? 0u : __float_as_uint(t);
+    return ((unsigned long long)tb << 32) | (unsigned)slot;
+}
+__device__ __forceinline__ unsigned long long coop_piece(int ray, int start, int end) {
+    return ((unsigned long long)ray << 58) | ((unsigned long long)start << 29) | (unsigned long long)end;
+}
+
+template <bool COUNT>
+__device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, Vec d, float &best_t,
+                          LaneCounts &c) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int n = s.node_count;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    L.ray[lane][0] = o.x; L.ray[lane][1] = o.y; L.ray[lane][2] = o.z;
+    L.ray[lane][3] = d.x; L.ray[lane][4] = d.y; L.ray[lane][5] = d.z;
+    L.key[lane] = ~0ull;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (COUNT && active) ++c.traversals;
+
+    int r = lane;                       /* ray of the piece this lane walks */
+    int i = active ? 0 : n, end = n;    /* the piece: [i, end) */
+    int lf = 0, lc = 0, k = 0;          /* pending leaf triangles */
+    Vec ro = o, rd = d;
+    unsigned long long mine = ~0ull;    /* best key found in the current piece */
+    int sp = 0;                         /* wave-uniform stack depth */
+    DNode nd = s.nodes[0];
+    for (;;) {
+        bool busy = (i < end) || (lc > 0);
+        /* ---- idle lanes pop donated pieces ---- */
+        const unsigned long long idle = __ballot(!busy);
+        if (idle != 0ull && sp > 0) {
+            const int nidle = __popcll(idle);
+            const int take = nidle < sp ? nidle : sp;
+            if (!busy) {
+                const int rank = __popcll(idle & lt_mask);
+                if (rank < take) {
+                    const unsigned long long pc = L.stack[sp - 1 - rank];
+                    r = (int)(pc >> 58);
+                    i = (int)((pc >> 29) & 0x1fffffff);
+                    end = (int)(pc & 0x1fffffff);
+                    ro = vec(L.ray[r][0], L.ray[r][1], L.ray[r][2]);
+                    rd = vec(L.ray[r][3], L.ray[r][4], L.ray[r][5]);
+                    nd = s.nodes[i];
+                    busy = true;
+                }
+            }
+            sp -= take;
+        }
+        if (!__any(busy)) break;
+        /* ---- one step per busy lane: a triangle of its pending leaf, or a node ---- */
+        bool donate = false;
+        int rest = 0;
+        if (busy) {
+            if (lc > 0) {
+                const int slot = lf + k;
+                float t;
+                if (COUNT) ++c.tris;
+                if (tri_hit(ro, rd, s.slots[slot], s.slot_cull + slot, t)) {
+                    const unsigned long long kk = coop_key(t, slot);
+                    mine = kk < mine ? kk : mine;
+                }
+                if (++k == lc) lc = 0;
+            } else {
+                const int i1 = i + 1 < n ? i + 1 : n - 1;
+                const int alt = nd.b < 0 ? (nd.a < n ? nd.a : n - 1) : i1;
+                const DNode n1 = s.nodes[i1];
+                const DNode n2 = s.nodes[alt];
+                const bool pass = box_hit_bf(ro, rd, nd);
+                if (COUNT) ++c.nodes;
+                if (nd.b < 0) {
+                    if (pass) {
+                        /* child1 = i+1; its subtree ends at skip(i+1) */
+                        rest = n1.b < 0 ? n1.a : i + 2;
+                        donate = rest < end;
+                        i = i + 1;
+                        nd = n1;
+                    } else {
+                        i = nd.a;
+                        nd = n2;
+                    }
+                } else {
+                    if (pass) { lf = nd.b; lc = nd.a; k = 0; }
+                    i = i + 1;
+                    nd = n1;
+                }
+            }
+            if (i >= end && lc == 0) {          /* piece finished: merge into its ray's key */
+                atomicMin(&L.key[r], mine);
+                mine = ~0ull;
+            }
+        }
+        /* ---- donate the remainder of a split walk while lanes are (about to be) idle ---- */
+        const unsigned long long want = __ballot(donate);
+        if (want != 0ull) {
+            const unsigned long long idle_next = __ballot(!((i < end) || (lc > 0)));
+            const int room = __popcll(idle_next) + 8 - sp;   /* keep a few pieces banked */
+            const int cap = kCoopStack - sp;
+            const int give = __popcll(want) < room ? __popcll(want) : (room > 0 ? room : 0);
+            const int g = give < cap ? give : cap;
+            if (donate) {
+                const int rank = __popcll(want & lt_mask);
+                if (rank < g) {
+                    L.stack[sp + rank] = coop_piece(r, rest, end);
+                    end = rest;
+                }
+            }
+            sp += g;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const unsigned long long kk = L.key[lane];
+    if (!active || kk == ~0ull) return -1;
+    const int slot = (int)(kk & 0xffffffffu);
+    float t = 0.0f;
+    (void)tri_hit(o, d, s.slots[slot], s.slot_cull + slot, t);   /* exact t (keeps the sign of a zero) */
+    best_t = t;
+    if (COUNT) ++c.hits;
+    return slot;
+}
+
+/* TRAV 5: the while-while walk with prefetch (TRAV 3) plus the piece sharing of
+ * TRAV 4 at round granularity.  A round = traversal phase (until every lane
+ * holds a leaf or is out of nodes) + triangle phase.  Lanes out of work at a
+ * round start pop donated pieces; during the traversal phase a lane that
+ * passes an interior node donates the rest of its piece while the wave's
+ * demand (idle lanes at the round start) exceeds the banked pieces.  The
+ * stack depth lives in LDS because donations happen under divergent control
+ * flow. */
+template <bool COUNT>
+__device__ int trace_share(const DeviceScene &s, CoopLds &L, bool active, Vec o, Vec d, float &best_t,
+                           LaneCounts &c) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int n = s.node_count;
+    const int last = n - 1;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    volatile int *spp = &L.sp;
+    L.ray[lane][0] = o.x; L.ray[lane][1] = o.y; L.ray[lane][2] = o.z;
+    L.ray[lane][3] = d.x; L.ray[lane][4] = d.y; L.ray[lane][5] = d.z;
+    L.key[lane] = ~0ull;
+    if (lane == 0) *spp = 0;
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_wave_barrier();
+    if (COUNT && active) ++c.traversals;
+
+    int r = lane;
+    int i = active ? 0 : n, end = active ? n : 0;
+    bool live = active;                 /* holds a piece whose key is not merged yet */
+    int lf = 0, lc = 0;
+    bool parked = false;
+    Vec ro = o, rd = d;
+    unsigned long long mine = ~0ull;
+    DNode nd = s.nodes[0];
+    for (;;) {
+        /* ---- merge finished pieces, refill idle lanes ---- */
+        if (live && !(i < end)) {
+            atomicMin(&L.key[r], mine);
+            mine = ~0ull;
+            live = false;
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_wave_barrier();
+        int sp = *spp;
+        const unsigned long long idle = __ballot(!(i < end));
+        int demand = 0;
+        if (idle != 0ull) {
+            const int nidle = __popcll(idle);
+            const int take = nidle < sp ? nidle : sp;
+            if (!(i < end)) {
+                const int rank = __popcll(idle & lt_mask);
+                if (rank < take) {
+                    const unsigned long long pc = L.stack[sp - 1 - rank];
+                    r = (int)(pc >> 58);
+                    i = (int)((pc >> 29) & 0x1fffffff);
+                    end = (int)(pc & 0x1fffffff);
+                    ro = vec(L.ray[r][0], L.ray[r][1], L.ray[r][2]);
+                    rd = vec(L.ray[r][3], L.ray[r][4], L.ray[r][5]);
+                    nd = s.nodes[i];
+                    live = true;
+                }
+            }
+            sp -= take;
+            demand = nidle - take;
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            if (lane == __builtin_ctzll(__ballot(true))) *spp = sp;
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (!__any(i < end)) break;
+        /* ---- traversal phase ---- */
+        while (i < end) {
+            const int i1 = i + 1 < n ? i + 1 : last;
+            const int alt = nd.b < 0 ? (nd.a < n ? nd.a : last) : i1;
+            const DNode n1 = s.nodes[i1];
+            const DNode n2 = s.nodes[alt];
+            bool pass;
+            if (parked) {
+                pass = true;
+                parked = false;
+            } else {
+                pass = box_hit_bf(ro, rd, nd);
+                if (COUNT) ++c.nodes;
+            }
+            bool donate = false;
+            int rest = 0;
+            if (nd.b < 0) {
+                if (pass) {
+                    rest = n1.b < 0 ? n1.a : i + 2;
+                    donate = demand > 0 && rest < end;
+                    i = i + 1;
+                    nd = n1;
+                } else {
+                    i = nd.a;
+                    nd = n2;
+                }
+            } else if (!pass) {
+                ++i;
+                nd = n1;
+            } else if (lc == 0) {
+                lf = nd.b;
+                lc = nd.a;
+                ++i;
+                nd = n1;
+            } else {
+                parked = true;
+                break;
+            }
+            if (demand > 0) {
+                const unsigned long long want = __ballot(donate);
+                if (want != 0ull) {
+                    const int sp0 = *spp;
+                    const int cap = kCoopStack - sp0;
+                    int g = __popcll(want);
+                    g = g < demand ? g : demand;
+                    g = g < cap ? g : cap;
+                    if (donate) {
+                        const int rank = __popcll(want & lt_mask);
+                        if (rank < g) {
+                            L.stack[sp0 + rank] = coop_piece(r, rest, end);
+                            end = rest;
+                        }
+                    }
+                    demand -= g;
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                    if (lane == __builtin_ctzll(__ballot(true))) *spp = sp0 + g;
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            if (__all(lc > 0 || i >= end)) break;
+        }
+        /* ---- triangle phase ---- */
+        if (lc > 0) {
+            DTriGeo g = s.slots[lf];
+            for (int k = 0; k < lc; ++k) {
+                const int slot = lf + k;
+                const DTriGeo gn = s.slots[k + 1 < lc ? slot + 1 : slot];
+                float t;
+                if (COUNT) ++c.tris;
+                if (tri_hit(ro, rd, g, s.slot_cull + slot, t)) {
+                    const unsigned long long kk = coop_key(t, slot);
+                    mine = kk < mine ? kk : mine;
+                }
+                g = gn;
+            }
+            lc = 0;
+        }
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long kk = L.key[lane];
+    if (!active || kk == ~0ull) return -1;
+    const int slot = (int)(kk & 0xffffffffu);
+    float t = 0.0f;
+    (void)tri_hit(o, d, s.slots[slot], s.slot_cull + slot, t);
+    best_t = t;
+    if (COUNT) ++c.hits;
+    return slot;
+}
+
+/* TRAV: 0 per-lane walk | 1 while-while | 2 while-while + prefetch | 3 as 2 with branch-free boxes */
+template <int TRAV, bool COUNT>
+__device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, Vec o, Vec d, float &best_t, LaneCounts &c) {
+    if (TRAV == 4) return trace_coop<COUNT>(s, *L, true, o, d, best_t, c);
+    if (TRAV == 5) return trace_share<COUNT>(s, *L, true, o, d, best_t, c);
+    if (TRAV == 1) return trace_closest_ww<COUNT>(s, o, d, best_t, c);
+    if (TRAV == 2) return trace_closest_wwp<COUNT, false>(s, o, d, best_t, c);
+    if (TRAV == 3) return trace_closest_wwp<COUNT, true>(s, o, d, best_t, c);
+    return trace_closest<COUNT>(s, o, d, best_t, c);
+}
+
 __device__ __forceinline__ void make_hit(const DeviceScene &s, Vec o, Vec d, float t, int slot, HitRec &h,
                                          int32_t *tri_out = nullptr) {
     const DTriGeo g = s.slots[slot];
@@ -162,8 +613,8 @@ __device__ __forceinline__ float pow5(float x) {
  * FULL=false: scenes whose materials are only diffuse/constant with GI off —
  * no recursion, no frame stack.  FULL=true: GI + reflective + refractive with
  * a per-lane frame stack of MAXF entries (≥ max_ray_depth + 1, host-checked). */
-template <bool FULL, int MAXF, bool COUNT>
-__device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt) {
+template <bool FULL, int MAXF, int TRAV, bool COUNT>
+__device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt, CoopLds *L) {
     Vec o, d;
     camera_ray(s, x, y, o, d);
     uint32_t depth = 0;
@@ -179,7 +630,7 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
             col = vec(0.f, 0.f, 0.f);
         } else {
             float t;
-            const int slot = trace_closest<COUNT>(s, o, d, t, cnt);
+            const int slot = trace<TRAV, COUNT>(s, L, o, d, t, cnt);
             if (slot < 0) {
                 col = vec(s.background[0], s.background[1], s.background[2]);
             } else {
@@ -302,7 +753,7 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
     return col;
 }
 
-template <bool FULL, int MAXF, bool COUNT>
+template <bool FULL, int MAXF, int TRAV, bool COUNT>
 __global__ __launch_bounds__(256) void k_render_tiles(DeviceScene s, DSettings st, const Tile *__restrict__ tiles,
                                                       int ntiles, float *__restrict__ out,
                                                       unsigned long long *__restrict__ counters) {
@@ -313,7 +764,9 @@ __global__ __launch_bounds__(256) void k_render_tiles(DeviceScene s, DSettings s
     const int lx = lane & 7, ly = lane >> 3;
     if (lx >= tl.w || ly >= tl.h) return;
     LaneCounts cnt = {0u, 0u, 0u, 0u};
-    const Vec c = shade_pixel<FULL, MAXF, COUNT>(s, st, tl.x + lx, tl.y + ly, cnt);
+    __shared__ CoopLds coop[TRAV >= 4 ? 4 : 1];
+    const Vec c = shade_pixel<FULL, MAXF, TRAV, COUNT>(s, st, tl.x + lx, tl.y + ly, cnt,
+                                                      &coop[TRAV >= 4 ? (threadIdx.x >> 6) : 0]);
     float *px = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
     px[0] = c.x;
     px[1] = c.y;
@@ -335,7 +788,7 @@ __global__ __launch_bounds__(256) void k_trace_rays(DeviceScene s, const float *
     const Vec d = vec(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
     LaneCounts cnt;
     float t;
-    const int slot = trace_closest<false>(s, o, d, t, cnt);
+    const int slot = trace_closest_ww<false>(s, o, d, t, cnt);
     crt_hit r;
     r.distance = 0.f;
     r.point[0] = r.point[1] = r.point[2] = 0.f;
@@ -445,6 +898,9 @@ struct crt_hip_scene {
     float *d_out = nullptr;
     unsigned long long *d_counters = nullptr;
     bool grid_empty = false;
+    int traversal = 2;             /* kernel walk variant, see trace<> (env CRT_TRAVERSAL) */
+    int tile_order = 1;            /* dispatch tiles by estimated work (env CRT_TILE_ORDER) */
+    std::vector<float> tile_work;  /* per 8x8 tile of the full frame */
 };
 
 namespace {
@@ -483,6 +939,17 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         plan.packed_pixels = total;
     }
     plan.ntiles = (int)tiles.size();
+    if (sc->tile_order && !tiles.empty() && !sc->tile_work.empty()) {
+        /* dispatch the expensive tiles first so the longest waves start at t=0 */
+        const int tx = (W + 7) / 8;
+        std::vector<std::pair<float, int>> key(tiles.size());
+        for (size_t k = 0; k < tiles.size(); ++k)
+            key[k] = {-sc->tile_work[(size_t)(tiles[k].y / 8) * tx + tiles[k].x / 8], (int)k};
+        std::stable_sort(key.begin(), key.end());
+        std::vector<Tile> sorted(tiles.size());
+        for (size_t k = 0; k < tiles.size(); ++k) sorted[k] = tiles[key[k].second];
+        tiles.swap(sorted);
+    }
     if (!tiles.empty()) {
         void *p = nullptr;
         HIP_TRY(hipMalloc(&p, tiles.size() * sizeof(Tile)));
@@ -541,9 +1008,20 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     const int blocks = (plan.ntiles + 3) / 4;
     const uint64_t frames = (uint64_t)st->max_ray_depth + 1;
     unsigned long long *cnt = sc->d_counters;
-#define CRT_LAUNCH(FULL, MAXF, COUNT)                                                                    \
-    hipLaunchKernelGGL((k_render_tiles<FULL, MAXF, COUNT>), dim3(blocks), dim3(256), 0, stream, sc->ds, ds, \
-                       plan.d_tiles, plan.ntiles, d_out, cnt)
+#define CRT_LAUNCH_T(FULL, MAXF, TRAV, COUNT)                                                               \
+    hipLaunchKernelGGL((k_render_tiles<FULL, MAXF, TRAV, COUNT>), dim3(blocks), dim3(256), 0, stream, sc->ds, \
+                       ds, plan.d_tiles, plan.ntiles, d_out, cnt)
+#define CRT_LAUNCH(FULL, MAXF, COUNT)                                                                       \
+    do {                                                                                                   \
+        switch (sc->traversal) {                                                                           \
+        case 0: CRT_LAUNCH_T(FULL, MAXF, 0, COUNT); break;                                                 \
+        case 1: CRT_LAUNCH_T(FULL, MAXF, 1, COUNT); break;                                                 \
+        case 3: CRT_LAUNCH_T(FULL, MAXF, 3, COUNT); break;                                                 \
+        case 4: CRT_LAUNCH_T(FULL, MAXF, 4, COUNT); break;                                                 \
+        case 5: CRT_LAUNCH_T(FULL, MAXF, 5, COUNT); break;                                                 \
+        default: CRT_LAUNCH_T(FULL, MAXF, 2, COUNT); break;                                                \
+        }                                                                                                  \
+    } while (0)
     if (!full) {
         if (count) CRT_LAUNCH(false, 0, true); else CRT_LAUNCH(false, 0, false);
     } else if (frames <= 4) {
@@ -588,6 +1066,9 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     HIP_TRY(hipSetDevice(device));
     std::unique_ptr<crt_hip_scene> sc(new crt_hip_scene());
     sc->device = device;
+    if (const char *e = std::getenv("CRT_TRAVERSAL")) sc->traversal = std::atoi(e);
+    if (const char *e = std::getenv("CRT_TILE_ORDER")) sc->tile_order = std::atoi(e);
+    if (sc->tile_order) sc->tile_work = tile_work_estimate(hs, (hs.width + 7) / 8, (hs.height + 7) / 8);
     crt_host_scene_info(h, &sc->info);
     sc->info.device_bytes = 0;
     for (const DMaterial &m : hs.materials) {

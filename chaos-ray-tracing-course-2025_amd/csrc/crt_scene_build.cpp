@@ -367,6 +367,43 @@ int prepare_scene(const crt_scene_desc *d, HostScene &hs) {
     return CRT_OK;
 }
 
+std::vector<float> tile_work_estimate(const HostScene &hs, int tiles_x, int tiles_y) {
+    std::vector<float> w((size_t)tiles_x * tiles_y, 0.f);
+    const size_t n = hs.ref_children.size() / 2;
+    const float *R = hs.cam_rot;
+    const float sx = hs.aspect * hs.tan_half_fov, sy = hs.tan_half_fov;
+    for (size_t i = 0; i < n; ++i) {
+        const int64_t cnt = hs.ref_leaf_off[i + 1] - hs.ref_leaf_off[i];
+        if (cnt == 0) continue;
+        const float *b = &hs.ref_bounds[6 * i];
+        float x0 = 1e30f, x1 = -1e30f, y0 = 1e30f, y1 = -1e30f;
+        bool behind = false;
+        for (int c = 0; c < 8; ++c) {
+            const float v[3] = {b[(c & 1) ? 3 : 0] - hs.cam_loc[0], b[(c & 2) ? 4 : 1] - hs.cam_loc[1],
+                                b[(c & 4) ? 5 : 2] - hs.cam_loc[2]};
+            /* camera space = world * R^T (ray dir = cam * R, crt_camera.cpp:31) */
+            const float cx = v[0] * R[0] + v[1] * R[1] + v[2] * R[2];
+            const float cy = v[0] * R[3] + v[1] * R[4] + v[2] * R[5];
+            const float cz = v[0] * R[6] + v[1] * R[7] + v[2] * R[8];
+            if (!(cz < -1e-6f)) { behind = true; break; }
+            const float px = (cx / -cz / sx + 1.0f) * 0.5f * hs.width;
+            const float py = (1.0f - cy / -cz / sy) * 0.5f * hs.height;
+            x0 = std::min(x0, px); x1 = std::max(x1, px);
+            y0 = std::min(y0, py); y1 = std::max(y1, py);
+        }
+        int tx0 = 0, tx1 = tiles_x - 1, ty0 = 0, ty1 = tiles_y - 1;
+        if (!behind) {
+            if (x1 < 0 || y1 < 0 || x0 >= hs.width || y0 >= hs.height) continue;
+            tx0 = std::max(0, (int)(x0 / 8)); tx1 = std::min(tiles_x - 1, (int)(x1 / 8));
+            ty0 = std::max(0, (int)(y0 / 8)); ty1 = std::min(tiles_y - 1, (int)(y1 / 8));
+        }
+        const float add = (float)cnt;
+        for (int ty = ty0; ty <= ty1; ++ty)
+            for (int tx = tx0; tx <= tx1; ++tx) w[(size_t)ty * tiles_x + tx] += add;
+    }
+    return w;
+}
+
 std::vector<DBucket> shard_buckets(int32_t width, int32_t height, int32_t bucket_size, int shard,
                                    int shard_count, int64_t *packed_pixels) {
     std::vector<DBucket> out;

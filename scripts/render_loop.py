@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Render a scene K times through the C-ABI (no torch) — driver for rocprofv3
+kernel traces / PMC passes and for in-process A/B of kernel variants.
+
+  render_loop.py [--scene NAME] [--width W --height H] [--frames K] [--depth D]
+                 [--ab VAR=a,b]   # A/B: one scene per env value, interleaved rounds
+"""
+import argparse
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "chaos-ray-tracing-course-2025_amd"))
+
+from crt_amd import native as N  # noqa: E402
+from crt_amd.scene_npz import load_npz  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--scene", default="14-01-acceleration-tree__scene1")
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--frames", type=int, default=5)
+    p.add_argument("--depth", type=int, default=3)
+    p.add_argument("--ab", default=None, help="ENVVAR=v1,v2,... — build one scene per value")
+    a = p.parse_args()
+    sc = load_npz(ROOT / "tests" / "golden" / "scenes" / f"{a.scene}.npz").set_resolution(a.width, a.height)
+    st = N.RendererSettings.default(max_ray_depth=a.depth)
+    variants = [("default", None)]
+    if a.ab:
+        var, vals = a.ab.split("=")
+        variants = [(f"{var}={v}", (var, v)) for v in vals.split(",")]
+    scenes = []
+    for name, kv in variants:
+        if kv:
+            os.environ[kv[0]] = kv[1]
+        scenes.append((name, N.HipScene(sc)))
+    times = {name: [] for name, _ in scenes}
+    ref = None
+    for _ in range(a.frames):
+        for name, g in scenes:
+            img, stats = g.render(st, with_stats=True)
+            times[name].append(stats["kernel_ms"])
+            if ref is None:
+                ref = img
+            elif not np.array_equal(ref.view(np.uint32), img.view(np.uint32)):
+                print(f"MISMATCH in variant {name}", flush=True)
+    out = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v)), "n": len(v)} for k, v in times.items()}
+    print(json.dumps({"scene": a.scene, "size": [a.width, a.height], "depth": a.depth, "kernel": out}))
+
+
+if __name__ == "__main__":
+    main()
