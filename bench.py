@@ -98,7 +98,10 @@ def main():
     settings = N.RendererSettings.default()
     gpu = N.HipScene(scene, device=local)
     W, H = a.width, a.height
-    stream = torch.cuda.current_stream()
+    # an explicit stream: the render kernel, the gather and the timing events
+    # all go on it (handle 0 would mean "the scene's own stream" to the C-ABI)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
 
     frame = torch.empty(W * H * 3, dtype=torch.float32, device="cuda")

@@ -149,6 +149,7 @@ EXPORTS = [
     ("crt_hip_trace_batch", C.c_int, [_P, _P, C.c_int64, _P]),
     ("crt_hip_count_work", C.c_int, [_P, C.POINTER(RendererSettings), C.POINTER(WorkCounts)]),
     ("crt_hip_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_double)]),
+    ("crt_hip_profile_waves", C.c_int, [_P, C.POINTER(RendererSettings), _P, C.c_int64, _P]),
     ("crt_renderer_settings_default", None, [C.POINTER(RendererSettings)]),
     ("crt_write_ppm", C.c_int, [C.c_char_p, _P, C.c_int32, C.c_int32, C.c_int32]),
     ("crt_hip_last_error", C.c_char_p, []),
@@ -393,6 +394,19 @@ class HipScene:
         out = np.zeros(len(rays), HIT_DTYPE)
         _check(lib().crt_hip_trace_batch(self._h, rays.ctypes.data, len(rays), out.ctypes.data))
         return out
+
+    def profile_waves(self, settings: RendererSettings | None = None):
+        """Diagnostic frame: (stamps[ntiles, 2] in 10-ns ticks, tile_xy[ntiles, 2]) in dispatch order."""
+        st = settings or RendererSettings.default()
+        n = lib().crt_hip_profile_waves(self._h, C.byref(st), None, 0, None)
+        if n < 0:
+            _check(n)
+        stamps = np.zeros((n, 2), np.uint64)
+        xy = np.zeros((n, 2), np.int32)
+        rc = lib().crt_hip_profile_waves(self._h, C.byref(st), stamps.ctypes.data, n, xy.ctypes.data)
+        if rc < 0:
+            _check(rc)
+        return stamps, xy
 
     def count_work(self, settings: RendererSettings | None = None) -> dict:
         st = settings or RendererSettings.default()

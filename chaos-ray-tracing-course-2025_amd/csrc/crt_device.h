@@ -44,6 +44,11 @@ CRT_HD Vec vec_mat(Vec v, const float m[9]) {
     return vec(r0, r1, r2);
 }
 
+/* Node record fields (crt_layout.h): interior b = -(depth+1), a = skip;
+ * leaf a = count | depth << 24, b = first slot. */
+CRT_HD int node_leaf_count(const DNode &n) { return n.a & 0xffffff; }
+CRT_HD int node_depth(const DNode &n) { return n.b < 0 ? -n.b - 1 : (int)((unsigned)n.a >> 24); }
+
 /* Camera::generate_ray (crt_camera.cpp:7-35). aspect and tan_half_fov are the
  * per-frame constants float(W)/H and std::tan(fov*0.5f), computed on the host. */
 CRT_HD void camera_ray(const DeviceScene &s, int x, int y, Vec &o, Vec &d) {
@@ -112,6 +117,114 @@ CRT_HD bool box_hit_bf(Vec o, Vec d, const DNode &n) {
            box_face_bf(n.hi_x, o.x, d.x, o.y, d.y, o.z, d.z, n.lo_y, n.hi_y, n.lo_z, n.hi_z) |
            box_face_bf(n.hi_y, o.y, d.y, o.z, d.z, o.x, d.x, n.lo_z, n.hi_z, n.lo_x, n.hi_x) |
            box_face_bf(n.hi_z, o.z, d.z, o.x, d.x, o.y, d.y, n.lo_x, n.hi_x, n.lo_y, n.hi_y));
+}
+
+/* ---- per-ray hoisted division ---------------------------------------- */
+/* hipcc lowers fp32 a/b to (LLVM AMDGPU LowerFDIV32):
+ *   y0 = rcp(b'); y1 = fma(fma(-b', y0, 1), y0, y0); q0 = a'*y1;
+ *   q1 = fma(fma(-b', q0, a'), y1, q0); q = div_fmas(fma(-b', q1, a'), y1, q1); div_fixup
+ * with a', b' = div_scale(a, b).  div_scale leaves both operands unchanged and
+ * div_fmas is a plain fma unless |exp(a) - exp(b)| approaches 96, b is
+ * denormal or a is near the denormal range; div_fixup only rewrites special
+ * values.  So for |b| in [2^-20, 2^20] and |a| in [2^-64, 2^64] the sequence
+ * below, with the b-only part (y1) computed once per ray and axis, returns
+ * the same bits as '/', i.e. the correctly rounded quotient.  Anything outside
+ * that window takes the compiler's '/'. */
+struct RayRcp {
+    float y1[3];
+    bool fast[3];
+};
+
+CRT_HD float rcp_refined(float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float y0 = __builtin_amdgcn_rcpf(b);
+#else
+    const float y0 = 1.0f / b;   /* host builds of this header never take the fast path */
+#endif
+    return fmaf(fmaf(-b, y0, 1.0f), y0, y0);
+}
+
+CRT_HD RayRcp make_ray_rcp(Vec d) {
+    RayRcp r;
+    const float dd[3] = {d.x, d.y, d.z};
+    for (int k = 0; k < 3; ++k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const float m = fabsf(dd[k]);
+        r.fast[k] = m >= 9.5367431640625e-7f && m <= 1048576.0f;   /* [2^-20, 2^20] */
+#else
+        r.fast[k] = false;
+#endif
+        r.y1[k] = rcp_refined(r.fast[k] ? dd[k] : 1.0f);
+    }
+    return r;
+}
+
+CRT_HD float div_hoisted(float a, float b, float y1, bool fast_b) {
+    const float m = fabsf(a);
+    if (fast_b && m >= 5.421010862427522e-20f && m <= 1.8446744073709552e19f) {   /* [2^-64, 2^64] */
+        const float q0 = a * y1;
+        const float q1 = fmaf(fmaf(-b, q0, a), y1, q0);
+        return fmaf(fmaf(-b, q1, a), y1, q1);
+    }
+    return a / b;
+}
+
+/* ray_intersect_aabb_p (crt_intersection.cpp:14-45), branch-free over the six
+ * faces, with the per-ray hoisted divisions (one slow-path branch per node,
+ * taken only when a numerator leaves the exactness window). */
+CRT_HD float div_fast(float a, float b, float y1) {
+    const float q0 = a * y1;
+    const float q1 = fmaf(fmaf(-b, q0, a), y1, q0);
+    return fmaf(fmaf(-b, q1, a), y1, q1);
+}
+CRT_HD bool in_window(float a) {
+    const float m = fabsf(a);
+    return m >= 5.421010862427522e-20f && m <= 1.8446744073709552e19f;   /* [2^-64, 2^64] */
+}
+CRT_HD int face_ok(float t, float d_a, float o_u, float d_u, float o_w, float d_w, float lo_u, float hi_u, float lo_w,
+                   float hi_w) {
+    const float pu = o_u + d_u * t;
+    const float pw = o_w + d_w * t;
+    return (int)!(fabsf(d_a) < 1e-6f) & (int)!(t < 0.0f) & (int)(pu >= lo_u) & (int)(pu <= hi_u) &
+           (int)(pw >= lo_w) & (int)(pw <= hi_w);
+}
+
+CRT_HD bool box_hit_r(Vec o, Vec d, const RayRcp &r, const DNode &n) {
+    const float a0 = n.lo_x - o.x, a1 = n.lo_y - o.y, a2 = n.lo_z - o.z;
+    const float a3 = n.hi_x - o.x, a4 = n.hi_y - o.y, a5 = n.hi_z - o.z;
+    float t0, t1, t2, t3, t4, t5;
+    const bool fast = ((int)r.fast[0] & (int)r.fast[1] & (int)r.fast[2] & (int)in_window(a0) & (int)in_window(a1) &
+                       (int)in_window(a2) & (int)in_window(a3) & (int)in_window(a4) & (int)in_window(a5)) != 0;
+    if (fast) {
+        t0 = div_fast(a0, d.x, r.y1[0]); t1 = div_fast(a1, d.y, r.y1[1]); t2 = div_fast(a2, d.z, r.y1[2]);
+        t3 = div_fast(a3, d.x, r.y1[0]); t4 = div_fast(a4, d.y, r.y1[1]); t5 = div_fast(a5, d.z, r.y1[2]);
+    } else {
+        t0 = a0 / d.x; t1 = a1 / d.y; t2 = a2 / d.z;
+        t3 = a3 / d.x; t4 = a4 / d.y; t5 = a5 / d.z;
+    }
+    return 0 != (face_ok(t0, d.x, o.y, d.y, o.z, d.z, n.lo_y, n.hi_y, n.lo_z, n.hi_z) |
+                 face_ok(t1, d.y, o.z, d.z, o.x, d.x, n.lo_z, n.hi_z, n.lo_x, n.hi_x) |
+                 face_ok(t2, d.z, o.x, d.x, o.y, d.y, n.lo_x, n.hi_x, n.lo_y, n.hi_y) |
+                 face_ok(t3, d.x, o.y, d.y, o.z, d.z, n.lo_y, n.hi_y, n.lo_z, n.hi_z) |
+                 face_ok(t4, d.y, o.z, d.z, o.x, d.x, n.lo_z, n.hi_z, n.lo_x, n.hi_x) |
+                 face_ok(t5, d.z, o.x, d.x, o.y, d.y, n.lo_x, n.hi_x, n.lo_y, n.hi_y));
+}
+
+/* ray_intersect_triangle (crt_intersection.cpp:47-93), branch-free. */
+CRT_HD bool tri_hit_bf(Vec o, Vec d, const DTriGeo &g, bool cull, float &t_out) {
+    const Vec N = vec(g.nx, g.ny, g.nz);
+    const Vec v0 = vec(g.v0x, g.v0y, g.v0z), v1 = vec(g.v1x, g.v1y, g.v1z), v2 = vec(g.v2x, g.v2y, g.v2z);
+    const float rn = vdot(N, d);
+    const float op = vdot(N, vsub(v0, o));
+    const float t = op / rn;
+    const Vec e0 = vsub(v1, v0), e1 = vsub(v2, v1), e2 = vsub(v0, v2);
+    const Vec p = vadd(o, vscale(d, t));
+    const Vec v0p = vsub(p, v0), v1p = vsub(p, v1), v2p = vsub(p, v2);
+    const int ok = (int)!(fabsf(rn) < 1e-6f) & (int)((op < 0.0f) | !cull) & (int)!(t < 0.0f) &
+                   (int)(vdot(N, vcross(e0, v0p)) >= 0.0f) & (int)(vdot(N, vcross(e1, v1p)) >= 0.0f) &
+                   (int)(vdot(N, vcross(e2, v2p)) >= 0.0f);
+    t_out = t;
+    return ok != 0;
 }
 
 /* ray_intersect_triangle (crt_intersection.cpp:47-93), distance only.  The

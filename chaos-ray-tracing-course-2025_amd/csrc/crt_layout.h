@@ -31,8 +31,8 @@ namespace crt_amd {
 struct alignas(16) DNode {
     float lo_x, lo_y, lo_z, hi_x;
     float hi_y, hi_z;
-    int32_t a;   /* interior: skip index (first node after the subtree) | leaf: slot count   */
-    int32_t b;   /* interior: -1                                         | leaf: first slot  */
+    int32_t a;   /* interior: skip index (first node after the subtree) | leaf: count | depth << 24 */
+    int32_t b;   /* interior: -(depth + 1)                               | leaf: first slot           */
 };
 static_assert(sizeof(DNode) == 32, "DNode must be 32 B");
 
@@ -78,6 +78,7 @@ struct DeviceScene {
     const DTriGeo *slots;
     const int32_t *slot_tri;
     const uint8_t *slot_cull;
+    const uint32_t *slot_cull_bits;   /* same flags, 1 bit per slot (scalar-path reads) */
     const DTriAttr *tri_attr;
     const DVec4 *vnormal;
     const DVec4 *vuv;

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -84,7 +85,7 @@ __device__ __forceinline__ int trace_closest(const DeviceScene &s, Vec o, Vec d,
             continue;
         }
         if (pass) {                    /* leaf: ray_intersect_triangle_span, strict '<' keeps the first */
-            for (int k = 0; k < nd.a; ++k) {
+            for (int k = 0; k < node_leaf_count(nd); ++k) {
                 const int slot = nd.b + k;
                 float t;
                 if (COUNT) ++c.tris;
@@ -135,7 +136,7 @@ __device__ __forceinline__ int trace_closest_ww(const DeviceScene &s, Vec o, Vec
                 ++i;
             } else if (lc == 0) {
                 lf = nd.b;
-                lc = nd.a;
+                lc = node_leaf_count(nd);
                 ++i;
             } else {
                 parked = true;   /* second leaf: wait here */
@@ -196,7 +197,7 @@ __device__ __forceinline__ int trace_closest_wwp(const DeviceScene &s, Vec o, Ve
                 nd = n1;
             } else if (lc == 0) {
                 lf = nd.b;
-                lc = nd.a;
+                lc = node_leaf_count(nd);
                 ++i;
                 nd = n1;
             } else {
@@ -336,7 +337,7 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
                         nd = n2;
                     }
                 } else {
-                    if (pass) { lf = nd.b; lc = nd.a; k = 0; }
+                    if (pass) { lf = nd.b; lc = node_leaf_count(nd); k = 0; }
                     i = i + 1;
                     nd = n1;
                 }
@@ -479,7 +480,7 @@ __device__ int trace_share(const DeviceScene &s, CoopLds &L, bool active, Vec o,
                 nd = n1;
             } else if (lc == 0) {
                 lf = nd.b;
-                lc = nd.a;
+                lc = node_leaf_count(nd);
                 ++i;
                 nd = n1;
             } else {
@@ -539,11 +540,89 @@ __device__ int trace_share(const DeviceScene &s, CoopLds &L, bool active, Vec o,
     return slot;
 }
 
+/* ---------------------------------------------------------------------- */
+/* Masked packet walk (TRAV 6) — coherent rays (primary rays of a tile)     */
+/* ---------------------------------------------------------------------- */
+/* The whole wave walks the traversal-ordered node array with ONE wave-uniform
+ * index, so node and triangle records come through the scalar path (SGPRs)
+ * and the control flow never diverges.  Each lane keeps 64 reach bits: bit D
+ * is set iff every ancestor at depths < D of the current depth-D node passed
+ * its box test for this lane's ray.  A node is tested for the lanes whose bit
+ * is set; an interior node where no lane passes is skipped, otherwise the walk
+ * descends with bit D+1 = this lane's pass.  Every lane therefore tests
+ * exactly the nodes, leaves and triangles the reference visits for its ray, in
+ * the reference's order (strict '<' keeps the first-found winner); the wave
+ * pays once per node of the union of its lanes' visit sets.  Tree depth is at
+ * most 40 (crt_acceleration_tree.h:12), within the 64 bits. */
+__device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+/* Scene records are read-only for the whole launch: reading them through the
+ * constant address space lets a wave-uniform index become an s_load into SGPRs. */
+template <class T>
+__device__ __forceinline__ T load_scalar(const T *p, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    using CT = const __attribute__((address_space(4))) T;
+    return ((CT *)p)[i];
+#else
+    return p[i];
+#endif
+}
+
+template <bool COUNT>
+__device__ int trace_packet(const DeviceScene &s, bool active, Vec o, Vec d, float &best_t, LaneCounts &c) {
+    int best = -1;
+    best_t = 0.0f;
+    const RayRcp rr = make_ray_rcp(d);
+    unsigned long long reach = active ? 1ull : 0ull;
+    if (COUNT && active) ++c.traversals;
+    const int n = s.node_count;
+    int i = 0;
+    while (i < n) {
+        i = uniform_i(i);
+        const DNode nd = load_scalar(s.nodes, i);
+        const int depth = node_depth(nd);
+        const bool in = ((reach >> depth) & 1ull) != 0ull;
+        const bool pass = in && box_hit_r(o, d, rr, nd);
+        if (COUNT && in) ++c.nodes;
+        const unsigned long long pm = __ballot(pass);
+        if (nd.b < 0) {
+            if (pm != 0ull) {
+                const unsigned long long bit = 2ull << depth;
+                reach = pass ? (reach | bit) : (reach & ~bit);
+                i = i + 1;
+            } else {
+                i = nd.a;
+            }
+        } else {
+            if (pm != 0ull) {
+                const int first = nd.b, cnt = node_leaf_count(nd);
+                for (int k = 0; k < cnt; ++k) {
+                    const int slot = uniform_i(first + k);
+                    const DTriGeo g = load_scalar(s.slots, slot);
+                    const bool cull = ((load_scalar(s.slot_cull_bits, slot >> 5) >> (slot & 31)) & 1u) != 0u;
+                    float t;
+                    if (COUNT && pass) ++c.tris;
+                    const bool h = tri_hit_bf(o, d, g, cull, t);
+                    if (pass && h && (best < 0 || t < best_t)) {
+                        best_t = t;
+                        best = slot;
+                    }
+                }
+            }
+            i = i + 1;
+        }
+    }
+    if (COUNT && best >= 0) ++c.hits;
+    return best;
+}
+
 /* TRAV: 0 per-lane walk | 1 while-while | 2 while-while + prefetch | 3 as 2 with branch-free boxes */
 template <int TRAV, bool COUNT>
-__device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, Vec o, Vec d, float &best_t, LaneCounts &c) {
-    if (TRAV == 4) return trace_coop<COUNT>(s, *L, true, o, d, best_t, c);
-    if (TRAV == 5) return trace_share<COUNT>(s, *L, true, o, d, best_t, c);
+__device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, bool active, Vec o, Vec d, float &best_t,
+                                     LaneCounts &c) {
+    if (TRAV == 4) return trace_coop<COUNT>(s, *L, active, o, d, best_t, c);
+    if (TRAV == 5) return trace_share<COUNT>(s, *L, active, o, d, best_t, c);
+    if (TRAV == 6) return trace_packet<COUNT>(s, active, o, d, best_t, c);
     if (TRAV == 1) return trace_closest_ww<COUNT>(s, o, d, best_t, c);
     if (TRAV == 2) return trace_closest_wwp<COUNT, false>(s, o, d, best_t, c);
     if (TRAV == 3) return trace_closest_wwp<COUNT, true>(s, o, d, best_t, c);
@@ -614,7 +693,8 @@ __device__ __forceinline__ float pow5(float x) {
  * no recursion, no frame stack.  FULL=true: GI + reflective + refractive with
  * a per-lane frame stack of MAXF entries (≥ max_ray_depth + 1, host-checked). */
 template <bool FULL, int MAXF, int TRAV, bool COUNT>
-__device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt, CoopLds *L) {
+__device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt, CoopLds *L,
+                           bool has_px) {
     Vec o, d;
     camera_ray(s, x, y, o, d);
     uint32_t depth = 0;
@@ -630,7 +710,7 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
             col = vec(0.f, 0.f, 0.f);
         } else {
             float t;
-            const int slot = trace<TRAV, COUNT>(s, L, o, d, t, cnt);
+            const int slot = trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
             if (slot < 0) {
                 col = vec(s.background[0], s.background[1], s.background[2]);
             } else {
@@ -756,21 +836,31 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
 template <bool FULL, int MAXF, int TRAV, bool COUNT>
 __global__ __launch_bounds__(256) void k_render_tiles(DeviceScene s, DSettings st, const Tile *__restrict__ tiles,
                                                       int ntiles, float *__restrict__ out,
-                                                      unsigned long long *__restrict__ counters) {
+                                                      unsigned long long *__restrict__ counters,
+                                                      unsigned long long *__restrict__ stamps) {
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int lane = (int)(threadIdx.x & 63);
     if (wave >= ntiles) return;
+    /* diagnostic build only (stamps != nullptr): wave start / end in s_memrealtime ticks (100 MHz) */
+    if (stamps && lane == 0) stamps[2 * wave] = __builtin_amdgcn_s_memrealtime();
     const Tile tl = tiles[wave];
     const int lx = lane & 7, ly = lane >> 3;
-    if (lx >= tl.w || ly >= tl.h) return;
+    const bool has_px = lx < tl.w && ly < tl.h;
+    /* the sharing walks keep pixel-less lanes as helpers (they take donated node
+     * ranges of the wave's rays); the other walks drop them */
+    constexpr bool kHelpers = (TRAV == 4 || TRAV == 5 || TRAV == 6) && !FULL;
+    if (!kHelpers && !has_px) return;
     LaneCounts cnt = {0u, 0u, 0u, 0u};
     __shared__ CoopLds coop[TRAV >= 4 ? 4 : 1];
-    const Vec c = shade_pixel<FULL, MAXF, TRAV, COUNT>(s, st, tl.x + lx, tl.y + ly, cnt,
-                                                      &coop[TRAV >= 4 ? (threadIdx.x >> 6) : 0]);
-    float *px = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
-    px[0] = c.x;
-    px[1] = c.y;
-    px[2] = c.z;
+    const Vec c = shade_pixel<FULL, MAXF, TRAV, COUNT>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt,
+                                                      &coop[TRAV >= 4 ? (threadIdx.x >> 6) : 0], has_px);
+    if (has_px) {
+        float *px = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
+        px[0] = c.x;
+        px[1] = c.y;
+        px[2] = c.z;
+    }
+    if (stamps && lane == 0) stamps[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
     if (COUNT) {
         atomicAdd(&counters[0], (unsigned long long)cnt.traversals);
         atomicAdd(&counters[1], (unsigned long long)cnt.nodes);
@@ -900,6 +990,7 @@ struct crt_hip_scene {
     bool grid_empty = false;
     int traversal = 2;             /* kernel walk variant, see trace<> (env CRT_TRAVERSAL) */
     int tile_order = 1;            /* dispatch tiles by estimated work (env CRT_TILE_ORDER) */
+    float split4 = 0.2f, split16 = 0.5f;   /* relative work above which a tile is split (env CRT_SPLIT="a,b") */
     std::vector<float> tile_work;  /* per 8x8 tile of the full frame */
 };
 
@@ -938,18 +1029,34 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         }
         plan.packed_pixels = total;
     }
-    plan.ntiles = (int)tiles.size();
     if (sc->tile_order && !tiles.empty() && !sc->tile_work.empty()) {
-        /* dispatch the expensive tiles first so the longest waves start at t=0 */
+        /* dispatch the expensive tiles first so the longest waves start at t=0;
+         * with a sharing walk, split the heaviest tiles so each of their waves
+         * carries fewer rays and the rest of its lanes help (4x4 or 2x2 pixels) */
         const int tx = (W + 7) / 8;
+        auto work = [&](const Tile &t) { return sc->tile_work[(size_t)(t.y / 8) * tx + t.x / 8]; };
+        float wmax = 0.f;
+        for (const Tile &t : tiles) wmax = std::max(wmax, work(t));
+        std::vector<Tile> split;
+        if (sc->traversal >= 4 && wmax > 0.f && (sc->split4 > 0.f || sc->split16 > 0.f)) {
+            for (const Tile &t : tiles) {
+                const float w = work(t) / wmax;
+                const int sub = (sc->split16 > 0.f && w >= sc->split16) ? 2 : (sc->split4 > 0.f && w >= sc->split4) ? 4 : 8;
+                for (int yy = 0; yy < t.h; yy += sub)
+                    for (int xx = 0; xx < t.w; xx += sub)
+                        split.push_back(Tile{t.x + xx, t.y + yy, std::min(sub, t.w - xx), std::min(sub, t.h - yy),
+                                             t.out_base + (int64_t)yy * t.out_stride + xx, t.out_stride, 0});
+            }
+            tiles.swap(split);
+        }
         std::vector<std::pair<float, int>> key(tiles.size());
-        for (size_t k = 0; k < tiles.size(); ++k)
-            key[k] = {-sc->tile_work[(size_t)(tiles[k].y / 8) * tx + tiles[k].x / 8], (int)k};
+        for (size_t k = 0; k < tiles.size(); ++k) key[k] = {-work(tiles[k]), (int)k};
         std::stable_sort(key.begin(), key.end());
         std::vector<Tile> sorted(tiles.size());
         for (size_t k = 0; k < tiles.size(); ++k) sorted[k] = tiles[key[k].second];
         tiles.swap(sorted);
     }
+    plan.ntiles = (int)tiles.size();
     if (!tiles.empty()) {
         void *p = nullptr;
         HIP_TRY(hipMalloc(&p, tiles.size() * sizeof(Tile)));
@@ -996,7 +1103,7 @@ DSettings to_dsettings(const crt_renderer_settings *st) {
 
 /* Pick and launch the kernel variant for this scene + settings. */
 int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const ShardPlan &plan, float *d_out,
-                  hipStream_t stream, bool count) {
+                  hipStream_t stream, bool count, unsigned long long *stamps = nullptr) {
     const bool gi = sc->info.gi_on && sc->has_diffuse && st->diffuse_reflection_ray_count > 0;
     const bool full = gi || sc->has_secondary;
     if (gi) {
@@ -1010,7 +1117,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     unsigned long long *cnt = sc->d_counters;
 #define CRT_LAUNCH_T(FULL, MAXF, TRAV, COUNT)                                                               \
     hipLaunchKernelGGL((k_render_tiles<FULL, MAXF, TRAV, COUNT>), dim3(blocks), dim3(256), 0, stream, sc->ds, \
-                       ds, plan.d_tiles, plan.ntiles, d_out, cnt)
+                       ds, plan.d_tiles, plan.ntiles, d_out, cnt, stamps)
 #define CRT_LAUNCH(FULL, MAXF, COUNT)                                                                       \
     do {                                                                                                   \
         switch (sc->traversal) {                                                                           \
@@ -1019,6 +1126,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         case 3: CRT_LAUNCH_T(FULL, MAXF, 3, COUNT); break;                                                 \
         case 4: CRT_LAUNCH_T(FULL, MAXF, 4, COUNT); break;                                                 \
         case 5: CRT_LAUNCH_T(FULL, MAXF, 5, COUNT); break;                                                 \
+        case 6: CRT_LAUNCH_T(FULL, MAXF, 6, COUNT); break;                                                 \
         default: CRT_LAUNCH_T(FULL, MAXF, 2, COUNT); break;                                                \
         }                                                                                                  \
     } while (0)
@@ -1068,6 +1176,10 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     sc->device = device;
     if (const char *e = std::getenv("CRT_TRAVERSAL")) sc->traversal = std::atoi(e);
     if (const char *e = std::getenv("CRT_TILE_ORDER")) sc->tile_order = std::atoi(e);
+    if (const char *e = std::getenv("CRT_SPLIT")) {
+        float a = 0.f, b = 0.f;
+        if (std::sscanf(e, "%f,%f", &a, &b) >= 1) { sc->split4 = a; sc->split16 = b; }
+    }
     if (sc->tile_order) sc->tile_work = tile_work_estimate(hs, (hs.width + 7) / 8, (hs.height + 7) / 8);
     crt_host_scene_info(h, &sc->info);
     sc->info.device_bytes = 0;
@@ -1082,6 +1194,12 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     if ((rc = upload(sc.get(), hs.slots, &ds.slots)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.slot_tri, &ds.slot_tri)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.slot_cull, &ds.slot_cull)) != CRT_OK) return rc;
+    {
+        std::vector<uint32_t> bits((hs.slot_cull.size() + 31) / 32 + 1, 0u);
+        for (size_t k = 0; k < hs.slot_cull.size(); ++k)
+            if (hs.slot_cull[k]) bits[k >> 5] |= 1u << (k & 31);
+        if ((rc = upload(sc.get(), bits, &ds.slot_cull_bits)) != CRT_OK) return rc;
+    }
     if ((rc = upload(sc.get(), hs.tri_attr, &ds.tri_attr)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.vnormal, &ds.vnormal)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.vuv, &ds.vuv)) != CRT_OK) return rc;
@@ -1279,6 +1397,31 @@ int crt_hip_trace_batch(crt_hip_scene *sc, const float *rays, int64_t n, crt_hit
     (void)hipFree(d_hits);
     if (e != hipSuccess) return set_error(CRT_E_HIP, hipGetErrorString(e));
     return CRT_OK;
+}
+
+int crt_hip_profile_waves(crt_hip_scene *sc, const crt_renderer_settings *st, uint64_t *stamps, int64_t cap,
+                          int32_t *tile_xy) {
+    if (!sc || !st) return set_error(CRT_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(sc->device));
+    const int nt = sc->full.ntiles;
+    if (!stamps || !tile_xy) return nt;      /* query the size */
+    if (cap < nt) return set_error(CRT_E_INVALID, "stamp buffer too small");
+    const size_t nfl = (size_t)sc->info.width * sc->info.height * 3;
+    if (!sc->d_out) HIP_TRY(hipMalloc(&sc->d_out, nfl * sizeof(float)));
+    unsigned long long *d = nullptr;
+    HIP_TRY(hipMalloc(&d, (size_t)nt * 2 * sizeof(unsigned long long)));
+    int rc = launch_render(sc, st, sc->full, sc->d_out, sc->stream, false, d);
+    hipError_t e = rc == CRT_OK ? hipStreamSynchronize(sc->stream) : hipSuccess;
+    if (rc == CRT_OK && e == hipSuccess)
+        e = hipMemcpy(stamps, d, (size_t)nt * 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    std::vector<Tile> tiles(nt);
+    if (rc == CRT_OK && e == hipSuccess)
+        e = hipMemcpy(tiles.data(), sc->full.d_tiles, (size_t)nt * sizeof(Tile), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (rc != CRT_OK) return rc;
+    if (e != hipSuccess) return set_error(CRT_E_HIP, hipGetErrorString(e));
+    for (int k = 0; k < nt; ++k) { tile_xy[2 * k] = tiles[k].x; tile_xy[2 * k + 1] = tiles[k].y; }
+    return nt;
 }
 
 int crt_hip_count_work(crt_hip_scene *sc, const crt_renderer_settings *st, crt_work_counts *out) {

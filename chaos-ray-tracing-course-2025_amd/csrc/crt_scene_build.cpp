@@ -344,9 +344,11 @@ int prepare_scene(const crt_scene_desc *d, HostScene &hs) {
         o.hi_x = bn[x].bounds.hi[0]; o.hi_y = bn[x].bounds.hi[1]; o.hi_z = bn[x].bounds.hi[2];
         if (bn[x].tris.empty()) {
             o.a = k + subtree[x];
-            o.b = -1;
+            o.b = -(bn[x].depth + 1);
         } else {
-            o.a = (int32_t)bn[x].tris.size();
+            if (bn[x].tris.size() >= (1u << 24) || bn[x].depth > 127)
+                return set_error(CRT_E_UNSUPPORTED, "leaf too large for the node record");
+            o.a = (int32_t)bn[x].tris.size() | (bn[x].depth << 24);
             o.b = (int32_t)hs.slots.size();
             for (int32_t t : bn[x].tris) {
                 const DTriAttr &at = hs.tri_attr[t];

@@ -225,6 +225,12 @@ int  crt_hip_trace_batch(crt_hip_scene *scene, const float *rays, int64_t n, crt
 int  crt_hip_count_work(crt_hip_scene *scene, const crt_renderer_settings *settings,
                         crt_work_counts *out);
 
+/* Diagnostics: render one full frame with per-wave s_memrealtime stamps
+ * (100 MHz ticks; stamps = 2 per 8x8 tile: start, end; tile_xy = tile origin,
+ * in dispatch order).  With NULL buffers returns the tile count. */
+int  crt_hip_profile_waves(crt_hip_scene *scene, const crt_renderer_settings *settings, uint64_t *stamps,
+                           int64_t cap, int32_t *tile_xy);
+
 /* Device-side stats of the last crt_hip_render_device launch on `scene`:
  * device time in ms between the launch's start/stop events (blocks). */
 int  crt_hip_last_kernel_ms(crt_hip_scene *scene, double *ms);

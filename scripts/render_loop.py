@@ -33,8 +33,9 @@ def main():
     st = N.RendererSettings.default(max_ray_depth=a.depth)
     variants = [("default", None)]
     if a.ab:
-        var, vals = a.ab.split("=")
-        variants = [(f"{var}={v}", (var, v)) for v in vals.split(",")]
+        var, vals = a.ab.split("=", 1)
+        sep = ";" if ";" in vals else ","
+        variants = [(f"{var}={v}", (var, v)) for v in vals.split(sep)]
     scenes = []
     for name, kv in variants:
         if kv:
