@@ -121,6 +121,14 @@ class WorkCounts(C.Structure):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
 
 
+class WaveCounts(C.Structure):
+    _fields_ = [("node_steps", C.c_uint64), ("triangle_steps", C.c_uint64), ("edge_steps", C.c_uint64),
+                ("waves", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
 # Every symbol include/crt_hip.h declares: (name, restype, argtypes)
 _P = C.c_void_p
 EXPORTS = [
@@ -149,6 +157,7 @@ EXPORTS = [
     ("crt_hip_trace_batch", C.c_int, [_P, _P, C.c_int64, _P]),
     ("crt_hip_count_work", C.c_int, [_P, C.POINTER(RendererSettings), C.POINTER(WorkCounts)]),
     ("crt_hip_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_double)]),
+    ("crt_hip_wave_counts", C.c_int, [_P, C.POINTER(WaveCounts)]),
     ("crt_hip_profile_waves", C.c_int, [_P, C.POINTER(RendererSettings), _P, C.c_int64, _P]),
     ("crt_renderer_settings_default", None, [C.POINTER(RendererSettings)]),
     ("crt_write_ppm", C.c_int, [C.c_char_p, _P, C.c_int32, C.c_int32, C.c_int32]),
@@ -412,6 +421,12 @@ class HipScene:
         st = settings or RendererSettings.default()
         w = WorkCounts()
         _check(lib().crt_hip_count_work(self._h, C.byref(st), C.byref(w)))
+        return w.as_dict()
+
+    def wave_counts(self) -> dict:
+        """Wave-level steps of the last count_work frame (packet walks only)."""
+        w = WaveCounts()
+        _check(lib().crt_hip_wave_counts(self._h, C.byref(w)))
         return w.as_dict()
 
     def close(self):

@@ -132,7 +132,8 @@ CRT_HD bool box_hit_bf(Vec o, Vec d, const DNode &n) {
  * that window takes the compiler's '/'. */
 struct RayRcp {
     float y1[3];
-    bool fast[3];
+    float gate[3];   /* +inf where the axis' faces are tested, -1 where |d| < 1e-6 discards them */
+    bool fast;       /* every box-face quotient of this ray is inside the exact window */
 };
 
 CRT_HD float rcp_refined(float b) {
@@ -144,71 +145,108 @@ CRT_HD float rcp_refined(float b) {
     return fmaf(fmaf(-b, y0, 1.0f), y0, y0);
 }
 
-CRT_HD RayRcp make_ray_rcp(Vec d) {
+/* 0, or a magnitude in [2^-40, 2^62].  If every box plane p and every origin
+ * component o satisfies this, each numerator a = p - o is 0 or has
+ * |a| in [2^-63, 2^63]: two such nonzero floats are multiples of ulp(2^-40) =
+ * 2^-63, and |p| + |o| <= 2^63.  A zero numerator gives a zero quotient whose
+ * sign may differ from '/', which no face test can observe (t < 0 is false
+ * for both zeros and o + d*(+-0) compares equal).  Faces with |d| < 1e-6 are
+ * discarded before their quotient is used, and |d| >= 1e-6 > 2^-20; so with
+ * |d| <= 2^20 every quotient a face test reads is the correctly rounded one. */
+CRT_HD bool coord_ok(float x) {
+    const float m = fabsf(x);
+    return x == 0.0f || (m >= 9.094947017729282e-13f && m <= 4.611686018427388e18f);
+}
+
+CRT_HD RayRcp make_ray_rcp(Vec o, Vec d, bool planes_ok) {
     RayRcp r;
-    const float dd[3] = {d.x, d.y, d.z};
-    for (int k = 0; k < 3; ++k) {
 #if defined(__HIP_DEVICE_COMPILE__)
-        const float m = fabsf(dd[k]);
-        r.fast[k] = m >= 9.5367431640625e-7f && m <= 1048576.0f;   /* [2^-20, 2^20] */
+    r.fast = planes_ok && coord_ok(o.x) && coord_ok(o.y) && coord_ok(o.z) && fabsf(d.x) <= 1048576.0f &&
+             fabsf(d.y) <= 1048576.0f && fabsf(d.z) <= 1048576.0f;
 #else
-        r.fast[k] = false;
+    (void)o;
+    (void)planes_ok;
+    r.fast = false;
 #endif
-        r.y1[k] = rcp_refined(r.fast[k] ? dd[k] : 1.0f);
-    }
+    r.y1[0] = rcp_refined(d.x);
+    r.y1[1] = rcp_refined(d.y);
+    r.y1[2] = rcp_refined(d.z);
+    r.gate[0] = fabsf(d.x) < 1e-6f ? -1.0f : INFINITY;
+    r.gate[1] = fabsf(d.y) < 1e-6f ? -1.0f : INFINITY;
+    r.gate[2] = fabsf(d.z) < 1e-6f ? -1.0f : INFINITY;
     return r;
 }
 
-CRT_HD float div_hoisted(float a, float b, float y1, bool fast_b) {
-    const float m = fabsf(a);
-    if (fast_b && m >= 5.421010862427522e-20f && m <= 1.8446744073709552e19f) {   /* [2^-64, 2^64] */
-        const float q0 = a * y1;
-        const float q1 = fmaf(fmaf(-b, q0, a), y1, q0);
-        return fmaf(fmaf(-b, q1, a), y1, q1);
-    }
-    return a / b;
-}
-
-/* ray_intersect_aabb_p (crt_intersection.cpp:14-45), branch-free over the six
- * faces, with the per-ray hoisted divisions (one slow-path branch per node,
- * taken only when a numerator leaves the exactness window). */
 CRT_HD float div_fast(float a, float b, float y1) {
     const float q0 = a * y1;
     const float q1 = fmaf(fmaf(-b, q0, a), y1, q0);
     return fmaf(fmaf(-b, q1, a), y1, q1);
 }
-CRT_HD bool in_window(float a) {
-    const float m = fabsf(a);
-    return m >= 5.421010862427522e-20f && m <= 1.8446744073709552e19f;   /* [2^-64, 2^64] */
-}
-CRT_HD int face_ok(float t, float d_a, float o_u, float d_u, float o_w, float d_w, float lo_u, float hi_u, float lo_w,
-                   float hi_w) {
+
+CRT_HD bool face_ok(float t, float d_a, float o_u, float d_u, float o_w, float d_w, float lo_u, float hi_u,
+                    float lo_w, float hi_w) {
     const float pu = o_u + d_u * t;
     const float pw = o_w + d_w * t;
-    return (int)!(fabsf(d_a) < 1e-6f) & (int)!(t < 0.0f) & (int)(pu >= lo_u) & (int)(pu <= hi_u) &
-           (int)(pw >= lo_w) & (int)(pw <= hi_w);
+    return !(fabsf(d_a) < 1e-6f) & !(t < 0.0f) & (pu >= lo_u) & (pu <= hi_u) & (pw >= lo_w) & (pw <= hi_w);
 }
 
-CRT_HD bool box_hit_r(Vec o, Vec d, const RayRcp &r, const DNode &n) {
-    const float a0 = n.lo_x - o.x, a1 = n.lo_y - o.y, a2 = n.lo_z - o.z;
-    const float a3 = n.hi_x - o.x, a4 = n.hi_y - o.y, a5 = n.hi_z - o.z;
-    float t0, t1, t2, t3, t4, t5;
-    const bool fast = ((int)r.fast[0] & (int)r.fast[1] & (int)r.fast[2] & (int)in_window(a0) & (int)in_window(a1) &
-                       (int)in_window(a2) & (int)in_window(a3) & (int)in_window(a4) & (int)in_window(a5)) != 0;
-    if (fast) {
-        t0 = div_fast(a0, d.x, r.y1[0]); t1 = div_fast(a1, d.y, r.y1[1]); t2 = div_fast(a2, d.z, r.y1[2]);
-        t3 = div_fast(a3, d.x, r.y1[0]); t4 = div_fast(a4, d.y, r.y1[1]); t5 = div_fast(a5, d.z, r.y1[2]);
-    } else {
-        t0 = a0 / d.x; t1 = a1 / d.y; t2 = a2 / d.z;
-        t3 = a3 / d.x; t4 = a4 / d.y; t5 = a5 / d.z;
-    }
-    return 0 != (face_ok(t0, d.x, o.y, d.y, o.z, d.z, n.lo_y, n.hi_y, n.lo_z, n.hi_z) |
-                 face_ok(t1, d.y, o.z, d.z, o.x, d.x, n.lo_z, n.hi_z, n.lo_x, n.hi_x) |
-                 face_ok(t2, d.z, o.x, d.x, o.y, d.y, n.lo_x, n.hi_x, n.lo_y, n.hi_y) |
-                 face_ok(t3, d.x, o.y, d.y, o.z, d.z, n.lo_y, n.hi_y, n.lo_z, n.hi_z) |
-                 face_ok(t4, d.y, o.z, d.z, o.x, d.x, n.lo_z, n.hi_z, n.lo_x, n.hi_x) |
-                 face_ok(t5, d.z, o.x, d.x, o.y, d.y, n.lo_x, n.hi_x, n.lo_y, n.hi_y));
+/* Fast-ray form of the face test as a signed margin: a face passes iff its
+ * margin is >= 0.  For a fast ray every term of a tested face is finite
+ * (|t| <= 2^63 / 1e-6, |d| <= 2^20, |o|, |plane| <= 2^62), a rounded
+ * difference has the sign of the exact one (denormals are on), and t = -0
+ * passes like !(t < 0); an axis with |d| < 1e-6 is gated to <= -1 even when
+ * its quotients are inf/NaN (minnum/maxnum return the non-NaN operand).  The
+ * two faces of an axis share d and the refined reciprocal, so their quotients
+ * and hit points are computed as float pairs (v_pk_mul/fma/add_f32); the
+ * compares and mask ANDs of face_ok become subtracts and min/max. */
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+CRT_HD f2 div_fast2(f2 a, float b, float y1) {
+    const f2 B = b, Y = y1;
+    const f2 q0 = a * Y;
+    const f2 q1 = __builtin_elementwise_fma(__builtin_elementwise_fma(-B, q0, a), Y, q0);
+    return __builtin_elementwise_fma(__builtin_elementwise_fma(-B, q1, a), Y, q1);
 }
+
+CRT_HD float min3f(float a, float b, float c) { return fminf(fminf(a, b), c); }
+
+/* margin of an axis' two faces (planes pl = lo, hi) */
+CRT_HD float axis_margin(f2 pl, float o_a, float d_a, float y1, float gate, float o_u, float d_u, float o_w,
+                         float d_w, float lo_u, float hi_u, float lo_w, float hi_w) {
+    const f2 t = div_fast2(pl - o_a, d_a, y1);
+    const f2 pu = o_u + d_u * t;
+    const f2 pw = o_w + d_w * t;
+    const f2 u0 = pu - lo_u, u1 = hi_u - pu, w0 = pw - lo_w, w1 = hi_w - pw;
+    const float m_lo = min3f(min3f(u0.x, u1.x, w0.x), w1.x, t.x);
+    const float m_hi = min3f(min3f(u0.y, u1.y, w0.y), w1.y, t.y);
+    return fminf(fmaxf(m_lo, m_hi), gate);
+}
+
+/* ray_intersect_aabb_p (crt_intersection.cpp:14-45), branch-free over the six
+ * faces, with the per-ray hoisted divisions (see coord_ok for when they are
+ * exact; other rays take the compiler's '/' and the plain compares). */
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"   /* no short-circuit: one branch-free OR */
+CRT_HD bool box_hit_r(Vec o, Vec d, const RayRcp &r, const DNode n) {
+    if (r.fast) {
+        const float mx = axis_margin((f2){n.lo_x, n.hi_x}, o.x, d.x, r.y1[0], r.gate[0], o.y, d.y, o.z, d.z, n.lo_y,
+                                     n.hi_y, n.lo_z, n.hi_z);
+        const float my = axis_margin((f2){n.lo_y, n.hi_y}, o.y, d.y, r.y1[1], r.gate[1], o.z, d.z, o.x, d.x, n.lo_z,
+                                     n.hi_z, n.lo_x, n.hi_x);
+        const float mz = axis_margin((f2){n.lo_z, n.hi_z}, o.z, d.z, r.y1[2], r.gate[2], o.x, d.x, o.y, d.y, n.lo_x,
+                                     n.hi_x, n.lo_y, n.hi_y);
+        return fmaxf(fmaxf(mx, my), mz) >= 0.0f;
+    }
+    const float t0 = (n.lo_x - o.x) / d.x, t1 = (n.lo_y - o.y) / d.y, t2 = (n.lo_z - o.z) / d.z;
+    const float t3 = (n.hi_x - o.x) / d.x, t4 = (n.hi_y - o.y) / d.y, t5 = (n.hi_z - o.z) / d.z;
+    return face_ok(t0, d.x, o.y, d.y, o.z, d.z, n.lo_y, n.hi_y, n.lo_z, n.hi_z) |
+           face_ok(t1, d.y, o.z, d.z, o.x, d.x, n.lo_z, n.hi_z, n.lo_x, n.hi_x) |
+           face_ok(t2, d.z, o.x, d.x, o.y, d.y, n.lo_x, n.hi_x, n.lo_y, n.hi_y) |
+           face_ok(t3, d.x, o.y, d.y, o.z, d.z, n.lo_y, n.hi_y, n.lo_z, n.hi_z) |
+           face_ok(t4, d.y, o.z, d.z, o.x, d.x, n.lo_z, n.hi_z, n.lo_x, n.hi_x) |
+           face_ok(t5, d.z, o.x, d.x, o.y, d.y, n.lo_x, n.hi_x, n.lo_y, n.hi_y);
+}
+#pragma clang diagnostic pop
 
 /* ray_intersect_triangle (crt_intersection.cpp:47-93), branch-free. */
 CRT_HD bool tri_hit_bf(Vec o, Vec d, const DTriGeo &g, bool cull, float &t_out) {
@@ -225,6 +263,28 @@ CRT_HD bool tri_hit_bf(Vec o, Vec d, const DTriGeo &g, bool cull, float &t_out) 
                    (int)(vdot(N, vcross(e2, v2p)) >= 0.0f);
     t_out = t;
     return ok != 0;
+}
+
+/* tri_hit_bf split in two: the plane stage (crt_intersection.cpp:49-63:
+ * parallel, culling and behind tests, t = op / rn) and the edge stage
+ * (:65-69: p = o + d*t and the three inside tests), same operations. */
+CRT_HD bool tri_plane(Vec o, Vec d, const DTriGeo &g, bool cull, float &t_out) {
+    const Vec N = vec(g.nx, g.ny, g.nz);
+    const Vec v0 = vec(g.v0x, g.v0y, g.v0z);
+    const float rn = vdot(N, d);
+    const float op = vdot(N, vsub(v0, o));
+    const float t = op / rn;
+    t_out = t;
+    return ((int)!(fabsf(rn) < 1e-6f) & (int)((op < 0.0f) | !cull) & (int)!(t < 0.0f)) != 0;
+}
+CRT_HD bool tri_edges(Vec o, Vec d, const DTriGeo &g, float t) {
+    const Vec N = vec(g.nx, g.ny, g.nz);
+    const Vec v0 = vec(g.v0x, g.v0y, g.v0z), v1 = vec(g.v1x, g.v1y, g.v1z), v2 = vec(g.v2x, g.v2y, g.v2z);
+    const Vec e0 = vsub(v1, v0), e1 = vsub(v2, v1), e2 = vsub(v0, v2);
+    const Vec p = vadd(o, vscale(d, t));
+    const Vec v0p = vsub(p, v0), v1p = vsub(p, v1), v2p = vsub(p, v2);
+    return ((int)(vdot(N, vcross(e0, v0p)) >= 0.0f) & (int)(vdot(N, vcross(e1, v1p)) >= 0.0f) &
+            (int)(vdot(N, vcross(e2, v2p)) >= 0.0f)) != 0;
 }
 
 /* ray_intersect_triangle (crt_intersection.cpp:47-93), distance only.  The

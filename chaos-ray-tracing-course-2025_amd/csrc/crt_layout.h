@@ -96,7 +96,7 @@ struct DeviceScene {
     float cam_loc[3];
     float cam_rot[9];
     int32_t width, height;
-    float inv_dummy;        /* keeps the struct 16-B friendly */
+    int32_t planes_ok;      /* every node plane is 0 or |p| in [2^-40, 2^62] (crt_device.h coord_ok) */
     float aspect;           /* float(width) / height            (crt_camera.cpp:23) */
     float tan_half_fov;     /* std::tan(fov_radians * 0.5f)     (crt_camera.cpp:26-27) */
     float background[3];

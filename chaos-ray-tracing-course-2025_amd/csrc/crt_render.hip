@@ -64,7 +64,11 @@ struct Frame {
     Vec alb;    /* diffuse: albedo sample | refract: .x = fresnel                */
 };
 
-struct LaneCounts { uint32_t traversals, nodes, tris, hits; };
+struct LaneCounts {
+    uint32_t traversals, nodes, tris, hits;
+    /* wave-uniform steps of the packet walks (kept by every lane, added once per wave) */
+    uint32_t wave_nodes, wave_tris, wave_edges;
+};
 
 /* ---------------------------------------------------------------------- */
 /* ray_intersect_acceleration_tree (crt_intersection.cpp:109-136)           */
@@ -568,11 +572,11 @@ __device__ __forceinline__ T load_scalar(const T *p, int i) {
 #endif
 }
 
-template <bool COUNT>
+template <bool COUNT, bool EARLY>
 __device__ int trace_packet(const DeviceScene &s, bool active, Vec o, Vec d, float &best_t, LaneCounts &c) {
     int best = -1;
     best_t = 0.0f;
-    const RayRcp rr = make_ray_rcp(d);
+    const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
     unsigned long long reach = active ? 1ull : 0ull;
     if (COUNT && active) ++c.traversals;
     const int n = s.node_count;
@@ -584,6 +588,7 @@ __device__ int trace_packet(const DeviceScene &s, bool active, Vec o, Vec d, flo
         const bool in = ((reach >> depth) & 1ull) != 0ull;
         const bool pass = in && box_hit_r(o, d, rr, nd);
         if (COUNT && in) ++c.nodes;
+        if (COUNT) ++c.wave_nodes;
         const unsigned long long pm = __ballot(pass);
         if (nd.b < 0) {
             if (pm != 0ull) {
@@ -602,10 +607,24 @@ __device__ int trace_packet(const DeviceScene &s, bool active, Vec o, Vec d, flo
                     const bool cull = ((load_scalar(s.slot_cull_bits, slot >> 5) >> (slot & 31)) & 1u) != 0u;
                     float t;
                     if (COUNT && pass) ++c.tris;
-                    const bool h = tri_hit_bf(o, d, g, cull, t);
-                    if (pass && h && (best < 0 || t < best_t)) {
-                        best_t = t;
-                        best = slot;
+                    if (COUNT) ++c.wave_tris;
+                    if (EARLY) {
+                        /* the edge tests only matter for a lane whose candidate
+                         * distance would replace its best: skip them when no lane
+                         * of the wave has one (same predicate, same arithmetic) */
+                        const bool pre = pass && tri_plane(o, d, g, cull, t) && (best < 0 || t < best_t);
+                        const bool any = __ballot(pre) != 0ull;
+                        if (COUNT && any) ++c.wave_edges;
+                        if (any && pre && tri_edges(o, d, g, t)) {
+                            best_t = t;
+                            best = slot;
+                        }
+                    } else {
+                        const bool h = tri_hit_bf(o, d, g, cull, t);
+                        if (pass && h && (best < 0 || t < best_t)) {
+                            best_t = t;
+                            best = slot;
+                        }
                     }
                 }
             }
@@ -622,7 +641,8 @@ __device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, bool acti
                                      LaneCounts &c) {
     if (TRAV == 4) return trace_coop<COUNT>(s, *L, active, o, d, best_t, c);
     if (TRAV == 5) return trace_share<COUNT>(s, *L, active, o, d, best_t, c);
-    if (TRAV == 6) return trace_packet<COUNT>(s, active, o, d, best_t, c);
+    if (TRAV == 6) return trace_packet<COUNT, false>(s, active, o, d, best_t, c);
+    if (TRAV == 7 || TRAV == 8) return trace_packet<COUNT, true>(s, active, o, d, best_t, c);
     if (TRAV == 1) return trace_closest_ww<COUNT>(s, o, d, best_t, c);
     if (TRAV == 2) return trace_closest_wwp<COUNT, false>(s, o, d, best_t, c);
     if (TRAV == 3) return trace_closest_wwp<COUNT, true>(s, o, d, best_t, c);
@@ -710,7 +730,11 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
             col = vec(0.f, 0.f, 0.f);
         } else {
             float t;
-            const int slot = trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
+            /* the packet walk pays for the union of its lanes' visit sets: it
+             * wins on camera rays (coherent by construction) and loses on the
+             * scattered secondary rays, which take the range-sharing walk */
+            const int slot = (TRAV >= 6 && depth != 0) ? trace<5, COUNT>(s, L, has_px, o, d, t, cnt)
+                                                       : trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
             if (slot < 0) {
                 col = vec(s.background[0], s.background[1], s.background[2]);
             } else {
@@ -833,14 +857,22 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
     return col;
 }
 
+#ifndef CRT_RENDER_BOUNDS
+#define CRT_RENDER_BOUNDS __launch_bounds__(256, (!FULL && TRAV == 8) ? 6 : 1)
+#endif
 template <bool FULL, int MAXF, int TRAV, bool COUNT>
-__global__ __launch_bounds__(256) void k_render_tiles(DeviceScene s, DSettings st, const Tile *__restrict__ tiles,
+__global__ CRT_RENDER_BOUNDS void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
+                                                  const Tile *__restrict__ tiles,
                                                       int ntiles, float *__restrict__ out,
                                                       unsigned long long *__restrict__ counters,
                                                       unsigned long long *__restrict__ stamps) {
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int lane = (int)(threadIdx.x & 63);
     if (wave >= ntiles) return;
+    /* The scene record is read through a pointer (not a by-value kernel
+     * argument): its fields are then loaded where they are used, so shading
+     * constants are not held in SGPRs across the tree walk (6 -> more waves/SIMD). */
+    const DeviceScene &s = *scene;
     /* diagnostic build only (stamps != nullptr): wave start / end in s_memrealtime ticks (100 MHz) */
     if (stamps && lane == 0) stamps[2 * wave] = __builtin_amdgcn_s_memrealtime();
     const Tile tl = tiles[wave];
@@ -848,9 +880,9 @@ __global__ __launch_bounds__(256) void k_render_tiles(DeviceScene s, DSettings s
     const bool has_px = lx < tl.w && ly < tl.h;
     /* the sharing walks keep pixel-less lanes as helpers (they take donated node
      * ranges of the wave's rays); the other walks drop them */
-    constexpr bool kHelpers = (TRAV == 4 || TRAV == 5 || TRAV == 6) && !FULL;
+    constexpr bool kHelpers = (TRAV >= 4) && !FULL;
     if (!kHelpers && !has_px) return;
-    LaneCounts cnt = {0u, 0u, 0u, 0u};
+    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
     __shared__ CoopLds coop[TRAV >= 4 ? 4 : 1];
     const Vec c = shade_pixel<FULL, MAXF, TRAV, COUNT>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt,
                                                       &coop[TRAV >= 4 ? (threadIdx.x >> 6) : 0], has_px);
@@ -866,6 +898,12 @@ __global__ __launch_bounds__(256) void k_render_tiles(DeviceScene s, DSettings s
         atomicAdd(&counters[1], (unsigned long long)cnt.nodes);
         atomicAdd(&counters[2], (unsigned long long)cnt.tris);
         atomicAdd(&counters[3], (unsigned long long)cnt.hits);
+        if (lane == 0) {
+            atomicAdd(&counters[4], (unsigned long long)cnt.wave_nodes);
+            atomicAdd(&counters[5], (unsigned long long)cnt.wave_tris);
+            atomicAdd(&counters[6], (unsigned long long)cnt.wave_edges);
+            atomicAdd(&counters[7], 1ull);
+        }
     }
 }
 
@@ -979,6 +1017,9 @@ struct crt_hip_scene {
     bool has_secondary = false;    /* any reflective / refractive material */
     bool has_diffuse = false;
     DeviceScene ds{};
+    DeviceScene ds_uploaded{};   /* what d_ds holds */
+    DeviceScene *d_ds = nullptr;
+    crt_wave_counts wave_counts{};   /* from the last crt_hip_count_work */
     std::vector<void *> allocs;
     hipStream_t stream = nullptr;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
@@ -988,7 +1029,7 @@ struct crt_hip_scene {
     float *d_out = nullptr;
     unsigned long long *d_counters = nullptr;
     bool grid_empty = false;
-    int traversal = 2;             /* kernel walk variant, see trace<> (env CRT_TRAVERSAL) */
+    int traversal = 7;             /* kernel walk variant, see trace<> (env CRT_TRAVERSAL) */
     int tile_order = 1;            /* dispatch tiles by estimated work (env CRT_TILE_ORDER) */
     float split4 = 0.2f, split16 = 0.5f;   /* relative work above which a tile is split (env CRT_SPLIT="a,b") */
     std::vector<float> tile_work;  /* per 8x8 tile of the full frame */
@@ -997,14 +1038,17 @@ struct crt_hip_scene {
 namespace {
 
 template <class T>
-int upload(crt_hip_scene *sc, const std::vector<T> &v, const T **dst) {
+int upload(crt_hip_scene *sc, const std::vector<T> &v, const T **dst, size_t pad = 0) {
+    /* pad: zeroed records after the data, so grouped reads past a run's end stay in bounds */
     *dst = nullptr;
-    if (v.empty()) return CRT_OK;
+    if (v.empty() && pad == 0) return CRT_OK;
     void *p = nullptr;
-    HIP_TRY(hipMalloc(&p, v.size() * sizeof(T)));
+    const size_t bytes = (v.size() + pad) * sizeof(T);
+    HIP_TRY(hipMalloc(&p, bytes));
     sc->allocs.push_back(p);
-    HIP_TRY(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
-    sc->info.device_bytes += (int64_t)(v.size() * sizeof(T));
+    if (pad) HIP_TRY(hipMemset(static_cast<char *>(p) + v.size() * sizeof(T), 0, pad * sizeof(T)));
+    if (!v.empty()) HIP_TRY(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    sc->info.device_bytes += (int64_t)bytes;
     *dst = static_cast<const T *>(p);
     return CRT_OK;
 }
@@ -1085,6 +1129,26 @@ int ensure_gi_tables(crt_hip_scene *sc) {
     return CRT_OK;
 }
 
+/* Device copy of sc->ds for the render kernels.  Re-uploaded only when the
+ * host record changed (first GI frame, new resolution); kernels of earlier
+ * frames may still read the old copy, so the device is drained first. */
+int sync_device_record(crt_hip_scene *sc, const DeviceScene **out) {
+    if (!sc->d_ds || std::memcmp(&sc->ds_uploaded, &sc->ds, sizeof(DeviceScene)) != 0) {
+        if (!sc->d_ds) {
+            void *p = nullptr;
+            HIP_TRY(hipMalloc(&p, sizeof(DeviceScene)));
+            sc->allocs.push_back(p);
+            sc->d_ds = static_cast<DeviceScene *>(p);
+        } else {
+            HIP_TRY(hipDeviceSynchronize());
+        }
+        HIP_TRY(hipMemcpy(sc->d_ds, &sc->ds, sizeof(DeviceScene), hipMemcpyHostToDevice));
+        std::memcpy(&sc->ds_uploaded, &sc->ds, sizeof(DeviceScene));
+    }
+    *out = sc->d_ds;
+    return CRT_OK;
+}
+
 int check_settings(const crt_renderer_settings *st) {
     if (!st) return set_error(CRT_E_INVALID, "null settings");
     return CRT_OK;
@@ -1111,12 +1175,17 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         if (rc != CRT_OK) return rc;
     }
     if (plan.ntiles == 0) return CRT_OK;
+    const DeviceScene *d_scene = nullptr;
+    {
+        const int rc = sync_device_record(sc, &d_scene);
+        if (rc != CRT_OK) return rc;
+    }
     const DSettings ds = to_dsettings(st);
     const int blocks = (plan.ntiles + 3) / 4;
     const uint64_t frames = (uint64_t)st->max_ray_depth + 1;
     unsigned long long *cnt = sc->d_counters;
 #define CRT_LAUNCH_T(FULL, MAXF, TRAV, COUNT)                                                               \
-    hipLaunchKernelGGL((k_render_tiles<FULL, MAXF, TRAV, COUNT>), dim3(blocks), dim3(256), 0, stream, sc->ds, \
+    hipLaunchKernelGGL((k_render_tiles<FULL, MAXF, TRAV, COUNT>), dim3(blocks), dim3(256), 0, stream, d_scene, \
                        ds, plan.d_tiles, plan.ntiles, d_out, cnt, stamps)
 #define CRT_LAUNCH(FULL, MAXF, COUNT)                                                                       \
     do {                                                                                                   \
@@ -1127,6 +1196,8 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         case 4: CRT_LAUNCH_T(FULL, MAXF, 4, COUNT); break;                                                 \
         case 5: CRT_LAUNCH_T(FULL, MAXF, 5, COUNT); break;                                                 \
         case 6: CRT_LAUNCH_T(FULL, MAXF, 6, COUNT); break;                                                 \
+        case 7: CRT_LAUNCH_T(FULL, MAXF, 7, COUNT); break;                                                 \
+        case 8: CRT_LAUNCH_T(FULL, MAXF, 8, COUNT); break;                                                 \
         default: CRT_LAUNCH_T(FULL, MAXF, 2, COUNT); break;                                                \
         }                                                                                                  \
     } while (0)
@@ -1191,6 +1262,15 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     int rc;
     if ((rc = upload(sc.get(), hs.nodes, &ds.nodes)) != CRT_OK) return rc;
     ds.node_count = (int32_t)hs.nodes.size();
+    {
+        auto ok = [](float x) {
+            const float m = std::fabs(x);
+            return x == 0.0f || (m >= 0x1p-40f && m <= 0x1p62f);
+        };
+        ds.planes_ok = 1;
+        for (const DNode &n : hs.nodes)
+            if (!(ok(n.lo_x) && ok(n.lo_y) && ok(n.lo_z) && ok(n.hi_x) && ok(n.hi_y) && ok(n.hi_z))) ds.planes_ok = 0;
+    }
     if ((rc = upload(sc.get(), hs.slots, &ds.slots)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.slot_tri, &ds.slot_tri)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.slot_cull, &ds.slot_cull)) != CRT_OK) return rc;
@@ -1223,7 +1303,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     HIP_TRY(hipEventCreate(&sc->ev_start));
     HIP_TRY(hipEventCreate(&sc->ev_stop));
     void *p = nullptr;
-    HIP_TRY(hipMalloc(&p, 4 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&p, 8 * sizeof(unsigned long long)));
     sc->allocs.push_back(p);
     sc->d_counters = static_cast<unsigned long long *>(p);
 
@@ -1433,16 +1513,26 @@ int crt_hip_count_work(crt_hip_scene *sc, const crt_renderer_settings *st, crt_w
     if (sc->grid_empty) return CRT_OK;
     const size_t nfl = (size_t)sc->info.width * sc->info.height * 3;
     if (!sc->d_out) HIP_TRY(hipMalloc(&sc->d_out, nfl * sizeof(float)));
-    HIP_TRY(hipMemsetAsync(sc->d_counters, 0, 4 * sizeof(unsigned long long), sc->stream));
+    HIP_TRY(hipMemsetAsync(sc->d_counters, 0, 8 * sizeof(unsigned long long), sc->stream));
     rc = launch_render(sc, st, sc->full, sc->d_out, sc->stream, true);
     if (rc != CRT_OK) return rc;
-    unsigned long long c[4];
+    unsigned long long c[8];
     HIP_TRY(hipMemcpyAsync(c, sc->d_counters, sizeof c, hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
     out->traversals = c[0];
     out->node_tests = c[1];
     out->triangle_tests = c[2];
     out->hits = c[3];
+    sc->wave_counts.node_steps = c[4];
+    sc->wave_counts.triangle_steps = c[5];
+    sc->wave_counts.edge_steps = c[6];
+    sc->wave_counts.waves = c[7];
+    return CRT_OK;
+}
+
+int crt_hip_wave_counts(crt_hip_scene *sc, crt_wave_counts *out) {
+    if (!sc || !out) return set_error(CRT_E_INVALID, "null argument");
+    *out = sc->wave_counts;
     return CRT_OK;
 }
 

@@ -225,6 +225,16 @@ int  crt_hip_trace_batch(crt_hip_scene *scene, const float *rays, int64_t n, crt
 int  crt_hip_count_work(crt_hip_scene *scene, const crt_renderer_settings *settings,
                         crt_work_counts *out);
 
+/* Wave-level steps of the last crt_hip_count_work frame, for the packet walks
+ * (a wave pays once per node / triangle of the union of its lanes' visit sets):
+ * node_steps / triangle_steps = wave iterations, edge_steps = triangle steps
+ * where some lane ran the edge stage, waves = waves launched.  Zero for walks
+ * without wave-uniform steps. */
+typedef struct crt_wave_counts {
+    uint64_t node_steps, triangle_steps, edge_steps, waves;
+} crt_wave_counts;
+int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
+
 /* Diagnostics: render one full frame with per-wave s_memrealtime stamps
  * (100 MHz ticks; stamps = 2 per 8x8 tile: start, end; tile_xy = tile origin,
  * in dispatch order).  With NULL buffers returns the tile count. */

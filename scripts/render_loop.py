@@ -28,6 +28,7 @@ def main():
     p.add_argument("--frames", type=int, default=5)
     p.add_argument("--depth", type=int, default=3)
     p.add_argument("--ab", default=None, help="ENVVAR=v1,v2,... — build one scene per value")
+    p.add_argument("--counts", action="store_true", help="print per-ray and per-wave work counts per variant")
     a = p.parse_args()
     sc = load_npz(ROOT / "tests" / "golden" / "scenes" / f"{a.scene}.npz").set_resolution(a.width, a.height)
     st = N.RendererSettings.default(max_ray_depth=a.depth)
@@ -52,6 +53,10 @@ def main():
             elif not np.array_equal(ref.view(np.uint32), img.view(np.uint32)):
                 print(f"MISMATCH in variant {name}", flush=True)
     out = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v)), "n": len(v)} for k, v in times.items()}
+    if a.counts:
+        for name, g in scenes:
+            out[name]["work"] = g.count_work(st)
+            out[name]["wave"] = g.wave_counts()
     print(json.dumps({"scene": a.scene, "size": [a.width, a.height], "depth": a.depth, "kernel": out}))
 
 

@@ -1,0 +1,81 @@
+"""GPU: the two callers of the render path — the crt_renderer CLI (drop-in for
+src/standalone/main.cpp) and the _crt module (drop-in for
+src/python/py_crt_module.cpp) — against the CPU oracle.
+
+The box has no reference scene files, so each test writes a .crtscene from a
+committed .npz (crt_amd.scene_json; its round trip through the loader is
+bit-exact, tests/test_loader.py::test_crtscene_writer_round_trip).
+"""
+import json
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import PKG, bits, scene_npz
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("14-01-acceleration-tree__scene1", 320, 180, {}),
+         ("09-03-reflective__scene5", 160, 90, {})]
+
+
+def _doc(name, w, h):
+    from crt_amd.scene_json import arrays_to_crtscene
+    sc = scene_npz(name).set_resolution(w, h)
+    doc = arrays_to_crtscene(sc.a)
+    doc["settings"]["image_settings"].update(width=w, height=h)
+    return sc, doc
+
+
+@pytest.mark.parametrize("name,w,h,over", CASES)
+def test_cli_ppm_matches_oracle(tmp_path, oracle, name, w, h, over):
+    from crt_amd import native
+    sc, doc = _doc(name, w, h)
+    scene = tmp_path / "scene.crtscene"
+    scene.write_text(json.dumps(doc))
+    out = tmp_path / "out.ppm"
+    r = subprocess.run([str(PKG / "bin" / "crt_renderer"), str(scene), str(out)], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("Execution time: ") and r.stdout.rstrip().endswith(" seconds.")
+    want = oracle.OracleScene(sc).render(native.RendererSettings.default(**over))
+    ref_ppm = tmp_path / "want.ppm"
+    native.write_ppm(ref_ppm, want)
+    assert out.read_bytes() == ref_ppm.read_bytes()
+
+
+def test_cli_errors(tmp_path):
+    exe = str(PKG / "bin" / "crt_renderer")
+    r = subprocess.run([exe, str(tmp_path / "missing.crtscene")], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "Could not open input file" in r.stderr
+    bad = tmp_path / "bad.crtscene"
+    bad.write_text("{")
+    r = subprocess.run([exe, str(bad), str(tmp_path / "o.ppm")], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "Could not parse JSON file" in r.stderr
+
+
+@pytest.mark.parametrize("name,w,h,over", CASES + [("11-01-refractive__scene8", 96, 54, {"max_ray_depth": 8})])
+def test_crt_module_matches_oracle(oracle, name, w, h, over):
+    if str(PKG) not in sys.path:
+        sys.path.insert(0, str(PKG))
+    import _crt
+    from crt_amd import native
+    sc, doc = _doc(name, w, h)
+    st = native.RendererSettings.default(**over)
+    settings = _crt.RendererSettings((st.max_ray_depth, st.diffuse_reflection_ray_count, st.shadow_bias,
+                                      st.reflection_bias, st.diffuse_reflection_bias, st.refraction_bias))
+    px = _crt.render_scene_from_dict(doc, str(PKG), settings)
+    assert len(px) == w * h and all(p[3] == 1.0 for p in px[:8])
+    got = np.array([p[:3] for p in px], np.float32).reshape(h, w, 3)[::-1]   # bottom row first
+    want = oracle.OracleScene(sc).render(st)
+    # _crt hands Python floats (doubles widened from fp32): exact round trip
+    rmse = float(np.sqrt(np.mean((got.astype(np.float64) - want) ** 2)))
+    assert rmse < 1e-4
+    if not over:
+        assert np.array_equal(bits(np.ascontiguousarray(got)), bits(want))
+    with pytest.raises(TypeError):
+        _crt.render_scene_from_dict(doc, str(PKG), (1, 2, 3, 4, 5, 6))
+    with pytest.raises(ValueError):
+        _crt.render_scene_from_dict({"settings": {}}, str(PKG), settings)

@@ -279,3 +279,18 @@ def test_integer_typing():
     assert math.copysign(1.0, light_intensity("-0.0")) == -1.0
     assert light_intensity("4294967295") == np.float32(4294967295.0)
     assert light_intensity("123456789012345678901") == np.float32(123456789012345678901.0)
+
+
+# ---------------------------------------------------------------- writer round trip
+@pytest.mark.parametrize("npz", sorted(SCENES.glob("*.npz")), ids=lambda p: p.stem)
+def test_crtscene_writer_round_trip(npz):
+    """crt_amd.scene_json writes a document the loader reads back to the same
+    description, bit for bit (what the CLI / _crt GPU tests rely on)."""
+    from crt_amd.native import SceneFile
+    from crt_amd.scene_json import arrays_to_crtscene
+    from crt_amd.scene_npz import desc_to_arrays
+    want = dict(np.load(npz))
+    got = desc_to_arrays(SceneFile(text=json.dumps(arrays_to_crtscene(want))).desc())
+    assert set(got) == set(want)
+    for k in want:
+        assert np.array_equal(bits(got[k]), bits(want[k])), k
