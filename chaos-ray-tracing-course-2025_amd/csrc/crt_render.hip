@@ -642,7 +642,7 @@ __device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, bool acti
     if (TRAV == 4) return trace_coop<COUNT>(s, *L, active, o, d, best_t, c);
     if (TRAV == 5) return trace_share<COUNT>(s, *L, active, o, d, best_t, c);
     if (TRAV == 6) return trace_packet<COUNT, false>(s, active, o, d, best_t, c);
-    if (TRAV == 7 || TRAV == 8) return trace_packet<COUNT, true>(s, active, o, d, best_t, c);
+    if (TRAV == 7) return trace_packet<COUNT, true>(s, active, o, d, best_t, c);
     if (TRAV == 1) return trace_closest_ww<COUNT>(s, o, d, best_t, c);
     if (TRAV == 2) return trace_closest_wwp<COUNT, false>(s, o, d, best_t, c);
     if (TRAV == 3) return trace_closest_wwp<COUNT, true>(s, o, d, best_t, c);
@@ -712,7 +712,7 @@ __device__ __forceinline__ float pow5(float x) {
  * FULL=false: scenes whose materials are only diffuse/constant with GI off —
  * no recursion, no frame stack.  FULL=true: GI + reflective + refractive with
  * a per-lane frame stack of MAXF entries (≥ max_ray_depth + 1, host-checked). */
-template <bool FULL, int MAXF, int TRAV, bool COUNT>
+template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT>
 __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt, CoopLds *L,
                            bool has_px) {
     Vec o, d;
@@ -733,8 +733,8 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
             /* the packet walk pays for the union of its lanes' visit sets: it
              * wins on camera rays (coherent by construction) and loses on the
              * scattered secondary rays, which take the range-sharing walk */
-            const int slot = (TRAV >= 6 && depth != 0) ? trace<5, COUNT>(s, L, has_px, o, d, t, cnt)
-                                                       : trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
+            const int slot = (SEC != TRAV && depth != 0) ? trace<SEC, COUNT>(s, L, has_px, o, d, t, cnt)
+                                                         : trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
             if (slot < 0) {
                 col = vec(s.background[0], s.background[1], s.background[2]);
             } else {
@@ -858,9 +858,9 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
 }
 
 #ifndef CRT_RENDER_BOUNDS
-#define CRT_RENDER_BOUNDS __launch_bounds__(256, (!FULL && TRAV == 8) ? 6 : 1)
+#define CRT_RENDER_BOUNDS __launch_bounds__(256)
 #endif
-template <bool FULL, int MAXF, int TRAV, bool COUNT>
+template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT>
 __global__ CRT_RENDER_BOUNDS void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
                                                   const Tile *__restrict__ tiles,
                                                       int ntiles, float *__restrict__ out,
@@ -884,7 +884,7 @@ __global__ CRT_RENDER_BOUNDS void k_render_tiles(const DeviceScene *__restrict__
     if (!kHelpers && !has_px) return;
     LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
     __shared__ CoopLds coop[TRAV >= 4 ? 4 : 1];
-    const Vec c = shade_pixel<FULL, MAXF, TRAV, COUNT>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt,
+    const Vec c = shade_pixel<FULL, MAXF, TRAV, SEC, COUNT>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt,
                                                       &coop[TRAV >= 4 ? (threadIdx.x >> 6) : 0], has_px);
     if (has_px) {
         float *px = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
@@ -905,6 +905,212 @@ __global__ CRT_RENDER_BOUNDS void k_render_tiles(const DeviceScene *__restrict__
             atomicAdd(&counters[7], 1ull);
         }
     }
+}
+
+/* ====================================================================== */
+/* Wavefront path: reflection / refraction recursion without GI (C3)       */
+/* ====================================================================== */
+/* With GI off, shade_ray (crt_renderer.cpp:46-145) draws no random numbers:
+ * each activation's colour is a pure function of its ray and of its
+ * children's colours.  So the recursion is run level by level: every ray of
+ * depth L is traced by one lane (no per-lane frame stack, no lane waiting for
+ * its pixel's other branches), its children are appended to the level-L+1
+ * queue, and a backward pass composes each activation's colour from its
+ * children with the reference's operations (reflective: albedo * L with the
+ * Vector quirk; refractive: fresnel blend, or the reflection colour on total
+ * internal reflection).  A child deeper than max_ray_depth is black without
+ * a trace, as in the reference (:47-48).  Level 0 is the camera rays of the
+ * tile plan (packet walk); deeper levels are scattered rays (range-sharing
+ * walk). */
+enum WKind : int32_t { wFinal = 0, wReflect = 1, wRefract2 = 2, wRefract1 = 3 };
+
+struct alignas(16) WRay {
+    float ox, oy, oz, dx, dy, dz;
+    int32_t id, depth;
+};
+
+struct alignas(16) WNode {
+    int32_t kind, c0, c1, pad;   /* children ids, -1 = black (deeper than max_ray_depth) */
+    float a0, a1, a2, a3;        /* reflective: albedo | refractive: a0 = fresnel */
+};
+
+struct WLevel {
+    const WRay *in;
+    int32_t n;               /* rays of this level (levels >= 1) */
+    int32_t depth;
+    WRay *out;               /* children of this level */
+    int32_t *out_count;
+    int32_t out_base;        /* id of out[0] */
+    WNode *nodes;            /* by ray id */
+    DVec4 *cols;             /* by ray id */
+};
+
+template <int TRAV, bool LEVEL0, bool COUNT>
+__global__ __launch_bounds__(256) void k_wf_level(const DeviceScene *__restrict__ scene, DSettings st,
+                                                  const Tile *__restrict__ tiles, int ntiles, WLevel lv,
+                                                  unsigned long long *__restrict__ counters) {
+    const DeviceScene &s = *scene;
+    const int gid = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int lane = (int)(threadIdx.x & 63);
+    bool has;
+    Vec o = vec(0.f, 0.f, 0.f), d = vec(0.f, 0.f, 1.f);
+    int id = gid, depth = 0;
+    if (LEVEL0) {
+        const int wave = gid >> 6;
+        if (wave >= ntiles) return;
+        const Tile tl = tiles[wave];
+        const int lx = lane & 7, ly = lane >> 3;
+        has = lx < tl.w && ly < tl.h;
+        if (has) camera_ray(s, tl.x + lx, tl.y + ly, o, d);
+    } else {
+        if ((gid & ~63) >= lv.n) return;   /* whole wave past the queue */
+        has = gid < lv.n;
+        if (has) {
+            const WRay r = lv.in[gid];
+            o = vec(r.ox, r.oy, r.oz);
+            d = vec(r.dx, r.dy, r.dz);
+            id = r.id;
+            depth = r.depth;
+        }
+    }
+    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    __shared__ CoopLds coop[4];
+    float t;
+    const int slot = trace<TRAV, COUNT>(s, &coop[threadIdx.x >> 6], has, o, d, t, cnt);
+
+    WNode node = {wFinal, -1, -1, 0, 0.f, 0.f, 0.f, 0.f};
+    Vec col = vec(0.f, 0.f, 0.f);
+    int nch = 0;
+    Vec co[2], cd[2];
+    if (has) {
+        if (slot < 0) {
+            col = vec(s.background[0], s.background[1], s.background[2]);
+        } else {
+            HitRec h;
+            make_hit(s, o, d, t, slot, h);
+            const DMaterial m = s.materials[h.mat];
+            if (m.type == CRT_MATERIAL_DIFFUSE) {
+                const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+                col = diffuse_finish(s, st, vec(0.f, 0.f, 0.f), h.p, h.n, alb);
+            } else if (m.type == CRT_MATERIAL_REFLECTIVE) {                 /* :103-107 */
+                const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+                if (s.reflections_on) {
+                    node.kind = wReflect;
+                    node.a0 = alb.x; node.a1 = alb.y; node.a2 = alb.z;
+                    co[0] = vadd(h.p, vscale(h.n, st.reflection_bias));
+                    cd[0] = vsub(d, vscale(vscale(h.n, 2.0f), vdot(d, h.n)));
+                    nch = 1;
+                } else {
+                    col = alb;
+                }
+            } else if (m.type == CRT_MATERIAL_REFRACTIVE) {                 /* :109-135 */
+                if (s.refractions_on) {
+                    Vec n = h.n;
+                    float n_out = 1.0f, n_in = m.ior;
+                    if (vdot(d, n) > 0.0f) {
+                        n = vneg(n);
+                        const float tmp = n_in; n_in = n_out; n_out = tmp;
+                    }
+                    bool has_refr = false;
+                    Vec rd = d;
+                    {   /* Vector::refract (crt_vector.cpp:11-27) */
+                        const float ca = -vdot(rd, n);
+                        const float sa = sqrtf(1.0f - ca * ca);
+                        if (!(sa > n_in / n_out)) {
+                            const float sb = sa * n_out / n_in;
+                            const float cb = sqrtf(1.0f - sb * sb);
+                            rd = vadd(rd, vscale(n, ca));
+                            rd = vnormalize(rd);
+                            rd = vscale(rd, sb);
+                            rd = vadd(rd, vscale(vneg(n), cb));
+                            has_refr = true;
+                        }
+                    }
+                    node.kind = has_refr ? wRefract2 : wRefract1;
+                    node.a0 = 0.5f * pow5(1.0f + vdot(d, n));
+                    co[0] = vadd(h.p, vscale(n, st.reflection_bias));
+                    cd[0] = vsub(d, vscale(vscale(n, 2.0f), vdot(d, n)));
+                    co[1] = vadd(h.p, vscale(vneg(n), 1e-2f));   /* refract_at's default bias (crt_ray.h:30-50) */
+                    cd[1] = rd;
+                    nch = has_refr ? 2 : 1;
+                }
+            } else {                                                         /* Constant :137-139 */
+                col = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+            }
+        }
+    }
+    /* children deeper than max_ray_depth are black without a trace: not queued */
+    if ((uint32_t)depth + 1u > st.max_ray_depth) nch = 0;
+    const unsigned long long b1 = __ballot(nch >= 1), b2 = __ballot(nch >= 2);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const int total = __popcll(b1) + __popcll(b2);
+    if (total > 0) {
+        int base = 0;
+        if (lane == __ffsll((long long)(b1 | b2)) - 1) base = atomicAdd(lv.out_count, total);
+        base = __shfl(base, __ffsll((long long)(b1 | b2)) - 1);
+        int k = base + __popcll(b1 & lt) + __popcll(b2 & lt);
+        for (int c = 0; c < nch; ++c, ++k) {
+            WRay r;
+            r.ox = co[c].x; r.oy = co[c].y; r.oz = co[c].z;
+            r.dx = cd[c].x; r.dy = cd[c].y; r.dz = cd[c].z;
+            r.id = lv.out_base + k;
+            r.depth = depth + 1;
+            lv.out[k] = r;
+            if (c == 0) node.c0 = r.id; else node.c1 = r.id;
+        }
+    }
+    if (has) {
+        lv.nodes[id] = node;
+        if (node.kind == wFinal) lv.cols[id] = DVec4{col.x, col.y, col.z, 0.f};
+    }
+    if (COUNT) {
+        atomicAdd(&counters[0], (unsigned long long)cnt.traversals);
+        atomicAdd(&counters[1], (unsigned long long)cnt.nodes);
+        atomicAdd(&counters[2], (unsigned long long)cnt.tris);
+        atomicAdd(&counters[3], (unsigned long long)cnt.hits);
+    }
+}
+
+__device__ __forceinline__ Vec wf_compose(const WNode &nd, const DVec4 *__restrict__ cols, Vec own) {
+    if (nd.kind == wFinal) return own;
+    const Vec black = vec(0.f, 0.f, 0.f);
+    const Vec c0 = nd.c0 >= 0 ? vec(cols[nd.c0].x, cols[nd.c0].y, cols[nd.c0].z) : black;
+    if (nd.kind == wReflect) return vmul_quirk(vec(nd.a0, nd.a1, nd.a2), c0);
+    if (nd.kind == wRefract1) return c0;   /* total internal reflection */
+    const Vec c1 = nd.c1 >= 0 ? vec(cols[nd.c1].x, cols[nd.c1].y, cols[nd.c1].z) : black;
+    const float fr = nd.a0;
+    return vadd(vscale(c0, fr), vscale(c1, 1.0f - fr));
+}
+
+/* levels >= 1, deepest first: colour of every activation of the level */
+__global__ __launch_bounds__(256) void k_wf_compose(const WNode *__restrict__ nodes, DVec4 *__restrict__ cols,
+                                                    int32_t begin, int32_t n) {
+    const int k = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (k >= n) return;
+    const int id = begin + k;
+    const WNode nd = nodes[id];
+    if (nd.kind == wFinal) return;
+    const Vec c = wf_compose(nd, cols, vec(0.f, 0.f, 0.f));
+    cols[id] = DVec4{c.x, c.y, c.z, 0.f};
+}
+
+/* level 0: compose the camera rays and write the pixels */
+__global__ __launch_bounds__(256) void k_wf_pixels(const WNode *__restrict__ nodes, const DVec4 *__restrict__ cols,
+                                                   const Tile *__restrict__ tiles, int ntiles,
+                                                   float *__restrict__ out) {
+    const int gid = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int wave = gid >> 6, lane = gid & 63;
+    if (wave >= ntiles) return;
+    const Tile tl = tiles[wave];
+    const int lx = lane & 7, ly = lane >> 3;
+    if (!(lx < tl.w && ly < tl.h)) return;
+    const WNode nd = nodes[gid];
+    const Vec own = vec(cols[gid].x, cols[gid].y, cols[gid].z);
+    const Vec c = wf_compose(nd, cols, own);
+    float *px = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
+    px[0] = c.x;
+    px[1] = c.y;
+    px[2] = c.z;
 }
 
 /* crt_hip_trace_batch: closest hit of arbitrary rays (a1–a4 KATs). */
@@ -1011,6 +1217,16 @@ void build_gi_host_tables() {
 
 }  // namespace
 
+/* Device buffers of the wavefront path, grown on demand (kept across frames). */
+struct WfBuffers {
+    crt_amd::WNode *nodes = nullptr;
+    crt_amd::DVec4 *cols = nullptr;
+    int64_t cap = 0;             /* ray ids */
+    crt_amd::WRay *q[2] = {nullptr, nullptr};
+    int64_t qcap[2] = {0, 0};
+    int32_t *counts = nullptr;   /* children queued per level */
+};
+
 struct crt_hip_scene {
     int device = 0;
     crt_scene_info info{};
@@ -1031,8 +1247,15 @@ struct crt_hip_scene {
     bool grid_empty = false;
     int traversal = 7;             /* kernel walk variant, see trace<> (env CRT_TRAVERSAL) */
     int tile_order = 1;            /* dispatch tiles by estimated work (env CRT_TILE_ORDER) */
-    float split4 = 0.2f, split16 = 0.5f;   /* relative work above which a tile is split (env CRT_SPLIT="a,b") */
+    /* a tile is split into 4x4 (2x2) pixel waves when its work estimate exceeds
+     * split4 (split16) times the mean work per resident wave slot, i.e. when it
+     * would run for several times the ideal makespan (env CRT_SPLIT="a,b") */
+    float split4 = 4.5f, split16 = 9.0f;
+    int wave_slots = 6144;   /* CUs x 4 SIMDs x 6 resident render waves */
+    int secondary = 0;       /* walk for secondary rays under TRAV 6/7 (0 = by scene, env CRT_SECONDARY) */
     std::vector<float> tile_work;  /* per 8x8 tile of the full frame */
+    int wavefront = 1;             /* level-by-level recursion when GI is off (env CRT_WAVEFRONT) */
+    WfBuffers wf;
 };
 
 namespace {
@@ -1079,12 +1302,13 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
          * carries fewer rays and the rest of its lanes help (4x4 or 2x2 pixels) */
         const int tx = (W + 7) / 8;
         auto work = [&](const Tile &t) { return sc->tile_work[(size_t)(t.y / 8) * tx + t.x / 8]; };
-        float wmax = 0.f;
-        for (const Tile &t : tiles) wmax = std::max(wmax, work(t));
+        double wsum = 0.0;
+        for (const Tile &t : tiles) wsum += work(t);
+        const float slot_work = (float)(wsum / sc->wave_slots);
         std::vector<Tile> split;
-        if (sc->traversal >= 4 && wmax > 0.f && (sc->split4 > 0.f || sc->split16 > 0.f)) {
+        if (sc->traversal >= 4 && slot_work > 0.f && (sc->split4 > 0.f || sc->split16 > 0.f)) {
             for (const Tile &t : tiles) {
-                const float w = work(t) / wmax;
+                const float w = work(t) / slot_work;
                 const int sub = (sc->split16 > 0.f && w >= sc->split16) ? 2 : (sc->split4 > 0.f && w >= sc->split4) ? 4 : 8;
                 for (int yy = 0; yy < t.h; yy += sub)
                     for (int xx = 0; xx < t.w; xx += sub)
@@ -1165,6 +1389,106 @@ DSettings to_dsettings(const crt_renderer_settings *st) {
     return d;
 }
 
+int wf_grow_ids(WfBuffers &w, int64_t need, int64_t used, hipStream_t stream) {
+    if (need <= w.cap) return CRT_OK;
+    const int64_t cap = std::max<int64_t>(need, 2 * w.cap);
+    void *pn = nullptr, *pc = nullptr;
+    HIP_TRY(hipMalloc(&pn, (size_t)cap * sizeof(WNode)));
+    HIP_TRY(hipMalloc(&pc, (size_t)cap * sizeof(DVec4)));
+    if (used > 0) {
+        HIP_TRY(hipMemcpyAsync(pn, w.nodes, (size_t)used * sizeof(WNode), hipMemcpyDeviceToDevice, stream));
+        HIP_TRY(hipMemcpyAsync(pc, w.cols, (size_t)used * sizeof(DVec4), hipMemcpyDeviceToDevice, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+    }
+    if (w.nodes) (void)hipFree(w.nodes);
+    if (w.cols) (void)hipFree(w.cols);
+    w.nodes = static_cast<WNode *>(pn);
+    w.cols = static_cast<DVec4 *>(pc);
+    w.cap = cap;
+    return CRT_OK;
+}
+
+int wf_grow_queue(WfBuffers &w, int k, int64_t need) {
+    if (need <= w.qcap[k]) return CRT_OK;
+    const int64_t cap = std::max<int64_t>(need, 2 * w.qcap[k]);
+    if (w.q[k]) (void)hipFree(w.q[k]);
+    w.q[k] = nullptr;
+    void *p = nullptr;
+    HIP_TRY(hipMalloc(&p, (size_t)cap * sizeof(WRay)));
+    w.q[k] = static_cast<WRay *>(p);
+    w.qcap[k] = cap;
+    return CRT_OK;
+}
+
+void wf_free(WfBuffers &w) {
+    for (void *p : {(void *)w.nodes, (void *)w.cols, (void *)w.q[0], (void *)w.q[1], (void *)w.counts})
+        if (p) (void)hipFree(p);
+    w = WfBuffers{};
+}
+
+/* One frame of the wavefront path (see k_wf_level).  The host reads each
+ * level's queue length before launching the next level, so the call returns
+ * after the last level has been traced (composition is left enqueued). */
+int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &plan, float *d_out,
+                     hipStream_t stream, bool count, const DeviceScene *d_scene, int sec) {
+    WfBuffers &w = sc->wf;
+    constexpr int kMaxLevels = 66;
+    if (!w.counts) {
+        void *p = nullptr;
+        HIP_TRY(hipMalloc(&p, kMaxLevels * sizeof(int32_t)));
+        w.counts = static_cast<int32_t *>(p);
+    }
+    HIP_TRY(hipMemsetAsync(w.counts, 0, kMaxLevels * sizeof(int32_t), stream));
+    const int64_t n0 = (int64_t)plan.ntiles * 64;
+    int rc;
+    if ((rc = wf_grow_ids(w, 3 * n0, 0, stream)) != CRT_OK) return rc;
+    if ((rc = wf_grow_queue(w, 0, 2 * n0)) != CRT_OK) return rc;
+    unsigned long long *cnt = sc->d_counters;
+    WLevel lv{nullptr, 0, 0, w.q[0], w.counts, (int32_t)n0, w.nodes, w.cols};
+    const int blocks0 = (plan.ntiles + 3) / 4;
+    if (count)
+        hipLaunchKernelGGL((k_wf_level<7, true, true>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,
+                           plan.d_tiles, plan.ntiles, lv, cnt);
+    else
+        hipLaunchKernelGGL((k_wf_level<7, true, false>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,
+                           plan.d_tiles, plan.ntiles, lv, cnt);
+    HIP_TRY(hipGetLastError());
+    std::vector<std::pair<int64_t, int64_t>> levels;   /* (first id, count) of levels >= 1 */
+    int64_t base = n0;
+    int cur = 0;
+    for (int L = 1; L < kMaxLevels; ++L) {
+        int32_t n = 0;
+        HIP_TRY(hipMemcpyAsync(&n, w.counts + (L - 1), sizeof n, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        if (n == 0) break;
+        if (base + 3 * (int64_t)n > INT32_MAX) return set_error(CRT_E_UNSUPPORTED, "wavefront ray ids exceed 2^31");
+        if ((rc = wf_grow_ids(w, base + 3 * (int64_t)n, base, stream)) != CRT_OK) return rc;
+        if ((rc = wf_grow_queue(w, cur ^ 1, 2 * (int64_t)n)) != CRT_OK) return rc;
+        WLevel l{w.q[cur], n, L, w.q[cur ^ 1], w.counts + L, (int32_t)(base + n), w.nodes, w.cols};
+        const int blocks = (int)((n + 255) / 256);
+#define CRT_WF(SEC, COUNT)                                                                                  \
+    hipLaunchKernelGGL((k_wf_level<SEC, false, COUNT>), dim3(blocks), dim3(256), 0, stream, d_scene, ds, \
+                       plan.d_tiles, plan.ntiles, l, cnt)
+        if (sec == 4) {
+            if (count) CRT_WF(4, true); else CRT_WF(4, false);
+        } else {
+            if (count) CRT_WF(5, true); else CRT_WF(5, false);
+        }
+#undef CRT_WF
+        HIP_TRY(hipGetLastError());
+        levels.emplace_back(base, n);
+        base += n;
+        cur ^= 1;
+    }
+    for (auto it = levels.rbegin(); it != levels.rend(); ++it)
+        hipLaunchKernelGGL(k_wf_compose, dim3((unsigned)((it->second + 255) / 256)), dim3(256), 0, stream, w.nodes,
+                           w.cols, (int32_t)it->first, (int32_t)it->second);
+    hipLaunchKernelGGL(k_wf_pixels, dim3(blocks0), dim3(256), 0, stream, w.nodes, w.cols, plan.d_tiles,
+                       plan.ntiles, d_out);
+    HIP_TRY(hipGetLastError());
+    return CRT_OK;
+}
+
 /* Pick and launch the kernel variant for this scene + settings. */
 int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const ShardPlan &plan, float *d_out,
                   hipStream_t stream, bool count, unsigned long long *stamps = nullptr) {
@@ -1181,38 +1505,66 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         if (rc != CRT_OK) return rc;
     }
     const DSettings ds = to_dsettings(st);
+    const int sec = sc->secondary > 0 ? sc->secondary : (gi ? 4 : 5);
+    if (full && !gi && sc->wavefront && sc->traversal >= 6 && !stamps)
+        return render_wavefront(sc, ds, plan, d_out, stream, count, d_scene, sec == 4 ? 4 : 5);
     const int blocks = (plan.ntiles + 3) / 4;
     const uint64_t frames = (uint64_t)st->max_ray_depth + 1;
     unsigned long long *cnt = sc->d_counters;
-#define CRT_LAUNCH_T(FULL, MAXF, TRAV, COUNT)                                                               \
-    hipLaunchKernelGGL((k_render_tiles<FULL, MAXF, TRAV, COUNT>), dim3(blocks), dim3(256), 0, stream, d_scene, \
-                       ds, plan.d_tiles, plan.ntiles, d_out, cnt, stamps)
-#define CRT_LAUNCH(FULL, MAXF, COUNT)                                                                       \
+#define CRT_LAUNCH_T(FULL, MAXF, TRAV, SEC, COUNT)                                                          \
+    hipLaunchKernelGGL((k_render_tiles<FULL, MAXF, TRAV, SEC, COUNT>), dim3(blocks), dim3(256), 0, stream,       \
+                       d_scene, ds, plan.d_tiles, plan.ntiles, d_out, cnt, stamps)
+#define CRT_LAUNCH_NF(TRAV, COUNT) CRT_LAUNCH_T(false, 0, TRAV, TRAV, COUNT)
+#define CRT_LAUNCH_F(MAXF, TRAV, COUNT)                                                                      \
+    do {                                                                                                   \
+        if (sec == 4) CRT_LAUNCH_T(true, MAXF, TRAV, 4, COUNT);                                            \
+        else CRT_LAUNCH_T(true, MAXF, TRAV, 5, COUNT);                                                      \
+    } while (0)
+#define CRT_LAUNCH(FULL, MAXF, COUNT, PACKET)                                                               \
     do {                                                                                                   \
         switch (sc->traversal) {                                                                           \
-        case 0: CRT_LAUNCH_T(FULL, MAXF, 0, COUNT); break;                                                 \
-        case 1: CRT_LAUNCH_T(FULL, MAXF, 1, COUNT); break;                                                 \
-        case 3: CRT_LAUNCH_T(FULL, MAXF, 3, COUNT); break;                                                 \
-        case 4: CRT_LAUNCH_T(FULL, MAXF, 4, COUNT); break;                                                 \
-        case 5: CRT_LAUNCH_T(FULL, MAXF, 5, COUNT); break;                                                 \
-        case 6: CRT_LAUNCH_T(FULL, MAXF, 6, COUNT); break;                                                 \
-        case 7: CRT_LAUNCH_T(FULL, MAXF, 7, COUNT); break;                                                 \
-        case 8: CRT_LAUNCH_T(FULL, MAXF, 8, COUNT); break;                                                 \
-        default: CRT_LAUNCH_T(FULL, MAXF, 2, COUNT); break;                                                \
+        case 0: CRT_LAUNCH_T(FULL, MAXF, 0, 0, COUNT); break;                                              \
+        case 3: CRT_LAUNCH_T(FULL, MAXF, 3, 3, COUNT); break;                                              \
+        case 4: CRT_LAUNCH_T(FULL, MAXF, 4, 4, COUNT); break;                                              \
+        case 5: CRT_LAUNCH_T(FULL, MAXF, 5, 5, COUNT); break;                                              \
+        case 6: PACKET(6); break;                                                                          \
+        default: PACKET(7); break;                                                                         \
         }                                                                                                  \
     } while (0)
+#define CRT_NF_T(T) CRT_LAUNCH_NF(T, true)
+#define CRT_NF_F(T) CRT_LAUNCH_NF(T, false)
+#define CRT_F4_T(T) CRT_LAUNCH_F(4, T, true)
+#define CRT_F4_F(T) CRT_LAUNCH_F(4, T, false)
+#define CRT_F16_T(T) CRT_LAUNCH_F(16, T, true)
+#define CRT_F16_F(T) CRT_LAUNCH_F(16, T, false)
+#define CRT_F64_T(T) CRT_LAUNCH_F(64, T, true)
+#define CRT_F64_F(T) CRT_LAUNCH_F(64, T, false)
+    /* secondary rays (recursion, GI) scatter: the packet walks hand them to a
+     * per-lane walk — cooperative range donation for GI fan-out, range sharing
+     * otherwise (env CRT_SECONDARY = 4 | 5) */
     if (!full) {
-        if (count) CRT_LAUNCH(false, 0, true); else CRT_LAUNCH(false, 0, false);
+        if (count) CRT_LAUNCH(false, 0, true, CRT_NF_T); else CRT_LAUNCH(false, 0, false, CRT_NF_F);
     } else if (frames <= 4) {
-        if (count) CRT_LAUNCH(true, 4, true); else CRT_LAUNCH(true, 4, false);
+        if (count) CRT_LAUNCH(true, 4, true, CRT_F4_T); else CRT_LAUNCH(true, 4, false, CRT_F4_F);
     } else if (frames <= 16) {
-        if (count) CRT_LAUNCH(true, 16, true); else CRT_LAUNCH(true, 16, false);
+        if (count) CRT_LAUNCH(true, 16, true, CRT_F16_T); else CRT_LAUNCH(true, 16, false, CRT_F16_F);
     } else if (frames <= 64) {
-        if (count) CRT_LAUNCH(true, 64, true); else CRT_LAUNCH(true, 64, false);
+        if (count) CRT_LAUNCH(true, 64, true, CRT_F64_T); else CRT_LAUNCH(true, 64, false, CRT_F64_F);
     } else {
         return set_error(CRT_E_UNSUPPORTED, "max_ray_depth > 63 with recursive materials is not supported");
     }
 #undef CRT_LAUNCH
+#undef CRT_LAUNCH_NF
+#undef CRT_LAUNCH_F
+#undef CRT_LAUNCH_T
+#undef CRT_NF_T
+#undef CRT_NF_F
+#undef CRT_F4_T
+#undef CRT_F4_F
+#undef CRT_F16_T
+#undef CRT_F16_F
+#undef CRT_F64_T
+#undef CRT_F64_F
     HIP_TRY(hipGetLastError());
     return CRT_OK;
 }
@@ -1247,11 +1599,18 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     sc->device = device;
     if (const char *e = std::getenv("CRT_TRAVERSAL")) sc->traversal = std::atoi(e);
     if (const char *e = std::getenv("CRT_TILE_ORDER")) sc->tile_order = std::atoi(e);
+    if (const char *e = std::getenv("CRT_SECONDARY")) sc->secondary = std::atoi(e);
+    if (const char *e = std::getenv("CRT_WAVEFRONT")) sc->wavefront = std::atoi(e);
     if (const char *e = std::getenv("CRT_SPLIT")) {
         float a = 0.f, b = 0.f;
         if (std::sscanf(e, "%f,%f", &a, &b) >= 1) { sc->split4 = a; sc->split16 = b; }
     }
     if (sc->tile_order) sc->tile_work = tile_work_estimate(hs, (hs.width + 7) / 8, (hs.height + 7) / 8);
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+            sc->wave_slots = prop.multiProcessorCount * 4 * 6;
+    }
     crt_host_scene_info(h, &sc->info);
     sc->info.device_bytes = 0;
     for (const DMaterial &m : hs.materials) {
@@ -1336,6 +1695,7 @@ void crt_hip_scene_destroy(crt_hip_scene *sc) {
     if (sc->stream) (void)hipStreamSynchronize(sc->stream);
     for (void *p : sc->allocs) (void)hipFree(p);
     if (sc->d_out) (void)hipFree(sc->d_out);
+    wf_free(sc->wf);
     for (auto &kv : sc->unpack_plans) (void)hipFree(kv.second.first);
     if (sc->ev_start) (void)hipEventDestroy(sc->ev_start);
     if (sc->ev_stop) (void)hipEventDestroy(sc->ev_stop);

@@ -29,8 +29,14 @@ def main():
     p.add_argument("--depth", type=int, default=3)
     p.add_argument("--ab", default=None, help="ENVVAR=v1,v2,... — build one scene per value")
     p.add_argument("--counts", action="store_true", help="print per-ray and per-wave work counts per variant")
+    p.add_argument("--synthetic", type=int, default=0, help="C5: synthetic mesh of N triangles instead of --scene")
     a = p.parse_args()
-    sc = load_npz(ROOT / "tests" / "golden" / "scenes" / f"{a.scene}.npz").set_resolution(a.width, a.height)
+    if a.synthetic:
+        from crt_amd.synthetic import c5_scene
+        sc = c5_scene(a.synthetic, width=a.width, height=a.height)
+        a.scene = f"synthetic-{a.synthetic}"
+    else:
+        sc = load_npz(ROOT / "tests" / "golden" / "scenes" / f"{a.scene}.npz").set_resolution(a.width, a.height)
     st = N.RendererSettings.default(max_ray_depth=a.depth)
     variants = [("default", None)]
     if a.ab:
