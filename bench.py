@@ -11,7 +11,8 @@ N=1: the frame is rendered into HBM (scene + image resident; no PCIe in the
 timed region).  N>1 (one process per GPU, torchrun): the reference's bucket
 grid is dealt round-robin to ranks, each rank renders its buckets packed, and
 the tiles are gathered to rank 0 over RCCL (torch.distributed "nccl") and
-unpacked there — one frame per step, strong scaling.
+unpacked there — one frame per step, strong scaling; frame k's gather runs on
+RCCL's stream while frame k+1 renders (double-buffered, FramePipeline).
 
 Also reported: the roofline of the render kernel (algorithmic bytes per launch
 ÷ measured kernel time vs 8 TB/s HBM) and the CPU oracle (restatement of the
@@ -35,6 +36,7 @@ import torch  # noqa: E402  (import before libcrt_hip so both share torch's HIP 
 import torch.distributed as dist  # noqa: E402
 
 from crt_amd import native as N  # noqa: E402
+from crt_amd.distributed import FramePipeline  # noqa: E402
 from crt_amd.scene_npz import load_npz  # noqa: E402
 
 SCENE_NPZ = ROOT / "tests" / "golden" / "scenes" / "14-01-acceleration-tree__scene1.npz"
@@ -51,6 +53,8 @@ def parse():
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (wall s)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
+    p.add_argument("--check", action="store_true", help="rank 0: compare the last frame with a 1-GPU render")
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                    help="per-launch HBM bytes measured by rocprofv3 --pmc (profiles/), if present")
     return p.parse_args()
@@ -90,9 +94,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(1, torch.cuda.device_count())   # more ranks than GPUs only in rehearsals (gloo)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(a.backend)
 
     scene = load_npz(SCENE_NPZ).set_resolution(a.width, a.height)
     settings = N.RendererSettings.default()
@@ -105,22 +113,41 @@ def main():
     sptr = stream.cuda_stream
 
     frame = torch.empty(W * H * 3, dtype=torch.float32, device="cuda")
+    timing = {"events": None, "i": 0}
+
+    def render_full():
+        ev = timing["events"]
+        if ev is not None:
+            ev[timing["i"]][0].record(stream)
+        gpu.render_device(settings, frame.data_ptr(), sptr)
+        if ev is not None:
+            ev[timing["i"]][1].record(stream)
+            timing["i"] += 1
+
+    def render_shard(packed):
+        ev = timing["events"]
+        if ev is not None:
+            ev[timing["i"]][0].record(stream)
+        gpu.render_shard(settings, rank, world, packed.data_ptr(), sptr)
+        if ev is not None:
+            ev[timing["i"]][1].record(stream)
+            timing["i"] += 1
+
     if world > 1:
-        stride = gpu.shard_stride(world)
-        packed = torch.empty(stride, dtype=torch.float32, device="cuda")
-        gathered = [torch.empty(stride, dtype=torch.float32, device="cuda") for _ in range(world)] \
-            if rank == 0 else None
-        gathered_flat = torch.empty(stride * world, dtype=torch.float32, device="cuda") if rank == 0 else None
+        # frame k's RCCL gather overlaps frame k+1's shard render (crt_amd.distributed.FramePipeline)
+        pipe = FramePipeline(rank, world, gpu.shard_stride(world),
+                             lambda n: torch.empty(n, dtype=torch.float32, device="cuda"), render_shard,
+                             lambda flat: gpu.unpack_shards(world, flat.data_ptr(), frame.data_ptr(), sptr), dist)
 
     def step():
         if world == 1:
-            gpu.render_device(settings, frame.data_ptr(), sptr)
-            return
-        gpu.render_shard(settings, rank, world, packed.data_ptr(), sptr)
-        dist.gather(packed, gathered, dst=0)
-        if rank == 0:
-            torch.cat(gathered, out=gathered_flat)
-            gpu.unpack_shards(world, gathered_flat.data_ptr(), frame.data_ptr(), sptr)
+            render_full()
+        else:
+            pipe.step()
+
+    def drain():
+        if world > 1:
+            pipe.drain()
 
     # work counters of one full frame (outside the timed region)
     counts = gpu.count_work(settings)
@@ -128,26 +155,19 @@ def main():
 
     for _ in range(a.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
 
     # kernel duration: event pairs around each render launch on the launch stream
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    timing["events"] = ev
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        ev[i][0].record(stream)
-        if world == 1:
-            gpu.render_device(settings, frame.data_ptr(), sptr)
-            ev[i][1].record(stream)
-        else:
-            gpu.render_shard(settings, rank, world, packed.data_ptr(), sptr)
-            ev[i][1].record(stream)
-            dist.gather(packed, gathered, dst=0)
-            if rank == 0:
-                torch.cat(gathered, out=gathered_flat)
-                gpu.unpack_shards(world, gathered_flat.data_ptr(), frame.data_ptr(), sptr)
+    for _ in range(a.steps):
+        step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -159,6 +179,14 @@ def main():
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
+
+    if a.check and rank == 0:
+        want = gpu.render(settings)
+        got = frame.view(H, W, 3).cpu().numpy()
+        same = np.array_equal(got.view(np.uint32), want.view(np.uint32))
+        print(f"check: last frame {'bit-identical to' if same else 'DIFFERS from'} the 1-GPU render", flush=True)
+        if not same:
+            raise SystemExit(1)
 
     ms_per_step = elapsed / a.steps * 1e3
     mrays = rays_per_frame * a.steps / elapsed / 1e6

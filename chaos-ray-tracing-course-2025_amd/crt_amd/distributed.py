@@ -37,6 +37,53 @@ class FrameSharder:
         dist.gather(self.packed, self.gather_list, dst=0, group=group)
 
 
+class FramePipeline:
+    """Frames rendered back to back, each sharded over the ranks, with frame
+    k's gather overlapping frame k+1's shard render (double-buffered).
+
+    `render(packed)` fills this rank's packed buckets of the next frame,
+    `unpack(gathered_flat)` (rank 0) scatters a gathered frame into the
+    output.  With the "nccl" backend `Work.wait()` only orders the caller's
+    current stream after the collective, so rank 0 issues
+    render(k+1) → gather(k+1) → wait(gather k) → unpack(k) and the GPU runs
+    the gather of frame k on RCCL's stream while frame k+1 renders.  A packed
+    buffer is reused two frames later, after its gather was waited on.
+    """
+
+    def __init__(self, rank: int, world: int, stride: int, alloc: Callable[[int], object],
+                 render: Callable[[object], None], unpack: Callable[[object], None], dist, group=None):
+        self.rank, self.world, self.stride = rank, world, stride
+        self.render, self.unpack, self.dist, self.group = render, unpack, dist, group
+        self.packed = [alloc(stride), alloc(stride)]
+        if rank == 0:
+            self.flat = [alloc(stride * world), alloc(stride * world)]
+            self.views = [[f[i * stride:(i + 1) * stride] for i in range(world)] for f in self.flat]
+        else:
+            self.flat = self.views = None
+        self.pending = None
+        self.frames = 0
+
+    def step(self) -> None:
+        b = self.frames % 2
+        self.render(self.packed[b])
+        work = self.dist.gather(self.packed[b], self.views[b] if self.rank == 0 else None, dst=0,
+                                group=self.group, async_op=True)
+        if self.pending is not None:
+            self._finish(*self.pending)
+        self.pending = (b, work)
+        self.frames += 1
+
+    def drain(self) -> None:
+        if self.pending is not None:
+            self._finish(*self.pending)
+            self.pending = None
+
+    def _finish(self, b: int, work) -> None:
+        work.wait()
+        if self.rank == 0:
+            self.unpack(self.flat[b])
+
+
 def unpack_numpy(gathered: np.ndarray, width: int, height: int, bucket_size: int, world: int,
                  stride: int) -> np.ndarray:
     """Host mirror of crt_hip_unpack_shards (used by CPU tests)."""

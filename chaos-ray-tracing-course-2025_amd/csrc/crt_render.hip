@@ -1506,6 +1506,10 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     }
     const DSettings ds = to_dsettings(st);
     const int sec = sc->secondary > 0 ? sc->secondary : (gi ? 4 : 5);
+    /* GI: a pixel's rays are mostly scattered secondaries; the packet walk's
+     * extra registers would cost a wave per SIMD, so every ray takes the
+     * cooperative walk (unless CRT_SECONDARY asks for the packet primary) */
+    const int trav = (gi && sc->traversal >= 6 && sc->secondary == 0) ? 4 : sc->traversal;
     if (full && !gi && sc->wavefront && sc->traversal >= 6 && !stamps)
         return render_wavefront(sc, ds, plan, d_out, stream, count, d_scene, sec == 4 ? 4 : 5);
     const int blocks = (plan.ntiles + 3) / 4;
@@ -1522,7 +1526,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     } while (0)
 #define CRT_LAUNCH(FULL, MAXF, COUNT, PACKET)                                                               \
     do {                                                                                                   \
-        switch (sc->traversal) {                                                                           \
+        switch (trav) {                                                                                    \
         case 0: CRT_LAUNCH_T(FULL, MAXF, 0, 0, COUNT); break;                                              \
         case 3: CRT_LAUNCH_T(FULL, MAXF, 3, 3, COUNT); break;                                              \
         case 4: CRT_LAUNCH_T(FULL, MAXF, 4, 4, COUNT); break;                                              \

@@ -79,3 +79,63 @@ def test_shard_plan_partitions_the_frame():
                 cover[y:y + h, x:x + w] += 1
         nx, ny = int(W / b + 0.5), int(H / b + 0.5)              # crt_renderer.cpp:160-161
         assert (cover == (1 if nx and ny else 0)).all()
+
+
+def _pipeline_worker(rank, world, port, W, H, frames, out_path):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path.insert(0, str(root / "chaos-ray-tracing-course-2025_amd"))
+    sys.path.insert(0, str(root))
+    import torch
+    import torch.distributed as dist
+    from crt_amd.distributed import FramePipeline, unpack_numpy
+    from crt_amd.native import RendererSettings, shard_plan
+    from crt_amd.scene_npz import load_npz
+    from oracle import pyoracle
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    sc = load_npz(root / "tests/golden/scenes/14-01-acceleration-tree__scene1.npz").set_resolution(W, H)
+    bucket = sc.desc().bucket_size
+    stride = max(3 * int((p[:, 2] * p[:, 3]).sum()) for p in
+                 (shard_plan(W, H, bucket, s, world) for s in range(world)))
+    orc = pyoracle.OracleScene(sc)
+    st = RendererSettings.default()
+    base = np.zeros(stride, np.float32)
+    for x, y, w, h, off, _ in shard_plan(W, H, bucket, rank, world):
+        for row in range(h):
+            base[3 * (off + row * w): 3 * (off + (row + 1) * w)] = orc.render_pixels(st, (y + row) * W + x, w).reshape(-1)
+    state = {"k": 0, "out": []}
+
+    def render(packed):                  # frame k = oracle frame * (k + 1)
+        packed.numpy()[:] = base * np.float32(state["k"] + 1)
+        state["k"] += 1
+
+    def unpack(flat):
+        state["out"].append(unpack_numpy(flat.numpy(), W, H, bucket, world, stride))
+
+    pipe = FramePipeline(rank, world, stride, lambda n: torch.zeros(n, dtype=torch.float32), render, unpack, dist)
+    for _ in range(frames):
+        pipe.step()
+    pipe.drain()
+    if rank == 0:
+        np.save(out_path, np.stack(state["out"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_frame_pipeline_keeps_frames_apart(tmp_path, oracle):
+    """Double-buffered frames (bench.py's N-GPU loop): every frame comes out
+    whole and in order although frame k+1 renders before frame k is unpacked."""
+    import torch.multiprocessing as mp
+    from crt_amd.native import RendererSettings
+    from conftest import bits, scene_npz
+    W, H, frames, world = 120, 72, 5, 2
+    out = tmp_path / "frames.npy"
+    mp.spawn(_pipeline_worker, args=(world, free_port(), W, H, frames, str(out)), nprocs=world, join=True)
+    got = np.load(out)
+    want = oracle.OracleScene(scene_npz("14-01-acceleration-tree__scene1").set_resolution(W, H)).render(
+        RendererSettings.default())
+    assert got.shape == (frames, H, W, 3)
+    for k in range(frames):
+        assert np.array_equal(bits(got[k]), bits(want * np.float32(k + 1)))
