@@ -158,6 +158,7 @@ EXPORTS = [
     ("crt_hip_count_work", C.c_int, [_P, C.POINTER(RendererSettings), C.POINTER(WorkCounts)]),
     ("crt_hip_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_double)]),
     ("crt_hip_wave_counts", C.c_int, [_P, C.POINTER(WaveCounts)]),
+    ("crt_hip_scene_set_option", C.c_int, [_P, C.c_char_p, C.c_int]),
     ("crt_hip_profile_waves", C.c_int, [_P, C.POINTER(RendererSettings), _P, C.c_int64, _P]),
     ("crt_renderer_settings_default", None, [C.POINTER(RendererSettings)]),
     ("crt_write_ppm", C.c_int, [C.c_char_p, _P, C.c_int32, C.c_int32, C.c_int32]),
@@ -339,7 +340,7 @@ class HostScene:
 #  device scene (HBM-resident) and rendering
 # --------------------------------------------------------------------------
 class HipScene:
-    def __init__(self, src, device: int = 0):
+    def __init__(self, src, device: int = 0, **options):
         h = C.c_void_p()
         if isinstance(src, HostScene):
             _check(lib().crt_hip_scene_upload(src.handle, device, C.byref(h)))
@@ -347,6 +348,13 @@ class HipScene:
             _check(lib().crt_hip_scene_create(_desc_ptr(src), device, C.byref(h)))
         self._h = h
         self.device = device
+        for k, v in options.items():
+            self.set_option(k, v)
+
+    def set_option(self, name: str, value: int) -> "HipScene":
+        """Walk selection (crt_hip_scene_set_option): traversal / secondary / wavefront / trace_walk."""
+        _check(lib().crt_hip_scene_set_option(self._h, name.encode(), int(value)))
+        return self
 
     @property
     def handle(self):

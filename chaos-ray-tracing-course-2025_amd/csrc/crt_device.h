@@ -5,6 +5,7 @@
  * HIP's default).  Reference lines are cited per function.
  */
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #include "crt_layout.h"
@@ -248,6 +249,73 @@ CRT_HD bool box_hit_r(Vec o, Vec d, const RayRcp &r, const DNode n) {
 }
 #pragma clang diagnostic pop
 
+/* ---- pruned walks ------------------------------------------------------ */
+/* Hull slab test of a PNode (crt_layout.h).  The hull is conservative by a
+ * margin (crt_scene_build.cpp) far above this test's own rounding (a
+ * reciprocal with ~1 ulp error, one rounding per subtract and multiply), so
+ * `alive` is false only when no triangle in the subtree can produce a hit
+ * with t <= lim.  The slab distances are (plane - o) * (1/d): on an axis the
+ * ray is parallel to (1/d = +-inf) they are correctly signed infinities, and
+ * a NaN (0 * inf) only arises for an origin exactly on an expanded hull
+ * plane, i.e. outside every triangle's box by the full margin, where the
+ * subtree cannot hold a hit anyway.  The final tests are negated so a NaN
+ * bound keeps the subtree. */
+struct PruneRay {
+    float ox, oy, oz;
+    float ix, iy, iz;      /* ~1/d */
+    bool on;               /* |o|_inf <= prune_origin_max: the margins hold for this ray */
+};
+
+CRT_HD float rcp_any(float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(b);
+#else
+    return 1.0f / b;
+#endif
+}
+
+CRT_HD PruneRay make_prune_ray(Vec o, Vec d, float omax) {
+    PruneRay p;
+    p.ox = o.x;
+    p.oy = o.y;
+    p.oz = o.z;
+    p.ix = rcp_any(d.x);
+    p.iy = rcp_any(d.y);
+    p.iz = rcp_any(d.z);
+    p.on = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z))) <= omax;
+    return p;
+}
+
+CRT_HD bool hull_alive(const PNode &n, const PruneRay &p, float lim) {
+    const float t0x = (n.tlo_x - p.ox) * p.ix, t1x = (n.thi_x - p.ox) * p.ix;
+    const float t0y = (n.tlo_y - p.oy) * p.iy, t1y = (n.thi_y - p.oy) * p.iy;
+    const float t0z = (n.tlo_z - p.oz) * p.iz, t1z = (n.thi_z - p.oz) * p.iz;
+    const float tin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+    const float tout = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+    return !p.on || (!(tin > lim) && !(tin > tout) && !(tout < 0.0f));
+}
+
+CRT_HD DNode cell_of(const PNode &p) {
+    DNode n;
+    n.lo_x = p.lo_x; n.lo_y = p.lo_y; n.lo_z = p.lo_z;
+    n.hi_x = p.hi_x; n.hi_y = p.hi_y; n.hi_z = p.hi_z;
+    n.a = p.a; n.b = p.b;
+    return n;
+}
+CRT_HD int pnode_leaf_count(const PNode &n) { return n.count; }
+CRT_HD int pnode_depth(const PNode &n) { return n.depth; }
+
+/* direction octant: bit k set iff d[k] < 0 (crt_layout.h PNode orders) */
+CRT_HD int ray_octant(Vec d) { return (d.x < 0.0f ? 1 : 0) | (d.y < 0.0f ? 2 : 0) | (d.z < 0.0f ? 4 : 0); }
+
+/* (t, slot) beats the best so far: the reference keeps the first hit found
+ * with strict '<' while visiting slots in increasing order
+ * (crt_intersection.cpp:100,122-125), i.e. the minimum of the key (t, slot);
+ * a walk in another order reproduces it with the slot as tie-break. */
+CRT_HD bool key_better(float t, int slot, float best_t, int best) {
+    return best < 0 || t < best_t || (t == best_t && slot < best);
+}
+
 /* ray_intersect_triangle (crt_intersection.cpp:47-93), branch-free. */
 CRT_HD bool tri_hit_bf(Vec o, Vec d, const DTriGeo &g, bool cull, float &t_out) {
     const Vec N = vec(g.nx, g.ny, g.nz);
@@ -309,6 +377,49 @@ CRT_HD bool tri_hit(Vec o, Vec d, const DTriGeo &g, const uint8_t *cull, float &
         return true;
     }
     return false;
+}
+
+/* Per-ray pruned walk (stackless) over one octant's PNode order: a node is
+ * entered iff its hull is alive for the best key so far and the reference's
+ * six-face test passes on its cell — the same eligibility rule as
+ * crt_intersection.cpp:116-133, so every leaf copy the reference could pick
+ * and that can still win is tested.  Returns the winning slot (-1: miss). */
+struct WalkCounts { uint32_t nodes, tris; };
+
+template <bool COUNT>
+CRT_HD int walk_pruned(const PNode *nodes, int n, const DTriGeo *slots, const uint8_t *cull, Vec o, Vec d,
+                       const RayRcp &rr, const PruneRay &pr, float &best_t, WalkCounts &c) {
+    int best = -1;
+    float lim = INFINITY;
+    best_t = 0.0f;
+    int i = 0;
+    while (i < n) {
+        const PNode nd = nodes[i];
+        bool pass = false;
+        if (hull_alive(nd, pr, lim)) {
+            pass = box_hit_r(o, d, rr, cell_of(nd));
+            if (COUNT) ++c.nodes;
+        }
+        if (nd.b < 0) {
+            i = pass ? i + 1 : nd.a;
+            continue;
+        }
+        if (pass) {
+            const int cnt = pnode_leaf_count(nd);
+            for (int k = 0; k < cnt; ++k) {
+                const int slot = nd.b + k;
+                float t;
+                if (COUNT) ++c.tris;
+                if (tri_hit(o, d, slots[slot], cull + slot, t) && key_better(t, slot, best_t, best)) {
+                    best_t = t;
+                    best = slot;
+                    lim = t;
+                }
+            }
+        }
+        ++i;
+    }
+    return best;
 }
 
 /* Full Intersection record of the winning triangle (crt_intersection.cpp:71-88):

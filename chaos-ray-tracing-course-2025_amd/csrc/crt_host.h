@@ -66,6 +66,10 @@ struct HostScene {
     std::vector<int32_t> slot_tri;
     std::vector<uint8_t> slot_cull;
 
+    /* pruned walks (crt_layout.h PNode): 8 octant orders x nodes.size() */
+    std::vector<PNode> pnodes;
+    float prune_origin_max = 0.f;
+
     /* shading */
     std::vector<DMaterial> materials;
     std::vector<DTexture> textures;

@@ -36,6 +36,29 @@ struct alignas(16) DNode {
 };
 static_assert(sizeof(DNode) == 32, "DNode must be 32 B");
 
+/* Node record of the pruned walks: the reference cell (the box the
+ * reference's six-face test runs on — it decides which leaf copies are
+ * eligible, crt_intersection.cpp:121) plus a conservative hull of every
+ * triangle in the subtree, widened by a bound on the triangle test's rounding
+ * (crt_scene_build.cpp: hull_margin).  A ray whose best hit so far is nearer
+ * than the hull's entry distance cannot find a better (t, slot) key inside,
+ * so the subtree is skipped without changing the result.  The node array is
+ * stored 8 times, once per direction octant, each in preorder with the
+ * near child (by the sign of d on the node's split axis, depth % 3) first;
+ * `a` is the skip index within that octant's order, `b`/leaf fields as DNode.
+ * Leaf slot numbers are the reference's visit order in every copy, so ties in
+ * t are broken exactly as the reference's first-found rule does. */
+struct alignas(16) PNode {
+    float lo_x, lo_y, lo_z, hi_x;
+    float hi_y, hi_z;
+    int32_t a, b;
+    float tlo_x, tlo_y, tlo_z, thi_x;
+    float thi_y, thi_z;
+    int32_t depth;   /* tree depth (indexes the packet walk's reach mask) */
+    int32_t count;   /* leaf: triangle copies, interior: 0 */
+};
+static_assert(sizeof(PNode) == 64, "PNode must be 64 B");
+
 struct alignas(16) DTriGeo {
     float v0x, v0y, v0z, v1x;
     float v1y, v1z, v2x, v2y;
@@ -75,6 +98,8 @@ struct DLight {
 struct DeviceScene {
     const DNode *nodes;
     int32_t node_count;
+    const PNode *pnodes;            /* 8 octant orders x node_count (pruned walks) */
+    float prune_origin_max;         /* hull margins hold for rays with |o|_inf <= this */
     const DTriGeo *slots;
     const int32_t *slot_tri;
     const uint8_t *slot_cull;

@@ -265,9 +265,35 @@ __device__ __forceinline__ unsigned long long coop_piece(int ray, int start, int
     return ((unsigned long long)ray << 58) | ((unsigned long long)start << 29) | (unsigned long long)end;
 }
 
-template <bool COUNT>
+/* Node access of the sharing walks: the reference-order DNode array, or
+ * (PRUNE) the octant-ordered PNode array of the piece's ray with its hull. */
+template <bool PRUNE> struct WalkNode;
+template <> struct WalkNode<false> {
+    using T = DNode;
+    static __device__ __forceinline__ const DNode *base(const DeviceScene &s, Vec) { return s.nodes; }
+    static __device__ __forceinline__ DNode cell(const DNode &n) { return n; }
+    static __device__ __forceinline__ bool alive(const DNode &, const PruneRay &, float) { return true; }
+};
+template <> struct WalkNode<true> {
+    using T = PNode;
+    static __device__ __forceinline__ const PNode *base(const DeviceScene &s, Vec d) {
+        return s.pnodes + (size_t)ray_octant(d) * (size_t)s.node_count;
+    }
+    static __device__ __forceinline__ DNode cell(const PNode &n) { return cell_of(n); }
+    static __device__ __forceinline__ bool alive(const PNode &n, const PruneRay &p, float lim) {
+        return hull_alive(n, p, lim);
+    }
+};
+
+__device__ __forceinline__ float key_t(unsigned long long k) {
+    return k == ~0ull ? INFINITY : __uint_as_float((unsigned)(k >> 32));
+}
+
+template <bool COUNT, bool PRUNE>
 __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, Vec d, float &best_t,
                           LaneCounts &c) {
+    using WN = WalkNode<PRUNE>;
+    using NT = typename WN::T;
     const int lane = (int)(threadIdx.x & 63);
     const int n = s.node_count;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
@@ -283,9 +309,12 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
     int i = active ? 0 : n, end = n;    /* the piece: [i, end) */
     int lf = 0, lc = 0, k = 0;          /* pending leaf triangles */
     Vec ro = o, rd = d;
+    const NT *nb = WN::base(s, d);
+    PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
+    float lim = INFINITY;               /* best t known for the piece's ray (pruning bound) */
     unsigned long long mine = ~0ull;    /* best key found in the current piece */
     int sp = 0;                         /* wave-uniform stack depth */
-    DNode nd = s.nodes[0];
+    NT nd = nb[0];
     for (;;) {
         bool busy = (i < end) || (lc > 0);
         /* ---- idle lanes pop donated pieces ---- */
@@ -302,7 +331,12 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
                     end = (int)(pc & 0x1fffffff);
                     ro = vec(L.ray[r][0], L.ray[r][1], L.ray[r][2]);
                     rd = vec(L.ray[r][3], L.ray[r][4], L.ray[r][5]);
-                    nd = s.nodes[i];
+                    nb = WN::base(s, rd);
+                    if (PRUNE) {
+                        pr = make_prune_ray(ro, rd, s.prune_origin_max);
+                        lim = key_t(L.key[r]);
+                    }
+                    nd = nb[i];
                     busy = true;
                 }
             }
@@ -320,18 +354,22 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
                 if (tri_hit(ro, rd, s.slots[slot], s.slot_cull + slot, t)) {
                     const unsigned long long kk = coop_key(t, slot);
                     mine = kk < mine ? kk : mine;
+                    if (PRUNE) lim = fminf(lim, t);
                 }
                 if (++k == lc) lc = 0;
             } else {
                 const int i1 = i + 1 < n ? i + 1 : n - 1;
                 const int alt = nd.b < 0 ? (nd.a < n ? nd.a : n - 1) : i1;
-                const DNode n1 = s.nodes[i1];
-                const DNode n2 = s.nodes[alt];
-                const bool pass = box_hit_bf(ro, rd, nd);
-                if (COUNT) ++c.nodes;
+                const NT n1 = nb[i1];
+                const NT n2 = nb[alt];
+                bool pass = false;
+                if (WN::alive(nd, pr, lim)) {
+                    pass = box_hit_bf(ro, rd, WN::cell(nd));
+                    if (COUNT) ++c.nodes;
+                }
                 if (nd.b < 0) {
                     if (pass) {
-                        /* child1 = i+1; its subtree ends at skip(i+1) */
+                        /* first child = i+1; its subtree ends at skip(i+1) */
                         rest = n1.b < 0 ? n1.a : i + 2;
                         donate = rest < end;
                         i = i + 1;
@@ -341,7 +379,7 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
                         nd = n2;
                     }
                 } else {
-                    if (pass) { lf = nd.b; lc = node_leaf_count(nd); k = 0; }
+                    if (pass) { lf = nd.b; lc = (nd.a & 0xffffff); k = 0; }
                     i = i + 1;
                     nd = n1;
                 }
@@ -392,10 +430,13 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
  * passes an interior node donates the rest of its piece while the wave's
  * demand (idle lanes at the round start) exceeds the banked pieces.  The
  * stack depth lives in LDS because donations happen under divergent control
- * flow. */
-template <bool COUNT>
+ * flow.  PRUNE: pieces walk their ray's octant order and skip dead hulls
+ * (TRAV 11). */
+template <bool COUNT, bool PRUNE>
 __device__ int trace_share(const DeviceScene &s, CoopLds &L, bool active, Vec o, Vec d, float &best_t,
                            LaneCounts &c) {
+    using WN = WalkNode<PRUNE>;
+    using NT = typename WN::T;
     const int lane = (int)(threadIdx.x & 63);
     const int n = s.node_count;
     const int last = n - 1;
@@ -415,8 +456,11 @@ __device__ int trace_share(const DeviceScene &s, CoopLds &L, bool active, Vec o,
     int lf = 0, lc = 0;
     bool parked = false;
     Vec ro = o, rd = d;
+    const NT *nb = WN::base(s, d);
+    PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
+    float lim = INFINITY;
     unsigned long long mine = ~0ull;
-    DNode nd = s.nodes[0];
+    NT nd = nb[0];
     for (;;) {
         /* ---- merge finished pieces, refill idle lanes ---- */
         if (live && !(i < end)) {
@@ -441,7 +485,12 @@ __device__ int trace_share(const DeviceScene &s, CoopLds &L, bool active, Vec o,
                     end = (int)(pc & 0x1fffffff);
                     ro = vec(L.ray[r][0], L.ray[r][1], L.ray[r][2]);
                     rd = vec(L.ray[r][3], L.ray[r][4], L.ray[r][5]);
-                    nd = s.nodes[i];
+                    nb = WN::base(s, rd);
+                    if (PRUNE) {
+                        pr = make_prune_ray(ro, rd, s.prune_origin_max);
+                        lim = key_t(L.key[r]);
+                    }
+                    nd = nb[i];
                     live = true;
                 }
             }
@@ -457,15 +506,18 @@ __device__ int trace_share(const DeviceScene &s, CoopLds &L, bool active, Vec o,
         while (i < end) {
             const int i1 = i + 1 < n ? i + 1 : last;
             const int alt = nd.b < 0 ? (nd.a < n ? nd.a : last) : i1;
-            const DNode n1 = s.nodes[i1];
-            const DNode n2 = s.nodes[alt];
+            const NT n1 = nb[i1];
+            const NT n2 = nb[alt];
             bool pass;
             if (parked) {
                 pass = true;
                 parked = false;
             } else {
-                pass = box_hit_bf(ro, rd, nd);
-                if (COUNT) ++c.nodes;
+                pass = false;
+                if (WN::alive(nd, pr, lim)) {
+                    pass = box_hit_bf(ro, rd, WN::cell(nd));
+                    if (COUNT) ++c.nodes;
+                }
             }
             bool donate = false;
             int rest = 0;
@@ -484,7 +536,7 @@ __device__ int trace_share(const DeviceScene &s, CoopLds &L, bool active, Vec o,
                 nd = n1;
             } else if (lc == 0) {
                 lf = nd.b;
-                lc = node_leaf_count(nd);
+                lc = nd.a & 0xffffff;
                 ++i;
                 nd = n1;
             } else {
@@ -526,6 +578,7 @@ __device__ int trace_share(const DeviceScene &s, CoopLds &L, bool active, Vec o,
                 if (tri_hit(ro, rd, g, s.slot_cull + slot, t)) {
                     const unsigned long long kk = coop_key(t, slot);
                     mine = kk < mine ? kk : mine;
+                    if (PRUNE) lim = fminf(lim, t);
                 }
                 g = gn;
             }
@@ -635,12 +688,135 @@ __device__ int trace_packet(const DeviceScene &s, bool active, Vec o, Vec d, flo
     return best;
 }
 
-/* TRAV: 0 per-lane walk | 1 while-while | 2 while-while + prefetch | 3 as 2 with branch-free boxes */
+/* ---------------------------------------------------------------------- */
+/* Pruned walks (TRAV 8 packet, TRAV 9 per lane) over the octant-ordered     */
+/* PNode arrays (crt_layout.h)                                               */
+/* ---------------------------------------------------------------------- */
+/* TRAV 8: the masked packet walk of TRAV 7 where a lane also drops a subtree
+ * whose triangle hull it cannot hit at or before its best t (hull_alive), and
+ * the wave walks the node order of the octant most of its lanes share, so
+ * near children come first and best t shrinks early.  The wave skips the
+ * six-face tests of a node no lane keeps alive.  Candidates are merged by
+ * the key (t, slot), which equals the reference's first-found rule in any
+ * visit order; every lane still tests its reference-eligible leaves only
+ * (a lane enters a node iff its ancestors' cells passed for its ray). */
+template <bool COUNT>
+__device__ int trace_packet_pruned(const DeviceScene &s, bool active, Vec o, Vec d, float &best_t, LaneCounts &c) {
+    int best = -1;
+    best_t = 0.0f;
+    float lim = INFINITY;
+    const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
+    const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
+    unsigned long long reach = active ? 1ull : 0ull;
+    if (COUNT && active) ++c.traversals;
+    const int n = s.node_count;
+    const int last = n - 1;
+    const int na = __popcll(__ballot(active));
+    int oct = 0;
+    if (2 * __popcll(__ballot(active && d.x < 0.0f)) > na) oct |= 1;
+    if (2 * __popcll(__ballot(active && d.y < 0.0f)) > na) oct |= 2;
+    if (2 * __popcll(__ballot(active && d.z < 0.0f)) > na) oct |= 4;
+    const PNode *nodes = s.pnodes + (size_t)uniform_i(oct) * (size_t)n;
+    /* The walk is a chain of dependent scalar loads (next index comes from the
+     * current record), so each step issues the loads of both possible
+     * successors — i+1 (descend / after a leaf) and the skip target — before
+     * it tests the current node; the whole 64-B record is read up front. */
+    int i = 0;
+    PNode cur = load_scalar(nodes, 0);
+    while (i < n) {
+        const bool interior = cur.b < 0;
+        const int i1 = i + 1 < n ? i + 1 : last;
+        const int i2 = interior ? (cur.a < n ? cur.a : last) : i1;
+        const PNode n1 = load_scalar(nodes, i1);
+        const PNode n2 = load_scalar(nodes, i2);
+        const int depth = pnode_depth(cur);
+        const bool in = ((reach >> depth) & 1ull) != 0ull;
+        const bool alive = in & hull_alive(cur, pr, lim);
+        if (COUNT) ++c.wave_nodes;
+        bool pass = false;
+        if (__ballot(alive) != 0ull) {
+            pass = alive && box_hit_r(o, d, rr, cell_of(cur));
+            if (COUNT && alive) ++c.nodes;
+        }
+        const unsigned long long pm = __ballot(pass);
+        if (interior) {
+            if (pm != 0ull) {
+                const unsigned long long bit = 2ull << depth;
+                reach = pass ? (reach | bit) : (reach & ~bit);
+                i = i + 1;
+                cur = n1;
+            } else {
+                i = cur.a;
+                cur = n2;
+            }
+            continue;
+        }
+        if (pm != 0ull) {
+            const int first = cur.b, cnt = pnode_leaf_count(cur);
+            DTriGeo g = load_scalar(s.slots, first);
+            uint32_t cw = load_scalar(s.slot_cull_bits, first >> 5);
+            for (int k = 0; k < cnt; ++k) {
+                const int slot = first + k;
+                const int sn = k + 1 < cnt ? slot + 1 : slot;
+                const DTriGeo gn = load_scalar(s.slots, sn);           /* next triangle in flight */
+                const uint32_t cwn = load_scalar(s.slot_cull_bits, sn >> 5);
+                const bool cull = ((cw >> (slot & 31)) & 1u) != 0u;
+                float t;
+                if (COUNT && pass) ++c.tris;
+                if (COUNT) ++c.wave_tris;
+                const bool pre = pass && tri_plane(o, d, g, cull, t) && key_better(t, slot, best_t, best);
+                const bool any = __ballot(pre) != 0ull;
+                if (COUNT && any) ++c.wave_edges;
+                if (any && pre && tri_edges(o, d, g, t)) {
+                    best_t = t;
+                    best = slot;
+                    lim = t;
+                }
+                g = gn;
+                cw = cwn;
+            }
+        }
+        i = i + 1;
+        cur = n1;
+    }
+    if (COUNT && best >= 0) ++c.hits;
+    return best;
+}
+
+/* TRAV 9: per-lane pruned walk (crt_device.h walk_pruned) over the lane's own
+ * octant order — scattered secondary rays. */
+template <bool COUNT>
+__device__ __forceinline__ int trace_lane_pruned(const DeviceScene &s, bool active, Vec o, Vec d, float &best_t,
+                                                 LaneCounts &c) {
+    best_t = 0.0f;
+    if (!active) return -1;
+    if (COUNT) ++c.traversals;
+    const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
+    const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
+    const int n = s.node_count;
+    WalkCounts wc = {0u, 0u};
+    const int best = walk_pruned<COUNT>(s.pnodes + (size_t)ray_octant(d) * (size_t)n, n, s.slots, s.slot_cull, o, d,
+                                        rr, pr, best_t, wc);
+    if (COUNT) {
+        c.nodes += wc.nodes;
+        c.tris += wc.tris;
+        if (best >= 0) ++c.hits;
+    }
+    return best;
+}
+
+/* TRAV: 0 per-lane walk | 1 while-while | 2 while-while + prefetch | 3 as 2 with branch-free boxes
+ *       4 cooperative | 5 range sharing | 6/7 packet | 8 pruned packet | 9 pruned per lane
+ *       10 / 11 pruned 4 / 5 */
 template <int TRAV, bool COUNT>
 __device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, bool active, Vec o, Vec d, float &best_t,
                                      LaneCounts &c) {
-    if (TRAV == 4) return trace_coop<COUNT>(s, *L, active, o, d, best_t, c);
-    if (TRAV == 5) return trace_share<COUNT>(s, *L, active, o, d, best_t, c);
+    if (TRAV == 8) return trace_packet_pruned<COUNT>(s, active, o, d, best_t, c);
+    if (TRAV == 9) return trace_lane_pruned<COUNT>(s, active, o, d, best_t, c);
+    if (TRAV == 4) return trace_coop<COUNT, false>(s, *L, active, o, d, best_t, c);
+    if (TRAV == 5) return trace_share<COUNT, false>(s, *L, active, o, d, best_t, c);
+    if (TRAV == 10) return trace_coop<COUNT, true>(s, *L, active, o, d, best_t, c);
+    if (TRAV == 11) return trace_share<COUNT, true>(s, *L, active, o, d, best_t, c);
     if (TRAV == 6) return trace_packet<COUNT, false>(s, active, o, d, best_t, c);
     if (TRAV == 7) return trace_packet<COUNT, true>(s, active, o, d, best_t, c);
     if (TRAV == 1) return trace_closest_ww<COUNT>(s, o, d, best_t, c);
@@ -880,12 +1056,14 @@ __global__ CRT_RENDER_BOUNDS void k_render_tiles(const DeviceScene *__restrict__
     const bool has_px = lx < tl.w && ly < tl.h;
     /* the sharing walks keep pixel-less lanes as helpers (they take donated node
      * ranges of the wave's rays); the other walks drop them */
-    constexpr bool kHelpers = (TRAV >= 4) && !FULL;
+    constexpr bool kHelpers = (TRAV >= 4) && !FULL;   /* sharing walks use them; packet walks ignore them */
     if (!kHelpers && !has_px) return;
     LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    __shared__ CoopLds coop[TRAV >= 4 ? 4 : 1];
+    constexpr bool kCoop = TRAV == 4 || TRAV == 5 || TRAV == 10 || TRAV == 11 ||
+                           SEC == 4 || SEC == 5 || SEC == 10 || SEC == 11;   /* LDS only for the sharing walks */
+    __shared__ CoopLds coop[kCoop ? 4 : 1];
     const Vec c = shade_pixel<FULL, MAXF, TRAV, SEC, COUNT>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt,
-                                                      &coop[TRAV >= 4 ? (threadIdx.x >> 6) : 0], has_px);
+                                                      &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px);
     if (has_px) {
         float *px = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
         px[0] = c.x;
@@ -905,6 +1083,38 @@ __global__ CRT_RENDER_BOUNDS void k_render_tiles(const DeviceScene *__restrict__
             atomicAdd(&counters[7], 1ull);
         }
     }
+}
+
+/* Calibration probe (measured-cost tile plan): the camera rays of a tile
+ * list traced with the frame's primary walk, no shading.  Each wave writes
+ * its cost: for the packet walks the wave's node + triangle + edge steps
+ * (what the wave pays: the union of its lanes' visit sets), for per-lane
+ * walks the largest lane's node + triangle tests. */
+template <int TRAV>
+__global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restrict__ scene,
+                                                     const Tile *__restrict__ tiles, int ntiles,
+                                                     uint32_t *__restrict__ wave_cost) {
+    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int lane = (int)(threadIdx.x & 63);
+    if (wave >= ntiles) return;
+    const DeviceScene &s = *scene;
+    const Tile tl = tiles[wave];
+    const int lx = lane & 7, ly = lane >> 3;
+    const bool has_px = lx < tl.w && ly < tl.h;
+    Vec o, d;
+    camera_ray(s, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), o, d);
+    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    constexpr bool kCoop = TRAV == 4 || TRAV == 5 || TRAV == 10 || TRAV == 11;
+    __shared__ CoopLds coop[kCoop ? 4 : 1];
+    float t;
+    (void)trace<TRAV, true>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px, o, d, t, cnt);
+    constexpr bool kPacket = TRAV >= 6 && TRAV <= 8;
+    uint32_t c = kPacket ? cnt.wave_nodes + cnt.wave_tris + cnt.wave_edges : cnt.nodes + cnt.tris;
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t o2 = (uint32_t)__shfl_xor((int)c, off);
+        c = c > o2 ? c : o2;
+    }
+    if (lane == 0) wave_cost[wave] = c;
 }
 
 /* ====================================================================== */
@@ -974,9 +1184,10 @@ __global__ __launch_bounds__(256) void k_wf_level(const DeviceScene *__restrict_
         }
     }
     LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    __shared__ CoopLds coop[4];
+    constexpr bool kCoop = TRAV == 4 || TRAV == 5 || TRAV == 10 || TRAV == 11;
+    __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
-    const int slot = trace<TRAV, COUNT>(s, &coop[threadIdx.x >> 6], has, o, d, t, cnt);
+    const int slot = trace<TRAV, COUNT>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has, o, d, t, cnt);
 
     WNode node = {wFinal, -1, -1, 0, 0.f, 0.f, 0.f, 0.f};
     Vec col = vec(0.f, 0.f, 0.f);
@@ -1115,14 +1326,14 @@ __global__ __launch_bounds__(256) void k_wf_pixels(const WNode *__restrict__ nod
 
 /* crt_hip_trace_batch: closest hit of arbitrary rays (a1–a4 KATs). */
 __global__ __launch_bounds__(256) void k_trace_rays(DeviceScene s, const float *__restrict__ rays, int64_t n,
-                                                    crt_hit *__restrict__ hits) {
+                                                    crt_hit *__restrict__ hits, int walk) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const Vec o = vec(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
     const Vec d = vec(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
     LaneCounts cnt;
     float t;
-    const int slot = trace_closest_ww<false>(s, o, d, t, cnt);
+    const int slot = walk == 1 ? trace_lane_pruned<false>(s, true, o, d, t, cnt) : trace_closest_ww<false>(s, o, d, t, cnt);
     crt_hit r;
     r.distance = 0.f;
     r.point[0] = r.point[1] = r.point[2] = 0.f;
@@ -1245,7 +1456,8 @@ struct crt_hip_scene {
     float *d_out = nullptr;
     unsigned long long *d_counters = nullptr;
     bool grid_empty = false;
-    int traversal = 7;             /* kernel walk variant, see trace<> (env CRT_TRAVERSAL) */
+    int traversal = 8;             /* kernel walk variant, see trace<> (env CRT_TRAVERSAL) */
+    int trace_walk = 1;            /* crt_hip_trace_batch: 0 reference-order walk, 1 pruned per-lane walk */
     int tile_order = 1;            /* dispatch tiles by estimated work (env CRT_TILE_ORDER) */
     /* a tile is split into 4x4 (2x2) pixel waves when its work estimate exceeds
      * split4 (split16) times the mean work per resident wave slot, i.e. when it
@@ -1254,6 +1466,15 @@ struct crt_hip_scene {
     int wave_slots = 6144;   /* CUs x 4 SIMDs x 6 resident render waves */
     int secondary = 0;       /* walk for secondary rays under TRAV 6/7 (0 = by scene, env CRT_SECONDARY) */
     std::vector<float> tile_work;  /* per 8x8 tile of the full frame */
+    /* measured-cost tile plan (calibrate_plan): per 8x8 tile of the full frame,
+     * the sub-tiles it is split into and their probed costs */
+    struct SubTile { int32_t dx, dy, w, h; float cost; };
+    std::vector<std::vector<SubTile>> calib;
+    int calib_walk = -1;           /* primary walk the calibration was measured with (-1: none) */
+    int calibrate = 1;             /* env CRT_CALIBRATE */
+    float calib_k = 4.0f;          /* split a wave whose cost exceeds k x (total cost / wave slots) (env CRT_CALIB_K) */
+    int calib_min = 2;             /* smallest sub-tile side (env CRT_CALIB_MIN: 1, 2, 4, 8) */
+    std::vector<void *> plan_allocs;   /* tile lists of the current plans */
     int wavefront = 1;             /* level-by-level recursion when GI is off (env CRT_WAVEFRONT) */
     WfBuffers wf;
 };
@@ -1296,7 +1517,31 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         }
         plan.packed_pixels = total;
     }
-    if (sc->tile_order && !tiles.empty() && !sc->tile_work.empty()) {
+    if (!sc->calib.empty() && !tiles.empty()) {
+        /* measured costs: split as calibrated, heaviest first */
+        const int tx = (W + 7) / 8;
+        std::vector<std::pair<float, Tile>> out;
+        out.reserve(tiles.size() * 2);
+        for (const Tile &t : tiles) {
+            const size_t k = (size_t)(t.y / 8) * tx + t.x / 8;
+            const auto &cal = sc->calib[k];
+            const bool aligned = t.x % 8 == 0 && t.y % 8 == 0 && t.w == std::min(8, W - t.x) &&
+                                 t.h == std::min(8, sc->info.height - t.y);
+            if (aligned) {
+                for (const auto &st : cal)
+                    out.push_back({st.cost, Tile{t.x + st.dx, t.y + st.dy, st.w, st.h,
+                                                 t.out_base + (int64_t)st.dy * t.out_stride + st.dx, t.out_stride, 0}});
+            } else {   /* bucket grid not on the 8x8 grid: keep the tile, cost of its 8x8 cell */
+                float c = 0.f;
+                for (const auto &st : cal) c += st.cost;
+                out.push_back({c, t});
+            }
+        }
+        std::stable_sort(out.begin(), out.end(),
+                         [](const std::pair<float, Tile> &a, const std::pair<float, Tile> &b) { return a.first > b.first; });
+        tiles.clear();
+        for (const auto &e : out) tiles.push_back(e.second);
+    } else if (sc->tile_order && !tiles.empty() && !sc->tile_work.empty()) {
         /* dispatch the expensive tiles first so the longest waves start at t=0;
          * with a sharing walk, split the heaviest tiles so each of their waves
          * carries fewer rays and the rest of its lanes help (4x4 or 2x2 pixels) */
@@ -1329,10 +1574,98 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         void *p = nullptr;
         HIP_TRY(hipMalloc(&p, tiles.size() * sizeof(Tile)));
         HIP_TRY(hipMemcpy(p, tiles.data(), tiles.size() * sizeof(Tile), hipMemcpyHostToDevice));
-        sc->allocs.push_back(p);
+        sc->plan_allocs.push_back(p);
         plan.d_tiles = static_cast<Tile *>(p);
     }
     return CRT_OK;
+}
+
+/* Probe costs of a tile list (k_probe_tiles) with walk `walk`, synchronously. */
+int probe_tiles(crt_hip_scene *sc, const DeviceScene *d_scene, int walk, const std::vector<Tile> &tiles,
+                std::vector<uint32_t> &cost, hipStream_t stream) {
+    cost.assign(tiles.size(), 0u);
+    if (tiles.empty()) return CRT_OK;
+    void *dt = nullptr, *dc = nullptr;
+    HIP_TRY(hipMalloc(&dt, tiles.size() * sizeof(Tile)));
+    hipError_t e = hipMalloc(&dc, tiles.size() * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemcpyAsync(dt, tiles.data(), tiles.size() * sizeof(Tile), hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess) {
+        const int n = (int)tiles.size();
+        const dim3 grid((unsigned)((n + 3) / 4));
+        const Tile *t = static_cast<const Tile *>(dt);
+        uint32_t *c = static_cast<uint32_t *>(dc);
+        switch (walk) {
+        case 6: hipLaunchKernelGGL(k_probe_tiles<6>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
+        case 7: hipLaunchKernelGGL(k_probe_tiles<7>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
+        default: hipLaunchKernelGGL(k_probe_tiles<8>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
+        }
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(cost.data(), dc, tiles.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    (void)hipFree(dt);
+    if (dc) (void)hipFree(dc);
+    if (e != hipSuccess) return set_error(CRT_E_HIP, std::string("tile probe: ") + hipGetErrorString(e));
+    return CRT_OK;
+}
+
+/* Measured-cost tile plan.  The frame's 8x8 tiles are probed with the primary
+ * walk; a tile whose wave cost exceeds k x (total cost / resident wave slots)
+ * would run past the ideal makespan, so it is split into quadrants, which are
+ * probed in turn, down to calib_min pixels.  The leaves and their costs give
+ * every later plan (full frame and shards): split as measured, dispatched
+ * heaviest first.  Results do not depend on the plan. */
+int calibrate_plan(crt_hip_scene *sc, const DeviceScene *d_scene, int walk, hipStream_t stream) {
+    const int W = sc->info.width, H = sc->info.height;
+    const int tx = (W + 7) / 8, ty = (H + 7) / 8;
+    struct Item { int k; int32_t dx, dy, w, h; };
+    std::vector<Item> cur;
+    cur.reserve((size_t)tx * ty);
+    for (int y = 0; y < ty; ++y)
+        for (int x = 0; x < tx; ++x)
+            cur.push_back(Item{y * tx + x, 0, 0, std::min(8, W - 8 * x), std::min(8, H - 8 * y)});
+    std::vector<std::vector<crt_hip_scene::SubTile>> cal((size_t)tx * ty);
+    double thresh = -1.0;
+    int side = 8;
+    while (!cur.empty()) {
+        std::vector<Tile> tl(cur.size());
+        for (size_t i = 0; i < cur.size(); ++i) {
+            const int x0 = 8 * (cur[i].k % tx) + cur[i].dx, y0 = 8 * (cur[i].k / tx) + cur[i].dy;
+            tl[i] = Tile{x0, y0, cur[i].w, cur[i].h, (int64_t)y0 * W + x0, W, 0};
+        }
+        std::vector<uint32_t> cost;
+        const int rc = probe_tiles(sc, d_scene, walk, tl, cost, stream);
+        if (rc != CRT_OK) return rc;
+        if (thresh < 0.0) {
+            double sum = 0.0;
+            for (uint32_t c : cost) sum += c;
+            thresh = sc->calib_k * sum / std::max(1, sc->wave_slots);
+        }
+        std::vector<Item> next;
+        const int half = side / 2;
+        for (size_t i = 0; i < cur.size(); ++i) {
+            const Item &it = cur[i];
+            if ((double)cost[i] > thresh && half >= sc->calib_min && (it.w > half || it.h > half)) {
+                for (int yy = 0; yy < it.h; yy += half)
+                    for (int xx = 0; xx < it.w; xx += half)
+                        next.push_back(Item{it.k, it.dx + xx, it.dy + yy, std::min(half, it.w - xx), std::min(half, it.h - yy)});
+            } else {
+                cal[it.k].push_back(crt_hip_scene::SubTile{it.dx, it.dy, it.w, it.h, (float)cost[i]});
+            }
+        }
+        cur.swap(next);
+        side = half;
+    }
+    sc->calib.swap(cal);
+    sc->calib_walk = walk;
+    return CRT_OK;
+}
+
+void free_plans(crt_hip_scene *sc) {
+    for (void *p : sc->plan_allocs) (void)hipFree(p);
+    sc->plan_allocs.clear();
+    sc->full = ShardPlan{};
+    sc->shard_plans.clear();
 }
 
 int ensure_gi_tables(crt_hip_scene *sc) {
@@ -1376,6 +1709,35 @@ int sync_device_record(crt_hip_scene *sc, const DeviceScene **out) {
 int check_settings(const crt_renderer_settings *st) {
     if (!st) return set_error(CRT_E_INVALID, "null settings");
     return CRT_OK;
+}
+
+/* The primary walk a tile plan is measured with (-1: keep the estimate plan):
+ * camera rays of diffuse frames and level 0 of the wavefront recursion. */
+int plan_walk(const crt_hip_scene *sc, const crt_renderer_settings *st) {
+    const bool gi = sc->info.gi_on && sc->has_diffuse && st->diffuse_reflection_ray_count > 0;
+    const bool full = gi || sc->has_secondary;
+    const bool packet = sc->traversal >= 6 && sc->traversal <= 8;
+    if (gi || !packet) return -1;
+    if (full) return sc->wavefront ? (sc->traversal == 8 ? 8 : 7) : -1;
+    return sc->traversal;
+}
+
+/* Calibrate the tile plan for this frame's primary walk once (see
+ * calibrate_plan), then rebuild the full-frame plan; shard plans are rebuilt
+ * on their next use. */
+int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t stream) {
+    if (!sc->calibrate || sc->grid_empty) return CRT_OK;
+    const int walk = plan_walk(sc, st);
+    if (walk < 0 || walk == sc->calib_walk) return CRT_OK;
+    const DeviceScene *d_scene = nullptr;
+    int rc = sync_device_record(sc, &d_scene);
+    if (rc != CRT_OK) return rc;
+    HIP_TRY(hipDeviceSynchronize());   /* earlier frames may still read the old tile lists */
+    if ((rc = calibrate_plan(sc, d_scene, walk, stream)) != CRT_OK) return rc;
+    free_plans(sc);
+    int64_t px = 0;
+    const std::vector<DBucket> all = shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size, 0, 1, &px);
+    return make_tile_plan(sc, all, true, sc->full);
 }
 
 DSettings to_dsettings(const crt_renderer_settings *st) {
@@ -1430,7 +1792,7 @@ void wf_free(WfBuffers &w) {
  * level's queue length before launching the next level, so the call returns
  * after the last level has been traced (composition is left enqueued). */
 int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &plan, float *d_out,
-                     hipStream_t stream, bool count, const DeviceScene *d_scene, int sec) {
+                     hipStream_t stream, bool count, const DeviceScene *d_scene, int sec, int primary) {
     WfBuffers &w = sc->wf;
     constexpr int kMaxLevels = 66;
     if (!w.counts) {
@@ -1446,12 +1808,15 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
     unsigned long long *cnt = sc->d_counters;
     WLevel lv{nullptr, 0, 0, w.q[0], w.counts, (int32_t)n0, w.nodes, w.cols};
     const int blocks0 = (plan.ntiles + 3) / 4;
-    if (count)
-        hipLaunchKernelGGL((k_wf_level<7, true, true>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,
-                           plan.d_tiles, plan.ntiles, lv, cnt);
-    else
-        hipLaunchKernelGGL((k_wf_level<7, true, false>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,
-                           plan.d_tiles, plan.ntiles, lv, cnt);
+#define CRT_WF0(T, COUNT)                                                                                   \
+    hipLaunchKernelGGL((k_wf_level<T, true, COUNT>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,      \
+                       plan.d_tiles, plan.ntiles, lv, cnt)
+    if (primary == 8) {
+        if (count) CRT_WF0(8, true); else CRT_WF0(8, false);
+    } else {
+        if (count) CRT_WF0(7, true); else CRT_WF0(7, false);
+    }
+#undef CRT_WF0
     HIP_TRY(hipGetLastError());
     std::vector<std::pair<int64_t, int64_t>> levels;   /* (first id, count) of levels >= 1 */
     int64_t base = n0;
@@ -1469,10 +1834,12 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
 #define CRT_WF(SEC, COUNT)                                                                                  \
     hipLaunchKernelGGL((k_wf_level<SEC, false, COUNT>), dim3(blocks), dim3(256), 0, stream, d_scene, ds, \
                        plan.d_tiles, plan.ntiles, l, cnt)
-        if (sec == 4) {
-            if (count) CRT_WF(4, true); else CRT_WF(4, false);
-        } else {
-            if (count) CRT_WF(5, true); else CRT_WF(5, false);
+        switch (sec) {
+        case 4: if (count) CRT_WF(4, true); else CRT_WF(4, false); break;
+        case 9: if (count) CRT_WF(9, true); else CRT_WF(9, false); break;
+        case 10: if (count) CRT_WF(10, true); else CRT_WF(10, false); break;
+        case 11: if (count) CRT_WF(11, true); else CRT_WF(11, false); break;
+        default: if (count) CRT_WF(5, true); else CRT_WF(5, false); break;
         }
 #undef CRT_WF
         HIP_TRY(hipGetLastError());
@@ -1505,70 +1872,60 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         if (rc != CRT_OK) return rc;
     }
     const DSettings ds = to_dsettings(st);
-    const int sec = sc->secondary > 0 ? sc->secondary : (gi ? 4 : 5);
-    /* GI: a pixel's rays are mostly scattered secondaries; the packet walk's
-     * extra registers would cost a wave per SIMD, so every ray takes the
-     * cooperative walk (unless CRT_SECONDARY asks for the packet primary) */
-    const int trav = (gi && sc->traversal >= 6 && sc->secondary == 0) ? 4 : sc->traversal;
-    if (full && !gi && sc->wavefront && sc->traversal >= 6 && !stamps)
-        return render_wavefront(sc, ds, plan, d_out, stream, count, d_scene, sec == 4 ? 4 : 5);
+    /* Walks: camera rays of diffuse-only frames take the packet walk
+     * (traversal 7, or 8 pruned).  Secondary rays scatter and take a per-lane
+     * sharing walk: for reflect/refract levels range sharing (5) or, pruned,
+     * cooperative donation (10: 4.98 ms vs 5.75 for 11 and 7.0 for 5 on C3);
+     * for GI fan-out cooperative donation (4) — its pruned form (10) needs
+     * 134 VGPRs (3 waves/SIMD) and loses on C4 (378 vs 320 ms); with GI every
+     * ray of the per-lane frame-stack kernel takes that walk (the packet walk's
+     * registers would cost a wave per SIMD).  CRT_SECONDARY / "secondary"
+     * overrides the secondary walk. */
+    const bool pruned = sc->traversal >= 8;
+    int sec = sc->secondary;
+    if (sec == 0) sec = gi ? 4 : (pruned ? 10 : 5);
+    const bool packet = sc->traversal >= 6 && sc->traversal <= 8;
+    if (full && !gi && sc->wavefront && packet && !stamps)
+        return render_wavefront(sc, ds, plan, d_out, stream, count, d_scene, sec, pruned ? 8 : 7);
+    /* frame-stack kernel: one walk for every ray (packet walks hand over to sec) */
+    const int trav = full ? (packet ? sec : sc->traversal) : sc->traversal;
     const int blocks = (plan.ntiles + 3) / 4;
     const uint64_t frames = (uint64_t)st->max_ray_depth + 1;
     unsigned long long *cnt = sc->d_counters;
-#define CRT_LAUNCH_T(FULL, MAXF, TRAV, SEC, COUNT)                                                          \
-    hipLaunchKernelGGL((k_render_tiles<FULL, MAXF, TRAV, SEC, COUNT>), dim3(blocks), dim3(256), 0, stream,       \
+#define CRT_LAUNCH_T(FULL, MAXF, TRAV, COUNT)                                                               \
+    hipLaunchKernelGGL((k_render_tiles<FULL, MAXF, TRAV, TRAV, COUNT>), dim3(blocks), dim3(256), 0, stream,      \
                        d_scene, ds, plan.d_tiles, plan.ntiles, d_out, cnt, stamps)
-#define CRT_LAUNCH_NF(TRAV, COUNT) CRT_LAUNCH_T(false, 0, TRAV, TRAV, COUNT)
-#define CRT_LAUNCH_F(MAXF, TRAV, COUNT)                                                                      \
-    do {                                                                                                   \
-        if (sec == 4) CRT_LAUNCH_T(true, MAXF, TRAV, 4, COUNT);                                            \
-        else CRT_LAUNCH_T(true, MAXF, TRAV, 5, COUNT);                                                      \
-    } while (0)
-#define CRT_LAUNCH(FULL, MAXF, COUNT, PACKET)                                                               \
+#define CRT_LAUNCH(FULL, MAXF, COUNT)                                                                       \
     do {                                                                                                   \
         switch (trav) {                                                                                    \
-        case 0: CRT_LAUNCH_T(FULL, MAXF, 0, 0, COUNT); break;                                              \
-        case 3: CRT_LAUNCH_T(FULL, MAXF, 3, 3, COUNT); break;                                              \
-        case 4: CRT_LAUNCH_T(FULL, MAXF, 4, 4, COUNT); break;                                              \
-        case 5: CRT_LAUNCH_T(FULL, MAXF, 5, 5, COUNT); break;                                              \
-        case 6: PACKET(6); break;                                                                          \
-        default: PACKET(7); break;                                                                         \
+        case 0: CRT_LAUNCH_T(FULL, MAXF, 0, COUNT); break;                                                 \
+        case 3: CRT_LAUNCH_T(FULL, MAXF, 3, COUNT); break;                                                 \
+        case 4: CRT_LAUNCH_T(FULL, MAXF, 4, COUNT); break;                                                 \
+        case 5: CRT_LAUNCH_T(FULL, MAXF, 5, COUNT); break;                                                 \
+        case 9: CRT_LAUNCH_T(FULL, MAXF, 9, COUNT); break;                                                 \
+        case 10: CRT_LAUNCH_T(FULL, MAXF, 10, COUNT); break;                                               \
+        case 11: CRT_LAUNCH_T(FULL, MAXF, 11, COUNT); break;                                               \
+        default: return set_error(CRT_E_INVALID, "no such walk for this kernel");                         \
         }                                                                                                  \
     } while (0)
-#define CRT_NF_T(T) CRT_LAUNCH_NF(T, true)
-#define CRT_NF_F(T) CRT_LAUNCH_NF(T, false)
-#define CRT_F4_T(T) CRT_LAUNCH_F(4, T, true)
-#define CRT_F4_F(T) CRT_LAUNCH_F(4, T, false)
-#define CRT_F16_T(T) CRT_LAUNCH_F(16, T, true)
-#define CRT_F16_F(T) CRT_LAUNCH_F(16, T, false)
-#define CRT_F64_T(T) CRT_LAUNCH_F(64, T, true)
-#define CRT_F64_F(T) CRT_LAUNCH_F(64, T, false)
-    /* secondary rays (recursion, GI) scatter: the packet walks hand them to a
-     * per-lane walk — cooperative range donation for GI fan-out, range sharing
-     * otherwise (env CRT_SECONDARY = 4 | 5) */
     if (!full) {
-        if (count) CRT_LAUNCH(false, 0, true, CRT_NF_T); else CRT_LAUNCH(false, 0, false, CRT_NF_F);
+        switch (trav) {
+        case 6: if (count) CRT_LAUNCH_T(false, 0, 6, true); else CRT_LAUNCH_T(false, 0, 6, false); break;
+        case 7: if (count) CRT_LAUNCH_T(false, 0, 7, true); else CRT_LAUNCH_T(false, 0, 7, false); break;
+        case 8: if (count) CRT_LAUNCH_T(false, 0, 8, true); else CRT_LAUNCH_T(false, 0, 8, false); break;
+        default: if (count) CRT_LAUNCH(false, 0, true); else CRT_LAUNCH(false, 0, false); break;
+        }
     } else if (frames <= 4) {
-        if (count) CRT_LAUNCH(true, 4, true, CRT_F4_T); else CRT_LAUNCH(true, 4, false, CRT_F4_F);
+        if (count) CRT_LAUNCH(true, 4, true); else CRT_LAUNCH(true, 4, false);
     } else if (frames <= 16) {
-        if (count) CRT_LAUNCH(true, 16, true, CRT_F16_T); else CRT_LAUNCH(true, 16, false, CRT_F16_F);
+        if (count) CRT_LAUNCH(true, 16, true); else CRT_LAUNCH(true, 16, false);
     } else if (frames <= 64) {
-        if (count) CRT_LAUNCH(true, 64, true, CRT_F64_T); else CRT_LAUNCH(true, 64, false, CRT_F64_F);
+        if (count) CRT_LAUNCH(true, 64, true); else CRT_LAUNCH(true, 64, false);
     } else {
         return set_error(CRT_E_UNSUPPORTED, "max_ray_depth > 63 with recursive materials is not supported");
     }
 #undef CRT_LAUNCH
-#undef CRT_LAUNCH_NF
-#undef CRT_LAUNCH_F
 #undef CRT_LAUNCH_T
-#undef CRT_NF_T
-#undef CRT_NF_F
-#undef CRT_F4_T
-#undef CRT_F4_F
-#undef CRT_F16_T
-#undef CRT_F16_F
-#undef CRT_F64_T
-#undef CRT_F64_F
     HIP_TRY(hipGetLastError());
     return CRT_OK;
 }
@@ -1580,8 +1937,10 @@ int render_into(crt_hip_scene *sc, const crt_renderer_settings *st, float *d_rgb
         HIP_TRY(hipMemsetAsync(d_rgb, 0, (size_t)sc->info.width * sc->info.height * 3 * sizeof(float), stream));
         return CRT_OK;
     }
+    int rc = ensure_plans(sc, st, stream);
+    if (rc != CRT_OK) return rc;
     HIP_TRY(hipEventRecord(sc->ev_start, stream));
-    int rc = launch_render(sc, st, sc->full, d_rgb, stream, count);
+    rc = launch_render(sc, st, sc->full, d_rgb, stream, count);
     if (rc != CRT_OK) return rc;
     HIP_TRY(hipEventRecord(sc->ev_stop, stream));
     return CRT_OK;
@@ -1605,6 +1964,10 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     if (const char *e = std::getenv("CRT_TILE_ORDER")) sc->tile_order = std::atoi(e);
     if (const char *e = std::getenv("CRT_SECONDARY")) sc->secondary = std::atoi(e);
     if (const char *e = std::getenv("CRT_WAVEFRONT")) sc->wavefront = std::atoi(e);
+    if (const char *e = std::getenv("CRT_TRACE_WALK")) sc->trace_walk = std::atoi(e);
+    if (const char *e = std::getenv("CRT_CALIBRATE")) sc->calibrate = std::atoi(e);
+    if (const char *e = std::getenv("CRT_CALIB_K")) sc->calib_k = (float)std::atof(e);
+    if (const char *e = std::getenv("CRT_CALIB_MIN")) sc->calib_min = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("CRT_SPLIT")) {
         float a = 0.f, b = 0.f;
         if (std::sscanf(e, "%f,%f", &a, &b) >= 1) { sc->split4 = a; sc->split16 = b; }
@@ -1625,6 +1988,8 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     int rc;
     if ((rc = upload(sc.get(), hs.nodes, &ds.nodes)) != CRT_OK) return rc;
     ds.node_count = (int32_t)hs.nodes.size();
+    if ((rc = upload(sc.get(), hs.pnodes, &ds.pnodes)) != CRT_OK) return rc;
+    ds.prune_origin_max = hs.prune_origin_max;
     {
         auto ok = [](float x) {
             const float m = std::fabs(x);
@@ -1698,6 +2063,7 @@ void crt_hip_scene_destroy(crt_hip_scene *sc) {
     (void)hipSetDevice(sc->device);
     if (sc->stream) (void)hipStreamSynchronize(sc->stream);
     for (void *p : sc->allocs) (void)hipFree(p);
+    for (void *p : sc->plan_allocs) (void)hipFree(p);
     if (sc->d_out) (void)hipFree(sc->d_out);
     wf_free(sc->wf);
     for (auto &kv : sc->unpack_plans) (void)hipFree(kv.second.first);
@@ -1771,6 +2137,8 @@ int crt_hip_render_shard(crt_hip_scene *sc, const crt_renderer_settings *st, int
     int rc = check_settings(st);
     if (rc != CRT_OK) return rc;
     HIP_TRY(hipSetDevice(sc->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : sc->stream;
+    if ((rc = ensure_plans(sc, st, s)) != CRT_OK) return rc;
     auto key = std::make_pair(shard, shard_count);
     auto it = sc->shard_plans.find(key);
     if (it == sc->shard_plans.end()) {
@@ -1781,7 +2149,6 @@ int crt_hip_render_shard(crt_hip_scene *sc, const crt_renderer_settings *st, int
         if ((rc = make_tile_plan(sc, b, false, plan)) != CRT_OK) return rc;
         it = sc->shard_plans.emplace(key, plan).first;
     }
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : sc->stream;
     HIP_TRY(hipEventRecord(sc->ev_start, s));
     rc = launch_render(sc, st, it->second, d_packed, s, false);
     if (rc != CRT_OK) return rc;
@@ -1832,7 +2199,7 @@ int crt_hip_trace_batch(crt_hip_scene *sc, const float *rays, int64_t n, crt_hit
     e = hipMemcpy(d_rays, rays, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_trace_rays, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, sc->stream, sc->ds, d_rays,
-                           n, d_hits);
+                           n, d_hits, sc->trace_walk);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipStreamSynchronize(sc->stream);
@@ -1847,6 +2214,10 @@ int crt_hip_profile_waves(crt_hip_scene *sc, const crt_renderer_settings *st, ui
                           int32_t *tile_xy) {
     if (!sc || !st) return set_error(CRT_E_INVALID, "null argument");
     HIP_TRY(hipSetDevice(sc->device));
+    {
+        const int rc = ensure_plans(sc, st, sc->stream);
+        if (rc != CRT_OK) return rc;
+    }
     const int nt = sc->full.ntiles;
     if (!stamps || !tile_xy) return nt;      /* query the size */
     if (cap < nt) return set_error(CRT_E_INVALID, "stamp buffer too small");
@@ -1877,6 +2248,7 @@ int crt_hip_count_work(crt_hip_scene *sc, const crt_renderer_settings *st, crt_w
     if (sc->grid_empty) return CRT_OK;
     const size_t nfl = (size_t)sc->info.width * sc->info.height * 3;
     if (!sc->d_out) HIP_TRY(hipMalloc(&sc->d_out, nfl * sizeof(float)));
+    if ((rc = ensure_plans(sc, st, sc->stream)) != CRT_OK) return rc;
     HIP_TRY(hipMemsetAsync(sc->d_counters, 0, 8 * sizeof(unsigned long long), sc->stream));
     rc = launch_render(sc, st, sc->full, sc->d_out, sc->stream, true);
     if (rc != CRT_OK) return rc;
@@ -1891,6 +2263,40 @@ int crt_hip_count_work(crt_hip_scene *sc, const crt_renderer_settings *st, crt_w
     sc->wave_counts.triangle_steps = c[5];
     sc->wave_counts.edge_steps = c[6];
     sc->wave_counts.waves = c[7];
+    return CRT_OK;
+}
+
+int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
+    if (!sc || !name) return set_error(CRT_E_INVALID, "null argument");
+    const std::string k(name);
+    if (k == "traversal") {
+        if (value < 0 || value > 11 || value == 1 || value == 2) return set_error(CRT_E_INVALID, "traversal must be 0, 3..11");
+        sc->traversal = value;
+    } else if (k == "secondary") {
+        if (value != 0 && value != 4 && value != 5 && value != 9 && value != 10 && value != 11)
+            return set_error(CRT_E_INVALID, "secondary must be 0, 4, 5, 9, 10 or 11");
+        sc->secondary = value;
+    } else if (k == "wavefront") {
+        sc->wavefront = value != 0;
+    } else if (k == "calibrate") {
+        sc->calibrate = value != 0;
+        if (!sc->calibrate && sc->calib_walk >= 0) {   /* back to the estimate plan */
+            HIP_TRY(hipDeviceSynchronize());
+            sc->calib.clear();
+            sc->calib_walk = -1;
+            free_plans(sc);
+            int64_t px = 0;
+            const int rc = make_tile_plan(sc, shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size, 0, 1, &px),
+                                          true, sc->full);
+            if (rc != CRT_OK) return rc;
+        }
+    } else if (k == "trace_walk") {
+        if (value != 0 && value != 1) return set_error(CRT_E_INVALID, "trace_walk must be 0 or 1");
+        sc->trace_walk = value;
+    } else {
+        return set_error(CRT_E_INVALID, "unknown option: " + k);
+    }
+    /* tile plans depend on the walk (tile splitting): rebuild on next use */
     return CRT_OK;
 }
 

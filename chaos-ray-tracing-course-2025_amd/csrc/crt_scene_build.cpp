@@ -137,6 +137,165 @@ void build_tree(const std::vector<Box6> &tri_boxes, const Box6 &root_box, std::v
     }
 }
 
+/* ---- pruned-walk structures (crt_layout.h PNode) ------------------------
+ *
+ * Why a hull can bound the t the reference computes.  ray_intersect_triangle
+ * (crt_intersection.cpp:47-93) accepts t = fl(op / rn) when the rounded
+ * point p = o + d*t passes the three rounded edge tests.  With q = o + d*t in
+ * exact arithmetic (the point the hull test sees):
+ *   - height of q above the plane through v0 with normal N:
+ *       N.(q - v0) = t*rn_exact - op_exact, and t*rn_computed = op_computed(1+e),
+ *     so the height is a few ulps of |o|, |v0| and |q - o| — the division's
+ *     error moves q along the (near-parallel) plane, not away from it;
+ *   - in the plane, each rounded edge test admits points at most a few ulps of
+ *     |p - v_i| outside its edge line; the three shifted lines bound the
+ *     triangle scaled about its incentre, whose corners move by that shift
+ *     times diam/inradius (slivers get wide margins).
+ * So q lies within c * 2^-24 * (diam * kappa + |o| + |v| + |q|) of the
+ * triangle's box, kappa = diam / inradius, c a small constant (< 100).  The
+ * hull below uses 2^-14 * (diam * kappa + 2 G) for rays with |o|_inf <= G,
+ * G = 4 max |vertex coordinate| — a margin of 2^10 over that bound — and the
+ * device's slab test (rcp, one rounding per product) adds errors far below
+ * it.  Triangles whose normal is not finite or whose area is 0 (no reliable
+ * bound) get an unbounded hull: their subtrees are never pruned. */
+inline float round_down(double v) {
+    float f = (float)v;
+    if ((double)f > v) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+    return f;
+}
+inline float round_up(double v) {
+    float f = (float)v;
+    if ((double)f < v) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+    return f;
+}
+
+struct HullD { double lo[3], hi[3]; };
+
+HullD triangle_hull(const float *a, const float *b, const float *c, const float *fn, double G) {
+    const double inf = std::numeric_limits<double>::infinity();
+    HullD h{{-inf, -inf, -inf}, {inf, inf, inf}};
+    bool finite = std::isfinite(fn[0]) && std::isfinite(fn[1]) && std::isfinite(fn[2]);
+    for (int k = 0; k < 3; ++k) finite = finite && std::isfinite(a[k]) && std::isfinite(b[k]) && std::isfinite(c[k]);
+    if (!finite) return h;
+    double e[3][3];
+    for (int k = 0; k < 3; ++k) {
+        e[0][k] = (double)b[k] - a[k];
+        e[1][k] = (double)c[k] - b[k];
+        e[2][k] = (double)a[k] - c[k];
+    }
+    double len[3];
+    for (int i = 0; i < 3; ++i) len[i] = std::sqrt(e[i][0] * e[i][0] + e[i][1] * e[i][1] + e[i][2] * e[i][2]);
+    const double cx = e[0][1] * (-e[2][2]) - e[0][2] * (-e[2][1]);
+    const double cy = e[0][2] * (-e[2][0]) - e[0][0] * (-e[2][2]);
+    const double cz = e[0][0] * (-e[2][1]) - e[0][1] * (-e[2][0]);
+    const double area2 = std::sqrt(cx * cx + cy * cy + cz * cz);   /* 2 * area */
+    const double perim = len[0] + len[1] + len[2];
+    if (!(area2 > 0.0) || !(perim > 0.0)) return h;
+    const double inradius = area2 / perim;
+    const double diam = std::max(len[0], std::max(len[1], len[2]));
+    const double kappa = diam / inradius;
+    const double eta = std::ldexp(diam * kappa + 2.0 * G, -14);
+    if (!std::isfinite(eta)) return h;
+    for (int k = 0; k < 3; ++k) {
+        const double lo = std::min((double)a[k], std::min((double)b[k], (double)c[k]));
+        const double hi = std::max((double)a[k], std::max((double)b[k], (double)c[k]));
+        h.lo[k] = lo - eta;
+        h.hi[k] = hi + eta;
+    }
+    return h;
+}
+
+void build_pruned_nodes(const std::vector<BuildNode> &bn, HostScene &hs) {
+    const int32_t n = (int32_t)bn.size();
+    double vmax = 0.0;
+    for (float v : hs.vpos)
+        if (std::isfinite(v)) vmax = std::max(vmax, (double)std::fabs(v));
+    const double G = 4.0 * vmax;
+    hs.prune_origin_max = (float)G;   /* rounding down is harmless: rays above it are not pruned */
+    if ((double)hs.prune_origin_max > G) hs.prune_origin_max = round_down(G);
+
+    const size_t nt = hs.tri_attr.size();
+    std::vector<HullD> th(nt);
+    for (size_t t = 0; t < nt; ++t) {
+        const DTriAttr &at = hs.tri_attr[t];
+        th[t] = triangle_hull(&hs.vpos[3 * (size_t)at.i0], &hs.vpos[3 * (size_t)at.i1], &hs.vpos[3 * (size_t)at.i2],
+                              &hs.face_normal[3 * t], G);
+    }
+    /* children are numbered after their parent (build_tree), so a reverse
+     * sweep sees both children before the parent */
+    const double inf = std::numeric_limits<double>::infinity();
+    std::vector<HullD> hull((size_t)n, HullD{{inf, inf, inf}, {-inf, -inf, -inf}});
+    for (int32_t x = n - 1; x >= 0; --x) {
+        HullD &h = hull[x];
+        auto merge = [&](const HullD &o) {
+            for (int k = 0; k < 3; ++k) {
+                h.lo[k] = std::min(h.lo[k], o.lo[k]);
+                h.hi[k] = std::max(h.hi[k], o.hi[k]);
+            }
+        };
+        if (!bn[x].tris.empty()) {
+            for (int32_t t : bn[x].tris) merge(th[t]);
+        } else {
+            for (int c = 0; c < 2; ++c)
+                if (bn[x].child[c] != -1) merge(hull[bn[x].child[c]]);
+        }
+    }
+    std::vector<int32_t> subtree((size_t)n, 1);
+    for (int32_t x = n - 1; x >= 0; --x)
+        if (bn[x].tris.empty())
+            for (int c = 0; c < 2; ++c)
+                if (bn[x].child[c] != -1) subtree[x] += subtree[bn[x].child[c]];
+    /* leaf slot ranges follow the reference's order (prepare_scene's flatten) */
+    std::vector<int32_t> first_slot((size_t)n, -1);
+    {
+        std::vector<int32_t> st{0};
+        int32_t next = 0;
+        while (!st.empty()) {
+            const int32_t x = st.back();
+            st.pop_back();
+            if (!bn[x].tris.empty()) {
+                first_slot[x] = next;
+                next += (int32_t)bn[x].tris.size();
+            } else {
+                if (bn[x].child[0] != -1) st.push_back(bn[x].child[0]);
+                if (bn[x].child[1] != -1) st.push_back(bn[x].child[1]);
+            }
+        }
+    }
+    hs.pnodes.assign((size_t)8 * n, PNode{});
+    std::vector<int32_t> st;
+    for (int oct = 0; oct < 8; ++oct) {
+        PNode *out = hs.pnodes.data() + (size_t)oct * n;
+        int32_t k = 0;
+        st.assign(1, 0);
+        while (!st.empty()) {
+            const int32_t x = st.back();
+            st.pop_back();
+            PNode &o = out[k];
+            o.lo_x = bn[x].bounds.lo[0]; o.lo_y = bn[x].bounds.lo[1]; o.lo_z = bn[x].bounds.lo[2];
+            o.hi_x = bn[x].bounds.hi[0]; o.hi_y = bn[x].bounds.hi[1]; o.hi_z = bn[x].bounds.hi[2];
+            o.tlo_x = round_down(hull[x].lo[0]); o.tlo_y = round_down(hull[x].lo[1]); o.tlo_z = round_down(hull[x].lo[2]);
+            o.thi_x = round_up(hull[x].hi[0]); o.thi_y = round_up(hull[x].hi[1]); o.thi_z = round_up(hull[x].hi[2]);
+            o.depth = bn[x].depth;
+            o.count = (int32_t)bn[x].tris.size();
+            if (bn[x].tris.empty()) {
+                o.a = k + subtree[x];
+                o.b = -(bn[x].depth + 1);
+                /* near child first: on a negative direction along the split
+                 * axis the upper half (child1) is entered first */
+                const bool neg = ((oct >> (bn[x].depth % 3)) & 1) != 0;
+                const int32_t near_c = bn[x].child[neg ? 1 : 0], far_c = bn[x].child[neg ? 0 : 1];
+                if (far_c != -1) st.push_back(far_c);
+                if (near_c != -1) st.push_back(near_c);
+            } else {
+                o.a = (int32_t)bn[x].tris.size() | (bn[x].depth << 24);
+                o.b = first_slot[x];
+            }
+            ++k;
+        }
+    }
+}
+
 }  // namespace
 
 int prepare_scene(const crt_scene_desc *d, HostScene &hs) {
@@ -366,6 +525,7 @@ int prepare_scene(const crt_scene_desc *d, HostScene &hs) {
     if (hs.slots.size() > (size_t)std::numeric_limits<int32_t>::max())
         return set_error(CRT_E_UNSUPPORTED, "too many leaf triangle copies");
     (void)pos;
+    build_pruned_nodes(bn, hs);
     return CRT_OK;
 }
 

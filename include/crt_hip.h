@@ -235,6 +235,16 @@ typedef struct crt_wave_counts {
 } crt_wave_counts;
 int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
 
+/* Walk selection (results are identical for every walk; work and speed
+ * differ).  Names: "traversal" (primary-ray walk: 7 = reference-order packet
+ * walk, whose work counters equal the reference's; 8 = pruned packet walk,
+ * default; 0..6, 9 = other variants), "secondary" (0 = by walk, 4, 5, 9),
+ * "wavefront" (0/1: level-by-level recursion when GI is off), "trace_walk"
+ * (crt_hip_trace_batch: 0 = reference order, 1 = pruned per-ray walk).
+ * Environment variables CRT_TRAVERSAL, CRT_SECONDARY, CRT_WAVEFRONT and
+ * CRT_TRACE_WALK set the initial values. */
+int  crt_hip_scene_set_option(crt_hip_scene *scene, const char *name, int value);
+
 /* Diagnostics: render one full frame with per-wave s_memrealtime stamps
  * (100 MHz ticks; stamps = 2 per 8x8 tile: start, end; tile_xy = tile origin,
  * in dispatch order).  With NULL buffers returns the tile count. */

@@ -49,13 +49,14 @@ TRACE_SCENES = [
 ]
 
 
+@pytest.mark.parametrize("walk", [0, 1], ids=["reference-order", "pruned"])
 @pytest.mark.parametrize("name,w,h", TRACE_SCENES)
-def test_trace_batch_bit_exact(N, oracle, name, w, h):
+def test_trace_batch_bit_exact(N, oracle, name, w, h, walk):
     sc = scene_npz(name).set_resolution(w, h)
     orc = oracle.OracleScene(sc)
     rays = camera_and_random_rays(orc, w, h)
     ref_hits, _, _ = orc.trace(rays)
-    gpu = N.HipScene(sc)
+    gpu = N.HipScene(sc, trace_walk=walk)
     got = gpu.trace(rays)
     ok, first, nbad = hits_equal(got, ref_hits)
     assert ok, f"{name}: {nbad} rays differ, first {first}: gpu={got[first]} oracle={ref_hits[first]}"
@@ -103,13 +104,52 @@ def test_c2_full_frame_bit_exact(N, oracle):
 
 
 def test_work_counts_match_oracle(N, oracle):
+    """The reference-order walks (traversal 7: packet camera rays, range sharing
+    for secondaries) test exactly the reference's nodes and triangles."""
     from crt_amd.native import WorkCounts
     sc = scene_npz("11-01-refractive__scene8").set_resolution(160, 90)
     st = N.RendererSettings.default(max_ray_depth=8)
     wc = WorkCounts()
     oracle.OracleScene(sc).render(st, counts=wc)
-    got = N.HipScene(sc).count_work(st)
+    got = N.HipScene(sc, traversal=7).count_work(st)
     assert got == wc.as_dict()
+
+
+@pytest.mark.parametrize("name,w,h,over", [
+    ("14-01-acceleration-tree__scene1", 480, 270, {}),
+    ("11-01-refractive__scene8", 240, 135, {"max_ray_depth": 8}),
+    ("15-01-conclusion__scene2", 64, 64, {}),
+])
+def test_pruned_walks_equal_reference_walks(N, oracle, name, w, h, over):
+    """Pruned walks (default) vs reference-order walks: same image bits, same
+    traversal and hit counts, fewer node and triangle tests."""
+    from crt_amd.native import WorkCounts
+    sc = scene_npz(name).set_resolution(w, h)
+    st = N.RendererSettings.default(**over)
+    fast = N.HipScene(sc, traversal=8, secondary=10)   # GI frames default to walk 4; force the pruned one
+    ref = N.HipScene(sc, traversal=7)
+    a, b = fast.render(st), ref.render(st)
+    assert np.array_equal(bits(a), bits(b))
+    ca, cb = fast.count_work(st), ref.count_work(st)
+    wc = WorkCounts()
+    oracle.OracleScene(sc).render(st, counts=wc)
+    assert cb == wc.as_dict()
+    assert ca["traversals"] == cb["traversals"] and ca["hits"] == cb["hits"]
+    assert ca["node_tests"] < cb["node_tests"] and ca["triangle_tests"] < cb["triangle_tests"]
+
+
+def test_pruned_synthetic_bit_exact(N, oracle):
+    """C5-style random mesh (deep tree): pruned render equals the oracle."""
+    from crt_amd.synthetic import c5_scene
+    sc = c5_scene(50_000, 160, 90)
+    st = N.RendererSettings.default()
+    want = oracle.OracleScene(sc).render(st)
+    gpu = N.HipScene(sc)
+    got = gpu.render(st)
+    assert np.array_equal(bits(got), bits(want))
+    c = gpu.count_work(st)
+    r = N.HipScene(sc, traversal=7).count_work(st)
+    assert c["hits"] == r["hits"] and c["node_tests"] * 2 < r["node_tests"]
 
 
 @pytest.mark.parametrize("shards", [1, 2, 3, 8])
