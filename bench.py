@@ -8,11 +8,18 @@ crt_renderer.cpp:29-44), so rays = traversals = 2,073,600 per frame; the count
 is re-measured by the instrumented kernel, not assumed.
 
 N=1: the frame is rendered into HBM (scene + image resident; no PCIe in the
-timed region).  N>1 (one process per GPU, torchrun): the reference's bucket
-grid is dealt round-robin to ranks, each rank renders its buckets packed, and
-the tiles are gathered to rank 0 over RCCL (torch.distributed "nccl") and
-unpacked there — one frame per step, strong scaling; frame k's gather runs on
-RCCL's stream while frame k+1 renders (double-buffered, FramePipeline).
+timed region).  N>1 (one process per GPU, torchrun), two modes:
+
+  --mode frames (default, weak scaling): every rank renders its own whole
+      frame per step into its own HBM (frame-parallel rendering of a frame
+      sequence: per-GPU work fixed, no data-path collective — pixels never need
+      to meet); value = all ranks' rays / the slowest rank's time.
+  --mode tiles (strong scaling, the north_star's image-tile sharding): the
+      reference's bucket grid is dealt round-robin to ranks, each rank renders
+      its buckets packed, the tiles are gathered to rank 0 over RCCL
+      (torch.distributed "nccl") and unpacked there — one frame per step;
+      frame k's gather runs on RCCL's stream while frame k+1 renders
+      (double-buffered, FramePipeline).
 
 Also reported: the roofline of the render kernel (algorithmic bytes per launch
 ÷ measured kernel time vs 8 TB/s HBM) and the CPU oracle (restatement of the
@@ -55,6 +62,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
     p.add_argument("--check", action="store_true", help="rank 0: compare the last frame with a 1-GPU render")
+    p.add_argument("--mode", choices=["frames", "tiles"], default="frames",
+                   help="N>1: frames = each GPU renders whole frames (weak scaling, default); "
+                        "tiles = one frame sharded over the GPUs + RCCL gather (strong scaling)")
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                    help="per-launch HBM bytes measured by rocprofv3 --pmc (profiles/), if present")
     return p.parse_args()
@@ -133,20 +143,21 @@ def main():
             ev[timing["i"]][1].record(stream)
             timing["i"] += 1
 
-    if world > 1:
+    tiles = world > 1 and a.mode == "tiles"
+    if tiles:
         # frame k's RCCL gather overlaps frame k+1's shard render (crt_amd.distributed.FramePipeline)
         pipe = FramePipeline(rank, world, gpu.shard_stride(world),
                              lambda n: torch.empty(n, dtype=torch.float32, device="cuda"), render_shard,
                              lambda flat: gpu.unpack_shards(world, flat.data_ptr(), frame.data_ptr(), sptr), dist)
 
     def step():
-        if world == 1:
-            render_full()
-        else:
+        if tiles:
             pipe.step()
+        else:
+            render_full()
 
     def drain():
-        if world > 1:
+        if tiles:
             pipe.drain()
 
     # work counters of one full frame (outside the timed region)
@@ -176,7 +187,7 @@ def main():
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
 
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda" if a.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 
@@ -189,10 +200,11 @@ def main():
             raise SystemExit(1)
 
     ms_per_step = elapsed / a.steps * 1e3
-    mrays = rays_per_frame * a.steps / elapsed / 1e6
+    frames_per_step = world if (world > 1 and not tiles) else 1
+    mrays = rays_per_frame * frames_per_step * a.steps / elapsed / 1e6
 
     # roofline of the render kernel: algorithmic bytes of one launch / its duration
-    shard_frac = 1.0 / world
+    shard_frac = 1.0 / world if tiles else 1.0
     alg_bytes = (NODE_BYTES * counts["node_tests"] + TRI_BYTES * counts["triangle_tests"]
                  + PIXEL_BYTES * W * H) * shard_frac
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
@@ -218,7 +230,7 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong" if tiles else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "scene file scenes/14-01-acceleration-tree/scene1.crtscene (parsed fixture tests/golden/scenes)",
@@ -226,7 +238,9 @@ def main():
                                    f"(max_ray_depth 3), primary rays (HEAD traces no shadow rays)",
                        "rays_per_frame": rays_per_frame, "node_tests_per_frame": counts["node_tests"],
                        "triangle_tests_per_frame": counts["triangle_tests"],
-                       "parallelism": f"bucket-shard{world}" if world > 1 else "single-gpu",
+                       "parallelism": (f"bucket-shard{world}+rccl-gather" if tiles else
+                                       f"frame-parallel{world}" if world > 1 else "single-gpu"),
+                       "frames_per_step": frames_per_step,
                        "frame_ms": round(ms_per_step, 5), "kernel_ms": round(kern_ms, 5)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic},

@@ -19,7 +19,7 @@ run() {
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-STEPS=${STEPS:-tests,smoke,bench,prof,pmc}
+STEPS=${STEPS:-tests,smoke,bench,prof,pmc,rehearse}
 [[ $STEPS == *tests* ]] && run pytest_gpu 900 python -m pytest tests -m gpu -q -rf
 [[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
 [[ $STEPS == *bench* ]] && run bench 600 python bench.py
@@ -30,4 +30,6 @@ if [[ $STEPS == *pmc* ]]; then
   run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc/fetch" -o run --output-format csv -- python3 scripts/render_loop.py --frames 3
   run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc/write" -o run --output-format csv -- python3 scripts/render_loop.py --frames 3
 fi
+# N=2 rehearsal on the one GPU (two ranks share cuda:0; gloo, so no RCCL duplicate-device refusal)
+[[ $STEPS == *rehearse* ]] && run rehearse2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 20 --warmup 3 --backend gloo
 exit 0
