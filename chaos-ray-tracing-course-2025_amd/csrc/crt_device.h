@@ -228,6 +228,17 @@ CRT_HD float axis_margin(f2 pl, float o_a, float d_a, float y1, float gate, floa
  * exact; other rays take the compiler's '/' and the plain compares). */
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"   /* no short-circuit: one branch-free OR */
+/* The fast-ray form alone (caller guarantees r.fast for every lane it uses). */
+CRT_HD bool box_hit_fast(Vec o, Vec d, const RayRcp &r, const DNode n) {
+    const float mx = axis_margin((f2){n.lo_x, n.hi_x}, o.x, d.x, r.y1[0], r.gate[0], o.y, d.y, o.z, d.z, n.lo_y,
+                                 n.hi_y, n.lo_z, n.hi_z);
+    const float my = axis_margin((f2){n.lo_y, n.hi_y}, o.y, d.y, r.y1[1], r.gate[1], o.z, d.z, o.x, d.x, n.lo_z,
+                                 n.hi_z, n.lo_x, n.hi_x);
+    const float mz = axis_margin((f2){n.lo_z, n.hi_z}, o.z, d.z, r.y1[2], r.gate[2], o.x, d.x, o.y, d.y, n.lo_x,
+                                 n.hi_x, n.lo_y, n.hi_y);
+    return fmaxf(fmaxf(mx, my), mz) >= 0.0f;
+}
+
 CRT_HD bool box_hit_r(Vec o, Vec d, const RayRcp &r, const DNode n) {
     if (r.fast) {
         const float mx = axis_margin((f2){n.lo_x, n.hi_x}, o.x, d.x, r.y1[0], r.gate[0], o.y, d.y, o.z, d.z, n.lo_y,

@@ -700,15 +700,22 @@ __device__ int trace_packet(const DeviceScene &s, bool active, Vec o, Vec d, flo
  * the key (t, slot), which equals the reference's first-found rule in any
  * visit order; every lane still tests its reference-eligible leaves only
  * (a lane enters a node iff its ancestors' cells passed for its ray). */
-template <bool COUNT>
-__device__ int trace_packet_pruned(const DeviceScene &s, bool active, Vec o, Vec d, float &best_t, LaneCounts &c) {
+/* Exact box test for rays outside the hoisted-division window (crt_device.h
+ * coord_ok) — out of line, so the packet walk's registers are sized for the
+ * fast path; camera rays of every course scene take the fast path. */
+__device__ __noinline__ bool box_hit_slow(Vec o, Vec d, const DNode n) {
+    const RayRcp r = make_ray_rcp(o, d, false);
+    return box_hit_r(o, d, r, n);
+}
+
+template <bool COUNT, bool FAST>
+__device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool active, Vec o, Vec d,
+                                                     const RayRcp &rr, float &best_t, LaneCounts &c) {
     int best = -1;
     best_t = 0.0f;
     float lim = INFINITY;
-    const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
     const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
     unsigned long long reach = active ? 1ull : 0ull;
-    if (COUNT && active) ++c.traversals;
     const int n = s.node_count;
     const int last = n - 1;
     const int na = __popcll(__ballot(active));
@@ -720,7 +727,9 @@ __device__ int trace_packet_pruned(const DeviceScene &s, bool active, Vec o, Vec
     /* The walk is a chain of dependent scalar loads (next index comes from the
      * current record), so each step issues the loads of both possible
      * successors — i+1 (descend / after a leaf) and the skip target — before
-     * it tests the current node; the whole 64-B record is read up front. */
+     * it tests the current node; the whole 64-B record is read up front.
+     * Predicates are combined without short-circuit so the only branches are
+     * wave-uniform (no exec-mask save/restore). */
     int i = 0;
     PNode cur = load_scalar(nodes, 0);
     while (i < n) {
@@ -735,7 +744,10 @@ __device__ int trace_packet_pruned(const DeviceScene &s, bool active, Vec o, Vec
         if (COUNT) ++c.wave_nodes;
         bool pass = false;
         if (__ballot(alive) != 0ull) {
-            pass = alive && box_hit_r(o, d, rr, cell_of(cur));
+            pass = alive & box_hit_fast(o, d, rr, cell_of(cur));
+            if (!FAST && __ballot(alive & !rr.fast) != 0ull) {
+                if (alive & !rr.fast) pass = box_hit_slow(o, d, cell_of(cur));
+            }
             if (COUNT && alive) ++c.nodes;
         }
         const unsigned long long pm = __ballot(pass);
@@ -764,13 +776,15 @@ __device__ int trace_packet_pruned(const DeviceScene &s, bool active, Vec o, Vec
                 float t;
                 if (COUNT && pass) ++c.tris;
                 if (COUNT) ++c.wave_tris;
-                const bool pre = pass && tri_plane(o, d, g, cull, t) && key_better(t, slot, best_t, best);
-                const bool any = __ballot(pre) != 0ull;
-                if (COUNT && any) ++c.wave_edges;
-                if (any && pre && tri_edges(o, d, g, t)) {
-                    best_t = t;
-                    best = slot;
-                    lim = t;
+                const bool plane = tri_plane(o, d, g, cull, t);
+                const bool better = (best < 0) | (t < best_t) | ((t == best_t) & (slot < best));
+                const bool pre = pass & plane & better;
+                if (__ballot(pre) != 0ull) {
+                    if (COUNT) ++c.wave_edges;
+                    const bool hit = pre & tri_edges(o, d, g, t);
+                    best_t = hit ? t : best_t;
+                    best = hit ? slot : best;
+                    lim = hit ? t : lim;
                 }
                 g = gn;
                 cw = cwn;
@@ -779,6 +793,17 @@ __device__ int trace_packet_pruned(const DeviceScene &s, bool active, Vec o, Vec
         i = i + 1;
         cur = n1;
     }
+    return best;
+}
+
+/* FAST (walk 12, picked by the host): every camera ray of the frame is in the
+ * hoisted-division window (camera_rays_fast), so the out-of-line exact box
+ * path is not compiled in — 77 instead of 82 VGPRs, 6 waves/SIMD. */
+template <bool COUNT, bool FAST>
+__device__ int trace_packet_pruned(const DeviceScene &s, bool active, Vec o, Vec d, float &best_t, LaneCounts &c) {
+    const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
+    if (COUNT && active) ++c.traversals;
+    const int best = trace_packet_pruned_t<COUNT, FAST>(s, active, o, d, rr, best_t, c);
     if (COUNT && best >= 0) ++c.hits;
     return best;
 }
@@ -811,7 +836,8 @@ __device__ __forceinline__ int trace_lane_pruned(const DeviceScene &s, bool acti
 template <int TRAV, bool COUNT>
 __device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, bool active, Vec o, Vec d, float &best_t,
                                      LaneCounts &c) {
-    if (TRAV == 8) return trace_packet_pruned<COUNT>(s, active, o, d, best_t, c);
+    if (TRAV == 8) return trace_packet_pruned<COUNT, false>(s, active, o, d, best_t, c);
+    if (TRAV == 12) return trace_packet_pruned<COUNT, true>(s, active, o, d, best_t, c);
     if (TRAV == 9) return trace_lane_pruned<COUNT>(s, active, o, d, best_t, c);
     if (TRAV == 4) return trace_coop<COUNT, false>(s, *L, active, o, d, best_t, c);
     if (TRAV == 5) return trace_share<COUNT, false>(s, *L, active, o, d, best_t, c);
@@ -1108,7 +1134,7 @@ __global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restri
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
     (void)trace<TRAV, true>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px, o, d, t, cnt);
-    constexpr bool kPacket = TRAV >= 6 && TRAV <= 8;
+    constexpr bool kPacket = (TRAV >= 6 && TRAV <= 8) || TRAV == 12;
     uint32_t c = kPacket ? cnt.wave_nodes + cnt.wave_tris + cnt.wave_edges : cnt.nodes + cnt.tris;
     for (int off = 32; off > 0; off >>= 1) {
         const uint32_t o2 = (uint32_t)__shfl_xor((int)c, off);
@@ -1458,6 +1484,7 @@ struct crt_hip_scene {
     bool grid_empty = false;
     int traversal = 8;             /* kernel walk variant, see trace<> (env CRT_TRAVERSAL) */
     int trace_walk = 1;            /* crt_hip_trace_batch: 0 reference-order walk, 1 pruned per-lane walk */
+    bool camera_fast = false;      /* every camera ray takes the fast box path (camera_rays_fast) */
     int tile_order = 1;            /* dispatch tiles by estimated work (env CRT_TILE_ORDER) */
     /* a tile is split into 4x4 (2x2) pixel waves when its work estimate exceeds
      * split4 (split16) times the mean work per resident wave slot, i.e. when it
@@ -1495,6 +1522,33 @@ int upload(crt_hip_scene *sc, const std::vector<T> &v, const T **dst, size_t pad
     sc->info.device_bytes += (int64_t)bytes;
     *dst = static_cast<const T *>(p);
     return CRT_OK;
+}
+
+/* Every camera ray of the frame takes the fast box path of make_ray_rcp:
+ * node planes and the camera origin inside the exact-division window, and
+ * d = normalize(v R) with |d_i| <= 2^20 for every pixel.  v = (dx, dy, -1),
+ * |dx| <= aspect tan(fov/2), |dy| <= tan(fov/2) (crt_camera.cpp:7-35): with R
+ * finite and bounded, w = v R is finite; with sigma_min(R) >= |det R| /
+ * |R|_F^2 far above the rounding of v R (and above 2^-50, so |w|^2 stays
+ * normal), w cannot round to 0 — then each |d_i| = |w_i| / |w| <= 1. */
+bool camera_rays_fast(const HostScene &hs, bool planes_ok) {
+    if (!planes_ok) return false;
+    for (int k = 0; k < 3; ++k)
+        if (!coord_ok(hs.cam_loc[k])) return false;
+    const double ta = std::fabs((double)hs.tan_half_fov), aa = std::fabs((double)hs.aspect) * ta;
+    if (!std::isfinite(ta) || !std::isfinite(aa) || ta > 0x1p40 || aa > 0x1p40) return false;
+    double R[9], fro = 0.0, mx = 0.0;
+    for (int k = 0; k < 9; ++k) {
+        R[k] = hs.cam_rot[k];
+        if (!std::isfinite(R[k]) || std::fabs(R[k]) > 0x1p40) return false;
+        fro += R[k] * R[k];
+        mx = std::max(mx, std::fabs(R[k]));
+    }
+    const double det = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) +
+                       R[2] * (R[3] * R[7] - R[4] * R[6]);
+    if (!(fro > 0.0)) return false;
+    const double smin = std::fabs(det) / fro;
+    return smin > 0x1p-50 && smin > 1e-4 * (2.0 + aa + ta) * mx;
 }
 
 int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool full_frame, ShardPlan &plan) {
@@ -1597,6 +1651,7 @@ int probe_tiles(crt_hip_scene *sc, const DeviceScene *d_scene, int walk, const s
         switch (walk) {
         case 6: hipLaunchKernelGGL(k_probe_tiles<6>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         case 7: hipLaunchKernelGGL(k_probe_tiles<7>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
+        case 12: hipLaunchKernelGGL(k_probe_tiles<12>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         default: hipLaunchKernelGGL(k_probe_tiles<8>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         }
         e = hipGetLastError();
@@ -1711,6 +1766,10 @@ int check_settings(const crt_renderer_settings *st) {
     return CRT_OK;
 }
 
+/* The packet walk camera rays take: walk 8 becomes its fast-only build 12
+ * when the host has proven every camera ray fast. */
+int camera_walk(const crt_hip_scene *sc, int trav) { return (trav == 8 && sc->camera_fast) ? 12 : trav; }
+
 /* The primary walk a tile plan is measured with (-1: keep the estimate plan):
  * camera rays of diffuse frames and level 0 of the wavefront recursion. */
 int plan_walk(const crt_hip_scene *sc, const crt_renderer_settings *st) {
@@ -1718,8 +1777,8 @@ int plan_walk(const crt_hip_scene *sc, const crt_renderer_settings *st) {
     const bool full = gi || sc->has_secondary;
     const bool packet = sc->traversal >= 6 && sc->traversal <= 8;
     if (gi || !packet) return -1;
-    if (full) return sc->wavefront ? (sc->traversal == 8 ? 8 : 7) : -1;
-    return sc->traversal;
+    if (full) return sc->wavefront ? camera_walk(sc, sc->traversal == 8 ? 8 : 7) : -1;
+    return camera_walk(sc, sc->traversal);
 }
 
 /* Calibrate the tile plan for this frame's primary walk once (see
@@ -1811,7 +1870,9 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
 #define CRT_WF0(T, COUNT)                                                                                   \
     hipLaunchKernelGGL((k_wf_level<T, true, COUNT>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,      \
                        plan.d_tiles, plan.ntiles, lv, cnt)
-    if (primary == 8) {
+    if (primary == 12) {
+        if (count) CRT_WF0(12, true); else CRT_WF0(12, false);
+    } else if (primary == 8) {
         if (count) CRT_WF0(8, true); else CRT_WF0(8, false);
     } else {
         if (count) CRT_WF0(7, true); else CRT_WF0(7, false);
@@ -1886,9 +1947,9 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     if (sec == 0) sec = gi ? 4 : (pruned ? 10 : 5);
     const bool packet = sc->traversal >= 6 && sc->traversal <= 8;
     if (full && !gi && sc->wavefront && packet && !stamps)
-        return render_wavefront(sc, ds, plan, d_out, stream, count, d_scene, sec, pruned ? 8 : 7);
+        return render_wavefront(sc, ds, plan, d_out, stream, count, d_scene, sec, camera_walk(sc, pruned ? 8 : 7));
     /* frame-stack kernel: one walk for every ray (packet walks hand over to sec) */
-    const int trav = full ? (packet ? sec : sc->traversal) : sc->traversal;
+    const int trav = full ? (packet ? sec : sc->traversal) : camera_walk(sc, sc->traversal);
     const int blocks = (plan.ntiles + 3) / 4;
     const uint64_t frames = (uint64_t)st->max_ray_depth + 1;
     unsigned long long *cnt = sc->d_counters;
@@ -1913,6 +1974,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         case 6: if (count) CRT_LAUNCH_T(false, 0, 6, true); else CRT_LAUNCH_T(false, 0, 6, false); break;
         case 7: if (count) CRT_LAUNCH_T(false, 0, 7, true); else CRT_LAUNCH_T(false, 0, 7, false); break;
         case 8: if (count) CRT_LAUNCH_T(false, 0, 8, true); else CRT_LAUNCH_T(false, 0, 8, false); break;
+        case 12: if (count) CRT_LAUNCH_T(false, 0, 12, true); else CRT_LAUNCH_T(false, 0, 12, false); break;
         default: if (count) CRT_LAUNCH(false, 0, true); else CRT_LAUNCH(false, 0, false); break;
         }
     } else if (frames <= 4) {
@@ -1999,6 +2061,8 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
         for (const DNode &n : hs.nodes)
             if (!(ok(n.lo_x) && ok(n.lo_y) && ok(n.lo_z) && ok(n.hi_x) && ok(n.hi_y) && ok(n.hi_z))) ds.planes_ok = 0;
     }
+    sc->camera_fast = camera_rays_fast(hs, ds.planes_ok != 0);
+    if (const char *e = std::getenv("CRT_CAMERA_FAST")) sc->camera_fast = sc->camera_fast && std::atoi(e) != 0;
     if ((rc = upload(sc.get(), hs.slots, &ds.slots)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.slot_tri, &ds.slot_tri)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.slot_cull, &ds.slot_cull)) != CRT_OK) return rc;
