@@ -160,6 +160,7 @@ EXPORTS = [
     ("crt_hip_wave_counts", C.c_int, [_P, C.POINTER(WaveCounts)]),
     ("crt_hip_scene_set_option", C.c_int, [_P, C.c_char_p, C.c_int]),
     ("crt_hip_profile_waves", C.c_int, [_P, C.POINTER(RendererSettings), _P, C.c_int64, _P]),
+    ("crt_hip_plan_tiles", C.c_int, [_P, C.POINTER(RendererSettings), _P, _P, C.c_int64]),
     ("crt_renderer_settings_default", None, [C.POINTER(RendererSettings)]),
     ("crt_write_ppm", C.c_int, [C.c_char_p, _P, C.c_int32, C.c_int32, C.c_int32]),
     ("crt_hip_last_error", C.c_char_p, []),
@@ -424,6 +425,19 @@ class HipScene:
         if rc < 0:
             _check(rc)
         return stamps, xy
+
+    def plan_tiles(self, settings: RendererSettings | None = None):
+        """Diagnostic: full-frame tile plan (dispatch order) → (xywh[n, 4], measured cost[n])."""
+        st = settings or RendererSettings.default()
+        n = lib().crt_hip_plan_tiles(self._h, C.byref(st), None, None, 0)
+        if n < 0:
+            _check(n)
+        xywh = np.zeros((n, 4), np.int32)
+        cost = np.zeros(n, np.float32)
+        rc = lib().crt_hip_plan_tiles(self._h, C.byref(st), xywh.ctypes.data, cost.ctypes.data, n)
+        if rc < 0:
+            _check(rc)
+        return xywh, cost
 
     def count_work(self, settings: RendererSettings | None = None) -> dict:
         st = settings or RendererSettings.default()

@@ -313,6 +313,12 @@ CRT_HD DNode cell_of(const PNode &p) {
     n.a = p.a; n.b = p.b;
     return n;
 }
+/* Octant `oct`'s node order: each order holds node_count records plus one
+ * zero record, so a walk may load the successors i+1 and skip(i) of any node
+ * without a bounds check. */
+CRT_HD const PNode *pnode_order(const PNode *base, int node_count, int oct) {
+    return base + (size_t)oct * (size_t)(node_count + 1);
+}
 CRT_HD int pnode_leaf_count(const PNode &n) { return n.count; }
 CRT_HD int pnode_depth(const PNode &n) { return n.depth; }
 

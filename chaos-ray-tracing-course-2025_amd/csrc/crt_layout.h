@@ -98,7 +98,7 @@ struct DLight {
 struct DeviceScene {
     const DNode *nodes;
     int32_t node_count;
-    const PNode *pnodes;            /* 8 octant orders x node_count (pruned walks) */
+    const PNode *pnodes;            /* 8 octant orders x (node_count + 1) (pruned walks; see pnode_order) */
     float prune_origin_max;         /* hull margins hold for rays with |o|_inf <= this */
     const DTriGeo *slots;
     const int32_t *slot_tri;

@@ -44,7 +44,7 @@ struct alignas(16) Tile {
     int32_t x, y, w, h;        /* pixel rectangle, w,h <= 8 */
     int64_t out_base;          /* output pixel index of (x, y) */
     int32_t out_stride;        /* output pixels per row */
-    int32_t pad;
+    int32_t prio;              /* 1: one of the frame's heaviest waves — raised issue priority */
 };
 
 struct alignas(16) UnpackBucket {
@@ -277,7 +277,7 @@ template <> struct WalkNode<false> {
 template <> struct WalkNode<true> {
     using T = PNode;
     static __device__ __forceinline__ const PNode *base(const DeviceScene &s, Vec d) {
-        return s.pnodes + (size_t)ray_octant(d) * (size_t)s.node_count;
+        return pnode_order(s.pnodes, s.node_count, ray_octant(d));
     }
     static __device__ __forceinline__ DNode cell(const PNode &n) { return cell_of(n); }
     static __device__ __forceinline__ bool alive(const PNode &n, const PruneRay &p, float lim) {
@@ -625,6 +625,18 @@ __device__ __forceinline__ T load_scalar(const T *p, int i) {
 #endif
 }
 
+/* Same, at a 32-bit byte offset from a wave-uniform base (SMEM base + offset
+ * addressing: no 64-bit address arithmetic per load). */
+template <class T>
+__device__ __forceinline__ T load_scalar_at(const char *base, uint32_t byte_off) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    using CT = const __attribute__((address_space(4))) T;
+    return *(CT *)((const __attribute__((address_space(4))) char *)base + byte_off);
+#else
+    return *(const T *)(base + byte_off);
+#endif
+}
+
 template <bool COUNT, bool EARLY>
 __device__ int trace_packet(const DeviceScene &s, bool active, Vec o, Vec d, float &best_t, LaneCounts &c) {
     int best = -1;
@@ -723,7 +735,7 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
     if (2 * __popcll(__ballot(active && d.x < 0.0f)) > na) oct |= 1;
     if (2 * __popcll(__ballot(active && d.y < 0.0f)) > na) oct |= 2;
     if (2 * __popcll(__ballot(active && d.z < 0.0f)) > na) oct |= 4;
-    const PNode *nodes = s.pnodes + (size_t)uniform_i(oct) * (size_t)n;
+    const PNode *nodes = pnode_order(s.pnodes, n, uniform_i(oct));
     /* The walk is a chain of dependent scalar loads (next index comes from the
      * current record), so each step issues the loads of both possible
      * successors — i+1 (descend / after a leaf) and the skip target — before
@@ -820,7 +832,7 @@ __device__ __forceinline__ int trace_lane_pruned(const DeviceScene &s, bool acti
     const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
     const int n = s.node_count;
     WalkCounts wc = {0u, 0u};
-    const int best = walk_pruned<COUNT>(s.pnodes + (size_t)ray_octant(d) * (size_t)n, n, s.slots, s.slot_cull, o, d,
+    const int best = walk_pruned<COUNT>(pnode_order(s.pnodes, n, ray_octant(d)), n, s.slots, s.slot_cull, o, d,
                                         rr, pr, best_t, wc);
     if (COUNT) {
         c.nodes += wc.nodes;
@@ -1078,6 +1090,10 @@ __global__ CRT_RENDER_BOUNDS void k_render_tiles(const DeviceScene *__restrict__
     /* diagnostic build only (stamps != nullptr): wave start / end in s_memrealtime ticks (100 MHz) */
     if (stamps && lane == 0) stamps[2 * wave] = __builtin_amdgcn_s_memrealtime();
     const Tile tl = tiles[wave];
+    /* the heaviest tiles set the frame length (their walks are long chains of
+     * dependent loads): they get issue priority over the light waves that
+     * share their SIMD (s_setprio; scheduling only, results unchanged) */
+    if (tl.prio) __builtin_amdgcn_s_setprio(3);
     const int lx = lane & 7, ly = lane >> 3;
     const bool has_px = lx < tl.w && ly < tl.h;
     /* the sharing walks keep pixel-less lanes as helpers (they take donated node
@@ -1195,6 +1211,7 @@ __global__ __launch_bounds__(256) void k_wf_level(const DeviceScene *__restrict_
         const int wave = gid >> 6;
         if (wave >= ntiles) return;
         const Tile tl = tiles[wave];
+        if (tl.prio) __builtin_amdgcn_s_setprio(3);
         const int lx = lane & 7, ly = lane >> 3;
         has = lx < tl.w && ly < tl.h;
         if (has) camera_ray(s, tl.x + lx, tl.y + ly, o, d);
@@ -1420,6 +1437,8 @@ struct ShardPlan {
     Tile *d_tiles = nullptr;
     int ntiles = 0;
     int64_t packed_pixels = 0;
+    std::vector<Tile> tiles;     /* host copy, dispatch order */
+    std::vector<float> cost;     /* measured cost per tile (calibrated plans), else empty */
 };
 
 struct GiTables { float *d = nullptr; };   /* 4 * 2^23 floats on one device */
@@ -1501,6 +1520,8 @@ struct crt_hip_scene {
     int calibrate = 1;             /* env CRT_CALIBRATE */
     float calib_k = 4.0f;          /* split a wave whose cost exceeds k x (total cost / wave slots) (env CRT_CALIB_K) */
     int calib_min = 2;             /* smallest sub-tile side (env CRT_CALIB_MIN: 1, 2, 4, 8) */
+    int prio_tiles = 1024;         /* heaviest tiles run at raised issue priority (env CRT_PRIO) */
+    float prio_min = 2.0f;         /* ... if they cost more than this x the mean per wave slot */
     std::vector<void *> plan_allocs;   /* tile lists of the current plans */
     int wavefront = 1;             /* level-by-level recursion when GI is off (env CRT_WAVEFRONT) */
     WfBuffers wf;
@@ -1594,7 +1615,18 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         std::stable_sort(out.begin(), out.end(),
                          [](const std::pair<float, Tile> &a, const std::pair<float, Tile> &b) { return a.first > b.first; });
         tiles.clear();
-        for (const auto &e : out) tiles.push_back(e.second);
+        plan.cost.clear();
+        for (const auto &e : out) {
+            tiles.push_back(e.second);
+            plan.cost.push_back(e.first);
+        }
+        /* issue priority for the heaviest waves, at most prio_tiles of them and
+         * only those costing more than prio_min x the mean per wave slot */
+        double csum = 0.0;
+        for (float c : plan.cost) csum += c;
+        const double slot_cost = csum / std::max(1, sc->wave_slots);
+        for (size_t k = 0; k < tiles.size() && (int)k < sc->prio_tiles; ++k)
+            tiles[k].prio = plan.cost[k] > sc->prio_min * slot_cost ? 1 : 0;
     } else if (sc->tile_order && !tiles.empty() && !sc->tile_work.empty()) {
         /* dispatch the expensive tiles first so the longest waves start at t=0;
          * with a sharing walk, split the heaviest tiles so each of their waves
@@ -1624,6 +1656,7 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         tiles.swap(sorted);
     }
     plan.ntiles = (int)tiles.size();
+    plan.tiles = tiles;
     if (!tiles.empty()) {
         void *p = nullptr;
         HIP_TRY(hipMalloc(&p, tiles.size() * sizeof(Tile)));
@@ -2030,6 +2063,8 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     if (const char *e = std::getenv("CRT_CALIBRATE")) sc->calibrate = std::atoi(e);
     if (const char *e = std::getenv("CRT_CALIB_K")) sc->calib_k = (float)std::atof(e);
     if (const char *e = std::getenv("CRT_CALIB_MIN")) sc->calib_min = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("CRT_PRIO")) sc->prio_tiles = std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("CRT_PRIO_MIN")) sc->prio_min = (float)std::atof(e);
     if (const char *e = std::getenv("CRT_SPLIT")) {
         float a = 0.f, b = 0.f;
         if (std::sscanf(e, "%f,%f", &a, &b) >= 1) { sc->split4 = a; sc->split16 = b; }
@@ -2301,6 +2336,24 @@ int crt_hip_profile_waves(crt_hip_scene *sc, const crt_renderer_settings *st, ui
     if (e != hipSuccess) return set_error(CRT_E_HIP, hipGetErrorString(e));
     for (int k = 0; k < nt; ++k) { tile_xy[2 * k] = tiles[k].x; tile_xy[2 * k + 1] = tiles[k].y; }
     return nt;
+}
+
+int crt_hip_plan_tiles(crt_hip_scene *sc, const crt_renderer_settings *st, int32_t *xywh, float *cost, int64_t cap) {
+    if (!sc || !st) return set_error(CRT_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(sc->device));
+    const int rc = ensure_plans(sc, st, sc->stream);
+    if (rc != CRT_OK) return rc;
+    const ShardPlan &p = sc->full;
+    if (!xywh) return p.ntiles;
+    if (cap < p.ntiles) return set_error(CRT_E_INVALID, "tile buffer too small");
+    for (int k = 0; k < p.ntiles; ++k) {
+        xywh[4 * k] = p.tiles[k].x;
+        xywh[4 * k + 1] = p.tiles[k].y;
+        xywh[4 * k + 2] = p.tiles[k].w;
+        xywh[4 * k + 3] = p.tiles[k].h;
+        if (cost) cost[k] = p.cost.empty() ? 0.f : p.cost[k];
+    }
+    return p.ntiles;
 }
 
 int crt_hip_count_work(crt_hip_scene *sc, const crt_renderer_settings *st, crt_work_counts *out) {

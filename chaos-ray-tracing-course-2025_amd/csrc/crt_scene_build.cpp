@@ -262,10 +262,10 @@ void build_pruned_nodes(const std::vector<BuildNode> &bn, HostScene &hs) {
             }
         }
     }
-    hs.pnodes.assign((size_t)8 * n, PNode{});
+    hs.pnodes.assign((size_t)8 * (n + 1), PNode{});   /* + one zero record per order: successor prefetch of the last node */
     std::vector<int32_t> st;
     for (int oct = 0; oct < 8; ++oct) {
-        PNode *out = hs.pnodes.data() + (size_t)oct * n;
+        PNode *out = hs.pnodes.data() + (size_t)oct * (n + 1);
         int32_t k = 0;
         st.assign(1, 0);
         while (!st.empty()) {

@@ -248,6 +248,12 @@ int  crt_hip_scene_set_option(crt_hip_scene *scene, const char *name, int value)
 /* Diagnostics: render one full frame with per-wave s_memrealtime stamps
  * (100 MHz ticks; stamps = 2 per 8x8 tile: start, end; tile_xy = tile origin,
  * in dispatch order).  With NULL buffers returns the tile count. */
+/* Diagnostics: the full-frame tile plan in dispatch order (x, y, w, h per
+ * tile) and each tile's measured walk cost (wave steps; 0 without a
+ * calibrated plan).  With NULL xywh returns the tile count. */
+int  crt_hip_plan_tiles(crt_hip_scene *scene, const crt_renderer_settings *settings, int32_t *xywh, float *cost,
+                        int64_t cap);
+
 int  crt_hip_profile_waves(crt_hip_scene *scene, const crt_renderer_settings *settings, uint64_t *stamps,
                            int64_t cap, int32_t *tile_xy);
 

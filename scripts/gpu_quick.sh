@@ -19,5 +19,6 @@ STEPS=${STEPS:-tests,ab,bench}
 [[ $STEPS == *ab* ]] && run ab_c2 300 python3 scripts/render_loop.py --frames 40 --ab "${AB:-CRT_CAMERA_FAST=0,1}"
 [[ $STEPS == *abc3* ]] && run ab_c3 300 python3 scripts/render_loop.py --scene 11-01-refractive__scene8 --depth 8 --frames 10 --ab "${AB3:-CRT_CAMERA_FAST=0,1}"
 [[ $STEPS == *abc5* ]] && run ab_c5 300 python3 scripts/render_loop.py --synthetic 1000000 --width 3840 --height 2160 --frames 5 --ab "${AB5:-CRT_CAMERA_FAST=0,1}"
+[[ $STEPS == *tilecost* ]] && run tilecost 300 python3 scripts/tile_cost_profile.py
 [[ $STEPS == *bench* ]] && run bench 300 python bench.py --no-cpu-baseline
 exit 0

@@ -71,7 +71,7 @@ int prune_sim_trace(const crt_scene_desc *desc, const float *rays, int64_t n, in
         const RayRcp rr = make_ray_rcp(o, d, false);
         const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
         WalkCounts c = {0u, 0u};
-        pr_slot[i] = walk_pruned<true>(hs.pnodes.data() + (size_t)ray_octant(d) * nn, nn, hs.slots.data(),
+        pr_slot[i] = walk_pruned<true>(pnode_order(hs.pnodes.data(), nn, ray_octant(d)), nn, hs.slots.data(),
                                        hs.slot_cull.data(), o, d, rr, pr, t, c);
         pr_t[i] = t;
         pn += c.nodes;
@@ -93,7 +93,7 @@ int64_t prune_sim_check_hulls(const crt_scene_desc *desc) {
     const int nn = (int)hs.nodes.size();
     int64_t bad = 0;
     for (int oct = 0; oct < 8; ++oct) {
-        const PNode *p = hs.pnodes.data() + (size_t)oct * nn;
+        const PNode *p = pnode_order(hs.pnodes.data(), nn, oct);
         /* walk with an explicit path of open interior nodes */
         int path[128];
         int depth_top = 0;
