@@ -103,10 +103,14 @@ class SceneInfo(C.Structure):
                 ("leaf_count", C.c_int64), ("leaf_ref_count", C.c_int64), ("max_depth", C.c_int32),
                 ("max_leaf_size", C.c_int32), ("device_bytes", C.c_int64), ("width", C.c_int32),
                 ("height", C.c_int32), ("bucket_size", C.c_int32), ("gi_on", C.c_int32),
-                ("reflections_on", C.c_int32), ("refractions_on", C.c_int32)]
+                ("reflections_on", C.c_int32), ("refractions_on", C.c_int32), ("tree_on_device", C.c_int32),
+                ("tree_build_ms", C.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+TREE_AUTO, TREE_HOST, TREE_DEVICE = 0, 1, 2   # crt_hip_scene_create_ex flags
 
 
 class RenderStats(C.Structure):
@@ -144,6 +148,8 @@ EXPORTS = [
     ("crt_host_scene_face_normals", C.c_int, [_P, _P]),
     ("crt_host_scene_destroy", None, [_P]),
     ("crt_hip_scene_create", C.c_int, [C.POINTER(SceneDesc), C.c_int, C.POINTER(_P)]),
+    ("crt_hip_scene_create_ex", C.c_int, [C.POINTER(SceneDesc), C.c_int, C.c_int, C.POINTER(_P)]),
+    ("crt_hip_scene_tree", C.c_int, [_P, _P, _P, _P, _P]),
     ("crt_hip_scene_upload", C.c_int, [_P, C.c_int, C.POINTER(_P)]),
     ("crt_hip_scene_info", C.c_int, [_P, C.POINTER(SceneInfo)]),
     ("crt_hip_scene_destroy", None, [_P]),
@@ -341,12 +347,15 @@ class HostScene:
 #  device scene (HBM-resident) and rendering
 # --------------------------------------------------------------------------
 class HipScene:
-    def __init__(self, src, device: int = 0, **options):
+    def __init__(self, src, device: int = 0, tree_build: str = "auto", **options):
+        """tree_build: "auto" | "host" | "device" — where the acceleration tree is
+        built (crt_hip_scene_create_ex; both builds give identical bits)."""
         h = C.c_void_p()
         if isinstance(src, HostScene):
             _check(lib().crt_hip_scene_upload(src.handle, device, C.byref(h)))
         else:
-            _check(lib().crt_hip_scene_create(_desc_ptr(src), device, C.byref(h)))
+            flag = {"auto": TREE_AUTO, "host": TREE_HOST, "device": TREE_DEVICE}[tree_build]
+            _check(lib().crt_hip_scene_create_ex(_desc_ptr(src), device, flag, C.byref(h)))
         self._h = h
         self.device = device
         for k, v in options.items():
@@ -365,6 +374,17 @@ class HipScene:
         i = SceneInfo()
         _check(lib().crt_hip_scene_info(self._h, C.byref(i)))
         return i.as_dict()
+
+    def tree(self):
+        """(bounds[n,6], children[n,2], leaf_offsets[n+1], leaf_tris[m]) in reference numbering."""
+        info = self.info()
+        n, m = info["node_count"], info["leaf_ref_count"]
+        b = np.zeros((n, 6), np.float32)
+        c = np.zeros((n, 2), np.int32)
+        o = np.zeros(n + 1, np.int64)
+        t = np.zeros(max(m, 1), np.int32)
+        _check(lib().crt_hip_scene_tree(self._h, b.ctypes.data, c.ctypes.data, o.ctypes.data, t.ctypes.data))
+        return b, c, o, t[:m]
 
     def render(self, settings: RendererSettings | None = None, with_stats: bool = False):
         """Blocking render_image: returns float32 [H, W, 3], top row first."""

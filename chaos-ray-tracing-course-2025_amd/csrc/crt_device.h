@@ -306,6 +306,74 @@ CRT_HD bool hull_alive(const PNode &n, const PruneRay &p, float lim) {
     return !p.on || (!(tin > lim) && !(tin > tout) && !(tout < 0.0f));
 }
 
+/* ---- hull margins (derivation: crt_scene_build.cpp) — host and device build */
+CRT_HD float round_down(double v) {
+    float f = (float)v;
+    if ((double)f > v) f = nextafterf(f, -INFINITY);
+    return f;
+}
+CRT_HD float round_up(double v) {
+    float f = (float)v;
+    if ((double)f < v) f = nextafterf(f, INFINITY);
+    return f;
+}
+
+struct HullD { double lo[3], hi[3]; };
+
+/* correctly rounded double sqrt / divide on both sides (the GPU's default
+ * f64 sqrt is not guaranteed to be), so host and device builds agree bit for bit */
+CRT_HD double sqrt_rn(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __dsqrt_rn(x);
+#else
+    return sqrt(x);
+#endif
+}
+CRT_HD double div_rn(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __ddiv_rn(a, b);
+#else
+    return a / b;
+#endif
+}
+
+/* Box of one triangle widened by 2^-14 (diam * kappa + 2 G); unbounded for a
+ * non-finite normal or vertex or a zero-area triangle.  Plain double
+ * arithmetic in a fixed order (no contraction), identical on host and GPU. */
+CRT_HD HullD triangle_hull(const float *a, const float *b, const float *c, const float *fn, double G) {
+    HullD h;
+    for (int k = 0; k < 3; ++k) { h.lo[k] = -(double)INFINITY; h.hi[k] = (double)INFINITY; }
+    bool finite = isfinite(fn[0]) && isfinite(fn[1]) && isfinite(fn[2]);
+    for (int k = 0; k < 3; ++k) finite = finite && isfinite(a[k]) && isfinite(b[k]) && isfinite(c[k]);
+    if (!finite) return h;
+    double e[3][3];
+    for (int k = 0; k < 3; ++k) {
+        e[0][k] = (double)b[k] - (double)a[k];
+        e[1][k] = (double)c[k] - (double)b[k];
+        e[2][k] = (double)a[k] - (double)c[k];
+    }
+    double len[3];
+    for (int i = 0; i < 3; ++i) len[i] = sqrt_rn(e[i][0] * e[i][0] + e[i][1] * e[i][1] + e[i][2] * e[i][2]);
+    const double cx = e[0][1] * (-e[2][2]) - e[0][2] * (-e[2][1]);
+    const double cy = e[0][2] * (-e[2][0]) - e[0][0] * (-e[2][2]);
+    const double cz = e[0][0] * (-e[2][1]) - e[0][1] * (-e[2][0]);
+    const double area2 = sqrt_rn(cx * cx + cy * cy + cz * cz);   /* 2 * area */
+    const double perim = len[0] + len[1] + len[2];
+    if (!(area2 > 0.0) || !(perim > 0.0)) return h;
+    const double inradius = div_rn(area2, perim);
+    const double diam = fmax(len[0], fmax(len[1], len[2]));
+    const double kappa = div_rn(diam, inradius);
+    const double eta = ldexp(diam * kappa + 2.0 * G, -14);
+    if (!isfinite(eta)) return h;
+    for (int k = 0; k < 3; ++k) {
+        const double lo = fmin((double)a[k], fmin((double)b[k], (double)c[k]));
+        const double hi = fmax((double)a[k], fmax((double)b[k], (double)c[k]));
+        h.lo[k] = lo - eta;
+        h.hi[k] = hi + eta;
+    }
+    return h;
+}
+
 CRT_HD DNode cell_of(const PNode &p) {
     DNode n;
     n.lo_x = p.lo_x; n.lo_y = p.lo_y; n.lo_z = p.lo_z;

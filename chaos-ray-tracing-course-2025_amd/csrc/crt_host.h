@@ -66,9 +66,15 @@ struct HostScene {
     std::vector<int32_t> slot_tri;
     std::vector<uint8_t> slot_cull;
 
-    /* pruned walks (crt_layout.h PNode): 8 octant orders x nodes.size() */
+    /* pruned walks (crt_layout.h PNode): 8 octant orders x (nodes.size() + 1) */
     std::vector<PNode> pnodes;
     float prune_origin_max = 0.f;
+    double prune_G = 0.0;           /* the G of the hull margins (crt_scene_build.cpp) */
+
+    /* root cell (crt_acceleration_tree.cpp:89-94); tree_on_host = false when
+     * prepare_scene skipped the tree (built on the device, crt_tree_build.h) */
+    float root_box[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    bool tree_on_host = true;
 
     /* shading */
     std::vector<DMaterial> materials;
@@ -82,7 +88,8 @@ struct HostScene {
     int32_t max_leaf_size = 0;
 };
 
-int prepare_scene(const crt_scene_desc *desc, HostScene &out);
+/* Mesh prep + (build_tree) the exact tree build and its flattening. */
+int prepare_scene(const crt_scene_desc *desc, HostScene &out, bool build_tree = true);
 
 /* Screen-space work estimate: every leaf cell is projected through the camera
  * and its triangle count added to the 8x8 tiles its image overlaps.  Used only

@@ -35,6 +35,7 @@
 
 #include "crt_device.h"
 #include "crt_host.h"
+#include "crt_tree_build.h"
 
 namespace crt_amd {
 
@@ -1523,6 +1524,14 @@ struct crt_hip_scene {
     int prio_tiles = 1024;         /* heaviest tiles run at raised issue priority (env CRT_PRIO) */
     float prio_min = 2.0f;         /* ... if they cost more than this x the mean per wave slot */
     std::vector<void *> plan_allocs;   /* tile lists of the current plans */
+    /* the tree in the reference's numbering (crt_hip_scene_tree): host copies
+     * for a host-built tree, device arrays for a device-built one */
+    std::vector<float> ref_bounds;
+    std::vector<int32_t> ref_children, ref_leaf_tris;
+    std::vector<int64_t> ref_leaf_off;
+    const float *dt_ref_bounds = nullptr;
+    const int32_t *dt_ref_children = nullptr, *dt_ref_leaf_tris = nullptr;
+    const int64_t *dt_ref_leaf_off = nullptr;
     int wavefront = 1;             /* level-by-level recursion when GI is off (env CRT_WAVEFRONT) */
     WfBuffers wf;
 };
@@ -2069,7 +2078,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
         float a = 0.f, b = 0.f;
         if (std::sscanf(e, "%f,%f", &a, &b) >= 1) { sc->split4 = a; sc->split16 = b; }
     }
-    if (sc->tile_order) sc->tile_work = tile_work_estimate(hs, (hs.width + 7) / 8, (hs.height + 7) / 8);
+    if (sc->tile_order && hs.tree_on_host) sc->tile_work = tile_work_estimate(hs, (hs.width + 7) / 8, (hs.height + 7) / 8);
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -2083,11 +2092,11 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     }
     DeviceScene &ds = sc->ds;
     int rc;
-    if ((rc = upload(sc.get(), hs.nodes, &ds.nodes)) != CRT_OK) return rc;
-    ds.node_count = (int32_t)hs.nodes.size();
-    if ((rc = upload(sc.get(), hs.pnodes, &ds.pnodes)) != CRT_OK) return rc;
     ds.prune_origin_max = hs.prune_origin_max;
-    {
+    if (hs.tree_on_host) {
+        if ((rc = upload(sc.get(), hs.nodes, &ds.nodes)) != CRT_OK) return rc;
+        ds.node_count = (int32_t)hs.nodes.size();
+        if ((rc = upload(sc.get(), hs.pnodes, &ds.pnodes)) != CRT_OK) return rc;
         auto ok = [](float x) {
             const float m = std::fabs(x);
             return x == 0.0f || (m >= 0x1p-40f && m <= 0x1p62f);
@@ -2095,18 +2104,48 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
         ds.planes_ok = 1;
         for (const DNode &n : hs.nodes)
             if (!(ok(n.lo_x) && ok(n.lo_y) && ok(n.lo_z) && ok(n.hi_x) && ok(n.hi_y) && ok(n.hi_z))) ds.planes_ok = 0;
-    }
-    sc->camera_fast = camera_rays_fast(hs, ds.planes_ok != 0);
-    if (const char *e = std::getenv("CRT_CAMERA_FAST")) sc->camera_fast = sc->camera_fast && std::atoi(e) != 0;
-    if ((rc = upload(sc.get(), hs.slots, &ds.slots)) != CRT_OK) return rc;
-    if ((rc = upload(sc.get(), hs.slot_tri, &ds.slot_tri)) != CRT_OK) return rc;
-    if ((rc = upload(sc.get(), hs.slot_cull, &ds.slot_cull)) != CRT_OK) return rc;
-    {
+        if ((rc = upload(sc.get(), hs.slots, &ds.slots)) != CRT_OK) return rc;
+        if ((rc = upload(sc.get(), hs.slot_tri, &ds.slot_tri)) != CRT_OK) return rc;
+        if ((rc = upload(sc.get(), hs.slot_cull, &ds.slot_cull)) != CRT_OK) return rc;
         std::vector<uint32_t> bits((hs.slot_cull.size() + 31) / 32 + 1, 0u);
         for (size_t k = 0; k < hs.slot_cull.size(); ++k)
             if (hs.slot_cull[k]) bits[k >> 5] |= 1u << (k & 31);
         if ((rc = upload(sc.get(), bits, &ds.slot_cull_bits)) != CRT_OK) return rc;
+        sc->ref_bounds = hs.ref_bounds;
+        sc->ref_children = hs.ref_children;
+        sc->ref_leaf_off = hs.ref_leaf_off;
+        sc->ref_leaf_tris = hs.ref_leaf_tris;
+    } else {
+        /* exact tree build on the device (crt_tree_build.hip) */
+        DeviceTree dt;
+        rc = build_tree_device(hs, nullptr, dt);
+        for (void *p : dt.allocs) sc->allocs.push_back(p);
+        if (rc != CRT_OK) return rc;
+        ds.nodes = dt.nodes;
+        ds.node_count = dt.node_count;
+        ds.pnodes = dt.pnodes;
+        ds.planes_ok = dt.planes_ok;
+        ds.slots = dt.slots;
+        ds.slot_tri = dt.slot_tri;
+        ds.slot_cull = dt.slot_cull;
+        ds.slot_cull_bits = dt.slot_cull_bits;
+        sc->dt_ref_bounds = dt.ref_bounds;
+        sc->dt_ref_children = dt.ref_children;
+        sc->dt_ref_leaf_off = dt.ref_leaf_off;
+        sc->dt_ref_leaf_tris = dt.ref_leaf_tris;
+        sc->info.node_count = dt.node_count;
+        sc->info.leaf_count = dt.leaf_count;
+        sc->info.leaf_ref_count = dt.slot_count;
+        sc->info.max_depth = dt.max_depth;
+        sc->info.max_leaf_size = dt.max_leaf_size;
+        sc->info.tree_build_ms = dt.build_ms;
+        sc->info.tree_on_device = 1;
+        const int64_t n = dt.node_count, m = dt.slot_count;
+        sc->info.device_bytes += n * (int64_t)sizeof(DNode) + 8 * (n + 1) * (int64_t)sizeof(PNode) +
+                                 m * (int64_t)(sizeof(DTriGeo) + 4 + 1) + (m / 32 + 1) * 4;
     }
+    sc->camera_fast = camera_rays_fast(hs, ds.planes_ok != 0);
+    if (const char *e = std::getenv("CRT_CAMERA_FAST")) sc->camera_fast = sc->camera_fast && std::atoi(e) != 0;
     if ((rc = upload(sc.get(), hs.tri_attr, &ds.tri_attr)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.vnormal, &ds.vnormal)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.vuv, &ds.vuv)) != CRT_OK) return rc;
@@ -2142,13 +2181,50 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     return CRT_OK;
 }
 
-int crt_hip_scene_create(const crt_scene_desc *desc, int device, crt_hip_scene **out) {
-    crt_host_scene *h = nullptr;
-    int rc = crt_host_scene_create(desc, &h);
+int crt_hip_scene_create_ex(const crt_scene_desc *desc, int device, int flags, crt_hip_scene **out) {
+    if (!desc || !out) return set_error(CRT_E_INVALID, "null argument");
+    int mode = flags & 3;
+    if (mode == CRT_SCENE_TREE_AUTO) {
+        if (const char *e = std::getenv("CRT_TREE_BUILD")) {
+            if (std::strcmp(e, "host") == 0) mode = CRT_SCENE_TREE_HOST;
+            if (std::strcmp(e, "device") == 0) mode = CRT_SCENE_TREE_DEVICE;
+        }
+    }
+    if (mode == CRT_SCENE_TREE_AUTO) {
+        int64_t nt = 0;
+        for (int i = 0; i < desc->mesh_count && desc->meshes; ++i) nt += desc->meshes[i].index_count / 3;
+        mode = nt >= CRT_SCENE_DEVICE_BUILD_MIN ? CRT_SCENE_TREE_DEVICE : CRT_SCENE_TREE_HOST;
+    }
+    if (mode != CRT_SCENE_TREE_HOST && mode != CRT_SCENE_TREE_DEVICE) return set_error(CRT_E_INVALID, "bad tree build flag");
+    std::unique_ptr<HostScene> hs(new HostScene());
+    int rc = prepare_scene(desc, *hs, mode == CRT_SCENE_TREE_HOST);
     if (rc != CRT_OK) return rc;
-    rc = crt_hip_scene_upload(h, device, out);
-    crt_host_scene_destroy(h);
-    return rc;
+    return crt_hip_scene_upload(reinterpret_cast<crt_host_scene *>(hs.get()), device, out);
+}
+
+int crt_hip_scene_create(const crt_scene_desc *desc, int device, crt_hip_scene **out) {
+    return crt_hip_scene_create_ex(desc, device, CRT_SCENE_TREE_AUTO, out);
+}
+
+int crt_hip_scene_tree(const crt_hip_scene *sc, float *bounds, int32_t *children, int64_t *leaf_offsets,
+                       int32_t *leaf_tris) {
+    if (!sc) return set_error(CRT_E_INVALID, "null argument");
+    const int64_t n = sc->info.node_count, m = sc->info.leaf_ref_count;
+    if (sc->info.tree_on_device) {
+        HIP_TRY(hipSetDevice(sc->device));
+        if (bounds) HIP_TRY(hipMemcpy(bounds, sc->dt_ref_bounds, (size_t)n * 6 * sizeof(float), hipMemcpyDeviceToHost));
+        if (children) HIP_TRY(hipMemcpy(children, sc->dt_ref_children, (size_t)n * 2 * sizeof(int32_t), hipMemcpyDeviceToHost));
+        if (leaf_offsets)
+            HIP_TRY(hipMemcpy(leaf_offsets, sc->dt_ref_leaf_off, (size_t)(n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+        if (leaf_tris && m > 0)
+            HIP_TRY(hipMemcpy(leaf_tris, sc->dt_ref_leaf_tris, (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost));
+        return CRT_OK;
+    }
+    if (bounds) std::memcpy(bounds, sc->ref_bounds.data(), sc->ref_bounds.size() * sizeof(float));
+    if (children) std::memcpy(children, sc->ref_children.data(), sc->ref_children.size() * sizeof(int32_t));
+    if (leaf_offsets) std::memcpy(leaf_offsets, sc->ref_leaf_off.data(), sc->ref_leaf_off.size() * sizeof(int64_t));
+    if (leaf_tris) std::memcpy(leaf_tris, sc->ref_leaf_tris.data(), sc->ref_leaf_tris.size() * sizeof(int32_t));
+    return CRT_OK;
 }
 
 int crt_hip_scene_info(const crt_hip_scene *sc, crt_scene_info *out) {

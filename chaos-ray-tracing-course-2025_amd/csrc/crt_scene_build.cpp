@@ -22,6 +22,7 @@
 #include <string>
 #include <vector>
 
+#include "crt_device.h"
 #include "crt_host.h"
 
 namespace crt_amd {
@@ -158,61 +159,24 @@ void build_tree(const std::vector<Box6> &tri_boxes, const Box6 &root_box, std::v
  * device's slab test (rcp, one rounding per product) adds errors far below
  * it.  Triangles whose normal is not finite or whose area is 0 (no reliable
  * bound) get an unbounded hull: their subtrees are never pruned. */
-inline float round_down(double v) {
-    float f = (float)v;
-    if ((double)f > v) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
-    return f;
-}
-inline float round_up(double v) {
-    float f = (float)v;
-    if ((double)f < v) f = std::nextafter(f, std::numeric_limits<float>::infinity());
-    return f;
-}
+/* round_down / round_up / HullD / triangle_hull: crt_device.h (shared with the
+ * device build, crt_tree_build.hip, so both builds produce the same bits). */
 
-struct HullD { double lo[3], hi[3]; };
-
-HullD triangle_hull(const float *a, const float *b, const float *c, const float *fn, double G) {
-    const double inf = std::numeric_limits<double>::infinity();
-    HullD h{{-inf, -inf, -inf}, {inf, inf, inf}};
-    bool finite = std::isfinite(fn[0]) && std::isfinite(fn[1]) && std::isfinite(fn[2]);
-    for (int k = 0; k < 3; ++k) finite = finite && std::isfinite(a[k]) && std::isfinite(b[k]) && std::isfinite(c[k]);
-    if (!finite) return h;
-    double e[3][3];
-    for (int k = 0; k < 3; ++k) {
-        e[0][k] = (double)b[k] - a[k];
-        e[1][k] = (double)c[k] - b[k];
-        e[2][k] = (double)a[k] - c[k];
-    }
-    double len[3];
-    for (int i = 0; i < 3; ++i) len[i] = std::sqrt(e[i][0] * e[i][0] + e[i][1] * e[i][1] + e[i][2] * e[i][2]);
-    const double cx = e[0][1] * (-e[2][2]) - e[0][2] * (-e[2][1]);
-    const double cy = e[0][2] * (-e[2][0]) - e[0][0] * (-e[2][2]);
-    const double cz = e[0][0] * (-e[2][1]) - e[0][1] * (-e[2][0]);
-    const double area2 = std::sqrt(cx * cx + cy * cy + cz * cz);   /* 2 * area */
-    const double perim = len[0] + len[1] + len[2];
-    if (!(area2 > 0.0) || !(perim > 0.0)) return h;
-    const double inradius = area2 / perim;
-    const double diam = std::max(len[0], std::max(len[1], len[2]));
-    const double kappa = diam / inradius;
-    const double eta = std::ldexp(diam * kappa + 2.0 * G, -14);
-    if (!std::isfinite(eta)) return h;
-    for (int k = 0; k < 3; ++k) {
-        const double lo = std::min((double)a[k], std::min((double)b[k], (double)c[k]));
-        const double hi = std::max((double)a[k], std::max((double)b[k], (double)c[k]));
-        h.lo[k] = lo - eta;
-        h.hi[k] = hi + eta;
-    }
-    return h;
-}
-
-void build_pruned_nodes(const std::vector<BuildNode> &bn, HostScene &hs) {
-    const int32_t n = (int32_t)bn.size();
+/* G of the hull margins: 4 max |vertex coordinate| (rounded down: rays above
+ * it are simply not pruned). */
+void set_prune_origin_max(HostScene &hs) {
     double vmax = 0.0;
     for (float v : hs.vpos)
         if (std::isfinite(v)) vmax = std::max(vmax, (double)std::fabs(v));
     const double G = 4.0 * vmax;
-    hs.prune_origin_max = (float)G;   /* rounding down is harmless: rays above it are not pruned */
+    hs.prune_G = G;
+    hs.prune_origin_max = (float)G;
     if ((double)hs.prune_origin_max > G) hs.prune_origin_max = round_down(G);
+}
+
+void build_pruned_nodes(const std::vector<BuildNode> &bn, HostScene &hs) {
+    const int32_t n = (int32_t)bn.size();
+    const double G = hs.prune_G;
 
     const size_t nt = hs.tri_attr.size();
     std::vector<HullD> th(nt);
@@ -298,7 +262,7 @@ void build_pruned_nodes(const std::vector<BuildNode> &bn, HostScene &hs) {
 
 }  // namespace
 
-int prepare_scene(const crt_scene_desc *d, HostScene &hs) {
+int prepare_scene(const crt_scene_desc *d, HostScene &hs, bool build_tree_on_host) {
     if (!d) return set_error(CRT_E_INVALID, "null scene description");
     if (d->camera.width <= 0 || d->camera.height <= 0)
         return set_error(CRT_E_INVALID, "image width/height must be positive");
@@ -420,8 +384,25 @@ int prepare_scene(const crt_scene_desc *d, HostScene &hs) {
     for (int64_t v = 0; v < nv; ++v) hs.vnormal[v] = DVec4{vnorm[v].x, vnorm[v].y, vnorm[v].z, 0.f};
 
     /* ---- tree build (crt_acceleration_tree.cpp:87-106) ---- */
+    set_prune_origin_max(hs);
     const float inf = std::numeric_limits<float>::infinity();
     Box6 root{{inf, inf, inf}, {-inf, -inf, -inf}};
+    if (!build_tree_on_host) {
+        /* root cell only (the same fold); the tree is built on the device */
+        for (int64_t t = 0; t < nt; ++t)
+            for (int32_t v : {hs.tri_attr[t].i0, hs.tri_attr[t].i1, hs.tri_attr[t].i2})
+                for (int k = 0; k < 3; ++k) {
+                    const float p = hs.vpos[3 * (size_t)v + k];
+                    root.lo[k] = std::min(root.lo[k], p);
+                    root.hi[k] = std::max(root.hi[k], p);
+                }
+        for (int k = 0; k < 3; ++k) {
+            hs.root_box[k] = root.lo[k];
+            hs.root_box[3 + k] = root.hi[k];
+        }
+        hs.tree_on_host = false;
+        return CRT_OK;
+    }
     std::vector<Box6> tri_boxes((size_t)nt);
     for (int64_t t = 0; t < nt; ++t) {
         Box6 b{{inf, inf, inf}, {-inf, -inf, -inf}};
@@ -436,6 +417,10 @@ int prepare_scene(const crt_scene_desc *d, HostScene &hs) {
             }
         }
         tri_boxes[t] = b;
+    }
+    for (int k = 0; k < 3; ++k) {
+        hs.root_box[k] = root.lo[k];
+        hs.root_box[3 + k] = root.hi[k];
     }
     std::vector<BuildNode> bn;
     build_tree(tri_boxes, root, bn);

@@ -133,6 +133,8 @@ typedef struct crt_scene_info {
     int32_t width, height;
     int32_t bucket_size;
     int32_t gi_on, reflections_on, refractions_on;
+    int32_t tree_on_device;    /* 1: tree built by crt_tree_build.hip on the GPU   */
+    double  tree_build_ms;     /* wall time of the device build (0 for host builds) */
 } crt_scene_info;
 
 typedef struct crt_render_stats {
@@ -182,8 +184,24 @@ void crt_host_scene_destroy(crt_host_scene *hs);
 /* ---- device scene ---------------------------------------------------- */
 typedef struct crt_hip_scene crt_hip_scene;
 
-/* crt_host_scene_create + crt_hip_scene_upload. */
+/* crt_host_scene_create + crt_hip_scene_upload (tree build chosen as
+ * CRT_SCENE_TREE_AUTO, see crt_hip_scene_create_ex). */
 int  crt_hip_scene_create(const crt_scene_desc *desc, int device, crt_hip_scene **out);
+
+/* Where the acceleration tree (crt_acceleration_tree.cpp:13-106) is built:
+ * AUTO = on the device from CRT_SCENE_DEVICE_BUILD_MIN triangles up (the env
+ * variable CRT_TREE_BUILD=host|device overrides), HOST = crt_scene_build.cpp,
+ * DEVICE = crt_tree_build.hip.  Both builds produce identical bits. */
+#define CRT_SCENE_TREE_AUTO   0
+#define CRT_SCENE_TREE_HOST   1
+#define CRT_SCENE_TREE_DEVICE 2
+#define CRT_SCENE_DEVICE_BUILD_MIN 65536
+int  crt_hip_scene_create_ex(const crt_scene_desc *desc, int device, int flags, crt_hip_scene **out);
+
+/* The scene's tree in the reference's preorder numbering, as
+ * crt_host_scene_tree (sizes from crt_hip_scene_info). */
+int  crt_hip_scene_tree(const crt_hip_scene *scene, float *bounds, int32_t *children, int64_t *leaf_offsets,
+                        int32_t *leaf_tris);
 /* Copy a prepared scene into HBM of `device` (the host scene may be destroyed after). */
 int  crt_hip_scene_upload(const crt_host_scene *hs, int device, crt_hip_scene **out);
 int  crt_hip_scene_info(const crt_hip_scene *scene, crt_scene_info *out);
