@@ -305,6 +305,7 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (COUNT && active) ++c.traversals;
+    if (COUNT) ++c.wave_tris;           /* coop walks: wave_tris = calls, wave_nodes = loop rounds */
 
     int r = lane;                       /* ray of the piece this lane walks */
     int i = active ? 0 : n, end = n;    /* the piece: [i, end) */
@@ -317,6 +318,7 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
     int sp = 0;                         /* wave-uniform stack depth */
     NT nd = nb[0];
     for (;;) {
+        if (COUNT) ++c.wave_nodes;
         bool busy = (i < end) || (lc > 0);
         /* ---- idle lanes pop donated pieces ---- */
         const unsigned long long idle = __ballot(!busy);
@@ -938,12 +940,16 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
     Frame stack[MAXF > 0 ? MAXF : 1];
     int sp = 0;
     Vec col;
+    /* Every pass of this loop traces exactly one ray per live lane, so all of a
+     * wave's lanes meet in the same walk call whatever their position in their
+     * own recursion (a miss shifts one lane's DFS against the others).  A call
+     * that shade_ray would answer without tracing (depth > max_ray_depth: black,
+     * crt_renderer.cpp:47-49) is resolved in the return loop below instead of
+     * costing a pass; its GI draws are still taken (gi_ray) in reference order. */
     for (;;) {
-        /* ---- enter shade_ray(ray) ---- */
+        /* ---- shade_ray(ray) with depth <= max_ray_depth ---- */
         bool called = false;
-        if (depth > st.max_ray_depth) {
-            col = vec(0.f, 0.f, 0.f);
-        } else {
+        {
             float t;
             /* the packet walk pays for the union of its lanes' visit sets: it
              * wins on camera rays (coherent by construction) and loses on the
@@ -1031,8 +1037,12 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
                 }
             }
         }
-        if (called) continue;
         if (!FULL) break;
+        if (called) {
+            if (depth <= st.max_ray_depth) continue;
+            col = vec(0.f, 0.f, 0.f);       /* the child call returns black untraced */
+            called = false;
+        }
         /* ---- return col to the pending activations ---- */
         while (sp > 0) {
             Frame &f = stack[sp - 1];
@@ -1042,8 +1052,12 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
                 if ((uint32_t)f.i < st.diffuse_reflection_ray_count) {
                     gi_ray(s, st, f, rng, o, d);
                     depth = (uint32_t)f.depth + 1;
-                    called = true;
-                    break;
+                    if (depth <= st.max_ray_depth) {
+                        called = true;
+                        break;
+                    }
+                    col = vec(0.f, 0.f, 0.f);
+                    continue;
                 }
                 --sp;
                 col = diffuse_finish(s, st, f.acc, f.p, f.n, f.alb);
@@ -1057,8 +1071,12 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
                     o = f.a;
                     d = f.b;
                     depth = (uint32_t)f.depth + 1;
-                    called = true;
-                    break;
+                    if (depth <= st.max_ray_depth) {
+                        called = true;
+                        break;
+                    }
+                    col = vec(0.f, 0.f, 0.f);
+                    continue;
                 }
                 --sp;   /* total internal reflection: the reflection colour is the result */
             } else {

@@ -27,6 +27,7 @@ def main():
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--frames", type=int, default=5)
     p.add_argument("--depth", type=int, default=3)
+    p.add_argument("--gi", type=int, default=4, help="diffuse_reflection_ray_count")
     p.add_argument("--ab", default=None, help="ENVVAR=v1,v2,... — build one scene per value")
     p.add_argument("--counts", action="store_true", help="print per-ray and per-wave work counts per variant")
     p.add_argument("--synthetic", type=int, default=0, help="C5: synthetic mesh of N triangles instead of --scene")
@@ -37,7 +38,7 @@ def main():
         a.scene = f"synthetic-{a.synthetic}"
     else:
         sc = load_npz(ROOT / "tests" / "golden" / "scenes" / f"{a.scene}.npz").set_resolution(a.width, a.height)
-    st = N.RendererSettings.default(max_ray_depth=a.depth)
+    st = N.RendererSettings.default(max_ray_depth=a.depth, diffuse_reflection_ray_count=a.gi)
     variants = [("default", None)]
     if a.ab:
         var, vals = a.ab.split("=", 1)
