@@ -141,6 +141,8 @@ EXPORTS = [
     ("crt_scene_file_desc", C.POINTER(SceneDesc), [_P]),
     ("crt_scene_file_set_resolution", C.c_int, [_P, C.c_int32, C.c_int32]),
     ("crt_scene_file_destroy", None, [_P]),
+    ("crt_image_decode_rgb8", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                        C.POINTER(C.c_int32), _P, C.c_size_t]),
     ("crt_host_scene_create", C.c_int, [C.POINTER(SceneDesc), C.POINTER(_P)]),
     ("crt_host_scene_info", C.c_int, [_P, C.POINTER(SceneInfo)]),
     ("crt_host_scene_tree", C.c_int, [_P, _P, _P, _P, _P]),
@@ -205,6 +207,18 @@ def _check(rc: int, exc=CrtError) -> None:
 
 def _fptr(a: np.ndarray):
     return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def decode_image(data: bytes) -> np.ndarray:
+    """read_stb's pixel bytes (crt_image_stbi.cpp:16-40) for an image file's
+    contents: uint8 (h, w, 3), top row first.  Raises CrtError where read_stb
+    would fail (undecodable file, component count != 3)."""
+    w, h, n = C.c_int32(), C.c_int32(), C.c_int32()
+    _check(lib().crt_image_decode_rgb8(data, len(data), C.byref(w), C.byref(h), C.byref(n), None, 0))
+    out = np.empty((h.value, w.value, 3), np.uint8)
+    _check(lib().crt_image_decode_rgb8(data, len(data), C.byref(w), C.byref(h), C.byref(n),
+                                       out.ctypes.data, out.nbytes))
+    return out
 
 
 # --------------------------------------------------------------------------

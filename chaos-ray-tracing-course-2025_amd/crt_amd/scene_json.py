@@ -20,7 +20,7 @@ from pathlib import Path
 import numpy as np
 
 _MAT_TYPES = {0: "diffuse", 1: "reflective", 2: "refractive", 3: "constant"}
-_TEX_TYPES = {0: "albedo", 1: "edges", 2: "checker"}
+_TEX_TYPES = {0: "albedo", 1: "edges", 2: "checker", 3: "bitmap"}
 
 
 def _f(x) -> float:
@@ -31,8 +31,12 @@ def _vec(v) -> list:
     return [_f(x) for x in v]
 
 
-def arrays_to_crtscene(a: dict) -> dict:
-    """crt_amd.scene_npz arrays -> a .crtscene JSON document (Python dict)."""
+def arrays_to_crtscene(a: dict, bitmap_files: dict | None = None) -> dict:
+    """crt_amd.scene_npz arrays -> a .crtscene JSON document (Python dict).
+
+    Bitmap textures are files next to the scene: `bitmap_files` maps a texture
+    index to its "file_path" (read as asset_root / relative path), whose image
+    must decode to the texels the arrays hold."""
     w, h = (int(x) for x in a["cam_size"])
     bucket, gi, refl, refr = (int(x) for x in a["flags"])
     doc: dict = {
@@ -55,8 +59,12 @@ def arrays_to_crtscene(a: dict) -> dict:
             d["albedo"] = _vec(f[0:3])
         elif t == 1:
             d.update(edge_color=_vec(f[0:3]), inner_color=_vec(f[3:6]), edge_width=_f(f[6]))
-        else:
+        elif t == 2:
             d.update(color_A=_vec(f[0:3]), color_B=_vec(f[3:6]), square_size=_f(f[6]))
+        else:
+            if not bitmap_files or i not in bitmap_files:
+                raise ValueError(f"bitmap texture {i} needs its image file (bitmap_files)")
+            d["file_path"] = bitmap_files[i]
         textures.append(d)
     doc["textures"] = textures
     mats = []
@@ -80,7 +88,7 @@ def arrays_to_crtscene(a: dict) -> dict:
     return doc
 
 
-def write_crtscene(a: dict, path: str | Path) -> Path:
+def write_crtscene(a: dict, path: str | Path, bitmap_files: dict | None = None) -> Path:
     path = Path(path)
-    path.write_text(json.dumps(arrays_to_crtscene(a)))
+    path.write_text(json.dumps(arrays_to_crtscene(a, bitmap_files)))
     return path

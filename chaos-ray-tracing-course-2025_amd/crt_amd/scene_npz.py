@@ -15,6 +15,11 @@ import numpy as np
 from .native import (CameraDesc, LightDesc, MaterialDesc, MeshDesc, SceneDesc, TextureDesc, Vec3)
 
 
+def _texels(b8: np.ndarray) -> np.ndarray:
+    """read_stb's conversion of decoded bytes: byte / 255.0f in fp32 (crt_image_stbi.cpp:29-37)."""
+    return (b8.astype(np.float32) / np.float32(255.0)).astype(np.float32)
+
+
 def desc_to_arrays(d: SceneDesc) -> dict:
     out = {
         "background": np.array([d.background_color.x, d.background_color.y, d.background_color.z], np.float32),
@@ -31,8 +36,14 @@ def desc_to_arrays(d: SceneDesc) -> dict:
     tex_f, tex_i = [], []
     for i in range(d.texture_count):
         t = d.textures[i]
-        if t.type == 3:
-            raise ValueError("bitmap textures are not serialised")
+        if t.type == 3:   # decoded texels (fp32 = byte / 255.0f, crt_image_stbi.cpp:29-37), top row first
+            n = t.bitmap_width * t.bitmap_height * 3
+            rgb = np.ctypeslib.as_array(t.bitmap_rgb, (n,)).copy().reshape(t.bitmap_height, t.bitmap_width, 3)
+            b8 = np.clip(np.rint(rgb * 255.0), 0, 255).astype(np.uint8)
+            if np.array_equal(_texels(b8).view(np.uint32), rgb.view(np.uint32)):
+                out[f"tex{i}_rgb8"] = b8          # lossless: the bytes read_stb produced
+            else:
+                out[f"tex{i}_rgb"] = rgb
         tex_i.append(t.type)
         tex_f.append([t.color0.x, t.color0.y, t.color0.z, t.color1.x, t.color1.y, t.color1.z, t.scalar])
     out["tex_i"] = np.array(tex_i, np.int32)
@@ -80,6 +91,14 @@ class ArrayScene:
             self._tex[i].color0 = Vec3(*f[0:3])
             self._tex[i].color1 = Vec3(*f[3:6])
             self._tex[i].scalar = float(f[6])
+            rgb = a.get(f"tex{i}_rgb")
+            if rgb is None and f"tex{i}_rgb8" in a:
+                rgb = _texels(a[f"tex{i}_rgb8"])
+            if rgb is not None:
+                rgb = np.ascontiguousarray(rgb, np.float32)
+                a[f"tex{i}_rgb"] = rgb
+                self._tex[i].bitmap_height, self._tex[i].bitmap_width = rgb.shape[0], rgb.shape[1]
+                self._tex[i].bitmap_rgb = rgb.ctypes.data_as(C.POINTER(C.c_float))
         nl = len(a["lights"])
         self._lights = (LightDesc * max(nl, 1))()
         for i in range(nl):

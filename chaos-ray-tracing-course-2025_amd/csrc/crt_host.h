@@ -28,11 +28,19 @@ struct SceneFile {
     std::vector<crt_material_desc> materials;
     std::vector<crt_texture_desc> textures;
     std::vector<crt_light_desc> lights;
+    /* decoded bitmap texels (rgb fp32, byte / 255.0f), indexed like textures */
+    std::vector<std::vector<float>> bitmaps;
     std::string warning;
     void relink();
 };
 
 int parse_scene_json(const char *text, size_t len, const char *asset_root, SceneFile &out);
+
+/* read_stb (crt_image_stbi.cpp:16-40) without stb: decode an image file's
+ * bytes into 8-bit RGB (crt_image_decode.cpp).  comps = the file's component
+ * count as stbi_load reports it; false (with why) where read_stb fails. */
+bool decode_image_rgb8(const uint8_t *bytes, size_t len, int &w, int &h, int &comps, std::vector<uint8_t> &rgb,
+                       std::string &why);
 
 /* The scene after mesh prep and tree build, in device layout (crt_layout.h). */
 struct HostScene {

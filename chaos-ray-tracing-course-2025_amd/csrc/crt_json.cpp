@@ -415,8 +415,8 @@ static bool get_int_array(const Value &v, std::vector<int32_t> &out) {     /* :6
     return true;
 }
 
-static bool parse_textures(const Value &v, SceneFile &sf,
-                           std::unordered_map<std::string, int32_t> &names, std::string &why) {   /* :375-453 */
+static bool parse_textures(const Value &v, SceneFile &sf, std::unordered_map<std::string, int32_t> &names,
+                           const char *asset_root, std::string &why) {   /* :375-453 */
     if (!v.IsArray()) return false;
     for (size_t i = 0; i < v.Size(); ++i) {
         const Value &t = v.items[i];
@@ -447,11 +447,35 @@ static bool parse_textures(const Value &v, SceneFile &sf,
         } else if (type->Equals("bitmap")) {                                  /* :349-368 */
             const Value *fp = t.Find("file_path");
             if (!fp || !fp->IsString()) return false;
-            /* read_stb (crt_image_stbi.cpp:16-40) needs stb_image, an absent
-             * submodule: decoding is out of scope, so this behaves like a failed
-             * read_stb and the whole texture list is dropped (crt_json.cpp:582-588). */
-            why = "bitmap texture '" + fp->str + "' needs an image decoder (stb) that this build lacks";
-            return false;
+            /* asset_root / file_path.relative_path() (:358-360): the root name
+             * and root directory are dropped, so "/textures/a.jpg" is read
+             * under the scene's directory */
+            std::string rel = fp->str;
+            while (!rel.empty() && rel[0] == '/') rel.erase(0, 1);
+            const std::string root = asset_root ? asset_root : "";
+            const std::string path = root.empty() ? rel : (root.back() == '/' ? root + rel : root + "/" + rel);
+            std::ifstream in(path, std::ios::in | std::ios::binary);
+            std::vector<uint8_t> bytes;
+            if (in.is_open()) bytes.assign(std::istreambuf_iterator<char>(in), std::istreambuf_iterator<char>());
+            int bw = 0, bh = 0, comps = 0;
+            std::vector<uint8_t> rgb;
+            std::string dwhy;
+            /* a failed read_stb drops the whole texture list (crt_json.cpp:582-588) */
+            if (!in.is_open()) {
+                why = "bitmap texture '" + fp->str + "': cannot open " + path;
+                return false;
+            }
+            if (!decode_image_rgb8(bytes.data(), bytes.size(), bw, bh, comps, rgb, dwhy) || comps != 3) {
+                why = "bitmap texture '" + fp->str + "': " + (dwhy.empty() ? "not 3 components" : dwhy);
+                return false;
+            }
+            d.type = CRT_TEXTURE_BITMAP;
+            d.bitmap_width = bw;
+            d.bitmap_height = bh;
+            std::vector<float> texels(rgb.size());
+            for (size_t k = 0; k < rgb.size(); ++k) texels[k] = rgb[k] / 255.0f;   /* crt_image_stbi.cpp:29-37 */
+            sf.bitmaps.resize(sf.textures.size() + 1);
+            sf.bitmaps.back() = std::move(texels);
         } else {
             return false;
         }
@@ -560,7 +584,7 @@ static bool parse_lights(const Value &v, SceneFile &sf) {                  /* :2
     return true;
 }
 
-static bool parse_scene(const Value &doc, SceneFile &sf, std::string &why) {   /* :541-647 */
+static bool parse_scene(const Value &doc, SceneFile &sf, const char *asset_root, std::string &why) {   /* :541-647 */
     if (!doc.IsObject()) return false;
     const Value *settings = doc.Find("settings");
     if (!settings || !settings->IsObject()) return false;
@@ -596,8 +620,9 @@ static bool parse_scene(const Value &doc, SceneFile &sf, std::string &why) {   /
     std::unordered_map<std::string, int32_t> names;
     if (const Value *tx = doc.Find("textures")) {                            /* :582-588 */
         std::string tex_why;
-        if (!parse_textures(*tx, sf, names, tex_why)) {
+        if (!parse_textures(*tx, sf, names, asset_root, tex_why)) {
             sf.textures.clear();
+            sf.bitmaps.clear();
             names.clear();
             sf.warning = tex_why.empty() ? "texture list rejected" : tex_why;
         }
@@ -650,6 +675,9 @@ void SceneFile::relink() {
     desc.mesh_count = (int32_t)meshes.size();
     desc.materials = materials.data();
     desc.material_count = (int32_t)materials.size();
+    bitmaps.resize(textures.size());
+    for (size_t i = 0; i < textures.size(); ++i)
+        textures[i].bitmap_rgb = bitmaps[i].empty() ? nullptr : bitmaps[i].data();
     desc.textures = textures.data();
     desc.texture_count = (int32_t)textures.size();
     desc.lights = lights.data();
@@ -657,13 +685,12 @@ void SceneFile::relink() {
 }
 
 int parse_scene_json(const char *text, size_t len, const char *asset_root, SceneFile &out) {
-    (void)asset_root;   /* only bitmap textures use it (crt_json.cpp:360) */
     json::Value doc;
     json::Parser p(text, len);
     if (!p.parse_document(doc)) return set_error(CRT_E_PARSE, "Could not parse JSON (syntax)");
     std::memset(&out.desc, 0, sizeof out.desc);
     std::string why;
-    if (!json::parse_scene(doc, out, why))
+    if (!json::parse_scene(doc, out, asset_root, why))
         return set_error(CRT_E_PARSE, why.empty() ? "Invalid CRT scene" : "Invalid CRT scene: " + why);
     out.relink();
     return CRT_OK;

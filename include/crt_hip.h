@@ -154,8 +154,10 @@ typedef struct crt_work_counts {
 /* ---- host: scene file loader (crt_json.cpp:541-647) ------------------ */
 typedef struct crt_scene_file crt_scene_file;
 /* Parse .crtscene JSON text. Same accept/reject rules and defaults as the
- * reference loader; bitmap textures need a JPEG/PNG decoder (stb, absent) and
- * make texture parsing fail exactly as a failed read_stb would. */
+ * reference loader.  Bitmap textures are read from asset_root /
+ * relative_path(file_path) (crt_json.cpp:349-368) and decoded by
+ * crt_image_decode_rgb8; a file that cannot be read or decoded makes texture
+ * parsing fail exactly as a failed read_stb would (crt_json.cpp:582-588). */
 int  crt_scene_file_parse(const char *json_text, size_t len, const char *asset_root,
                           crt_scene_file **out);
 int  crt_scene_file_load(const char *path, crt_scene_file **out);
@@ -163,6 +165,15 @@ const crt_scene_desc *crt_scene_file_desc(const crt_scene_file *f);
 /* Override image size (the reference CLI has no flags; BASELINE configs need it). */
 int  crt_scene_file_set_resolution(crt_scene_file *f, int32_t width, int32_t height);
 void crt_scene_file_destroy(crt_scene_file *f);
+
+/* Replaces read_stb (src/core/crt_image_stbi.cpp:16-40, stbi_load with
+ * STBI_rgb): decode an image file held in memory into 8-bit RGB, top row
+ * first.  JPEG (baseline + progressive, stb_image's integer IDCT, upsampling
+ * and colour conversion — csrc/crt_image_decode.cpp).  *file_components is the
+ * file's component count as stbi_load reports it (the loader requires 3).
+ * With rgb_out NULL only the size is returned; otherwise cap >= w*h*3. */
+int  crt_image_decode_rgb8(const uint8_t *bytes, size_t len, int32_t *width, int32_t *height,
+                           int32_t *file_components, uint8_t *rgb_out, size_t cap);
 
 /* ---- host: scene preparation (no GPU needed) ------------------------- */
 typedef struct crt_host_scene crt_host_scene;

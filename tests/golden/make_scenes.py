@@ -23,6 +23,7 @@ SCENES = [
     "11-01-refractive/scene0", "11-01-refractive/scene1", "11-01-refractive/scene2",
     "11-01-refractive/scene3", "11-01-refractive/scene4", "11-01-refractive/scene5",
     "11-01-refractive/scene6", "11-01-refractive/scene7", "11-01-refractive/scene8",
+    "12-01-textures/scene3", "12-01-textures/scene4",
     "13-01-optimizations/scene0",
     "14-01-acceleration-tree/scene0", "14-01-acceleration-tree/scene1",
     "15-01-conclusion/scene0", "15-01-conclusion/scene1", "15-01-conclusion/scene2",

@@ -71,6 +71,8 @@ RENDER_CASES = [
     ("09-02-diffuse-smooth-shading__scene3", 160, 90, {}, True),
     ("09-03-reflective__scene5", 160, 90, {}, True),
     ("15-01-conclusion__scene1", 160, 90, {}, True),
+    ("12-01-textures__scene3", 192, 108, {}, True),     # JPEG bitmap texture
+    ("12-01-textures__scene4", 192, 108, {}, True),     # albedo / edges / checker / bitmap
     ("11-01-refractive__scene8", 160, 90, {"max_ray_depth": 8}, False),
     ("11-01-refractive__scene3", 160, 90, {}, False),
     ("15-01-conclusion__scene2", 48, 48, {}, False),

@@ -7,24 +7,28 @@ committed .npz (crt_amd.scene_json; its round trip through the loader is
 bit-exact, tests/test_loader.py::test_crtscene_writer_round_trip).
 """
 import json
+import shutil
 import subprocess
 import sys
 
 import numpy as np
 import pytest
 
-from conftest import PKG, bits, scene_npz
+from conftest import GOLDEN, PKG, bits, scene_npz
 
 pytestmark = pytest.mark.gpu
 
 CASES = [("14-01-acceleration-tree__scene1", 320, 180, {}),
-         ("09-03-reflective__scene5", 160, 90, {})]
+         ("09-03-reflective__scene5", 160, 90, {}),
+         ("12-01-textures__scene4", 192, 108, {})]      # bitmap texture read + decoded by the loader
 
 
 def _doc(name, w, h):
     from crt_amd.scene_json import arrays_to_crtscene
     sc = scene_npz(name).set_resolution(w, h)
-    doc = arrays_to_crtscene(sc.a)
+    # bitmap textures: the course's JPEG, next to the scene (tests/golden/textures)
+    bitmaps = {i: "/textures/dragon.jpg" for i, t in enumerate(sc.a["tex_i"]) if t == 3}
+    doc = arrays_to_crtscene(sc.a, bitmaps)
     doc["settings"]["image_settings"].update(width=w, height=h)
     return sc, doc
 
@@ -35,6 +39,7 @@ def test_cli_ppm_matches_oracle(tmp_path, oracle, name, w, h, over):
     sc, doc = _doc(name, w, h)
     scene = tmp_path / "scene.crtscene"
     scene.write_text(json.dumps(doc))
+    shutil.copytree(GOLDEN / "textures", tmp_path / "textures")
     out = tmp_path / "out.ppm"
     r = subprocess.run([str(PKG / "bin" / "crt_renderer"), str(scene), str(out)], capture_output=True, text=True,
                        timeout=120)
@@ -66,7 +71,7 @@ def test_crt_module_matches_oracle(oracle, name, w, h, over):
     st = native.RendererSettings.default(**over)
     settings = _crt.RendererSettings((st.max_ray_depth, st.diffuse_reflection_ray_count, st.shadow_bias,
                                       st.reflection_bias, st.diffuse_reflection_bias, st.refraction_bias))
-    px = _crt.render_scene_from_dict(doc, str(PKG), settings)
+    px = _crt.render_scene_from_dict(doc, str(GOLDEN), settings)
     assert len(px) == w * h and all(p[3] == 1.0 for p in px[:8])
     got = np.array([p[:3] for p in px], np.float32).reshape(h, w, 3)[::-1]   # bottom row first
     want = oracle.OracleScene(sc).render(st)

@@ -61,12 +61,13 @@ def test_scene_files_the_reference_rejects(rel):
 
 
 @pytest.mark.skipif(not has_reference(), reason="needs /root/reference scene files")
-def test_bitmap_scenes_need_a_decoder():
-    """12-01 textures include a JPEG bitmap: without stb the texture list is
-    dropped (crt_json.cpp:582-588) and the name lookup of the material fails."""
-    from crt_amd.native import ParseError, SceneFile
-    with pytest.raises(ParseError, match="bitmap"):
-        SceneFile(path=REFERENCE / "scenes" / "12-01-textures" / "scene0.crtscene")
+def test_bitmap_scenes_load_with_the_decoder():
+    """12-01 textures include a JPEG bitmap (read from the scene's directory,
+    crt_json.cpp:358-360, decoded by csrc/crt_image_decode.cpp): the texture
+    list survives and materials resolve the bitmap by name."""
+    from crt_amd.native import SceneFile
+    d = SceneFile(path=REFERENCE / "scenes" / "12-01-textures" / "scene3.crtscene").desc()
+    assert d.textures[d.materials[0].albedo_texture_index].type == 3
 
 
 # ---------------------------------------------------------------- defaults & rules
@@ -290,7 +291,9 @@ def test_crtscene_writer_round_trip(npz):
     from crt_amd.scene_json import arrays_to_crtscene
     from crt_amd.scene_npz import desc_to_arrays
     want = dict(np.load(npz))
-    got = desc_to_arrays(SceneFile(text=json.dumps(arrays_to_crtscene(want))).desc())
+    bitmaps = {i: "/textures/dragon.jpg" for i, t in enumerate(want["tex_i"]) if t == 3}   # tests/golden/textures
+    sf = SceneFile(text=json.dumps(arrays_to_crtscene(want, bitmaps)), asset_root=str(SCENES.parent))
+    got = desc_to_arrays(sf.desc())
     assert set(got) == set(want)
     for k in want:
         assert np.array_equal(bits(got[k]), bits(want[k])), k
