@@ -64,3 +64,29 @@ def test_no_gpu_means_loud_failure_not_fallback():
     with pytest.raises(N.CrtError) as e:
         N.HipScene(scene_npz("14-01-acceleration-tree__scene0"))
     assert e.value.code == N.CRT_E_HIP
+
+
+def test_blender_extension_package(tmp_path):
+    """scripts/package_blender.py: the add-on's files + _crt + lib/libcrt_hip.so;
+    the packaged _crt imports from the extracted directory (rpath $ORIGIN/lib)
+    and exposes the reference module's API (py_crt_module.cpp:16-169)."""
+    import subprocess
+    import sys
+    import zipfile
+    import pytest
+    from conftest import REFERENCE, has_reference
+    if not has_reference():
+        pytest.skip("needs the reference's src/blender add-on files")
+    out = tmp_path / "ext.zip"
+    subprocess.run([sys.executable, str(ROOT / "scripts" / "package_blender.py"), "--addon-src",
+                    str(REFERENCE / "src" / "blender"), "--out", str(out)], check=True, capture_output=True)
+    names = zipfile.ZipFile(out).namelist()
+    assert {"__init__.py", "bl_crt_engine.py", "blender_manifest.toml", "lib/libcrt_hip.so"} <= set(names)
+    assert any(n.startswith("_crt") and n.endswith(".so") for n in names)
+    zipfile.ZipFile(out).extractall(tmp_path / "x")
+    code = ("import sys; sys.path.insert(0, sys.argv[1]); import _crt; "
+            "s = _crt.RendererSettings((3, 4, 0.01, 0.01, 0.01, 0.01)); "
+            "print(_crt.DEFAULT_MAX_RAY_DEPTH, s.max_ray_depth, hasattr(_crt, 'render_scene_from_dict'))")
+    r = subprocess.run([sys.executable, "-c", code, str(tmp_path / "x")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["3", "3", "True"]

@@ -80,7 +80,8 @@ def test_crt_module_matches_oracle(oracle, name, w, h, over):
     assert rmse < 1e-4
     if not over:
         assert np.array_equal(bits(np.ascontiguousarray(got)), bits(want))
+    # the scene is parsed before the settings are checked (py_crt_module.cpp:90-99)
     with pytest.raises(TypeError):
-        _crt.render_scene_from_dict(doc, str(PKG), (1, 2, 3, 4, 5, 6))
+        _crt.render_scene_from_dict(doc, str(GOLDEN), (1, 2, 3, 4, 5, 6))
     with pytest.raises(ValueError):
         _crt.render_scene_from_dict({"settings": {}}, str(PKG), settings)
