@@ -823,6 +823,156 @@ __device__ int trace_packet_pruned(const DeviceScene &s, bool active, Vec o, Vec
     return best;
 }
 
+#ifndef CRT_WIN_NEXT_PREFETCH
+#define CRT_WIN_NEXT_PREFETCH 0   /* A/B: no gain, costs 11 spilled VGPRs */
+#endif
+#ifndef CRT_WIN_TRI_PREFETCH
+#define CRT_WIN_TRI_PREFETCH 1
+#endif
+/* ---------------------------------------------------------------------- */
+/* Window walk (TRAV 13, small tiles of ≤ 16 camera rays)                    */
+/* ---------------------------------------------------------------------- */
+/* The packet walk pays one dependent node load and ~90 instructions per node
+ * step whatever the number of rays; for the few heavy tiles that set a C2
+ * frame's length (2x2 / 4x4 splits of the dragon's silhouette, ~200 us waves
+ * of one-node steps) that is a latency chain.  Here a wave holds R rays (4 or
+ * 16) and K = 64 / R consecutive nodes of the walk's preorder at once: lane
+ * (slot s, ray r) loads node i + s and evaluates its hull and box tests for
+ * ray r, so a window of K nodes costs one round of loads.  The reach masks
+ * then advance over the window exactly as the packet walk would visit those
+ * nodes in order (bit depth+1 of an interior node := this ray entered it; a
+ * node is entered iff its reach bit is set and its box passed), every lane
+ * replaying its ray's sequence; evaluating a node no ray reaches is wasted
+ * work, never a change of result.  Hull tests use the best t known at the
+ * window's start (only ever larger than the packet walk's, so pruning stays
+ * conservative).  Each entered leaf's triangles are tested by the lane that
+ * entered it, and a ray's candidates are merged over its K lanes by the key
+ * (t, slot) — the reference's first-found rule in any order (key_better).
+ * The next window starts after the last one, or past the subtree of a window
+ * node no ray entered. */
+__device__ __forceinline__ int wave_max_i(int v) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const int o2 = __shfl_xor(v, off);
+        v = v > o2 ? v : o2;
+    }
+    return v;
+}
+
+template <bool COUNT>
+__device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool active, Vec o, Vec d, float &best_t,
+                            LaneCounts &c) {
+    const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
+    const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
+    const bool lead = sl == 0;                       /* one lane per ray for votes and counters */
+    if (COUNT && active && lead) ++c.traversals;
+    int best = -1;
+    best_t = 0.0f;
+    float lim = INFINITY;
+    unsigned long long reach = active ? 1ull : 0ull;
+    const int n = s.node_count;
+    const int K = 64 / R;
+    const int na = __popcll(__ballot(active && lead));
+    int oct = 0;
+    if (2 * __popcll(__ballot(active && lead && d.x < 0.0f)) > na) oct |= 1;
+    if (2 * __popcll(__ballot(active && lead && d.y < 0.0f)) > na) oct |= 2;
+    if (2 * __popcll(__ballot(active && lead && d.z < 0.0f)) > na) oct |= 4;
+    const PNode *nodes = pnode_order(s.pnodes, n, uniform_i(oct));
+    const unsigned long long rmask = (R >= 64) ? ~0ull : ((1ull << R) - 1ull);
+    int i = 0;
+    PNode nd = nodes[sl < n ? sl : n - 1];
+    while (i < n) {
+        const int j = i + sl;
+        const bool valid = j < n;
+        const bool interior = nd.count == 0;
+        const bool alive = valid & active & hull_alive(nd, pr, lim);
+        const bool pass = alive & box_hit_fast(o, d, rr, cell_of(nd));
+        const unsigned long long P = __ballot(pass);
+        /* replay the packet walk's reach update over the window, in order */
+        const int meta = nd.depth | (interior ? 256 : 0);
+        const int kk = n - i < K ? n - i : K;
+        bool my_in = false;
+        for (int a = 0; a < kk; ++a) {
+            const int m = __builtin_amdgcn_readlane(meta, a * R);
+            const int dd = m & 255;
+            const bool in = ((reach >> dd) & 1ull) != 0ull;
+            const bool e = in & (((P >> (a * R + r)) & 1ull) != 0ull);
+            if (m & 256) {
+                const unsigned long long bit = 2ull << dd;
+                reach = e ? (reach | bit) : (reach & ~bit);
+            }
+            my_in = (a == sl) ? in : my_in;
+        }
+        if (COUNT) {
+            if (my_in & alive) ++c.nodes;
+            ++c.wave_nodes;
+        }
+        const bool enter = my_in & pass;
+        const unsigned long long E = __ballot(enter);
+        /* skip past the subtree of a window node no ray entered */
+        const bool dead = valid & interior & (((E >> (sl * R)) & rmask) == 0ull);
+        const int skip_to = wave_max_i(dead ? nd.a : 0);
+        const int next = uniform_i(i + K > skip_to ? i + K : skip_to);
+        /* the next window's nodes are in flight while this window's leaves are tested */
+#if CRT_WIN_NEXT_PREFETCH
+        const int jn = next + sl;
+        const PNode nd_next = nodes[jn < n ? jn : n - 1];
+#endif
+        /* triangles of the entered leaves, one leaf per lane (next triangle
+         * prefetched), then a per-ray merge over the ray's K lanes */
+        const bool leaf = enter & !interior;
+        if (__ballot(leaf) != 0ull) {
+            float lt = best_t;
+            int ls = best;
+            if (leaf) {
+                const int first = nd.b, cnt = nd.count;
+                DTriGeo g = s.slots[first];
+                uint8_t cl = s.slot_cull[first];
+                for (int k = 0; k < cnt; ++k) {
+                    const int slot = first + k;
+#if CRT_WIN_TRI_PREFETCH
+                    const int sn = k + 1 < cnt ? slot + 1 : slot;
+                    const DTriGeo gn = s.slots[sn];
+                    const uint8_t cn = s.slot_cull[sn];
+#else
+                    g = s.slots[slot];
+                    cl = s.slot_cull[slot];
+                    const DTriGeo gn = g;
+                    const uint8_t cn = cl;
+#endif
+                    float t;
+                    if (COUNT) ++c.tris;
+                    if (tri_plane(o, d, g, cl != 0, t) && key_better(t, slot, lt, ls) && tri_edges(o, d, g, t)) {
+                        lt = t;
+                        ls = slot;
+                    }
+                    g = gn;
+                    cl = cn;
+                }
+            }
+            if (COUNT) c.wave_tris += (uint32_t)wave_max_i(leaf ? nd.count : 0);
+            for (int off = R; off < 64; off <<= 1) {
+                const float ot = __shfl_xor(lt, off);
+                const int os = __shfl_xor(ls, off);
+                if (os >= 0 && key_better(ot, os, lt, ls)) {
+                    lt = ot;
+                    ls = os;
+                }
+            }
+            best_t = lt;
+            best = ls;
+            lim = best >= 0 ? best_t : INFINITY;
+        }
+#if CRT_WIN_NEXT_PREFETCH
+        nd = nd_next;
+#else
+        nd = nodes[next + sl < n ? next + sl : n - 1];
+#endif
+        i = next;
+    }
+    if (COUNT && best >= 0 && lead) ++c.hits;
+    return best;
+}
+
 /* TRAV 9: per-lane pruned walk (crt_device.h walk_pruned) over the lane's own
  * octant order — scattered secondary rays. */
 template <bool COUNT>
@@ -852,7 +1002,7 @@ template <int TRAV, bool COUNT>
 __device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, bool active, Vec o, Vec d, float &best_t,
                                      LaneCounts &c) {
     if (TRAV == 8) return trace_packet_pruned<COUNT, false>(s, active, o, d, best_t, c);
-    if (TRAV == 12) return trace_packet_pruned<COUNT, true>(s, active, o, d, best_t, c);
+    if (TRAV == 12 || TRAV == 13) return trace_packet_pruned<COUNT, true>(s, active, o, d, best_t, c);
     if (TRAV == 9) return trace_lane_pruned<COUNT>(s, active, o, d, best_t, c);
     if (TRAV == 4) return trace_coop<COUNT, false>(s, *L, active, o, d, best_t, c);
     if (TRAV == 5) return trace_share<COUNT, false>(s, *L, active, o, d, best_t, c);
@@ -923,6 +1073,19 @@ __device__ __forceinline__ float pow5(float x) {
     r = r * r;
     r = r * xd;
     return (float)r;
+}
+
+/* shade_ray of a camera ray whose closest hit is known, for frames without
+ * recursion (FULL=false: diffuse / constant materials, GI off) — the same
+ * operations as shade_pixel<false>. */
+__device__ __forceinline__ Vec shade_primary(const DeviceScene &s, const DSettings &st, Vec o, Vec d, int slot, float t) {
+    if (slot < 0) return vec(s.background[0], s.background[1], s.background[2]);
+    HitRec h;
+    make_hit(s, o, d, t, slot, h);
+    const DMaterial m = s.materials[h.mat];
+    const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+    if (m.type == CRT_MATERIAL_DIFFUSE) return diffuse_finish(s, st, vec(0.f, 0.f, 0.f), h.p, h.n, alb);
+    return alb;
 }
 
 /* shade_ray for one camera ray (crt_renderer.cpp:46-155).
@@ -1090,11 +1253,14 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
     return col;
 }
 
+#ifndef CRT_WINDOW_WAVES
+#define CRT_WINDOW_WAVES 4   /* min waves/SIMD asked of the walk-13 kernel (A/B: 4 beats 1, 5, 6 on C2 and C5) */
+#endif
 #ifndef CRT_RENDER_BOUNDS
 #define CRT_RENDER_BOUNDS __launch_bounds__(256)
 #endif
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT>
-__global__ CRT_RENDER_BOUNDS void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
+__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT_WINDOW_WAVES : 1))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
                                                   const Tile *__restrict__ tiles,
                                                       int ntiles, float *__restrict__ out,
                                                       unsigned long long *__restrict__ counters,
@@ -1113,6 +1279,43 @@ __global__ CRT_RENDER_BOUNDS void k_render_tiles(const DeviceScene *__restrict__
      * dependent loads): they get issue priority over the light waves that
      * share their SIMD (s_setprio; scheduling only, results unchanged) */
     if (tl.prio) __builtin_amdgcn_s_setprio(3);
+    if constexpr (TRAV == 13 && !FULL) {
+        /* tiles of <= 16 rays (the measured plan's splits of heavy tiles): window walk */
+        const int tw = uniform_i(tl.w), th = uniform_i(tl.h);
+        const int npx = tw * th;
+        if (npx <= 16) {
+            const int R = npx <= 4 ? 4 : 16;
+            const int r = lane & (R - 1), sl = lane / R;
+            const bool act = r < npx;
+            const int px = act ? r % tw : 0, py = act ? r / tw : 0;
+            Vec o, d;
+            camera_ray(s, tl.x + px, tl.y + py, o, d);
+            LaneCounts cw = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+            float t;
+            const int slot = trace_window<COUNT>(s, R, r, sl, act, o, d, t, cw);
+            if (act && sl == 0) {
+                const Vec c = shade_primary(s, st, o, d, slot, t);
+                float *pxo = out + 3 * (tl.out_base + (int64_t)py * tl.out_stride + px);
+                pxo[0] = c.x;
+                pxo[1] = c.y;
+                pxo[2] = c.z;
+            }
+            if (stamps && lane == 0) stamps[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
+            if (COUNT) {
+                atomicAdd(&counters[0], (unsigned long long)cw.traversals);
+                atomicAdd(&counters[1], (unsigned long long)cw.nodes);
+                atomicAdd(&counters[2], (unsigned long long)cw.tris);
+                atomicAdd(&counters[3], (unsigned long long)cw.hits);
+                if (lane == 0) {
+                    atomicAdd(&counters[4], (unsigned long long)cw.wave_nodes);
+                    atomicAdd(&counters[5], (unsigned long long)cw.wave_tris);
+                    atomicAdd(&counters[6], (unsigned long long)cw.wave_edges);
+                    atomicAdd(&counters[7], 1ull);
+                }
+            }
+            return;
+        }
+    }
     const int lx = lane & 7, ly = lane >> 3;
     const bool has_px = lx < tl.w && ly < tl.h;
     /* the sharing walks keep pixel-less lanes as helpers (they take donated node
@@ -1169,7 +1372,7 @@ __global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restri
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
     (void)trace<TRAV, true>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px, o, d, t, cnt);
-    constexpr bool kPacket = (TRAV >= 6 && TRAV <= 8) || TRAV == 12;
+    constexpr bool kPacket = (TRAV >= 6 && TRAV <= 8) || TRAV == 12 || TRAV == 13;
     uint32_t c = kPacket ? cnt.wave_nodes + cnt.wave_tris + cnt.wave_edges : cnt.nodes + cnt.tris;
     for (int off = 32; off > 0; off >>= 1) {
         const uint32_t o2 = (uint32_t)__shfl_xor((int)c, off);
@@ -1458,6 +1661,7 @@ struct ShardPlan {
     int64_t packed_pixels = 0;
     std::vector<Tile> tiles;     /* host copy, dispatch order */
     std::vector<float> cost;     /* measured cost per tile (calibrated plans), else empty */
+    bool has_small = false;      /* some tile has <= 16 pixels (walk 13 runs them with the window walk) */
 };
 
 struct GiTables { float *d = nullptr; };   /* 4 * 2^23 floats on one device */
@@ -1537,6 +1741,7 @@ struct crt_hip_scene {
     std::vector<std::vector<SubTile>> calib;
     int calib_walk = -1;           /* primary walk the calibration was measured with (-1: none) */
     int calibrate = 1;             /* env CRT_CALIBRATE */
+    int window_walk = 1;           /* camera walk 12 -> 13 (window walk for split tiles), env CRT_WINDOW */
     float calib_k = 4.0f;          /* split a wave whose cost exceeds k x (total cost / wave slots) (env CRT_CALIB_K) */
     int calib_min = 2;             /* smallest sub-tile side (env CRT_CALIB_MIN: 1, 2, 4, 8) */
     int prio_tiles = 1024;         /* heaviest tiles run at raised issue priority (env CRT_PRIO) */
@@ -1683,6 +1888,8 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         tiles.swap(sorted);
     }
     plan.ntiles = (int)tiles.size();
+    plan.has_small = false;
+    for (const Tile &t : tiles) plan.has_small = plan.has_small || t.w * t.h <= 16;
     plan.tiles = tiles;
     if (!tiles.empty()) {
         void *p = nullptr;
@@ -1712,6 +1919,7 @@ int probe_tiles(crt_hip_scene *sc, const DeviceScene *d_scene, int walk, const s
         case 6: hipLaunchKernelGGL(k_probe_tiles<6>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         case 7: hipLaunchKernelGGL(k_probe_tiles<7>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         case 12: hipLaunchKernelGGL(k_probe_tiles<12>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
+        case 13: hipLaunchKernelGGL(k_probe_tiles<13>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         default: hipLaunchKernelGGL(k_probe_tiles<8>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         }
         e = hipGetLastError();
@@ -1828,7 +2036,9 @@ int check_settings(const crt_renderer_settings *st) {
 
 /* The packet walk camera rays take: walk 8 becomes its fast-only build 12
  * when the host has proven every camera ray fast. */
-int camera_walk(const crt_hip_scene *sc, int trav) { return (trav == 8 && sc->camera_fast) ? 12 : trav; }
+int camera_walk(const crt_hip_scene *sc, int trav) {
+    return (trav == 8 && sc->camera_fast) ? (sc->window_walk ? 13 : 12) : trav;
+}
 
 /* The primary walk a tile plan is measured with (-1: keep the estimate plan):
  * camera rays of diffuse frames and level 0 of the wavefront recursion. */
@@ -2009,7 +2219,8 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     if (full && !gi && sc->wavefront && packet && !stamps)
         return render_wavefront(sc, ds, plan, d_out, stream, count, d_scene, sec, camera_walk(sc, pruned ? 8 : 7));
     /* frame-stack kernel: one walk for every ray (packet walks hand over to sec) */
-    const int trav = full ? (packet ? sec : sc->traversal) : camera_walk(sc, sc->traversal);
+    int trav = full ? (packet ? sec : sc->traversal) : camera_walk(sc, sc->traversal);
+    if (trav == 13 && !plan.has_small) trav = 12;   /* no split tiles: the leaner packet-only kernel */
     const int blocks = (plan.ntiles + 3) / 4;
     const uint64_t frames = (uint64_t)st->max_ray_depth + 1;
     unsigned long long *cnt = sc->d_counters;
@@ -2035,6 +2246,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         case 7: if (count) CRT_LAUNCH_T(false, 0, 7, true); else CRT_LAUNCH_T(false, 0, 7, false); break;
         case 8: if (count) CRT_LAUNCH_T(false, 0, 8, true); else CRT_LAUNCH_T(false, 0, 8, false); break;
         case 12: if (count) CRT_LAUNCH_T(false, 0, 12, true); else CRT_LAUNCH_T(false, 0, 12, false); break;
+        case 13: if (count) CRT_LAUNCH_T(false, 0, 13, true); else CRT_LAUNCH_T(false, 0, 13, false); break;
         default: if (count) CRT_LAUNCH(false, 0, true); else CRT_LAUNCH(false, 0, false); break;
         }
     } else if (frames <= 4) {
@@ -2088,6 +2300,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     if (const char *e = std::getenv("CRT_WAVEFRONT")) sc->wavefront = std::atoi(e);
     if (const char *e = std::getenv("CRT_TRACE_WALK")) sc->trace_walk = std::atoi(e);
     if (const char *e = std::getenv("CRT_CALIBRATE")) sc->calibrate = std::atoi(e);
+    if (const char *e = std::getenv("CRT_WINDOW")) sc->window_walk = std::atoi(e);
     if (const char *e = std::getenv("CRT_CALIB_K")) sc->calib_k = (float)std::atof(e);
     if (const char *e = std::getenv("CRT_CALIB_MIN")) sc->calib_min = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("CRT_PRIO")) sc->prio_tiles = std::max(0, std::atoi(e));
@@ -2489,6 +2702,8 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         sc->secondary = value;
     } else if (k == "wavefront") {
         sc->wavefront = value != 0;
+    } else if (k == "window") {
+        sc->window_walk = value != 0;
     } else if (k == "calibrate") {
         sc->calibrate = value != 0;
         if (!sc->calibrate && sc->calib_walk >= 0) {   /* back to the estimate plan */

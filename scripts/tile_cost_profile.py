@@ -29,7 +29,10 @@ heavy = cost > np.percentile(cost, 99)
 out = {"tiles": int(len(cost)), "span_us": float(e.max()), "cost_total": float(cost.sum()),
        "cost_max": float(cost.max()), "cost_p50": float(np.median(cost)), "cost_p99": float(np.percentile(cost, 99)),
        "us_per_step_heavy": float(np.median(dur[heavy] / np.maximum(cost[heavy], 1))),
-       "top_by_duration": [[int(xywh[k, 0]), int(xywh[k, 1]), int(xywh[k, 2]), float(cost[k]), round(float(s[k]), 1),
-                            round(float(dur[k]), 1)] for k in top]}
+       "top_by_duration": [[int(xywh[k, 0]), int(xywh[k, 1]), int(xywh[k, 2]), int(xywh[k, 3]), float(cost[k]),
+                            round(float(s[k]), 1), round(float(dur[k]), 1)] for k in top],
+       "by_size": {f"{w}x{h}": [int(((xywh[:, 2] == w) & (xywh[:, 3] == h)).sum()),
+                                round(float(dur[(xywh[:, 2] == w) & (xywh[:, 3] == h)].max()), 1)]
+                   for w, h in sorted({(int(a), int(b)) for a, b in xywh[:, 2:4]})}}
 np.savez_compressed(ROOT / "gpurun_out" / f"tilecost_{scene}.npz", xywh=xywh, cost=cost, stamps=st)
 print(json.dumps(out))
