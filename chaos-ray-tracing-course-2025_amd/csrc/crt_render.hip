@@ -1744,6 +1744,7 @@ struct crt_hip_scene {
     int window_walk = 1;           /* camera walk 12 -> 13 (window walk for split tiles), env CRT_WINDOW */
     float calib_k = 4.0f;          /* split a wave whose cost exceeds k x (total cost / wave slots) (env CRT_CALIB_K) */
     int calib_min = 2;             /* smallest sub-tile side (env CRT_CALIB_MIN: 1, 2, 4, 8) */
+    int calib_direct = 0;          /* split a heavy tile straight to calib_min-sided tiles (env CRT_CALIB_DIRECT) */
     int prio_tiles = 1024;         /* heaviest tiles run at raised issue priority (env CRT_PRIO) */
     float prio_min = 2.0f;         /* ... if they cost more than this x the mean per wave slot */
     std::vector<void *> plan_allocs;   /* tile lists of the current plans */
@@ -1965,7 +1966,7 @@ int calibrate_plan(crt_hip_scene *sc, const DeviceScene *d_scene, int walk, hipS
             thresh = sc->calib_k * sum / std::max(1, sc->wave_slots);
         }
         std::vector<Item> next;
-        const int half = side / 2;
+        const int half = sc->calib_direct ? sc->calib_min : side / 2;
         for (size_t i = 0; i < cur.size(); ++i) {
             const Item &it = cur[i];
             if ((double)cost[i] > thresh && half >= sc->calib_min && (it.w > half || it.h > half)) {
@@ -2303,6 +2304,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     if (const char *e = std::getenv("CRT_WINDOW")) sc->window_walk = std::atoi(e);
     if (const char *e = std::getenv("CRT_CALIB_K")) sc->calib_k = (float)std::atof(e);
     if (const char *e = std::getenv("CRT_CALIB_MIN")) sc->calib_min = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("CRT_CALIB_DIRECT")) sc->calib_direct = std::atoi(e);
     if (const char *e = std::getenv("CRT_PRIO")) sc->prio_tiles = std::max(0, std::atoi(e));
     if (const char *e = std::getenv("CRT_PRIO_MIN")) sc->prio_min = (float)std::atof(e);
     if (const char *e = std::getenv("CRT_SPLIT")) {
