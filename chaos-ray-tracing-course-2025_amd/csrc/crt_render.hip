@@ -1260,7 +1260,7 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
 #define CRT_RENDER_BOUNDS __launch_bounds__(256)
 #endif
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT>
-__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT_WINDOW_WAVES : 1))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
+__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 || TRAV == 14 ? CRT_WINDOW_WAVES : 1))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
                                                   const Tile *__restrict__ tiles,
                                                       int ntiles, float *__restrict__ out,
                                                       unsigned long long *__restrict__ counters,
@@ -1279,7 +1279,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
      * dependent loads): they get issue priority over the light waves that
      * share their SIMD (s_setprio; scheduling only, results unchanged) */
     if (tl.prio) __builtin_amdgcn_s_setprio(3);
-    if constexpr (TRAV == 13 && !FULL) {
+    if constexpr ((TRAV == 13 || TRAV == 14) && !FULL) {
         /* tiles of <= 16 rays (the measured plan's splits of heavy tiles): window walk */
         const int tw = uniform_i(tl.w), th = uniform_i(tl.h);
         const int npx = tw * th;
@@ -1662,6 +1662,10 @@ struct ShardPlan {
     std::vector<Tile> tiles;     /* host copy, dispatch order */
     std::vector<float> cost;     /* measured cost per tile (calibrated plans), else empty */
     bool has_small = false;      /* some tile has <= 16 pixels (walk 13 runs them with the window walk) */
+    /* the same tiles partitioned (cost order kept inside each part) for the
+     * two-kernel launch of walk 13: window-walk tiles, then 8x8 tiles */
+    Tile *d_split = nullptr;
+    int nsmall = 0, nbig = 0;
 };
 
 struct GiTables { float *d = nullptr; };   /* 4 * 2^23 floats on one device */
@@ -1718,6 +1722,9 @@ struct crt_hip_scene {
     std::vector<void *> allocs;
     hipStream_t stream = nullptr;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    /* second stream + fork/join events of the two-kernel walk-13 launch */
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     ShardPlan full;
     std::map<std::pair<int, int>, ShardPlan> shard_plans;
     std::map<int, std::pair<UnpackBucket *, int>> unpack_plans;
@@ -1742,6 +1749,7 @@ struct crt_hip_scene {
     int calib_walk = -1;           /* primary walk the calibration was measured with (-1: none) */
     int calibrate = 1;             /* env CRT_CALIBRATE */
     int window_walk = 1;           /* camera walk 12 -> 13 (window walk for split tiles), env CRT_WINDOW */
+    int split_launch = 0;          /* walk 13 as two concurrent kernels (window tiles | 8x8 tiles), env CRT_SPLIT_LAUNCH; A/B: fork/join costs more than the 8x8 kernel gains (C2 0.226 vs 0.177 ms) */
     float calib_k = 4.0f;          /* split a wave whose cost exceeds k x (total cost / wave slots) (env CRT_CALIB_K) */
     int calib_min = 2;             /* smallest sub-tile side (env CRT_CALIB_MIN: 1, 2, 4, 8) */
     int calib_direct = 0;          /* split a heavy tile straight to calib_min-sided tiles (env CRT_CALIB_DIRECT) */
@@ -1898,6 +1906,23 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         HIP_TRY(hipMemcpy(p, tiles.data(), tiles.size() * sizeof(Tile), hipMemcpyHostToDevice));
         sc->plan_allocs.push_back(p);
         plan.d_tiles = static_cast<Tile *>(p);
+    }
+    plan.d_split = nullptr;
+    plan.nsmall = plan.nbig = 0;
+    if (plan.has_small) {
+        std::vector<Tile> part;
+        part.reserve(tiles.size());
+        for (const Tile &t : tiles)
+            if (t.w * t.h <= 16) part.push_back(t);
+        plan.nsmall = (int)part.size();
+        for (const Tile &t : tiles)
+            if (t.w * t.h > 16) part.push_back(t);
+        plan.nbig = (int)part.size() - plan.nsmall;
+        void *p = nullptr;
+        HIP_TRY(hipMalloc(&p, part.size() * sizeof(Tile)));
+        HIP_TRY(hipMemcpy(p, part.data(), part.size() * sizeof(Tile), hipMemcpyHostToDevice));
+        sc->plan_allocs.push_back(p);
+        plan.d_split = static_cast<Tile *>(p);
     }
     return CRT_OK;
 }
@@ -2141,7 +2166,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
 #define CRT_WF0(T, COUNT)                                                                                   \
     hipLaunchKernelGGL((k_wf_level<T, true, COUNT>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,      \
                        plan.d_tiles, plan.ntiles, lv, cnt)
-    if (primary == 12) {
+    if (primary == 12 || primary == 13) {   /* level 0 keeps 8x8 tiles' packet walk (no window build) */
         if (count) CRT_WF0(12, true); else CRT_WF0(12, false);
     } else if (primary == 8) {
         if (count) CRT_WF0(8, true); else CRT_WF0(8, false);
@@ -2241,6 +2266,36 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         default: return set_error(CRT_E_INVALID, "no such walk for this kernel");                         \
         }                                                                                                  \
     } while (0)
+    if (!full && trav == 13 && plan.d_split && sc->split_launch && !stamps) {
+        /* window-walk tiles (kernel 14, ~120 VGPRs) on a second stream, 8x8
+         * tiles (kernel 12, 75 VGPRs, 6 waves/SIMD) on the caller's stream,
+         * concurrently; the caller's stream waits for both */
+        if (!sc->stream2) {
+            HIP_TRY(hipStreamCreateWithFlags(&sc->stream2, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&sc->ev_fork, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&sc->ev_join, hipEventDisableTiming));
+        }
+        HIP_TRY(hipEventRecord(sc->ev_fork, stream));
+        HIP_TRY(hipStreamWaitEvent(sc->stream2, sc->ev_fork, 0));
+        const int bs = (plan.nsmall + 3) / 4, bb = (plan.nbig + 3) / 4;
+        if (count) {
+            hipLaunchKernelGGL((k_render_tiles<false, 0, 14, 14, true>), dim3(bs), dim3(256), 0, sc->stream2, d_scene, ds,
+                               plan.d_split, plan.nsmall, d_out, cnt, stamps);
+            if (bb > 0)
+                hipLaunchKernelGGL((k_render_tiles<false, 0, 12, 12, true>), dim3(bb), dim3(256), 0, stream, d_scene, ds,
+                                   plan.d_split + plan.nsmall, plan.nbig, d_out, cnt, stamps);
+        } else {
+            hipLaunchKernelGGL((k_render_tiles<false, 0, 14, 14, false>), dim3(bs), dim3(256), 0, sc->stream2, d_scene,
+                               ds, plan.d_split, plan.nsmall, d_out, cnt, stamps);
+            if (bb > 0)
+                hipLaunchKernelGGL((k_render_tiles<false, 0, 12, 12, false>), dim3(bb), dim3(256), 0, stream, d_scene,
+                                   ds, plan.d_split + plan.nsmall, plan.nbig, d_out, cnt, stamps);
+        }
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(sc->ev_join, sc->stream2));
+        HIP_TRY(hipStreamWaitEvent(stream, sc->ev_join, 0));
+        return CRT_OK;
+    }
     if (!full) {
         switch (trav) {
         case 6: if (count) CRT_LAUNCH_T(false, 0, 6, true); else CRT_LAUNCH_T(false, 0, 6, false); break;
@@ -2302,6 +2357,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     if (const char *e = std::getenv("CRT_TRACE_WALK")) sc->trace_walk = std::atoi(e);
     if (const char *e = std::getenv("CRT_CALIBRATE")) sc->calibrate = std::atoi(e);
     if (const char *e = std::getenv("CRT_WINDOW")) sc->window_walk = std::atoi(e);
+    if (const char *e = std::getenv("CRT_SPLIT_LAUNCH")) sc->split_launch = std::atoi(e);
     if (const char *e = std::getenv("CRT_CALIB_K")) sc->calib_k = (float)std::atof(e);
     if (const char *e = std::getenv("CRT_CALIB_MIN")) sc->calib_min = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("CRT_CALIB_DIRECT")) sc->calib_direct = std::atoi(e);
@@ -2477,6 +2533,10 @@ void crt_hip_scene_destroy(crt_hip_scene *sc) {
     for (auto &kv : sc->unpack_plans) (void)hipFree(kv.second.first);
     if (sc->ev_start) (void)hipEventDestroy(sc->ev_start);
     if (sc->ev_stop) (void)hipEventDestroy(sc->ev_stop);
+    if (sc->stream2) (void)hipStreamSynchronize(sc->stream2);
+    if (sc->ev_fork) (void)hipEventDestroy(sc->ev_fork);
+    if (sc->ev_join) (void)hipEventDestroy(sc->ev_join);
+    if (sc->stream2) (void)hipStreamDestroy(sc->stream2);
     if (sc->stream) (void)hipStreamDestroy(sc->stream);
     delete sc;
 }
@@ -2706,6 +2766,8 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         sc->wavefront = value != 0;
     } else if (k == "window") {
         sc->window_walk = value != 0;
+    } else if (k == "split_launch") {
+        sc->split_launch = value != 0;
     } else if (k == "calibrate") {
         sc->calibrate = value != 0;
         if (!sc->calibrate && sc->calib_walk >= 0) {   /* back to the estimate plan */
