@@ -269,7 +269,10 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  * walk, whose work counters equal the reference's; 8 = pruned packet walk,
  * default; 0..6, 9 = other variants), "secondary" (0 = by walk, 4, 5, 9),
  * "wavefront" (0/1: level-by-level recursion when GI is off), "trace_walk"
- * (crt_hip_trace_batch: 0 = reference order, 1 = pruned per-ray walk).
+ * (crt_hip_trace_batch: 0 = reference order, 1 = pruned per-ray walk),
+ * "window" (0/1, default 1: the plan's split tiles of <= 16 camera rays take
+ * the window walk), "split_launch" (0/1, default 0: window tiles and 8x8
+ * tiles as two concurrent kernels), "calibrate" (0/1: measured-cost tile plan).
  * Environment variables CRT_TRAVERSAL, CRT_SECONDARY, CRT_WAVEFRONT and
  * CRT_TRACE_WALK set the initial values. */
 int  crt_hip_scene_set_option(crt_hip_scene *scene, const char *name, int value);

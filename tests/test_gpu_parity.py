@@ -185,3 +185,26 @@ def test_shard_render_and_unpack(N, shards):
         hip.hipFree(gathered)
         hip.hipFree(frame)
     del native
+
+
+@pytest.mark.parametrize("calib_k", ["4", "1.5"])
+def test_window_walk_equals_packet_walk(N, oracle, monkeypatch, calib_k):
+    """Walk 13 (window walk for the plan's split tiles) against
+    walk 12 and the oracle on the C2 frame; a low split threshold puts many
+    4x4 (16 rays x 4 nodes) and 2x2 (4 rays x 16 nodes) tiles through it, and
+    the two-kernel launch option must give the same bits."""
+    monkeypatch.setenv("CRT_CALIB_K", calib_k)
+    sc = scene_npz("14-01-acceleration-tree__scene1")
+    st = N.RendererSettings.default()
+    win = N.HipScene(sc)
+    xywh, _ = win.plan_tiles(st)
+    sizes = {(int(w), int(h)) for w, h in xywh[:, 2:4]}
+    assert (2, 2) in sizes or (4, 4) in sizes
+    a = win.render(st)
+    b = N.HipScene(sc, window=0).render(st)
+    c = N.HipScene(sc, split_launch=1).render(st)
+    want = oracle.OracleScene(sc).render(st)
+    assert np.array_equal(bits(a), bits(want))
+    assert np.array_equal(bits(b), bits(want)) and np.array_equal(bits(c), bits(want))
+    ca, cb = win.count_work(st), N.HipScene(sc, window=0).count_work(st)
+    assert ca["traversals"] == cb["traversals"] == 1920 * 1080 and ca["hits"] == cb["hits"]
