@@ -46,7 +46,19 @@ from crt_amd import native as N  # noqa: E402
 from crt_amd.distributed import FramePipeline  # noqa: E402
 from crt_amd.scene_npz import load_npz  # noqa: E402
 
-SCENE_NPZ = ROOT / "tests" / "golden" / "scenes" / "14-01-acceleration-tree__scene1.npz"
+SCENES = ROOT / "tests" / "golden" / "scenes"
+# BASELINE.json configs: c2 is the headline (metric) workload; the others are
+# the remaining single-GPU-sized configs, for --config runs (N>1 as for c2)
+CONFIGS = {
+    "c2": {"scene": "14-01-acceleration-tree__scene1", "size": (1920, 1080), "settings": {}, "cpu_size": (1920, 1080),
+           "label": "14-01-acceleration-tree/scene1", "note": "primary rays (HEAD traces no shadow rays)"},
+    "c3": {"scene": "11-01-refractive__scene8", "size": (1920, 1080), "settings": {"max_ray_depth": 8},
+           "cpu_size": (480, 270), "label": "11-01-refractive/scene8", "note": "depth-8 reflect/refract recursion"},
+    "c4": {"scene": "15-01-conclusion__scene2", "size": (3840, 2160), "settings": {}, "cpu_size": (240, 135),
+           "label": "15-01-conclusion/scene2", "note": "GI 4 rays, depth 3 (the CLI default scene)"},
+    "c5": {"synthetic": 1_000_000, "size": (3840, 2160), "settings": {}, "cpu_size": (480, 270),
+           "label": "synthetic 1M-triangle random mesh", "note": "deep KD-tree, HBM-resident scene"},
+}
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 NODE_BYTES, TRI_BYTES, PIXEL_BYTES = 32, 52, 12   # SURVEY §8(d) algorithmic bytes
 
@@ -56,8 +68,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--width", type=int, default=1920)
-    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--config", choices=sorted(CONFIGS), default="c2",
+                   help="BASELINE config (c2 = the headline metric workload)")
+    p.add_argument("--width", type=int, default=None, help="override the config's image width")
+    p.add_argument("--height", type=int, default=None, help="override the config's image height")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (wall s)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
@@ -70,7 +84,14 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(scene, settings, seconds: float) -> dict:
+def make_scene(cfg: dict, width: int, height: int):
+    if "synthetic" in cfg:
+        from crt_amd.synthetic import c5_scene
+        return c5_scene(cfg["synthetic"], width=width, height=height)
+    return load_npz(SCENES / f"{cfg['scene']}.npz").set_resolution(width, height)
+
+
+def cpu_baseline(scene, settings, seconds: float, size_note: str = "") -> dict:
     from oracle import pyoracle
     from crt_amd.native import WorkCounts
     threads = min(16, os.cpu_count() or 1)
@@ -94,7 +115,7 @@ def cpu_baseline(scene, settings, seconds: float) -> dict:
     except OSError:
         pass
     return {"value": rays / el / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{frames} full frames of the same workload, oracle/crt_oracle.cpp render_image "
+            "sample": f"{frames} full frames of the same workload{size_note}, oracle/crt_oracle.cpp render_image "
                       f"(bucket queue, {threads} threads, g++ -O3 no FMA) on {model or 'host CPU'}, "
                       f"{el:.1f} s wall"}
 
@@ -112,10 +133,11 @@ def main():
         else:
             dist.init_process_group(a.backend)
 
-    scene = load_npz(SCENE_NPZ).set_resolution(a.width, a.height)
-    settings = N.RendererSettings.default()
+    cfg = CONFIGS[a.config]
+    W, H = a.width or cfg["size"][0], a.height or cfg["size"][1]
+    scene = make_scene(cfg, W, H)
+    settings = N.RendererSettings.default(**cfg["settings"])
     gpu = N.HipScene(scene, device=local)
-    W, H = a.width, a.height
     # an explicit stream: the render kernel, the gather and the timing events
     # all go on it (handle 0 would mean "the scene's own stream" to the C-ABI)
     stream = torch.cuda.Stream()
@@ -211,7 +233,7 @@ def main():
     traffic = None
     try:
         tj = json.loads(Path(a.traffic_json).read_text())
-        if tj.get("workload") == f"14-01/scene1 {W}x{H}" and world == 1:
+        if a.config == "c2" and tj.get("workload") == f"14-01/scene1 {W}x{H}" and world == 1:
             traffic = tj.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -220,9 +242,12 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
-            cpu = cpu_baseline(scene, settings, a.cpu_seconds)
+            cw, ch = cfg["cpu_size"] if (W, H) == cfg["size"] else (W, H)
+            note = "" if (cw, ch) == (W, H) else f" at {cw}x{ch} (same scene and settings; Mrays/s is per-ray work, size-independent up to image content)"
+            cpu = cpu_baseline(scene if (cw, ch) == (W, H) else make_scene(cfg, cw, ch), settings, a.cpu_seconds, note)
         out = {
-            "metric": "Mrays/sec + frame ms, 1920x1080 scene 14-01",
+            "metric": ("Mrays/sec + frame ms, 1920x1080 scene 14-01" if a.config == "c2"
+                       else f"Mrays/sec + frame ms, {W}x{H} {cfg['label']}"),
             "value": round(mrays, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -233,9 +258,11 @@ def main():
             "scaling": "strong" if tiles else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "scene file scenes/14-01-acceleration-tree/scene1.crtscene (parsed fixture tests/golden/scenes)",
-            "config": {"workload": f"14-01-acceleration-tree/scene1 {W}x{H}, RendererSettings defaults "
-                                   f"(max_ray_depth 3), primary rays (HEAD traces no shadow rays)",
+            "data": (f"scene file scenes/{cfg['label']}.crtscene (parsed fixture tests/golden/scenes)" if "scene" in cfg
+                     else "synthetic mesh (crt_amd.synthetic.c5_scene, SURVEY §8(d) C5 spec)"),
+            "config": {"workload": f"{cfg['label']} {W}x{H}, RendererSettings defaults "
+                                   f"(max_ray_depth {settings.max_ray_depth}), {cfg['note']}",
+                       "config": a.config,
                        "rays_per_frame": rays_per_frame, "node_tests_per_frame": counts["node_tests"],
                        "triangle_tests_per_frame": counts["triangle_tests"],
                        "parallelism": (f"bucket-shard{world}+rccl-gather" if tiles else
