@@ -1253,6 +1253,11 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
     return col;
 }
 
+#ifndef CRT_GI_WAVES
+#define CRT_GI_WAVES 5       /* min waves/SIMD asked of the depth<=3 frame-stack (GI) kernels: 96 VGPRs
+                                * + 17 spilled beat 114 VGPRs at 4 waves (C4 1080^2: 102.8 vs 111.7 ms) and
+                                * 80 VGPRs at 6 waves (116.6 ms) in same-box A/B */
+#endif
 #ifndef CRT_WINDOW_WAVES
 #define CRT_WINDOW_WAVES 4   /* min waves/SIMD asked of the walk-13 kernel (A/B: 4 beats 1, 5, 6 on C2 and C5) */
 #endif
@@ -1260,7 +1265,7 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
 #define CRT_RENDER_BOUNDS __launch_bounds__(256)
 #endif
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT>
-__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 || TRAV == 14 ? CRT_WINDOW_WAVES : 1))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
+__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 || TRAV == 14 ? CRT_WINDOW_WAVES : (FULL && MAXF == 4 ? CRT_GI_WAVES : 1)))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
                                                   const Tile *__restrict__ tiles,
                                                       int ntiles, float *__restrict__ out,
                                                       unsigned long long *__restrict__ counters,
