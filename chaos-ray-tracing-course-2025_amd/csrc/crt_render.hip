@@ -1425,7 +1425,13 @@ struct WLevel {
 };
 
 template <int TRAV, bool LEVEL0, bool COUNT>
-__global__ __launch_bounds__(256) void k_wf_level(const DeviceScene *__restrict__ scene, DSettings st,
+#ifndef CRT_WF_WAVES
+#define CRT_WF_WAVES 1       /* min waves/SIMD asked of the wavefront levels >= 1 */
+#endif
+#ifndef CRT_WF0_WAVES
+#define CRT_WF0_WAVES 1      /* ... and of level 0 (camera rays) */
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CRT_WF0_WAVES : CRT_WF_WAVES))) void k_wf_level(const DeviceScene *__restrict__ scene, DSettings st,
                                                   const Tile *__restrict__ tiles, int ntiles, WLevel lv,
                                                   unsigned long long *__restrict__ counters) {
     const DeviceScene &s = *scene;
