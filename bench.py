@@ -137,7 +137,9 @@ def main():
     W, H = a.width or cfg["size"][0], a.height or cfg["size"][1]
     scene = make_scene(cfg, W, H)
     settings = N.RendererSettings.default(**cfg["settings"])
-    gpu = N.HipScene(scene, device=local)
+    # the library's own start/stop events (crt_hip_last_kernel_ms) would sit inside
+    # this script's timing events and add ~8 us per frame: timing here uses torch's
+    gpu = N.HipScene(scene, device=local, events=0)
     # an explicit stream: the render kernel, the gather and the timing events
     # all go on it (handle 0 would mean "the scene's own stream" to the C-ABI)
     stream = torch.cuda.Stream()

@@ -1760,6 +1760,8 @@ struct crt_hip_scene {
     int calib_walk = -1;           /* primary walk the calibration was measured with (-1: none) */
     int calibrate = 1;             /* env CRT_CALIBRATE */
     int window_walk = 1;           /* camera walk 12 -> 13 (window walk for split tiles), env CRT_WINDOW */
+    int record_events = 1;         /* start/stop events around every render (crt_hip_last_kernel_ms), option "events" */
+    bool events_valid = false;
     int split_launch = 0;          /* walk 13 as two concurrent kernels (window tiles | 8x8 tiles), env CRT_SPLIT_LAUNCH; A/B: fork/join costs more than the 8x8 kernel gains (C2 0.226 vs 0.177 ms) */
     float calib_k = 4.0f;          /* split a wave whose cost exceeds k x (total cost / wave slots) (env CRT_CALIB_K) */
     int calib_min = 2;             /* smallest sub-tile side (env CRT_CALIB_MIN: 1, 2, 4, 8) */
@@ -2340,10 +2342,11 @@ int render_into(crt_hip_scene *sc, const crt_renderer_settings *st, float *d_rgb
     }
     int rc = ensure_plans(sc, st, stream);
     if (rc != CRT_OK) return rc;
-    HIP_TRY(hipEventRecord(sc->ev_start, stream));
+    if (sc->record_events) HIP_TRY(hipEventRecord(sc->ev_start, stream));
     rc = launch_render(sc, st, sc->full, d_rgb, stream, count);
     if (rc != CRT_OK) return rc;
-    HIP_TRY(hipEventRecord(sc->ev_stop, stream));
+    if (sc->record_events) HIP_TRY(hipEventRecord(sc->ev_stop, stream));
+    sc->events_valid = sc->record_events != 0;
     return CRT_OK;
 }
 
@@ -2369,6 +2372,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     if (const char *e = std::getenv("CRT_CALIBRATE")) sc->calibrate = std::atoi(e);
     if (const char *e = std::getenv("CRT_WINDOW")) sc->window_walk = std::atoi(e);
     if (const char *e = std::getenv("CRT_SPLIT_LAUNCH")) sc->split_launch = std::atoi(e);
+    if (const char *e = std::getenv("CRT_EVENTS")) sc->record_events = std::atoi(e);
     if (const char *e = std::getenv("CRT_CALIB_K")) sc->calib_k = (float)std::atof(e);
     if (const char *e = std::getenv("CRT_CALIB_MIN")) sc->calib_min = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("CRT_CALIB_DIRECT")) sc->calib_direct = std::atoi(e);
@@ -2576,7 +2580,8 @@ int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rg
     if (stats) {
         std::memset(stats, 0, sizeof *stats);
         float ms = 0.f;
-        if (!sc->grid_empty && sc->full.ntiles > 0) HIP_TRY(hipEventElapsedTime(&ms, sc->ev_start, sc->ev_stop));
+        if (!sc->grid_empty && sc->full.ntiles > 0 && sc->events_valid)
+            HIP_TRY(hipEventElapsedTime(&ms, sc->ev_start, sc->ev_stop));
         stats->kernel_ms = ms;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         stats->width = sc->info.width;
@@ -2588,6 +2593,7 @@ int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rg
 int crt_hip_last_kernel_ms(crt_hip_scene *sc, double *ms) {
     if (!sc || !ms) return set_error(CRT_E_INVALID, "null argument");
     HIP_TRY(hipSetDevice(sc->device));
+    if (!sc->events_valid) return set_error(CRT_E_INVALID, "no timed render (option \"events\" is off)");
     HIP_TRY(hipEventSynchronize(sc->ev_stop));
     float f = 0.f;
     HIP_TRY(hipEventElapsedTime(&f, sc->ev_start, sc->ev_stop));
@@ -2628,10 +2634,11 @@ int crt_hip_render_shard(crt_hip_scene *sc, const crt_renderer_settings *st, int
         if ((rc = make_tile_plan(sc, b, false, plan)) != CRT_OK) return rc;
         it = sc->shard_plans.emplace(key, plan).first;
     }
-    HIP_TRY(hipEventRecord(sc->ev_start, s));
+    if (sc->record_events) HIP_TRY(hipEventRecord(sc->ev_start, s));
     rc = launch_render(sc, st, it->second, d_packed, s, false);
     if (rc != CRT_OK) return rc;
-    HIP_TRY(hipEventRecord(sc->ev_stop, s));
+    if (sc->record_events) HIP_TRY(hipEventRecord(sc->ev_stop, s));
+    sc->events_valid = sc->record_events != 0;
     return CRT_OK;
 }
 
@@ -2779,6 +2786,8 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         sc->window_walk = value != 0;
     } else if (k == "split_launch") {
         sc->split_launch = value != 0;
+    } else if (k == "events") {
+        sc->record_events = value != 0;
     } else if (k == "calibrate") {
         sc->calibrate = value != 0;
         if (!sc->calibrate && sc->calib_walk >= 0) {   /* back to the estimate plan */
