@@ -126,6 +126,7 @@ struct DeviceScene {
     float tan_half_fov;     /* std::tan(fov_radians * 0.5f)     (crt_camera.cpp:26-27) */
     float background[3];
     int32_t gi_on, reflections_on, refractions_on;
+    int32_t oct_mask;       /* per-lane pruned walks: node order = octant(d) & oct_mask (7: the ray's own octant) */
 };
 
 /* Renderer settings as the kernels see them (crt_renderer.h:18-25). */

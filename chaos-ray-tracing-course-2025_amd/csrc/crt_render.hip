@@ -278,7 +278,7 @@ template <> struct WalkNode<false> {
 template <> struct WalkNode<true> {
     using T = PNode;
     static __device__ __forceinline__ const PNode *base(const DeviceScene &s, Vec d) {
-        return pnode_order(s.pnodes, s.node_count, ray_octant(d));
+        return pnode_order(s.pnodes, s.node_count, ray_octant(d) & s.oct_mask);
     }
     static __device__ __forceinline__ DNode cell(const PNode &n) { return cell_of(n); }
     static __device__ __forceinline__ bool alive(const PNode &n, const PruneRay &p, float lim) {
@@ -313,6 +313,7 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
     Vec ro = o, rd = d;
     const NT *nb = WN::base(s, d);
     PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
+    RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);   /* hoisted exact divisions (box_hit_r) */
     float lim = INFINITY;               /* best t known for the piece's ray (pruning bound) */
     unsigned long long mine = ~0ull;    /* best key found in the current piece */
     int sp = 0;                         /* wave-uniform stack depth */
@@ -335,6 +336,7 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
                     ro = vec(L.ray[r][0], L.ray[r][1], L.ray[r][2]);
                     rd = vec(L.ray[r][3], L.ray[r][4], L.ray[r][5]);
                     nb = WN::base(s, rd);
+                    rr = make_ray_rcp(ro, rd, s.planes_ok != 0);
                     if (PRUNE) {
                         pr = make_prune_ray(ro, rd, s.prune_origin_max);
                         lim = key_t(L.key[r]);
@@ -367,7 +369,7 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
                 const NT n2 = nb[alt];
                 bool pass = false;
                 if (WN::alive(nd, pr, lim)) {
-                    pass = box_hit_bf(ro, rd, WN::cell(nd));
+                    pass = box_hit_r(ro, rd, rr, WN::cell(nd));
                     if (COUNT) ++c.nodes;
                 }
                 if (nd.b < 0) {
@@ -1422,6 +1424,7 @@ struct WLevel {
     int32_t out_base;        /* id of out[0] */
     WNode *nodes;            /* by ray id */
     DVec4 *cols;             /* by ray id */
+    int32_t rpw;             /* levels >= 1: rays per wave (lanes rpw..63 start idle and take donated pieces) */
 };
 
 template <int TRAV, bool LEVEL0, bool COUNT>
@@ -1449,10 +1452,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         has = lx < tl.w && ly < tl.h;
         if (has) camera_ray(s, tl.x + lx, tl.y + ly, o, d);
     } else {
-        if ((gid & ~63) >= lv.n) return;   /* whole wave past the queue */
-        has = gid < lv.n;
+        const int ray0 = (gid >> 6) * lv.rpw;
+        if (ray0 >= lv.n) return;          /* whole wave past the queue */
+        const int ray = ray0 + lane;
+        has = lane < lv.rpw && ray < lv.n;
         if (has) {
-            const WRay r = lv.in[gid];
+            const WRay r = lv.in[ray];
             o = vec(r.ox, r.oy, r.oz);
             d = vec(r.dx, r.dy, r.dz);
             id = r.id;
@@ -1555,6 +1560,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         atomicAdd(&counters[1], (unsigned long long)cnt.nodes);
         atomicAdd(&counters[2], (unsigned long long)cnt.tris);
         atomicAdd(&counters[3], (unsigned long long)cnt.hits);
+        /* levels >= 1 (coop walks): loop rounds per wave — sum, longest wave, waves */
+        if (!LEVEL0 && kCoop && lane == 0) {
+            atomicAdd(&counters[4], (unsigned long long)cnt.wave_nodes);
+            atomicMax(&counters[6], (unsigned long long)cnt.wave_nodes);
+            atomicAdd(&counters[7], 1ull);
+        }
     }
 }
 
@@ -1778,6 +1789,9 @@ struct crt_hip_scene {
     const int32_t *dt_ref_children = nullptr, *dt_ref_leaf_tris = nullptr;
     const int64_t *dt_ref_leaf_off = nullptr;
     int wavefront = 1;             /* level-by-level recursion when GI is off (env CRT_WAVEFRONT) */
+    int wf_oct_mask = 7;           /* node-order octant mask of wavefront levels >= 1 (env CRT_WF_OCT, option "wf_oct") */
+    int wf_oct_uploaded = -1;
+    int wf_rays_per_wave = 32;     /* rays per wave of wavefront levels >= 1, coop walks (env CRT_WF_RPW, option "wf_rpw"); C3: 64 4.70, 32 4.53, 16 4.58 ms */
     WfBuffers wf;
 };
 
@@ -2052,16 +2066,21 @@ int ensure_gi_tables(crt_hip_scene *sc) {
  * host record changed (first GI frame, new resolution); kernels of earlier
  * frames may still read the old copy, so the device is drained first. */
 int sync_device_record(crt_hip_scene *sc, const DeviceScene **out) {
-    if (!sc->d_ds || std::memcmp(&sc->ds_uploaded, &sc->ds, sizeof(DeviceScene)) != 0) {
+    if (!sc->d_ds || std::memcmp(&sc->ds_uploaded, &sc->ds, sizeof(DeviceScene)) != 0 ||
+        sc->wf_oct_mask != sc->wf_oct_uploaded) {
+        sc->wf_oct_uploaded = sc->wf_oct_mask;
         if (!sc->d_ds) {
             void *p = nullptr;
-            HIP_TRY(hipMalloc(&p, sizeof(DeviceScene)));
+            HIP_TRY(hipMalloc(&p, 2 * sizeof(DeviceScene)));
             sc->allocs.push_back(p);
             sc->d_ds = static_cast<DeviceScene *>(p);
         } else {
             HIP_TRY(hipDeviceSynchronize());
         }
-        HIP_TRY(hipMemcpy(sc->d_ds, &sc->ds, sizeof(DeviceScene), hipMemcpyHostToDevice));
+        /* [0]: the frame's record; [1]: the same for wavefront levels >= 1 (secondary node order) */
+        DeviceScene two[2] = {sc->ds, sc->ds};
+        two[1].oct_mask = sc->wf_oct_mask;
+        HIP_TRY(hipMemcpy(sc->d_ds, two, sizeof two, hipMemcpyHostToDevice));
         std::memcpy(&sc->ds_uploaded, &sc->ds, sizeof(DeviceScene));
     }
     *out = sc->d_ds;
@@ -2174,7 +2193,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
     if ((rc = wf_grow_ids(w, 3 * n0, 0, stream)) != CRT_OK) return rc;
     if ((rc = wf_grow_queue(w, 0, 2 * n0)) != CRT_OK) return rc;
     unsigned long long *cnt = sc->d_counters;
-    WLevel lv{nullptr, 0, 0, w.q[0], w.counts, (int32_t)n0, w.nodes, w.cols};
+    WLevel lv{nullptr, 0, 0, w.q[0], w.counts, (int32_t)n0, w.nodes, w.cols, 64};
     const int blocks0 = (plan.ntiles + 3) / 4;
 #define CRT_WF0(T, COUNT)                                                                                   \
     hipLaunchKernelGGL((k_wf_level<T, true, COUNT>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,      \
@@ -2199,10 +2218,14 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
         if (base + 3 * (int64_t)n > INT32_MAX) return set_error(CRT_E_UNSUPPORTED, "wavefront ray ids exceed 2^31");
         if ((rc = wf_grow_ids(w, base + 3 * (int64_t)n, base, stream)) != CRT_OK) return rc;
         if ((rc = wf_grow_queue(w, cur ^ 1, 2 * (int64_t)n)) != CRT_OK) return rc;
-        WLevel l{w.q[cur], n, L, w.q[cur ^ 1], w.counts + L, (int32_t)(base + n), w.nodes, w.cols};
-        const int blocks = (int)((n + 255) / 256);
+        /* coop walks: fewer rays per wave put idle lanes on the long walks (donated pieces) */
+        const bool coop = sec == 4 || sec == 5 || sec == 10 || sec == 11;
+        const int rpw = coop ? std::min(64, std::max(1, sc->wf_rays_per_wave)) : 64;
+        WLevel l{w.q[cur], n, L, w.q[cur ^ 1], w.counts + L, (int32_t)(base + n), w.nodes, w.cols, rpw};
+        const int64_t waves = ((int64_t)n + rpw - 1) / rpw;
+        const int blocks = (int)((waves + 3) / 4);
 #define CRT_WF(SEC, COUNT)                                                                                  \
-    hipLaunchKernelGGL((k_wf_level<SEC, false, COUNT>), dim3(blocks), dim3(256), 0, stream, d_scene, ds, \
+    hipLaunchKernelGGL((k_wf_level<SEC, false, COUNT>), dim3(blocks), dim3(256), 0, stream, d_scene + 1, ds, \
                        plan.d_tiles, plan.ntiles, l, cnt)
         switch (sec) {
         case 4: if (count) CRT_WF(4, true); else CRT_WF(4, false); break;
@@ -2368,6 +2391,8 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     if (const char *e = std::getenv("CRT_TILE_ORDER")) sc->tile_order = std::atoi(e);
     if (const char *e = std::getenv("CRT_SECONDARY")) sc->secondary = std::atoi(e);
     if (const char *e = std::getenv("CRT_WAVEFRONT")) sc->wavefront = std::atoi(e);
+    if (const char *e = std::getenv("CRT_WF_OCT")) sc->wf_oct_mask = std::atoi(e) & 7;
+    if (const char *e = std::getenv("CRT_WF_RPW")) sc->wf_rays_per_wave = std::min(64, std::max(1, std::atoi(e)));
     if (const char *e = std::getenv("CRT_TRACE_WALK")) sc->trace_walk = std::atoi(e);
     if (const char *e = std::getenv("CRT_CALIBRATE")) sc->calibrate = std::atoi(e);
     if (const char *e = std::getenv("CRT_WINDOW")) sc->window_walk = std::atoi(e);
@@ -2466,6 +2491,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     ds.tan_half_fov = hs.tan_half_fov;
     std::memcpy(ds.background, hs.background, sizeof ds.background);
     ds.gi_on = hs.gi_on;
+    ds.oct_mask = 7;
     ds.reflections_on = hs.reflections_on;
     ds.refractions_on = hs.refractions_on;
 
@@ -2786,6 +2812,12 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         sc->window_walk = value != 0;
     } else if (k == "split_launch") {
         sc->split_launch = value != 0;
+    } else if (k == "wf_oct") {
+        if (value < 0 || value > 7) return set_error(CRT_E_INVALID, "wf_oct must be 0..7");
+        sc->wf_oct_mask = value;
+    } else if (k == "wf_rpw") {
+        if (value < 1 || value > 64) return set_error(CRT_E_INVALID, "wf_rpw must be 1..64");
+        sc->wf_rays_per_wave = value;
     } else if (k == "events") {
         sc->record_events = value != 0;
     } else if (k == "calibrate") {

@@ -257,8 +257,10 @@ int  crt_hip_count_work(crt_hip_scene *scene, const crt_renderer_settings *setti
 /* Wave-level steps of the last crt_hip_count_work frame, for the packet walks
  * (a wave pays once per node / triangle of the union of its lanes' visit sets):
  * node_steps / triangle_steps = wave iterations, edge_steps = triangle steps
- * where some lane ran the edge stage, waves = waves launched.  Zero for walks
- * without wave-uniform steps. */
+ * where some lane ran the edge stage, waves = waves launched.  For wavefront
+ * levels >= 1 (cooperative walks): node_steps = loop rounds summed over waves,
+ * edge_steps = the longest wave's rounds, waves = waves of those levels.
+ * Zero for walks without wave-uniform steps. */
 typedef struct crt_wave_counts {
     uint64_t node_steps, triangle_steps, edge_steps, waves;
 } crt_wave_counts;
@@ -272,9 +274,13 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  * (crt_hip_trace_batch: 0 = reference order, 1 = pruned per-ray walk),
  * "window" (0/1, default 1: the plan's split tiles of <= 16 camera rays take
  * the window walk), "split_launch" (0/1, default 0: window tiles and 8x8
- * tiles as two concurrent kernels), "calibrate" (0/1: measured-cost tile plan).
- * Environment variables CRT_TRAVERSAL, CRT_SECONDARY, CRT_WAVEFRONT and
- * CRT_TRACE_WALK set the initial values. */
+ * tiles as two concurrent kernels), "calibrate" (0/1: measured-cost tile plan),
+ * "events" (0/1: per-render start/stop events), "wf_rpw" (1..64, default 32:
+ * rays per wave of wavefront levels >= 1 under the cooperative walks; the
+ * other lanes start idle and take donated pieces), "wf_oct" (0..7, default 7:
+ * node-order octant mask of those levels' pruned walks).
+ * Environment variables CRT_TRAVERSAL, CRT_SECONDARY, CRT_WAVEFRONT,
+ * CRT_TRACE_WALK, CRT_WF_RPW and CRT_WF_OCT set the initial values. */
 int  crt_hip_scene_set_option(crt_hip_scene *scene, const char *name, int value);
 
 /* Diagnostics: render one full frame with per-wave s_memrealtime stamps

@@ -208,3 +208,25 @@ def test_window_walk_equals_packet_walk(N, oracle, monkeypatch, calib_k):
     assert np.array_equal(bits(b), bits(want)) and np.array_equal(bits(c), bits(want))
     ca, cb = win.count_work(st), N.HipScene(sc, window=0).count_work(st)
     assert ca["traversals"] == cb["traversals"] == 1920 * 1080 and ca["hits"] == cb["hits"]
+
+
+@pytest.mark.parametrize("opt,values", [("wf_rpw", [64, 32, 5, 1]), ("wf_oct", [7, 0, 4])])
+def test_wavefront_level_layouts_bit_identical(N, oracle, opt, values):
+    """Wavefront levels >= 1 (reflect/refract recursion, C3 scene at depth 8):
+    rays per wave (idle lanes take donated pieces) and the node order of the
+    secondary walks change only the schedule, never the image bits; the work
+    counts keep the traversal and hit totals."""
+    sc = scene_npz("11-01-refractive__scene8").set_resolution(240, 135)
+    st = N.RendererSettings.default(max_ray_depth=8)
+    base = N.HipScene(sc)
+    want = base.render(st)
+    ref = oracle.OracleScene(sc).render(st)
+    assert float(np.sqrt(np.mean((want.astype(np.float64) - ref) ** 2))) < RMSE_TOL
+    cw = base.count_work(st)
+    for v in values:
+        g = N.HipScene(sc).set_option(opt, v)
+        assert np.array_equal(bits(g.render(st)), bits(want)), f"{opt}={v}"
+        c = g.count_work(st)
+        assert c["traversals"] == cw["traversals"] and c["hits"] == cw["hits"], f"{opt}={v}"
+    with pytest.raises(Exception):
+        N.HipScene(sc).set_option(opt, 99)
