@@ -1094,6 +1094,161 @@ __device__ __forceinline__ Vec shade_primary(const DeviceScene &s, const DSettin
  * FULL=false: scenes whose materials are only diffuse/constant with GI off —
  * no recursion, no frame stack.  FULL=true: GI + reflective + refractive with
  * a per-lane frame stack of MAXF entries (≥ max_ray_depth + 1, host-checked). */
+/* One pass of shade_pixel's loop: trace the lane's current ray (a wave-wide
+ * walk call), shade the hit, and return colours to the pending activations
+ * until one of them needs another ray.  Returns true when (o, d) holds that
+ * next ray, false when the pixel's colour is in col. */
+template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT>
+__device__ __forceinline__ bool shade_pass(const DeviceScene &s, const DSettings &st, LaneCounts &cnt, CoopLds *L,
+                                           bool has_px, Vec &o, Vec &d, uint32_t &depth, Pcg32 &rng, Frame *stack,
+                                           int &sp, Vec &col) {
+    /* Every pass of this loop traces exactly one ray per live lane, so all of a
+     * wave's lanes meet in the same walk call whatever their position in their
+     * own recursion (a miss shifts one lane's DFS against the others).  A call
+     * that shade_ray would answer without tracing (depth > max_ray_depth: black,
+     * crt_renderer.cpp:47-49) is resolved in the return loop below instead of
+     * costing a pass; its GI draws are still taken (gi_ray) in reference order. */
+    /* ---- shade_ray(ray) with depth <= max_ray_depth ---- */
+    bool called = false;
+    {
+        float t;
+        /* the packet walk pays for the union of its lanes' visit sets: it
+         * wins on camera rays (coherent by construction) and loses on the
+         * scattered secondary rays, which take the range-sharing walk */
+        const int slot = (SEC != TRAV && depth != 0) ? trace<SEC, COUNT>(s, L, has_px, o, d, t, cnt)
+                                                     : trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
+        if (slot < 0) {
+            col = vec(s.background[0], s.background[1], s.background[2]);
+        } else {
+            HitRec h;
+            make_hit(s, o, d, t, slot, h);
+            const DMaterial m = s.materials[h.mat];
+            if (m.type == CRT_MATERIAL_DIFFUSE) {
+                const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+                if (FULL && s.gi_on && st.diffuse_reflection_ray_count > 0) {
+                    Frame &f = stack[sp++];
+                    f.kind = kDiffuseGI;
+                    f.depth = (int32_t)depth;
+                    f.i = 0;
+                    f.acc = vec(0.f, 0.f, 0.f);
+                    f.p = h.p;
+                    f.n = h.n;
+                    f.a = vnormalize(vcross(d, h.n));       /* right   */
+                    f.b = vcross(f.a, h.n);                  /* forward */
+                    f.alb = alb;
+                    gi_ray(s, st, f, rng, o, d);
+                    depth = depth + 1;
+                    called = true;
+                } else {
+                    col = diffuse_finish(s, st, vec(0.f, 0.f, 0.f), h.p, h.n, alb);
+                }
+            } else if (FULL && m.type == CRT_MATERIAL_REFLECTIVE) {          /* :103-107 */
+                const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+                if (s.reflections_on) {
+                    Frame &f = stack[sp++];
+                    f.kind = kReflect;
+                    f.depth = (int32_t)depth;
+                    f.acc = alb;
+                    o = vadd(h.p, vscale(h.n, st.reflection_bias));
+                    d = vsub(d, vscale(vscale(h.n, 2.0f), vdot(d, h.n)));
+                    depth = depth + 1;
+                    called = true;
+                } else {
+                    col = alb;
+                }
+            } else if (FULL && m.type == CRT_MATERIAL_REFRACTIVE) {          /* :109-135 */
+                if (!s.refractions_on) {
+                    col = vec(0.f, 0.f, 0.f);
+                } else {
+                    Vec n = h.n;
+                    float n_out = 1.0f, n_in = m.ior;
+                    if (vdot(d, n) > 0.0f) {
+                        n = vneg(n);
+                        const float tmp = n_in; n_in = n_out; n_out = tmp;
+                    }
+                    Frame &f = stack[sp++];
+                    f.kind = kRefractA;
+                    f.depth = (int32_t)depth;
+                    f.has_refr = 0;
+                    {   /* Vector::refract (crt_vector.cpp:11-27) */
+                        Vec rd = d;
+                        const float ca = -vdot(rd, n);
+                        const float sa = sqrtf(1.0f - ca * ca);
+                        if (!(sa > n_in / n_out)) {
+                            const float sb = sa * n_out / n_in;
+                            const float cb = sqrtf(1.0f - sb * sb);
+                            rd = vadd(rd, vscale(n, ca));
+                            rd = vnormalize(rd);
+                            rd = vscale(rd, sb);
+                            rd = vadd(rd, vscale(vneg(n), cb));
+                            f.has_refr = 1;
+                        }
+                        /* refracted_at → refract_at with its default 1e-2f bias (crt_ray.h:30-50) */
+                        f.a = vadd(h.p, vscale(vneg(n), 1e-2f));
+                        f.b = rd;
+                    }
+                    f.alb.x = 0.5f * pow5(1.0f + vdot(d, n));
+                    o = vadd(h.p, vscale(n, st.reflection_bias));
+                    d = vsub(d, vscale(vscale(n, 2.0f), vdot(d, n)));
+                    depth = depth + 1;
+                    called = true;
+                }
+            } else {                                                          /* Constant :137-139 */
+                col = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+            }
+        }
+    }
+    if (!FULL) return false;
+    if (called) {
+        if (depth <= st.max_ray_depth) return true;
+        col = vec(0.f, 0.f, 0.f);       /* the child call returns black untraced */
+        called = false;
+    }
+    /* ---- return col to the pending activations ---- */
+    while (sp > 0) {
+        Frame &f = stack[sp - 1];
+        if (f.kind == kDiffuseGI) {
+            f.acc = vadd(f.acc, col);
+            f.i += 1;
+            if ((uint32_t)f.i < st.diffuse_reflection_ray_count) {
+                gi_ray(s, st, f, rng, o, d);
+                depth = (uint32_t)f.depth + 1;
+                if (depth <= st.max_ray_depth) {
+                    called = true;
+                    break;
+                }
+                col = vec(0.f, 0.f, 0.f);
+                continue;
+            }
+            --sp;
+            col = diffuse_finish(s, st, f.acc, f.p, f.n, f.alb);
+        } else if (f.kind == kReflect) {
+            --sp;
+            col = vmul_quirk(f.acc, col);
+        } else if (f.kind == kRefractA) {
+            if (f.has_refr) {
+                f.kind = kRefractB;
+                f.acc = col;
+                o = f.a;
+                d = f.b;
+                depth = (uint32_t)f.depth + 1;
+                if (depth <= st.max_ray_depth) {
+                    called = true;
+                    break;
+                }
+                col = vec(0.f, 0.f, 0.f);
+                continue;
+            }
+            --sp;   /* total internal reflection: the reflection colour is the result */
+        } else {
+            --sp;
+            const float fr = f.alb.x;
+            col = vadd(vscale(f.acc, fr), vscale(col, 1.0f - fr));
+        }
+    }
+    return called;
+}
+
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT>
 __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt, CoopLds *L,
                            bool has_px) {
@@ -1105,152 +1260,7 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
     Frame stack[MAXF > 0 ? MAXF : 1];
     int sp = 0;
     Vec col;
-    /* Every pass of this loop traces exactly one ray per live lane, so all of a
-     * wave's lanes meet in the same walk call whatever their position in their
-     * own recursion (a miss shifts one lane's DFS against the others).  A call
-     * that shade_ray would answer without tracing (depth > max_ray_depth: black,
-     * crt_renderer.cpp:47-49) is resolved in the return loop below instead of
-     * costing a pass; its GI draws are still taken (gi_ray) in reference order. */
-    for (;;) {
-        /* ---- shade_ray(ray) with depth <= max_ray_depth ---- */
-        bool called = false;
-        {
-            float t;
-            /* the packet walk pays for the union of its lanes' visit sets: it
-             * wins on camera rays (coherent by construction) and loses on the
-             * scattered secondary rays, which take the range-sharing walk */
-            const int slot = (SEC != TRAV && depth != 0) ? trace<SEC, COUNT>(s, L, has_px, o, d, t, cnt)
-                                                         : trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
-            if (slot < 0) {
-                col = vec(s.background[0], s.background[1], s.background[2]);
-            } else {
-                HitRec h;
-                make_hit(s, o, d, t, slot, h);
-                const DMaterial m = s.materials[h.mat];
-                if (m.type == CRT_MATERIAL_DIFFUSE) {
-                    const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
-                    if (FULL && s.gi_on && st.diffuse_reflection_ray_count > 0) {
-                        Frame &f = stack[sp++];
-                        f.kind = kDiffuseGI;
-                        f.depth = (int32_t)depth;
-                        f.i = 0;
-                        f.acc = vec(0.f, 0.f, 0.f);
-                        f.p = h.p;
-                        f.n = h.n;
-                        f.a = vnormalize(vcross(d, h.n));       /* right   */
-                        f.b = vcross(f.a, h.n);                  /* forward */
-                        f.alb = alb;
-                        gi_ray(s, st, f, rng, o, d);
-                        depth = depth + 1;
-                        called = true;
-                    } else {
-                        col = diffuse_finish(s, st, vec(0.f, 0.f, 0.f), h.p, h.n, alb);
-                    }
-                } else if (FULL && m.type == CRT_MATERIAL_REFLECTIVE) {          /* :103-107 */
-                    const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
-                    if (s.reflections_on) {
-                        Frame &f = stack[sp++];
-                        f.kind = kReflect;
-                        f.depth = (int32_t)depth;
-                        f.acc = alb;
-                        o = vadd(h.p, vscale(h.n, st.reflection_bias));
-                        d = vsub(d, vscale(vscale(h.n, 2.0f), vdot(d, h.n)));
-                        depth = depth + 1;
-                        called = true;
-                    } else {
-                        col = alb;
-                    }
-                } else if (FULL && m.type == CRT_MATERIAL_REFRACTIVE) {          /* :109-135 */
-                    if (!s.refractions_on) {
-                        col = vec(0.f, 0.f, 0.f);
-                    } else {
-                        Vec n = h.n;
-                        float n_out = 1.0f, n_in = m.ior;
-                        if (vdot(d, n) > 0.0f) {
-                            n = vneg(n);
-                            const float tmp = n_in; n_in = n_out; n_out = tmp;
-                        }
-                        Frame &f = stack[sp++];
-                        f.kind = kRefractA;
-                        f.depth = (int32_t)depth;
-                        f.has_refr = 0;
-                        {   /* Vector::refract (crt_vector.cpp:11-27) */
-                            Vec rd = d;
-                            const float ca = -vdot(rd, n);
-                            const float sa = sqrtf(1.0f - ca * ca);
-                            if (!(sa > n_in / n_out)) {
-                                const float sb = sa * n_out / n_in;
-                                const float cb = sqrtf(1.0f - sb * sb);
-                                rd = vadd(rd, vscale(n, ca));
-                                rd = vnormalize(rd);
-                                rd = vscale(rd, sb);
-                                rd = vadd(rd, vscale(vneg(n), cb));
-                                f.has_refr = 1;
-                            }
-                            /* refracted_at → refract_at with its default 1e-2f bias (crt_ray.h:30-50) */
-                            f.a = vadd(h.p, vscale(vneg(n), 1e-2f));
-                            f.b = rd;
-                        }
-                        f.alb.x = 0.5f * pow5(1.0f + vdot(d, n));
-                        o = vadd(h.p, vscale(n, st.reflection_bias));
-                        d = vsub(d, vscale(vscale(n, 2.0f), vdot(d, n)));
-                        depth = depth + 1;
-                        called = true;
-                    }
-                } else {                                                          /* Constant :137-139 */
-                    col = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
-                }
-            }
-        }
-        if (!FULL) break;
-        if (called) {
-            if (depth <= st.max_ray_depth) continue;
-            col = vec(0.f, 0.f, 0.f);       /* the child call returns black untraced */
-            called = false;
-        }
-        /* ---- return col to the pending activations ---- */
-        while (sp > 0) {
-            Frame &f = stack[sp - 1];
-            if (f.kind == kDiffuseGI) {
-                f.acc = vadd(f.acc, col);
-                f.i += 1;
-                if ((uint32_t)f.i < st.diffuse_reflection_ray_count) {
-                    gi_ray(s, st, f, rng, o, d);
-                    depth = (uint32_t)f.depth + 1;
-                    if (depth <= st.max_ray_depth) {
-                        called = true;
-                        break;
-                    }
-                    col = vec(0.f, 0.f, 0.f);
-                    continue;
-                }
-                --sp;
-                col = diffuse_finish(s, st, f.acc, f.p, f.n, f.alb);
-            } else if (f.kind == kReflect) {
-                --sp;
-                col = vmul_quirk(f.acc, col);
-            } else if (f.kind == kRefractA) {
-                if (f.has_refr) {
-                    f.kind = kRefractB;
-                    f.acc = col;
-                    o = f.a;
-                    d = f.b;
-                    depth = (uint32_t)f.depth + 1;
-                    if (depth <= st.max_ray_depth) {
-                        called = true;
-                        break;
-                    }
-                    col = vec(0.f, 0.f, 0.f);
-                    continue;
-                }
-                --sp;   /* total internal reflection: the reflection colour is the result */
-            } else {
-                --sp;
-                const float fr = f.alb.x;
-                col = vadd(vscale(f.acc, fr), vscale(col, 1.0f - fr));
-            }
-        }
-        if (!called) break;
+    while (shade_pass<FULL, MAXF, TRAV, SEC, COUNT>(s, st, cnt, L, has_px, o, d, depth, rng, stack, sp, col)) {
     }
     return col;
 }
@@ -1353,6 +1363,82 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 || TR
             atomicAdd(&counters[6], (unsigned long long)cnt.wave_edges);
             atomicAdd(&counters[7], 1ull);
         }
+    }
+}
+
+/* Frame-stack kernel with pixel refill (GI frames, cooperative walk).  A
+ * persistent grid of waves pulls pixels from the tile list in plan order
+ * (one global counter, one atomic per wave and pass): a lane whose pixel is
+ * finished takes the next one at the top of the following pass, so a wave no
+ * longer waits for its tile's longest pixel with the other lanes idle.  Every
+ * pixel runs exactly shade_pixel's sequence (camera ray, PCG seeded by (x, y),
+ * the same passes), so the image bits do not depend on which lane or wave
+ * renders it.  Lanes without a pixel stay in the walk calls as helpers (they
+ * take donated pieces); the wave leaves when the list is exhausted and none
+ * of its lanes holds a pixel. */
+template <int MAXF, int TRAV, bool COUNT>
+__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(MAXF == 4 ? CRT_GI_WAVES : 1))) void k_render_refill(
+    const DeviceScene *__restrict__ scene, DSettings st, const Tile *__restrict__ tiles, int ntiles,
+    float *__restrict__ out, int32_t *__restrict__ next_px, unsigned long long *__restrict__ counters) {
+    const int lane = (int)(threadIdx.x & 63);
+    const DeviceScene &s = *scene;
+    const int total = ntiles * 64;   /* pixel slots: tile k, lane j -> (j & 7, j >> 3) inside tile k */
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    __shared__ CoopLds coop[4];
+    CoopLds *L = &coop[threadIdx.x >> 6];
+    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    bool has = false, dry = false;
+    int64_t opx = 0;
+    Vec o = vec(0.f, 0.f, 0.f), d = vec(0.f, 0.f, 1.f), col = vec(0.f, 0.f, 0.f);
+    uint32_t depth = 0;
+    Pcg32 rng = make_pcg(0u, 0u);
+    Frame stack[MAXF];
+    int sp = 0;
+    for (;;) {
+        /* ---- lanes without a pixel take the next slots of the list ---- */
+        const unsigned long long need = __ballot(!has && !dry);
+        if (need != 0ull) {
+            const int leader = __ffsll((long long)need) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(next_px, __popcll(need));
+            base = __shfl(base, leader);
+            if (!has && !dry) {
+                const int k = base + __popcll(need & lt);
+                if (k >= total) {
+                    dry = true;
+                } else {
+                    const Tile tl = tiles[k >> 6];
+                    const int lx = k & 7, ly = (k >> 3) & 7;
+                    if (lx < tl.w && ly < tl.h) {   /* slots outside a partial tile: retry next pass */
+                        has = true;
+                        opx = tl.out_base + (int64_t)ly * tl.out_stride + lx;
+                        camera_ray(s, tl.x + lx, tl.y + ly, o, d);
+                        depth = 0;
+                        rng = make_pcg((uint32_t)(tl.x + lx), (uint32_t)(tl.y + ly));
+                        sp = 0;
+                    }
+                }
+            }
+        }
+        if (!__any(has)) {
+            if (__any(!dry)) continue;
+            break;
+        }
+        const bool more = shade_pass<true, MAXF, TRAV, TRAV, COUNT>(s, st, cnt, L, has, o, d, depth, rng, stack, sp,
+                                                                     col);
+        if (has && !more) {
+            float *px = out + 3 * opx;
+            px[0] = col.x;
+            px[1] = col.y;
+            px[2] = col.z;
+            has = false;
+        }
+    }
+    if (COUNT) {
+        atomicAdd(&counters[0], (unsigned long long)cnt.traversals);
+        atomicAdd(&counters[1], (unsigned long long)cnt.nodes);
+        atomicAdd(&counters[2], (unsigned long long)cnt.tris);
+        atomicAdd(&counters[3], (unsigned long long)cnt.hits);
     }
 }
 
@@ -1752,6 +1838,9 @@ struct crt_hip_scene {
     std::map<int, std::pair<UnpackBucket *, int>> unpack_plans;
     float *d_out = nullptr;
     unsigned long long *d_counters = nullptr;
+    int32_t *d_next_px = nullptr;      /* pixel-refill list head (k_render_refill) */
+    int gi_refill = 1;                 /* GI frames: persistent waves with pixel refill (env CRT_GI_REFILL, option "gi_refill") */
+    int refill_waves = 5120;           /* waves of the refill grid: CUs x 4 SIMDs x CRT_GI_WAVES (env CRT_REFILL_WAVES) */
     bool grid_empty = false;
     int traversal = 8;             /* kernel walk variant, see trace<> (env CRT_TRAVERSAL) */
     int trace_walk = 1;            /* crt_hip_trace_batch: 0 reference-order walk, 1 pruned per-lane walk */
@@ -2341,6 +2430,22 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         case 13: if (count) CRT_LAUNCH_T(false, 0, 13, true); else CRT_LAUNCH_T(false, 0, 13, false); break;
         default: if (count) CRT_LAUNCH(false, 0, true); else CRT_LAUNCH(false, 0, false); break;
         }
+    } else if (gi && trav == 4 && sc->gi_refill && sc->d_next_px && !stamps && frames <= 64) {
+        /* GI: persistent waves with pixel refill (k_render_refill) */
+        HIP_TRY(hipMemsetAsync(sc->d_next_px, 0, sizeof(int32_t), stream));
+        const int nw = std::max(1, std::min(plan.ntiles, sc->refill_waves));
+        const unsigned rb = (unsigned)((nw + 3) / 4);
+#define CRT_REFILL(MAXF, COUNT)                                                                             \
+    hipLaunchKernelGGL((k_render_refill<MAXF, 4, COUNT>), dim3(rb), dim3(256), 0, stream, d_scene, ds,       \
+                       plan.d_tiles, plan.ntiles, d_out, sc->d_next_px, cnt)
+        if (frames <= 4) {
+            if (count) CRT_REFILL(4, true); else CRT_REFILL(4, false);
+        } else if (frames <= 16) {
+            if (count) CRT_REFILL(16, true); else CRT_REFILL(16, false);
+        } else {
+            if (count) CRT_REFILL(64, true); else CRT_REFILL(64, false);
+        }
+#undef CRT_REFILL
     } else if (frames <= 4) {
         if (count) CRT_LAUNCH(true, 4, true); else CRT_LAUNCH(true, 4, false);
     } else if (frames <= 16) {
@@ -2391,6 +2496,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     if (const char *e = std::getenv("CRT_TILE_ORDER")) sc->tile_order = std::atoi(e);
     if (const char *e = std::getenv("CRT_SECONDARY")) sc->secondary = std::atoi(e);
     if (const char *e = std::getenv("CRT_WAVEFRONT")) sc->wavefront = std::atoi(e);
+    if (const char *e = std::getenv("CRT_GI_REFILL")) sc->gi_refill = std::atoi(e) != 0;
     if (const char *e = std::getenv("CRT_WF_OCT")) sc->wf_oct_mask = std::atoi(e) & 7;
     if (const char *e = std::getenv("CRT_WF_RPW")) sc->wf_rays_per_wave = std::min(64, std::max(1, std::atoi(e)));
     if (const char *e = std::getenv("CRT_TRACE_WALK")) sc->trace_walk = std::atoi(e);
@@ -2410,9 +2516,12 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     if (sc->tile_order && hs.tree_on_host) sc->tile_work = tile_work_estimate(hs, (hs.width + 7) / 8, (hs.height + 7) / 8);
     {
         hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) {
             sc->wave_slots = prop.multiProcessorCount * 4 * 6;
+            sc->refill_waves = prop.multiProcessorCount * 4 * CRT_GI_WAVES;
+        }
     }
+    if (const char *e = std::getenv("CRT_REFILL_WAVES")) sc->refill_waves = std::max(1, std::atoi(e));
     crt_host_scene_info(h, &sc->info);
     sc->info.device_bytes = 0;
     for (const DMaterial &m : hs.materials) {
@@ -2502,6 +2611,10 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     HIP_TRY(hipMalloc(&p, 8 * sizeof(unsigned long long)));
     sc->allocs.push_back(p);
     sc->d_counters = static_cast<unsigned long long *>(p);
+    p = nullptr;
+    HIP_TRY(hipMalloc(&p, 64));
+    sc->allocs.push_back(p);
+    sc->d_next_px = static_cast<int32_t *>(p);
 
     int64_t px = 0;
     const std::vector<DBucket> all = shard_buckets(hs.width, hs.height, hs.bucket_size, 0, 1, &px);
@@ -2812,6 +2925,8 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         sc->window_walk = value != 0;
     } else if (k == "split_launch") {
         sc->split_launch = value != 0;
+    } else if (k == "gi_refill") {
+        sc->gi_refill = value != 0;
     } else if (k == "wf_oct") {
         if (value < 0 || value > 7) return set_error(CRT_E_INVALID, "wf_oct must be 0..7");
         sc->wf_oct_mask = value;

@@ -278,9 +278,11 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  * "events" (0/1: per-render start/stop events), "wf_rpw" (1..64, default 32:
  * rays per wave of wavefront levels >= 1 under the cooperative walks; the
  * other lanes start idle and take donated pieces), "wf_oct" (0..7, default 7:
- * node-order octant mask of those levels' pruned walks).
+ * node-order octant mask of those levels' pruned walks), "gi_refill" (0/1,
+ * default 1: GI frames run persistent waves that refill finished lanes with
+ * the next pixel of the tile list).
  * Environment variables CRT_TRAVERSAL, CRT_SECONDARY, CRT_WAVEFRONT,
- * CRT_TRACE_WALK, CRT_WF_RPW and CRT_WF_OCT set the initial values. */
+ * CRT_TRACE_WALK, CRT_WF_RPW, CRT_WF_OCT and CRT_GI_REFILL set the initial values. */
 int  crt_hip_scene_set_option(crt_hip_scene *scene, const char *name, int value);
 
 /* Diagnostics: render one full frame with per-wave s_memrealtime stamps

@@ -230,3 +230,21 @@ def test_wavefront_level_layouts_bit_identical(N, oracle, opt, values):
         assert c["traversals"] == cw["traversals"] and c["hits"] == cw["hits"], f"{opt}={v}"
     with pytest.raises(Exception):
         N.HipScene(sc).set_option(opt, 99)
+
+
+@pytest.mark.parametrize("w,h", [(70, 45), (96, 96)])
+def test_gi_pixel_refill_bit_identical(N, oracle, w, h):
+    """GI frames (15-01/scene2): persistent waves refilling finished lanes with
+    the next pixel give the same bits as one wave per 8x8 tile, including
+    partial tiles (70x45: the bucket grid's last row/column absorbs the rest),
+    and match the oracle within the tolerance this scene is held to."""
+    sc = scene_npz("15-01-conclusion__scene2").set_resolution(w, h)
+    st = N.RendererSettings.default()
+    got = N.HipScene(sc).set_option("gi_refill", 1).render(st)
+    tiles = N.HipScene(sc).set_option("gi_refill", 0).render(st)
+    assert np.array_equal(bits(got), bits(tiles))
+    want = oracle.OracleScene(sc).render(st)
+    assert float(np.sqrt(np.mean((got.astype(np.float64) - want) ** 2))) < RMSE_TOL   # as test_render_matches_oracle
+    ca = N.HipScene(sc).set_option("gi_refill", 1).count_work(st)
+    cb = N.HipScene(sc).set_option("gi_refill", 0).count_work(st)
+    assert ca == cb
