@@ -112,11 +112,9 @@ struct DeviceScene {
     const DVec4 *texels;
     const DLight *lights;
     int32_t light_count;
-    /* GI angle tables (cosf/sinf of pi*u and 2*pi*u for the 2^23 values of u) */
-    const float *gi_cos_pi;
-    const float *gi_sin_pi;
-    const float *gi_cos_2pi;
-    const float *gi_sin_2pi;
+    /* GI angle tables: (cosf, sinf) pairs of pi*u and of 2*pi*u for the 2^23 values of u */
+    const float *gi_pi;
+    const float *gi_2pi;
     /* camera (crt_camera.cpp:7-35), per-frame constants precomputed on host */
     float cam_loc[3];
     float cam_rot[9];

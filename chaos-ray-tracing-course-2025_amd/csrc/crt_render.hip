@@ -1051,15 +1051,19 @@ __device__ __forceinline__ Vec diffuse_finish(const DeviceScene &s, const DSetti
     return vdiv(acc, (float)(st.diffuse_reflection_ray_count + 1));
 }
 
+struct alignas(8) F2 { float c, s; };
+
 /* One GI sample direction (crt_renderer.cpp:61-77).  rng.uniform() is
  * m * 2^-23 with m = next() >> 9, so cosf/sinf of pi*u and 2pi*u are table
  * lookups computed by the host's libm — bit-identical to the reference. */
 __device__ __forceinline__ void gi_ray(const DeviceScene &s, const DSettings &st, const Frame &f, Pcg32 &rng, Vec &o,
                                        Vec &d) {
     const uint32_t m1 = rng.next() >> 9;
-    Vec dir = vec(s.gi_cos_pi[m1], s.gi_sin_pi[m1], 0.0f);
+    const F2 cs1 = reinterpret_cast<const F2 *>(s.gi_pi)[m1];
+    Vec dir = vec(cs1.c, cs1.s, 0.0f);
     const uint32_t m2 = rng.next() >> 9;
-    const float c = s.gi_cos_2pi[m2], sn = s.gi_sin_2pi[m2];
+    const F2 cs2 = reinterpret_cast<const F2 *>(s.gi_2pi)[m2];
+    const float c = cs2.c, sn = cs2.s;
     const float roty[9] = {c, 0.0f, -sn, 0.0f, 1.0f, 0.0f, sn, 0.0f, c};      /* crt_matrix.cpp:14-20 */
     dir = vec_mat(dir, roty);
     const float basis[9] = {f.a.x, f.a.y, f.a.z, f.n.x, f.n.y, f.n.z, f.b.x, f.b.y, f.b.z};   /* from_axes */
@@ -1787,7 +1791,9 @@ constexpr int64_t kGiN = int64_t(1) << 23;
 void build_gi_host_tables() {
     if (!g_gi_host.empty()) return;
     g_gi_host.resize((size_t)(4 * kGiN));
-    float *cpi = g_gi_host.data(), *spi = cpi + kGiN, *c2 = spi + kGiN, *s2 = c2 + kGiN;
+    /* (cos, sin) pairs: one 8-B read per angle (the tables are 64 MB each and
+     * read at random: one cache line per angle instead of two) */
+    float *pi2 = g_gi_host.data(), *tau2 = pi2 + 2 * kGiN;
     unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::thread> pool;
     for (unsigned w = 0; w < nt; ++w) {
@@ -1796,10 +1802,10 @@ void build_gi_host_tables() {
                 const float u = (float)m * (1.0f / 8388608.0f);          /* = uniform() exactly */
                 const float a = kPi * u;                                  /* crt_renderer.cpp:68 */
                 const float b = 2.0f * kPi * u;                           /* crt_renderer.cpp:71 */
-                cpi[m] = std::cos(a);
-                spi[m] = std::sin(a);
-                c2[m] = std::cos(b);
-                s2[m] = std::sin(b);
+                pi2[2 * m] = std::cos(a);
+                pi2[2 * m + 1] = std::sin(a);
+                tau2[2 * m] = std::cos(b);
+                tau2[2 * m + 1] = std::sin(b);
             }
         });
     }
@@ -2134,7 +2140,7 @@ void free_plans(crt_hip_scene *sc) {
 }
 
 int ensure_gi_tables(crt_hip_scene *sc) {
-    if (sc->ds.gi_cos_pi) return CRT_OK;
+    if (sc->ds.gi_pi) return CRT_OK;
     std::lock_guard<std::mutex> g(g_gi_mu);
     GiTables &t = g_gi[sc->device];
     if (!t.d) {
@@ -2144,10 +2150,8 @@ int ensure_gi_tables(crt_hip_scene *sc) {
         HIP_TRY(hipMemcpy(p, g_gi_host.data(), (size_t)(4 * kGiN) * sizeof(float), hipMemcpyHostToDevice));
         t.d = static_cast<float *>(p);
     }
-    sc->ds.gi_cos_pi = t.d;
-    sc->ds.gi_sin_pi = t.d + kGiN;
-    sc->ds.gi_cos_2pi = t.d + 2 * kGiN;
-    sc->ds.gi_sin_2pi = t.d + 3 * kGiN;
+    sc->ds.gi_pi = t.d;
+    sc->ds.gi_2pi = t.d + 2 * kGiN;
     return CRT_OK;
 }
 

@@ -16,7 +16,7 @@ for f in sorted(root.rglob("*counter_collection.csv")):
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add(r["Dispatch_Id"])
     for k, v in agg.items():
-        if "k_render" not in k and "k_wf_level" not in k:
+        if "k_render" not in k and "k_wf_level" not in k:  # k_render_tiles, k_render_refill, wavefront levels
             continue
         n = len(disp[k])
         out.setdefault(k, {}).update({c: x / n for c, x in v.items()})
