@@ -1381,7 +1381,10 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 || TR
  * take donated pieces); the wave leaves when the list is exhausted and none
  * of its lanes holds a pixel. */
 template <int MAXF, int TRAV, bool COUNT>
-__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(MAXF == 4 ? CRT_GI_WAVES : 1))) void k_render_refill(
+#ifndef CRT_GI10_WAVES
+#define CRT_GI10_WAVES 4     /* min waves/SIMD of the refill kernel with the pruned walk (TRAV 10) */
+#endif
+__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(MAXF == 4 ? (TRAV == 10 ? CRT_GI10_WAVES : CRT_GI_WAVES) : 1))) void k_render_refill(
     const DeviceScene *__restrict__ scene, DSettings st, const Tile *__restrict__ tiles, int ntiles,
     float *__restrict__ out, int32_t *__restrict__ next_px, unsigned long long *__restrict__ counters) {
     const int lane = (int)(threadIdx.x & 63);
@@ -2434,15 +2437,18 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         case 13: if (count) CRT_LAUNCH_T(false, 0, 13, true); else CRT_LAUNCH_T(false, 0, 13, false); break;
         default: if (count) CRT_LAUNCH(false, 0, true); else CRT_LAUNCH(false, 0, false); break;
         }
-    } else if (gi && trav == 4 && sc->gi_refill && sc->d_next_px && !stamps && frames <= 64) {
+    } else if (gi && (trav == 4 || trav == 10) && sc->gi_refill && sc->d_next_px && !stamps && frames <= 64) {
         /* GI: persistent waves with pixel refill (k_render_refill) */
         HIP_TRY(hipMemsetAsync(sc->d_next_px, 0, sizeof(int32_t), stream));
         const int nw = std::max(1, std::min(plan.ntiles, sc->refill_waves));
         const unsigned rb = (unsigned)((nw + 3) / 4);
-#define CRT_REFILL(MAXF, COUNT)                                                                             \
-    hipLaunchKernelGGL((k_render_refill<MAXF, 4, COUNT>), dim3(rb), dim3(256), 0, stream, d_scene, ds,       \
+#define CRT_REFILL_T(MAXF, T, COUNT)                                                                        \
+    hipLaunchKernelGGL((k_render_refill<MAXF, T, COUNT>), dim3(rb), dim3(256), 0, stream, d_scene, ds,       \
                        plan.d_tiles, plan.ntiles, d_out, sc->d_next_px, cnt)
-        if (frames <= 4) {
+#define CRT_REFILL(MAXF, COUNT) CRT_REFILL_T(MAXF, 4, COUNT)
+        if (frames <= 4 && trav == 10) {   /* pruned cooperative walk for GI (secondary = 10) */
+            if (count) CRT_REFILL_T(4, 10, true); else CRT_REFILL_T(4, 10, false);
+        } else if (frames <= 4) {
             if (count) CRT_REFILL(4, true); else CRT_REFILL(4, false);
         } else if (frames <= 16) {
             if (count) CRT_REFILL(16, true); else CRT_REFILL(16, false);
@@ -2450,6 +2456,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
             if (count) CRT_REFILL(64, true); else CRT_REFILL(64, false);
         }
 #undef CRT_REFILL
+#undef CRT_REFILL_T
     } else if (frames <= 4) {
         if (count) CRT_LAUNCH(true, 4, true); else CRT_LAUNCH(true, 4, false);
     } else if (frames <= 16) {
