@@ -79,6 +79,9 @@ def parse():
     p.add_argument("--mode", choices=["frames", "tiles"], default="frames",
                    help="N>1: frames = each GPU renders whole frames (weak scaling, default); "
                         "tiles = one frame sharded over the GPUs + RCCL gather (strong scaling)")
+    p.add_argument("--event-every", type=int, default=5,
+                   help="bracket every k-th render of the timed region with HIP events (kernel time sample; "
+                        "an event pair between two renders costs ~7 us of a ~165 us C2 step)")
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                    help="per-launch HBM bytes measured by rocprofv3 --pmc (profiles/), if present")
     return p.parse_args()
@@ -147,25 +150,25 @@ def main():
     sptr = stream.cuda_stream
 
     frame = torch.empty(W * H * 3, dtype=torch.float32, device="cuda")
-    timing = {"events": None, "i": 0}
+    timing = {"events": None, "i": 0, "n": 0}
+
+    def timed(launch):
+        # HIP events on the launch stream around every k-th render of the timed region
+        ev = timing["events"]
+        rec = ev is not None and timing["n"] % a.event_every == 0
+        timing["n"] += 1
+        if rec:
+            ev[timing["i"]][0].record(stream)
+        launch()
+        if rec:
+            ev[timing["i"]][1].record(stream)
+            timing["i"] += 1
 
     def render_full():
-        ev = timing["events"]
-        if ev is not None:
-            ev[timing["i"]][0].record(stream)
-        gpu.render_device(settings, frame.data_ptr(), sptr)
-        if ev is not None:
-            ev[timing["i"]][1].record(stream)
-            timing["i"] += 1
+        timed(lambda: gpu.render_device(settings, frame.data_ptr(), sptr))
 
     def render_shard(packed):
-        ev = timing["events"]
-        if ev is not None:
-            ev[timing["i"]][0].record(stream)
-        gpu.render_shard(settings, rank, world, packed.data_ptr(), sptr)
-        if ev is not None:
-            ev[timing["i"]][1].record(stream)
-            timing["i"] += 1
+        timed(lambda: gpu.render_shard(settings, rank, world, packed.data_ptr(), sptr))
 
     tiles = world > 1 and a.mode == "tiles"
     if tiles:
@@ -193,9 +196,10 @@ def main():
     drain()
     torch.cuda.synchronize()
 
-    # kernel duration: event pairs around each render launch on the launch stream
+    # kernel duration: event pairs around every k-th render launch of the timed region, on the launch stream
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     timing["events"] = ev
+    timing["n"] = 0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -208,7 +212,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev[:timing["i"]]]))
 
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda" if a.backend == "nccl" else "cpu")
