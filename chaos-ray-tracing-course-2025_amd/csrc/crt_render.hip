@@ -1518,6 +1518,7 @@ struct WLevel {
     WNode *nodes;            /* by ray id */
     DVec4 *cols;             /* by ray id */
     int32_t rpw;             /* levels >= 1: rays per wave (lanes rpw..63 start idle and take donated pieces) */
+    int32_t group;           /* child queue order: 1 = per wave, first children then second children */
 };
 
 template <int TRAV, bool LEVEL0, bool COUNT>
@@ -1633,8 +1634,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         int base = 0;
         if (lane == __ffsll((long long)(b1 | b2)) - 1) base = atomicAdd(lv.out_count, total);
         base = __shfl(base, __ffsll((long long)(b1 | b2)) - 1);
-        int k = base + __popcll(b1 & lt) + __popcll(b2 & lt);
-        for (int c = 0; c < nch; ++c, ++k) {
+        /* group 0: a lane's children side by side; group 1: the wave's first
+         * children (reflection rays) then its second children (refraction
+         * rays), so next-level waves hold rays of one kind */
+        const int k0 = lv.group ? base + __popcll(b1 & lt) : base + __popcll(b1 & lt) + __popcll(b2 & lt);
+        const int k1 = lv.group ? base + __popcll(b1) + __popcll(b2 & lt) : k0 + 1;
+        for (int c = 0; c < nch; ++c) {
+            const int k = c == 0 ? k0 : k1;
             WRay r;
             r.ox = co[c].x; r.oy = co[c].y; r.oz = co[c].z;
             r.dx = cd[c].x; r.dy = cd[c].y; r.dz = cd[c].z;
@@ -1887,6 +1893,7 @@ struct crt_hip_scene {
     const int32_t *dt_ref_children = nullptr, *dt_ref_leaf_tris = nullptr;
     const int64_t *dt_ref_leaf_off = nullptr;
     int wavefront = 1;             /* level-by-level recursion when GI is off (env CRT_WAVEFRONT) */
+    int wf_group = 0;              /* child queue grouped by kind per wave (env CRT_WF_GROUP, option "wf_group"); C3 A/B: no gain (4.60 vs 4.56 ms at 32 rays/wave, worse at 64) */
     int wf_oct_mask = 7;           /* node-order octant mask of wavefront levels >= 1 (env CRT_WF_OCT, option "wf_oct") */
     int wf_oct_uploaded = -1;
     int wf_rays_per_wave = 32;     /* rays per wave of wavefront levels >= 1, coop walks (env CRT_WF_RPW, option "wf_rpw"); C3: 64 4.70, 32 4.53, 16 4.58 ms */
@@ -2289,7 +2296,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
     if ((rc = wf_grow_ids(w, 3 * n0, 0, stream)) != CRT_OK) return rc;
     if ((rc = wf_grow_queue(w, 0, 2 * n0)) != CRT_OK) return rc;
     unsigned long long *cnt = sc->d_counters;
-    WLevel lv{nullptr, 0, 0, w.q[0], w.counts, (int32_t)n0, w.nodes, w.cols, 64};
+    WLevel lv{nullptr, 0, 0, w.q[0], w.counts, (int32_t)n0, w.nodes, w.cols, 64, sc->wf_group};
     const int blocks0 = (plan.ntiles + 3) / 4;
 #define CRT_WF0(T, COUNT)                                                                                   \
     hipLaunchKernelGGL((k_wf_level<T, true, COUNT>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,      \
@@ -2317,7 +2324,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
         /* coop walks: fewer rays per wave put idle lanes on the long walks (donated pieces) */
         const bool coop = sec == 4 || sec == 5 || sec == 10 || sec == 11;
         const int rpw = coop ? std::min(64, std::max(1, sc->wf_rays_per_wave)) : 64;
-        WLevel l{w.q[cur], n, L, w.q[cur ^ 1], w.counts + L, (int32_t)(base + n), w.nodes, w.cols, rpw};
+        WLevel l{w.q[cur], n, L, w.q[cur ^ 1], w.counts + L, (int32_t)(base + n), w.nodes, w.cols, rpw, sc->wf_group};
         const int64_t waves = ((int64_t)n + rpw - 1) / rpw;
         const int blocks = (int)((waves + 3) / 4);
 #define CRT_WF(SEC, COUNT)                                                                                  \
@@ -2508,6 +2515,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     if (const char *e = std::getenv("CRT_SECONDARY")) sc->secondary = std::atoi(e);
     if (const char *e = std::getenv("CRT_WAVEFRONT")) sc->wavefront = std::atoi(e);
     if (const char *e = std::getenv("CRT_GI_REFILL")) sc->gi_refill = std::atoi(e) != 0;
+    if (const char *e = std::getenv("CRT_WF_GROUP")) sc->wf_group = std::atoi(e) != 0;
     if (const char *e = std::getenv("CRT_WF_OCT")) sc->wf_oct_mask = std::atoi(e) & 7;
     if (const char *e = std::getenv("CRT_WF_RPW")) sc->wf_rays_per_wave = std::min(64, std::max(1, std::atoi(e)));
     if (const char *e = std::getenv("CRT_TRACE_WALK")) sc->trace_walk = std::atoi(e);
@@ -2938,6 +2946,8 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         sc->split_launch = value != 0;
     } else if (k == "gi_refill") {
         sc->gi_refill = value != 0;
+    } else if (k == "wf_group") {
+        sc->wf_group = value != 0;
     } else if (k == "wf_oct") {
         if (value < 0 || value > 7) return set_error(CRT_E_INVALID, "wf_oct must be 0..7");
         sc->wf_oct_mask = value;

@@ -278,7 +278,9 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  * "events" (0/1: per-render start/stop events), "wf_rpw" (1..64, default 32:
  * rays per wave of wavefront levels >= 1 under the cooperative walks; the
  * other lanes start idle and take donated pieces), "wf_oct" (0..7, default 7:
- * node-order octant mask of those levels' pruned walks), "gi_refill" (0/1,
+ * node-order octant mask of those levels' pruned walks), "wf_group" (0/1,
+ * default 0: queue each wave's first children before its second children),
+ * "gi_refill" (0/1,
  * default 1: GI frames run persistent waves that refill finished lanes with
  * the next pixel of the tile list).
  * Environment variables CRT_TRAVERSAL, CRT_SECONDARY, CRT_WAVEFRONT,

@@ -154,13 +154,24 @@ def test_pruned_synthetic_bit_exact(N, oracle):
     assert c["hits"] == r["hits"] and c["node_tests"] * 2 < r["node_tests"]
 
 
-@pytest.mark.parametrize("shards", [1, 2, 3, 8])
-def test_shard_render_and_unpack(N, shards):
+SHARD_CASES = [
+    ("14-01-acceleration-tree__scene1", 333, 200, {}, [1, 2, 3, 8]),
+    ("15-01-conclusion__scene2", 70, 45, {}, [2, 3]),                       # GI: refill kernel per shard
+    ("11-01-refractive__scene8", 150, 100, {"max_ray_depth": 8}, [2, 3]),   # wavefront levels per shard
+]
+
+
+@pytest.mark.parametrize("name,w,h,over,shards",
+                         [(n, w, h, o, k) for n, w, h, o, ks in SHARD_CASES for k in ks])
+def test_shard_render_and_unpack(N, name, w, h, over, shards):
+    """Bucket shards (multi-GPU tiles mode) rendered packed and unpacked equal
+    the full-frame render bit for bit, for primary-only, GI and depth-8
+    reflect/refract frames."""
     import ctypes as C
     from crt_amd import native
-    sc = scene_npz("14-01-acceleration-tree__scene1").set_resolution(333, 200)
+    sc = scene_npz(name).set_resolution(w, h)
     gpu = N.HipScene(sc)
-    st = N.RendererSettings.default()
+    st = N.RendererSettings.default(**over)
     full = gpu.render(st)
     stride = gpu.shard_stride(shards)
     # device buffers through the HIP runtime the library already uses
@@ -210,7 +221,7 @@ def test_window_walk_equals_packet_walk(N, oracle, monkeypatch, calib_k):
     assert ca["traversals"] == cb["traversals"] == 1920 * 1080 and ca["hits"] == cb["hits"]
 
 
-@pytest.mark.parametrize("opt,values", [("wf_rpw", [64, 32, 5, 1]), ("wf_oct", [7, 0, 4])])
+@pytest.mark.parametrize("opt,values", [("wf_rpw", [64, 32, 5, 1]), ("wf_oct", [7, 0, 4]), ("wf_group", [0, 1])])
 def test_wavefront_level_layouts_bit_identical(N, oracle, opt, values):
     """Wavefront levels >= 1 (reflect/refract recursion, C3 scene at depth 8):
     rays per wave (idle lanes take donated pieces) and the node order of the
@@ -228,8 +239,9 @@ def test_wavefront_level_layouts_bit_identical(N, oracle, opt, values):
         assert np.array_equal(bits(g.render(st)), bits(want)), f"{opt}={v}"
         c = g.count_work(st)
         assert c["traversals"] == cw["traversals"] and c["hits"] == cw["hits"], f"{opt}={v}"
-    with pytest.raises(Exception):
-        N.HipScene(sc).set_option(opt, 99)
+    if opt != "wf_group":
+        with pytest.raises(Exception):
+            N.HipScene(sc).set_option(opt, 99)
 
 
 @pytest.mark.parametrize("w,h", [(70, 45), (96, 96)])
