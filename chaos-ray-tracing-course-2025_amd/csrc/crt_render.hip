@@ -65,6 +65,19 @@ struct Frame {
     Vec alb;    /* diffuse: albedo sample | refract: .x = fresnel                */
 };
 
+/* global (address space 1) load: a global_load instead of a flat one, whose
+ * completion is tracked by vmcnt alone (flat loads also count in lgkmcnt, so
+ * every wait on them drains the LDS queue too) */
+template <class T>
+__device__ __forceinline__ T load_global(const T *p, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    using GT = const __attribute__((address_space(1))) T;
+    return ((GT *)p)[i];
+#else
+    return p[i];
+#endif
+}
+
 struct LaneCounts {
     uint32_t traversals, nodes, tris, hits;
     /* wave-uniform steps of the packet walks (kept by every lane, added once per wave) */
@@ -317,7 +330,7 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
     float lim = INFINITY;               /* best t known for the piece's ray (pruning bound) */
     unsigned long long mine = ~0ull;    /* best key found in the current piece */
     int sp = 0;                         /* wave-uniform stack depth */
-    NT nd = nb[0];
+    NT nd = load_global(nb, 0);
     for (;;) {
         if (COUNT) ++c.wave_nodes;
         bool busy = (i < end) || (lc > 0);
@@ -341,7 +354,7 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
                         pr = make_prune_ray(ro, rd, s.prune_origin_max);
                         lim = key_t(L.key[r]);
                     }
-                    nd = nb[i];
+                    nd = load_global(nb, i);
                     busy = true;
                 }
             }
@@ -356,7 +369,11 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
                 const int slot = lf + k;
                 float t;
                 if (COUNT) ++c.tris;
-                if (tri_hit(ro, rd, s.slots[slot], s.slot_cull + slot, t)) {
+                /* the whole record and its cull flag in one round trip; branch-free
+                 * test (a wave's scattered lanes take every branch of tri_hit anyway) */
+                const DTriGeo g = load_global(s.slots, slot);
+                const bool cl = load_global(s.slot_cull, slot) != 0;
+                if (tri_hit_bf(ro, rd, g, cl, t)) {
                     const unsigned long long kk = coop_key(t, slot);
                     mine = kk < mine ? kk : mine;
                     if (PRUNE) lim = fminf(lim, t);
@@ -365,8 +382,8 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
             } else {
                 const int i1 = i + 1 < n ? i + 1 : n - 1;
                 const int alt = nd.b < 0 ? (nd.a < n ? nd.a : n - 1) : i1;
-                const NT n1 = nb[i1];
-                const NT n2 = nb[alt];
+                const NT n1 = load_global(nb, i1);
+                const NT n2 = load_global(nb, alt);
                 bool pass = false;
                 if (WN::alive(nd, pr, lim)) {
                     pass = box_hit_r(ro, rd, rr, WN::cell(nd));
