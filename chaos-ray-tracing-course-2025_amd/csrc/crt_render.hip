@@ -1037,17 +1037,18 @@ __device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, bool acti
 
 __device__ __forceinline__ void make_hit(const DeviceScene &s, Vec o, Vec d, float t, int slot, HitRec &h,
                                          int32_t *tri_out = nullptr) {
-    const DTriGeo g = s.slots[slot];
-    const int32_t tri = s.slot_tri[slot];
-    const DTriAttr at = s.tri_attr[tri];
+    const DTriGeo g = load_global(s.slots, slot);
+    const int32_t tri = load_global(s.slot_tri, slot);
+    const DTriAttr at = load_global(s.tri_attr, tri);
     const DVec4 zero = {0.f, 0.f, 0.f, 0.f};
     DVec4 n0 = zero, n1 = zero, n2 = zero;
     if (at.mat_flags < 0) {
-        n0 = s.vnormal[at.i0];
-        n1 = s.vnormal[at.i1];
-        n2 = s.vnormal[at.i2];
+        n0 = load_global(s.vnormal, at.i0);
+        n1 = load_global(s.vnormal, at.i1);
+        n2 = load_global(s.vnormal, at.i2);
     }
-    hit_record(o, d, t, g, at, n0, n1, n2, s.vuv[at.i0], s.vuv[at.i1], s.vuv[at.i2], h);
+    hit_record(o, d, t, g, at, n0, n1, n2, load_global(s.vuv, at.i0), load_global(s.vuv, at.i1),
+               load_global(s.vuv, at.i2), h);
     if (tri_out) *tri_out = tri;
 }
 
@@ -1076,10 +1077,10 @@ struct alignas(8) F2 { float c, s; };
 __device__ __forceinline__ void gi_ray(const DeviceScene &s, const DSettings &st, const Frame &f, Pcg32 &rng, Vec &o,
                                        Vec &d) {
     const uint32_t m1 = rng.next() >> 9;
-    const F2 cs1 = reinterpret_cast<const F2 *>(s.gi_pi)[m1];
+    const F2 cs1 = load_global(reinterpret_cast<const F2 *>(s.gi_pi), (int)m1);
     Vec dir = vec(cs1.c, cs1.s, 0.0f);
     const uint32_t m2 = rng.next() >> 9;
-    const F2 cs2 = reinterpret_cast<const F2 *>(s.gi_2pi)[m2];
+    const F2 cs2 = load_global(reinterpret_cast<const F2 *>(s.gi_2pi), (int)m2);
     const float c = cs2.c, sn = cs2.s;
     const float roty[9] = {c, 0.0f, -sn, 0.0f, 1.0f, 0.0f, sn, 0.0f, c};      /* crt_matrix.cpp:14-20 */
     dir = vec_mat(dir, roty);
