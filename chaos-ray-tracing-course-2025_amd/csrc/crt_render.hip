@@ -1467,6 +1467,25 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(MAXF == 4 ? (TRA
     }
 }
 
+/* The GI refill kernels are compiled in a translation unit of their own
+ * (crt_render_gi.hip, which includes this file with CRT_GI_TU defined) so that
+ * they can take their own LLVM scheduling strategy (max-memory-clause: C4
+ * 1080^2 77.3 -> 75.3 ms, profiles/r01/ab_wf_waves_sched_strategy.log) while
+ * the C2 camera kernel keeps the default one. */
+#define CRT_REFILL_INSTANCES(X) X(4, 4, false) X(4, 4, true) X(4, 10, false) X(4, 10, true) \
+    X(16, 4, false) X(16, 4, true) X(64, 4, false) X(64, 4, true)
+#define CRT_REFILL_SIG(MAXF, T, C) void k_render_refill<MAXF, T, C>(const DeviceScene *__restrict__, DSettings, \
+    const Tile *__restrict__, int, float *__restrict__, int32_t *__restrict__, unsigned long long *__restrict__);
+#ifdef CRT_GI_TU
+#define CRT_REFILL_INST(MAXF, T, C) template __global__ CRT_REFILL_SIG(MAXF, T, C)
+CRT_REFILL_INSTANCES(CRT_REFILL_INST)
+#else
+#define CRT_REFILL_EXTERN(MAXF, T, C) extern template __global__ CRT_REFILL_SIG(MAXF, T, C)
+CRT_REFILL_INSTANCES(CRT_REFILL_EXTERN)
+#endif
+
+#ifndef CRT_GI_TU
+
 /* Calibration probe (measured-cost tile plan): the camera rays of a tile
  * list traced with the frame's primary walk, no shading.  Each wave writes
  * its cost: for the packet walks the wave's node + triangle + edge steps
@@ -1778,7 +1797,9 @@ __global__ __launch_bounds__(256) void k_unpack(const UnpackBucket *__restrict__
     }
 }
 
+#endif  // CRT_GI_TU
 }  // namespace crt_amd
+#ifndef CRT_GI_TU
 
 /* ====================================================================== */
 /*  C-ABI                                                                  */
@@ -3003,3 +3024,4 @@ int crt_hip_wave_counts(crt_hip_scene *sc, crt_wave_counts *out) {
 }
 
 }  // extern "C"
+#endif  // CRT_GI_TU
