@@ -1479,12 +1479,12 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(MAXF == 4 ? (TRA
 #ifdef CRT_GI_TU
 #define CRT_REFILL_INST(MAXF, T, C) template __global__ CRT_REFILL_SIG(MAXF, T, C)
 CRT_REFILL_INSTANCES(CRT_REFILL_INST)
-#else
+#elif !defined(CRT_SIDE_TU)
 #define CRT_REFILL_EXTERN(MAXF, T, C) extern template __global__ CRT_REFILL_SIG(MAXF, T, C)
 CRT_REFILL_INSTANCES(CRT_REFILL_EXTERN)
 #endif
 
-#ifndef CRT_GI_TU
+
 
 /* Calibration probe (measured-cost tile plan): the camera rays of a tile
  * list traced with the frame's primary walk, no shading.  Each wave writes
@@ -1716,6 +1716,21 @@ __device__ __forceinline__ Vec wf_compose(const WNode &nd, const DVec4 *__restri
     return vadd(vscale(c0, fr), vscale(c1, 1.0f - fr));
 }
 
+/* Wavefront levels >= 1 (C3): own translation unit (crt_render_wf.hip) and
+ * LLVM scheduling strategy, as for the GI refill kernels above. */
+#define CRT_WF_INSTANCES(X) X(4, false) X(4, true) X(5, false) X(5, true) X(9, false) X(9, true) \
+    X(10, false) X(10, true) X(11, false) X(11, true)
+#define CRT_WF_SIG(SEC, C) void k_wf_level<SEC, false, C>(const DeviceScene *__restrict__, DSettings, \
+    const Tile *__restrict__, int, WLevel, unsigned long long *__restrict__);
+#ifdef CRT_WF_TU
+#define CRT_WF_INST(SEC, C) template __global__ CRT_WF_SIG(SEC, C)
+CRT_WF_INSTANCES(CRT_WF_INST)
+#elif !defined(CRT_SIDE_TU)
+#define CRT_WF_EXTERN(SEC, C) extern template __global__ CRT_WF_SIG(SEC, C)
+CRT_WF_INSTANCES(CRT_WF_EXTERN)
+#endif
+
+#ifndef CRT_SIDE_TU
 /* levels >= 1, deepest first: colour of every activation of the level */
 __global__ __launch_bounds__(256) void k_wf_compose(const WNode *__restrict__ nodes, DVec4 *__restrict__ cols,
                                                     int32_t begin, int32_t n) {
@@ -1797,9 +1812,9 @@ __global__ __launch_bounds__(256) void k_unpack(const UnpackBucket *__restrict__
     }
 }
 
-#endif  // CRT_GI_TU
+#endif  // CRT_SIDE_TU
 }  // namespace crt_amd
-#ifndef CRT_GI_TU
+#ifndef CRT_SIDE_TU
 
 /* ====================================================================== */
 /*  C-ABI                                                                  */
@@ -3024,4 +3039,4 @@ int crt_hip_wave_counts(crt_hip_scene *sc, crt_wave_counts *out) {
 }
 
 }  // extern "C"
-#endif  // CRT_GI_TU
+#endif  // CRT_SIDE_TU
