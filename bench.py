@@ -7,48 +7,53 @@ traces exactly one ray per pixel on this scene (its shadow-ray loop is dead code
 crt_renderer.cpp:29-44), so rays = traversals = 2,073,600 per frame; the count
 is re-measured by the instrumented kernel, not assumed.
 
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+
 N=1: the frame is rendered into HBM (scene + image resident; no PCIe in the
-timed region).  N>1 (one process per GPU, torchrun), two modes:
+timed region).  The end-to-end figure of the reference's call (render_image
+returns a host image, main.cpp:37-43: render + D2H into a pinned host buffer)
+is reported beside it as config.e2e_ms.
 
-  --mode frames (default, weak scaling): every rank renders its own whole
-      frame per step into its own HBM (frame-parallel rendering of a frame
-      sequence: per-GPU work fixed, no data-path collective — pixels never need
-      to meet); value = all ranks' rays / the slowest rank's time.
-  --mode tiles (strong scaling, the north_star's image-tile sharding): the
-      reference's bucket grid is dealt round-robin to ranks, each rank renders
-      its buckets packed, the tiles are gathered to rank 0 over RCCL
-      (torch.distributed "nccl") and unpacked there — one frame per step;
-      frame k's gather runs on RCCL's stream while frame k+1 renders
-      (double-buffered, FramePipeline).
+N>1: one process per GPU.  Without torchrun's environment, `--gpus N` starts
+the N rank processes itself (python -m torch.distributed.run, before this
+process touches the GPU) and exits with their status.  Default mode `tiles`
+(strong scaling, the north_star's image-tile sharding): the reference's bucket
+grid (crt_renderer.cpp:160-174) is dealt bucket k -> rank k mod N, each rank
+renders its buckets packed, the packed shards are gathered to rank 0 over RCCL
+(torch.distributed "nccl") and unpacked there, one frame per step; frame k's
+gather runs on RCCL's stream while frame k+1 renders (FramePipeline).
+`--payload u8` gathers write_ppm's 8-bit components (device quantise-and-pack,
+crt_image_ppm.cpp:9-23) instead of fp32 (4x fewer bytes into rank 0).  The
+frame-parallel mode (`frames`, weak scaling: every rank renders whole frames)
+is reported as a secondary field.
 
-Also reported: the roofline of the render kernel (algorithmic bytes per launch
-÷ measured kernel time vs 8 TB/s HBM) and the CPU oracle (restatement of the
-reference, same threads-over-buckets structure) timed on this host.
+Also reported: the roofline of the render kernel (see roofline_block) and the
+CPU baseline (oracle/crt_oracle.cpp, the from-scratch restatement of the
+reference's render_image with its bucket queue and thread pool) timed on this
+host in child processes that never touch the GPU: all cores of the affinity
+mask, and one core pinned.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
-sys.path.insert(0, str(ROOT / "chaos-ray-tracing-course-2025_amd"))
-sys.path.insert(0, str(ROOT))
-
-import numpy as np  # noqa: E402
-import torch  # noqa: E402  (import before libcrt_hip so both share torch's HIP runtime)
-import torch.distributed as dist  # noqa: E402
-
-from crt_amd import native as N  # noqa: E402
-from crt_amd.distributed import FramePipeline  # noqa: E402
-from crt_amd.scene_npz import load_npz  # noqa: E402
+PKG = ROOT / "chaos-ray-tracing-course-2025_amd"
+for _p in (str(PKG), str(ROOT)):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
 
 SCENES = ROOT / "tests" / "golden" / "scenes"
 # BASELINE.json configs: c2 is the headline (metric) workload; the others are
-# the remaining single-GPU-sized configs, for --config runs (N>1 as for c2)
+# the remaining configs, for --config runs
 CONFIGS = {
     "c2": {"scene": "14-01-acceleration-tree__scene1", "size": (1920, 1080), "settings": {}, "cpu_size": (1920, 1080),
            "label": "14-01-acceleration-tree/scene1", "note": "primary rays (HEAD traces no shadow rays)"},
@@ -59,11 +64,18 @@ CONFIGS = {
     "c5": {"synthetic": 1_000_000, "size": (3840, 2160), "settings": {}, "cpu_size": (480, 270),
            "label": "synthetic 1M-triangle random mesh", "note": "deep KD-tree, HBM-resident scene"},
 }
-HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
-NODE_BYTES, TRI_BYTES, PIXEL_BYTES = 32, 52, 12   # SURVEY §8(d) algorithmic bytes
+
+# Peaks (/opt/skills/guides/MI355X_MICROARCH.md): HBM3E 8 TB/s; L2 ~34.5 TB/s
+# aggregate; VALU issue: a wave64 VALU instruction occupies a SIMD-32 for 2
+# cycles -> 256 CUs x 4 SIMDs x 2.4 GHz / 2 wave-instructions/s.
+HBM_PEAK_GBS = 8000.0
+L2_PEAK_GBS = 34500.0
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2.0
+NODE_BYTES, TRI_BYTES, PIXEL_BYTES = 32, 52, 12      # SURVEY §8(d) algorithmic bytes
+PNODE_BYTES, SLOT_BYTES = 64, 48                     # device records (crt_layout.h)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
@@ -72,43 +84,96 @@ def parse():
                    help="BASELINE config (c2 = the headline metric workload)")
     p.add_argument("--width", type=int, default=None, help="override the config's image width")
     p.add_argument("--height", type=int, default=None, help="override the config's image height")
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (wall s)")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample, all cores (wall s)")
+    p.add_argument("--cpu-single-seconds", type=float, default=6.0, help="bounded single-core CPU sample (wall s)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
+    p.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (render + D2H) timing")
+    p.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo stages "
+                                                    "shards through host memory, for rehearsals on one GPU)")
     p.add_argument("--check", action="store_true", help="rank 0: compare the last frame with a 1-GPU render")
-    p.add_argument("--mode", choices=["frames", "tiles"], default="frames",
-                   help="N>1: frames = each GPU renders whole frames (weak scaling, default); "
-                        "tiles = one frame sharded over the GPUs + RCCL gather (strong scaling)")
+    p.add_argument("--mode", choices=["tiles", "frames"], default="tiles",
+                   help="N>1: tiles = one frame sharded over the GPUs + RCCL gather (strong scaling, default); "
+                        "frames = each GPU renders whole frames (weak scaling)")
+    p.add_argument("--payload", choices=["f32", "u8"], default="f32",
+                   help="tiles mode: gather fp32 RGB (the render_image image) or write_ppm's 8-bit components")
+    p.add_argument("--no-secondary", action="store_true", help="N>1: skip the secondary frames-mode measurement")
     p.add_argument("--event-every", type=int, default=5,
                    help="bracket every k-th render of the timed region with HIP events (kernel time sample; "
                         "an event pair between two renders costs ~7 us of a ~165 us C2 step)")
-    p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
-                   help="per-launch HBM bytes measured by rocprofv3 --pmc (profiles/), if present")
-    return p.parse_args()
+    p.add_argument("--pmc-json", default=None,
+                   help="PMC record of the render kernel (profiles/r02/pmc_<config>.json by default); used for "
+                        "the issue roofline and measured HBM traffic when its build id equals the library's")
+    p.add_argument("--selftest-launch", action="store_true",
+                   help="launcher plumbing only: ranks join the process group and report; no GPU work")
+    p.add_argument("--cpu-worker", default=None, help=argparse.SUPPRESS)
+    return p.parse_args(argv)
 
 
+# --------------------------------------------------------------------------
+#  N>1 launcher (parent process: never touches the GPU)
+# --------------------------------------------------------------------------
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nproc: int, argv: list[str]) -> int:
+    """Start `nproc` rank processes of this script under torch.distributed.run
+    (one per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their environment) as
+    children, and return their exit status.  Nothing here initialises HIP."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(Path(__file__).resolve()), *argv]
+    print(f"bench: launching {nproc} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
+# --------------------------------------------------------------------------
+#  CPU baseline (child processes: oracle only, no GPU)
+# --------------------------------------------------------------------------
 def make_scene(cfg: dict, width: int, height: int):
     if "synthetic" in cfg:
         from crt_amd.synthetic import c5_scene
         return c5_scene(cfg["synthetic"], width=width, height=height)
+    from crt_amd.scene_npz import load_npz
     return load_npz(SCENES / f"{cfg['scene']}.npz").set_resolution(width, height)
 
 
-def cpu_baseline(scene, settings, seconds: float, size_note: str = "") -> dict:
+def cpu_worker(spec: dict) -> dict:
+    """Times the oracle's render_image (bucket queue + thread pool, like
+    crt_renderer.cpp:157-199) on whole frames: at least `min_frames`, until
+    `seconds` of wall time.  Scene build stays outside the timer (main.cpp:37)."""
+    if spec.get("pin") is not None:
+        os.sched_setaffinity(0, {int(spec["pin"])})
+    from crt_amd.native import RendererSettings, WorkCounts
     from oracle import pyoracle
-    from crt_amd.native import WorkCounts
-    threads = min(16, os.cpu_count() or 1)
+    cfg = CONFIGS[spec["config"]]
+    scene = make_scene(cfg, spec["w"], spec["h"])
+    st = RendererSettings.default(**cfg["settings"])
     orc = pyoracle.OracleScene(scene)
-    frames, rays = 0, 0
+    wc = WorkCounts()
+    orc.render(st, nthreads=spec["threads"], counts=wc)      # warm-up frame, and the frame's ray count
+    rays = int(wc.traversals)
+    times = []
     t0 = time.perf_counter()
-    while True:
-        wc = WorkCounts()
-        orc.render(settings, nthreads=threads, counts=wc)
-        frames += 1
-        rays += wc.traversals
-        el = time.perf_counter() - t0
-        if el >= seconds or frames >= 200:
-            break
+    while len(times) < spec["min_frames"] or (time.perf_counter() - t0 < spec["seconds"] and len(times) < 500):
+        s = time.perf_counter()
+        orc.render(st, nthreads=spec["threads"])
+        times.append(time.perf_counter() - s)
+    return {"rays_per_frame": rays, "frames": len(times), "best_s": min(times),
+            "median_s": statistics.median(times), "wall_s": time.perf_counter() - t0}
+
+
+def run_cpu_worker(spec: dict) -> dict:
+    out = subprocess.run([sys.executable, str(Path(__file__).resolve()), "--cpu-worker", json.dumps(spec)],
+                         capture_output=True, text=True, check=True)
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def cpu_info() -> dict:
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -117,24 +182,161 @@ def cpu_baseline(scene, settings, seconds: float, size_note: str = "") -> dict:
                 break
     except OSError:
         pass
-    return {"value": rays / el / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{frames} full frames of the same workload{size_note}, oracle/crt_oracle.cpp render_image "
-                      f"(bucket queue, {threads} threads, g++ -O3 no FMA) on {model or 'host CPU'}, "
-                      f"{el:.1f} s wall"}
+    quota = None
+    try:   # cgroup v2 CPU quota: "max 100000" or "<quota> <period>"
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"model": model or "host CPU", "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": quota}
+
+
+def cpu_baseline(config: str, w: int, h: int, seconds: float, single_seconds: float, size_note: str) -> dict:
+    info = cpu_info()
+    threads = info["affinity_cpus"]          # hardware_concurrency() of this process (crt_renderer.cpp:178)
+    multi = run_cpu_worker({"config": config, "w": w, "h": h, "threads": threads, "pin": None,
+                            "seconds": seconds, "min_frames": 5})
+    pin = sorted(os.sched_getaffinity(0))[0]
+    single = run_cpu_worker({"config": config, "w": w, "h": h, "threads": 1, "pin": pin,
+                             "seconds": single_seconds, "min_frames": 2})
+    rays = multi["rays_per_frame"]
+    return {
+        "value": round(rays / multi["median_s"] / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+        "best": round(rays / multi["best_s"] / 1e6, 3), "frame_ms_median": round(multi["median_s"] * 1e3, 3),
+        "frame_ms_best": round(multi["best_s"] * 1e3, 3),
+        "single_core": {"value": round(single["rays_per_frame"] / single["median_s"] / 1e6, 3), "unit": "Mrays/s",
+                        "frame_ms_median": round(single["median_s"] * 1e3, 3), "frames": single["frames"],
+                        "pinned_cpu": pin},
+        "cpu_model": info["model"], "cgroup_cpu_quota": info["cgroup_cpu_quota"],
+        "sample": f"{multi['frames']} whole frames{size_note} of the same workload, oracle/crt_oracle.cpp "
+                  f"render_image (24-px bucket queue + {threads} threads = the affinity mask, g++ -O3, no FMA) in a "
+                  f"child process on {info['model']}; value = rays / median frame time; single_core = the same "
+                  f"on one pinned CPU ({single['frames']} frames)",
+    }
+
+
+# --------------------------------------------------------------------------
+#  roofline
+# --------------------------------------------------------------------------
+def roofline_block(kernel_ms: float, counts: dict, waves: dict, npx: int, pmc: dict | None,
+                   build_id: str, shard_frac: float) -> dict:
+    """Bounds of the dominant render kernel, per launch:
+      s8d     — SURVEY §8(d) algorithmic bytes (32 B/node test + 52 B/triangle
+                test + 12 B/pixel, the kernel's own pruned counts) / kernel time:
+                a work rate; lanes share these records through the caches, so
+                it is not an HBM occupancy (it can exceed the HBM peak).
+      l2      — wave-unique record bytes (per wave step one 64-B node record,
+                per triangle step one 48-B slot record; crt_hip_wave_counts)
+                + 12 B/pixel, against the L2 bandwidth.
+      hbm     — measured HBM bytes (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE of
+                this build) against the HBM peak.
+      valu    — measured VALU wave-instructions (SQ_INSTS_VALU of this build)
+                against the VALU issue rate.
+    `bound` names the candidate with the largest fraction."""
+    sec = kernel_ms * 1e-3
+    s8d = (NODE_BYTES * counts["node_tests"] + TRI_BYTES * counts["triangle_tests"] + PIXEL_BYTES * npx) * shard_frac
+    uniq = (PNODE_BYTES * waves.get("node_steps", 0) + SLOT_BYTES * waves.get("triangle_steps", 0)
+            + PIXEL_BYTES * npx) * shard_frac
+    cand = {"l2": {"achieved": uniq / sec / 1e9, "peak": L2_PEAK_GBS, "unit": "GB/s",
+                   "bytes_per_launch": int(uniq)}}
+    fresh = pmc is not None and pmc.get("build_id") == build_id
+    traffic = None
+    if fresh:
+        traffic = pmc.get("hbm_bytes_per_launch")
+        if traffic:
+            traffic = traffic * shard_frac
+            cand["hbm"] = {"achieved": traffic / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "bytes_per_launch": int(traffic)}
+        if pmc.get("valu_insts_per_launch"):
+            v = pmc["valu_insts_per_launch"] * shard_frac
+            cand["valu"] = {"achieved": v / sec / 1e9, "peak": VALU_PEAK_GINST, "unit": "Ginst/s",
+                            "insts_per_launch": int(v), "salu_insts_per_launch": pmc.get("salu_insts_per_launch")}
+    for c in cand.values():
+        c["frac"] = round(c["achieved"] / c["peak"], 5)
+        c["achieved"] = round(c["achieved"], 2)
+    bound = max(cand, key=lambda k: cand[k]["frac"])
+    b = cand[bound]
+    return {"bound": {"valu": "valu_issue", "l2": "l2", "hbm": "hbm"}[bound], "achieved": b["achieved"],
+            "peak": b["peak"], "unit": b["unit"], "frac": b["frac"],
+            "traffic": int(traffic) if traffic else None,
+            "pmc": (f"{pmc.get('source', '?')} (build {build_id})" if fresh else
+                    f"stale or absent (library build {build_id}); traffic/valu omitted"),
+            "candidates": cand,
+            "s8d_work_rate": {"achieved": round(s8d / sec / 1e9, 2), "unit": "GB/s", "bytes_per_launch": int(s8d),
+                              "note": "SURVEY §8(d) algorithmic bytes / kernel time: lanes share records through "
+                                      "the caches, so this is a work rate, not HBM occupancy"}}
+
+
+def load_pmc(path: str | None, config: str, w: int, h: int) -> dict | None:
+    p = Path(path) if path else ROOT / "profiles" / "r02" / f"pmc_{config}.json"
+    try:
+        d = json.loads(p.read_text())
+    except (OSError, ValueError):
+        return None
+    if d.get("config") != config or d.get("size") != [w, h]:
+        return None
+    d["source"] = str(p.relative_to(ROOT)) if p.is_relative_to(ROOT) else str(p)
+    return d
+
+
+# --------------------------------------------------------------------------
+#  ranks
+# --------------------------------------------------------------------------
+def selftest_launch(a) -> None:
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group(a.backend if a.backend != "nccl" else "gloo")
+        import torch
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        world = dist.get_world_size()
+        ok = int(t.item()) == world
+    else:
+        ok = True
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(json.dumps({"selftest": "launch", "n_gpus": world, "requested": a.gpus, "all_reduce_ok": ok,
+                          "scaling": "strong" if a.mode == "tiles" else "weak"}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
-    a = parse()
+    argv = sys.argv[1:]
+    a = parse(argv)
+    if a.cpu_worker is not None:
+        print(json.dumps(cpu_worker(json.loads(a.cpu_worker))), flush=True)
+        return 0
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(a.gpus, argv)
+    if a.selftest_launch:
+        selftest_launch(a)
+        return 0
+
+    import numpy as np
+    import torch  # import before libcrt_hip so both share torch's HIP runtime
+    import torch.distributed as dist
+    from crt_amd import native as N
+    from crt_amd.distributed import FramePipeline
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    local = local % max(1, torch.cuda.device_count())   # more ranks than GPUs only in rehearsals (gloo)
+    ndev = max(1, torch.cuda.device_count())
+    if world > ndev and a.backend == "nccl":
+        raise SystemExit(f"bench: {world} ranks need {world} GPUs for RCCL (found {ndev}); "
+                         f"rehearse with --backend gloo")
+    local = local % ndev                       # more ranks than GPUs only in gloo rehearsals
     torch.cuda.set_device(local)
     if world > 1:
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(a.backend)
+        world = dist.get_world_size()          # what the process group actually initialised
+    dist_backend = dist.get_backend() if world > 1 else None
+    host_staged = world > 1 and dist_backend != "nccl"
 
     cfg = CONFIGS[a.config]
     W, H = a.width or cfg["size"][0], a.height or cfg["size"][1]
@@ -143,13 +345,16 @@ def main():
     # the library's own start/stop events (crt_hip_last_kernel_ms) would sit inside
     # this script's timing events and add ~8 us per frame: timing here uses torch's
     gpu = N.HipScene(scene, device=local, events=0)
+    build_id = N.build_id()
     # an explicit stream: the render kernel, the gather and the timing events
     # all go on it (handle 0 would mean "the scene's own stream" to the C-ABI)
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
 
-    frame = torch.empty(W * H * 3, dtype=torch.float32, device="cuda")
+    npx = W * H
+    frame = torch.empty(npx * 3, dtype=torch.float32, device="cuda")
+    frame8 = torch.empty(npx * 3, dtype=torch.uint8, device="cuda")
     timing = {"events": None, "i": 0, "n": 0}
 
     def timed(launch):
@@ -164,93 +369,143 @@ def main():
             ev[timing["i"]][1].record(stream)
             timing["i"] += 1
 
-    def render_full():
-        timed(lambda: gpu.render_device(settings, frame.data_ptr(), sptr))
+    u8 = a.payload == "u8"
+    stride = gpu.shard_stride(world) if world > 1 else npx * 3
+    shard_f32 = torch.empty(stride, dtype=torch.float32, device="cuda")   # u8 payload / host staging scratch
 
     def render_shard(packed):
-        timed(lambda: gpu.render_shard(settings, rank, world, packed.data_ptr(), sptr))
+        # packed: this rank's slot of the gather (device, or host for gloo)
+        dst = shard_f32 if (u8 or host_staged) else packed
+        timed(lambda: gpu.render_shard(settings, rank, world, dst.data_ptr(), sptr))
+        if u8:
+            tgt = packed if not host_staged else shard_u8
+            N.quantize_rgb8(shard_f32.data_ptr(), stride, tgt.data_ptr(), 255, sptr)
+            if host_staged:
+                packed.copy_(shard_u8)
+        elif host_staged:
+            packed.copy_(shard_f32)
 
-    tiles = world > 1 and a.mode == "tiles"
-    if tiles:
-        # frame k's RCCL gather overlaps frame k+1's shard render (crt_amd.distributed.FramePipeline)
-        pipe = FramePipeline(rank, world, gpu.shard_stride(world),
-                             lambda n: torch.empty(n, dtype=torch.float32, device="cuda"), render_shard,
-                             lambda flat: gpu.unpack_shards(world, flat.data_ptr(), frame.data_ptr(), sptr), dist)
+    def unpack(flat):
+        src = flat
+        if host_staged:
+            src = flat_dev_u8 if u8 else flat_dev
+            src.copy_(flat)
+        if u8:
+            gpu.unpack_shards_rgb8(world, src.data_ptr(), frame8.data_ptr(), sptr)
+        else:
+            gpu.unpack_shards(world, src.data_ptr(), frame.data_ptr(), sptr)
 
-    def step():
-        if tiles:
+    mode = a.mode if world > 1 else "single"
+    if world > 1:
+        dt = torch.uint8 if u8 else torch.float32
+        shard_u8 = torch.empty(stride, dtype=torch.uint8, device="cuda")
+        if host_staged and rank == 0:
+            flat_dev = torch.empty(stride * world, dtype=torch.float32, device="cuda")
+            flat_dev_u8 = torch.empty(stride * world, dtype=torch.uint8, device="cuda")
+        dev = "cpu" if host_staged else "cuda"
+        pipe = FramePipeline(rank, world, stride, lambda n: torch.empty(n, dtype=dt, device=dev), render_shard,
+                             unpack, dist)
+
+    def step(m):
+        if m == "tiles":
             pipe.step()
         else:
-            render_full()
+            timed(lambda: gpu.render_device(settings, frame.data_ptr(), sptr))
 
-    def drain():
-        if tiles:
+    def drain(m):
+        if m == "tiles":
             pipe.drain()
 
     # work counters of one full frame (outside the timed region)
     counts = gpu.count_work(settings)
+    waves = gpu.wave_counts()
     rays_per_frame = counts["traversals"]
 
-    for _ in range(a.warmup):
-        step()
-    drain()
-    torch.cuda.synchronize()
+    def measure(m, steps):
+        for _ in range(a.warmup):
+            step(m)
+        drain(m)
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        timing["events"], timing["n"], timing["i"] = ev, 0, 0
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step(m)
+        drain(m)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        km = float(np.mean([s.elapsed_time(e) for s, e in ev[:timing["i"]]]))
+        timing["events"] = None
+        if world > 1:   # max over ranks
+            t = torch.tensor([el, km], dtype=torch.float64, device="cuda" if dist_backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el, km = float(t[0]), float(t[1])
+        return el, km
 
-    # kernel duration: event pairs around every k-th render launch of the timed region, on the launch stream
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    timing["events"] = ev
-    timing["n"] = 0
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    drain()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev[:timing["i"]]]))
+    elapsed, kern_ms = measure(mode, a.steps)
 
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda" if a.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-
+    check = None
     if a.check and rank == 0:
         want = gpu.render(settings)
-        got = frame.view(H, W, 3).cpu().numpy()
-        same = np.array_equal(got.view(np.uint32), want.view(np.uint32))
-        print(f"check: last frame {'bit-identical to' if same else 'DIFFERS from'} the 1-GPU render", flush=True)
+        if mode == "tiles" and u8:
+            wd = torch.from_numpy(want).reshape(-1).to("cuda")
+            w8 = torch.empty(npx * 3, dtype=torch.uint8, device="cuda")
+            N.quantize_rgb8(wd.data_ptr(), npx * 3, w8.data_ptr(), 255, sptr)
+            torch.cuda.synchronize()
+            same = torch.equal(w8, frame8)
+        else:
+            got = frame.view(H, W, 3).cpu().numpy()
+            same = np.array_equal(got.view(np.uint32), want.view(np.uint32))
+        check = "bit-identical" if same else "DIFFERS"
+        print(f"check: last frame {'bit-identical to' if same else 'DIFFERS from'} the 1-GPU render "
+              f"(mode {mode}, payload {a.payload}, world {world}, backend {dist_backend or 'none'})", flush=True)
         if not same:
             raise SystemExit(1)
 
     ms_per_step = elapsed / a.steps * 1e3
-    frames_per_step = world if (world > 1 and not tiles) else 1
+    frames_per_step = world if mode == "frames" else 1
     mrays = rays_per_frame * frames_per_step * a.steps / elapsed / 1e6
 
-    # roofline of the render kernel: algorithmic bytes of one launch / its duration
-    shard_frac = 1.0 / world if tiles else 1.0
-    alg_bytes = (NODE_BYTES * counts["node_tests"] + TRI_BYTES * counts["triangle_tests"]
-                 + PIXEL_BYTES * W * H) * shard_frac
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    try:
-        tj = json.loads(Path(a.traffic_json).read_text())
-        if a.config == "c2" and tj.get("workload") == f"14-01/scene1 {W}x{H}" and world == 1:
-            traffic = tj.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
+    secondary = None
+    if world > 1 and mode == "tiles" and not a.no_secondary:
+        el2, km2 = measure("frames", a.steps)
+        secondary = {"mode": "frames", "scaling": "weak", "value": round(rays_per_frame * world * a.steps / el2 / 1e6, 3),
+                     "unit": "Mrays/s", "ms_per_step": round(el2 / a.steps * 1e3, 5), "kernel_ms": round(km2, 5),
+                     "frames_per_step": world}
+
+    # end-to-end frame time of the reference's call: render_image returns a
+    # host image (crt_image.h:11-27), the CLI times the whole call (main.cpp:37-43)
+    e2e = None
+    if world == 1 and not a.no_e2e:
+        host = torch.empty(npx * 3, dtype=torch.float32, pin_memory=True)
+        for _ in range(3):
+            gpu.render_host(settings, host.data_ptr())
+        ts = []
+        for _ in range(max(5, min(a.steps, 50))):
+            s = time.perf_counter()
+            gpu.render_host(settings, host.data_ptr())
+            ts.append(time.perf_counter() - s)
+        e2e = statistics.median(ts) * 1e3
+
+    shard_frac = 1.0 / world if mode == "tiles" else 1.0
+    pmc = load_pmc(a.pmc_json, a.config, W, H)
+    roof = roofline_block(kern_ms, counts, waves, npx, pmc, build_id, shard_frac)
 
     out = None
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
             cw, ch = cfg["cpu_size"] if (W, H) == cfg["size"] else (W, H)
-            note = "" if (cw, ch) == (W, H) else f" at {cw}x{ch} (same scene and settings; Mrays/s is per-ray work, size-independent up to image content)"
-            cpu = cpu_baseline(scene if (cw, ch) == (W, H) else make_scene(cfg, cw, ch), settings, a.cpu_seconds, note)
+            note = "" if (cw, ch) == (W, H) else f" at {cw}x{ch} (same scene and settings; Mrays/s is per-ray work)"
+            cpu = cpu_baseline(a.config, cw, ch, a.cpu_seconds, a.cpu_single_seconds, note)
+        parallel = {"single": "single-gpu", "tiles": f"bucket-shard{world}+{'rccl' if dist_backend == 'nccl' else dist_backend}"
+                    f"-gather-{a.payload}", "frames": f"frame-parallel{world}"}[mode]
         out = {
             "metric": ("Mrays/sec + frame ms, 1920x1080 scene 14-01" if a.config == "c2"
                        else f"Mrays/sec + frame ms, {W}x{H} {cfg['label']}"),
@@ -261,7 +516,7 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": "strong" if tiles else "weak",
+            "scaling": "strong" if mode == "tiles" else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": (f"scene file scenes/{cfg['label']}.crtscene (parsed fixture tests/golden/scenes)" if "scene" in cfg
@@ -271,19 +526,24 @@ def main():
                        "config": a.config,
                        "rays_per_frame": rays_per_frame, "node_tests_per_frame": counts["node_tests"],
                        "triangle_tests_per_frame": counts["triangle_tests"],
-                       "parallelism": (f"bucket-shard{world}+rccl-gather" if tiles else
-                                       f"frame-parallel{world}" if world > 1 else "single-gpu"),
+                       "parallelism": parallel, "world_size_initialised": world,
+                       "dist_backend": dist_backend, "payload": a.payload if mode == "tiles" else None,
                        "frames_per_step": frames_per_step,
-                       "frame_ms": round(ms_per_step, 5), "kernel_ms": round(kern_ms, 5)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic},
+                       "frame_ms": round(ms_per_step, 5), "kernel_ms": round(kern_ms, 5),
+                       "e2e_ms": round(e2e, 4) if e2e is not None else None,
+                       "e2e_note": ("crt_hip_render into a pinned host buffer: render + D2H of the fp32 image, "
+                                    "the reference's render_image call (main.cpp:37-43)") if e2e is not None else None,
+                       "check": check, "build_id": build_id},
+            "roofline": roof,
+            "secondary": secondary,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -161,6 +161,8 @@ EXPORTS = [
     ("crt_hip_shard_stride", C.c_int64, [_P, C.c_int]),
     ("crt_hip_render_shard", C.c_int, [_P, C.POINTER(RendererSettings), C.c_int, C.c_int, _P, _P]),
     ("crt_hip_unpack_shards", C.c_int, [_P, C.c_int, _P, _P, _P]),
+    ("crt_hip_unpack_shards_rgb8", C.c_int, [_P, C.c_int, _P, _P, _P]),
+    ("crt_hip_quantize_rgb8", C.c_int, [_P, C.c_int64, C.c_int32, _P, _P]),
     ("crt_shard_plan", C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int, C.c_int, _P, C.c_int64]),
     ("crt_hip_trace_batch", C.c_int, [_P, _P, C.c_int64, _P]),
     ("crt_hip_count_work", C.c_int, [_P, C.POINTER(RendererSettings), C.POINTER(WorkCounts)]),
@@ -173,6 +175,7 @@ EXPORTS = [
     ("crt_write_ppm", C.c_int, [C.c_char_p, _P, C.c_int32, C.c_int32, C.c_int32]),
     ("crt_hip_last_error", C.c_char_p, []),
     ("crt_hip_abi_version", C.c_int, []),
+    ("crt_hip_build_id", C.c_char_p, []),
 ]
 
 _lib = None
@@ -198,6 +201,11 @@ def lib() -> C.CDLL:
 def last_error() -> str:
     m = lib().crt_hip_last_error()
     return m.decode() if m else ""
+
+
+def build_id() -> str:
+    """Hash of the loaded library's sources and build flags (crt_hip_build_id)."""
+    return lib().crt_hip_build_id().decode()
 
 
 def _check(rc: int, exc=CrtError) -> None:
@@ -411,6 +419,13 @@ class HipScene:
             return out, {"kernel_ms": stats.kernel_ms, "total_ms": stats.total_ms}
         return out
 
+    def render_host(self, settings: RendererSettings, host_ptr: int) -> dict:
+        """Blocking render_image into caller memory at host_ptr (W*H*3 fp32; pinned
+        memory makes the D2H a direct DMA).  Returns the call's stats."""
+        stats = RenderStats()
+        _check(lib().crt_hip_render(self._h, C.byref(settings), C.c_void_p(host_ptr), C.byref(stats)))
+        return {"kernel_ms": stats.kernel_ms, "total_ms": stats.total_ms}
+
     def render_device(self, settings: RendererSettings, d_rgb: int, stream: int | None = None) -> None:
         _check(lib().crt_hip_render_device(self._h, C.byref(settings), C.c_void_p(d_rgb),
                                            C.c_void_p(stream or 0)))
@@ -435,6 +450,10 @@ class HipScene:
     def unpack_shards(self, count: int, d_gathered: int, d_rgb: int, stream: int | None = None) -> None:
         _check(lib().crt_hip_unpack_shards(self._h, count, C.c_void_p(d_gathered), C.c_void_p(d_rgb),
                                            C.c_void_p(stream or 0)))
+
+    def unpack_shards_rgb8(self, count: int, d_gathered: int, d_rgb8: int, stream: int | None = None) -> None:
+        _check(lib().crt_hip_unpack_shards_rgb8(self._h, count, C.c_void_p(d_gathered), C.c_void_p(d_rgb8),
+                                                C.c_void_p(stream or 0)))
 
     def last_kernel_ms(self) -> float:
         v = C.c_double()
@@ -506,6 +525,13 @@ def shard_plan(width: int, height: int, bucket_size: int, shard: int, shard_coun
     if n:
         lib().crt_shard_plan(width, height, bucket_size, shard, shard_count, out.ctypes.data, n)
     return out
+
+
+def quantize_rgb8(d_rgb: int, n: int, d_out: int, max_color_component: int = 255, stream: int | None = None) -> None:
+    """Device write_ppm conversion of n floats at d_rgb into n bytes at d_out
+    (crt_hip_quantize_rgb8, current device, `stream` or the null stream)."""
+    _check(lib().crt_hip_quantize_rgb8(C.c_void_p(d_rgb), n, max_color_component, C.c_void_p(d_out),
+                                       C.c_void_p(stream or 0)))
 
 
 def write_ppm(path: str | os.PathLike, rgb: np.ndarray, max_color_component: int = 255) -> None:

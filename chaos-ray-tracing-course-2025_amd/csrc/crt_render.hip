@@ -1797,18 +1797,44 @@ __global__ __launch_bounds__(256) void k_trace_rays(DeviceScene s, const float *
     hits[i] = r;
 }
 
-/* Scatter gathered shard buffers back into the row-major frame. */
-__global__ __launch_bounds__(256) void k_unpack(const UnpackBucket *__restrict__ buckets, const float *__restrict__ src,
-                                                float *__restrict__ dst, int width) {
+/* Scatter gathered shard buffers back into the row-major frame (fp32 RGB or
+ * the quantised 8-bit RGB of k_quantize). */
+template <class T>
+__global__ __launch_bounds__(256) void k_unpack(const UnpackBucket *__restrict__ buckets, const T *__restrict__ src,
+                                                T *__restrict__ dst, int width) {
     const UnpackBucket b = buckets[blockIdx.x];
     const int npx = b.w * b.h;
     for (int p = (int)threadIdx.x; p < npx; p += (int)blockDim.x) {
         const int lx = p % b.w, ly = p / b.w;
-        const float *s = src + b.src + 3 * (int64_t)p;
-        float *d = dst + 3 * ((int64_t)(b.y + ly) * width + (b.x + lx));
+        const T *s = src + b.src + 3 * (int64_t)p;
+        T *d = dst + 3 * ((int64_t)(b.y + ly) * width + (b.x + lx));
         d[0] = s[0];
         d[1] = s[1];
         d[2] = s[2];
+    }
+}
+
+/* write_ppm's per-component conversion (crt_image_ppm.cpp:15-18):
+ * clamp(static_cast<int>(c * max), 0, max), with x86 cvttss2si semantics for
+ * the cast (NaN / out of range -> INT_MIN -> 0).  Four components per thread:
+ * 16-B loads, one 4-B store (HBM-bound: 5 B moved per component). */
+__global__ __launch_bounds__(256) void k_quantize(const float *__restrict__ src, uint8_t *__restrict__ dst, int64_t n,
+                                                  float maxf, int maxi) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = 4 * q;
+    if (i >= n) return;
+    auto cv = [&](float c) -> uint32_t {
+        int v = trunc_x86(c * maxf);
+        v = v < 0 ? 0 : (v > maxi ? maxi : v);
+        return (uint32_t)v;
+    };
+    if (i + 4 <= n && ((reinterpret_cast<uintptr_t>(src + i) & 15u) == 0) &&
+        ((reinterpret_cast<uintptr_t>(dst + i) & 3u) == 0)) {
+        const float4 c = *reinterpret_cast<const float4 *>(src + i);
+        const uint32_t w = cv(c.x) | (cv(c.y) << 8) | (cv(c.z) << 16) | (cv(c.w) << 24);
+        *reinterpret_cast<uint32_t *>(dst + i) = w;
+    } else {
+        for (int64_t k = i; k < n && k < i + 4; ++k) dst[k] = (uint8_t)cv(src[k]);
     }
 }
 
@@ -1885,7 +1911,11 @@ struct WfBuffers {
     crt_amd::WRay *q[2] = {nullptr, nullptr};
     int64_t qcap[2] = {0, 0};
     int32_t *counts = nullptr;   /* children queued per level */
+    int count_cap = 0;
 };
+
+/* Deepest recursion the wavefront path accepts (levels are launched one by one). */
+constexpr int kWfMaxDepth = 4096;
 
 struct crt_hip_scene {
     int device = 0;
@@ -2338,11 +2368,20 @@ void wf_free(WfBuffers &w) {
 int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &plan, float *d_out,
                      hipStream_t stream, bool count, const DeviceScene *d_scene, int sec, int primary) {
     WfBuffers &w = sc->wf;
-    constexpr int kMaxLevels = 66;
-    if (!w.counts) {
+    /* levels 0..max_ray_depth are traced (a child deeper than max_ray_depth is
+     * never queued, crt_renderer.cpp:47-48), so the loop below always drains
+     * the queue: counts[max_ray_depth] is written by nobody and stays 0 */
+    if (ds.max_ray_depth > (uint32_t)kWfMaxDepth)
+        return set_error(CRT_E_UNSUPPORTED, "max_ray_depth > " + std::to_string(kWfMaxDepth) +
+                                                " with reflective/refractive materials is not supported");
+    const int kMaxLevels = (int)ds.max_ray_depth + 2;
+    if (!w.counts || w.count_cap < kMaxLevels) {
+        if (w.counts) (void)hipFree(w.counts);
+        w.counts = nullptr;
         void *p = nullptr;
-        HIP_TRY(hipMalloc(&p, kMaxLevels * sizeof(int32_t)));
+        HIP_TRY(hipMalloc(&p, (size_t)kMaxLevels * sizeof(int32_t)));
         w.counts = static_cast<int32_t *>(p);
+        w.count_cap = kMaxLevels;
     }
     HIP_TRY(hipMemsetAsync(w.counts, 0, kMaxLevels * sizeof(int32_t), stream));
     const int64_t n0 = (int64_t)plan.ntiles * 64;
@@ -2854,7 +2893,11 @@ int crt_hip_render_shard(crt_hip_scene *sc, const crt_renderer_settings *st, int
     return CRT_OK;
 }
 
-int crt_hip_unpack_shards(crt_hip_scene *sc, int shard_count, const float *d_gathered, float *d_rgb, void *stream) {
+}  // extern "C"
+
+namespace {
+template <class T>
+int unpack_shards_t(crt_hip_scene *sc, int shard_count, const T *d_gathered, T *d_rgb, void *stream) {
     if (!sc || !d_gathered || !d_rgb || shard_count <= 0) return set_error(CRT_E_INVALID, "bad argument");
     HIP_TRY(hipSetDevice(sc->device));
     auto it = sc->unpack_plans.find(shard_count);
@@ -2876,12 +2919,37 @@ int crt_hip_unpack_shards(crt_hip_scene *sc, int shard_count, const float *d_gat
     }
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : sc->stream;
     if (sc->grid_empty)
-        HIP_TRY(hipMemsetAsync(d_rgb, 0, (size_t)sc->info.width * sc->info.height * 3 * sizeof(float), s));
+        HIP_TRY(hipMemsetAsync(d_rgb, 0, (size_t)sc->info.width * sc->info.height * 3 * sizeof(T), s));
     if (it->second.second > 0) {
-        hipLaunchKernelGGL(k_unpack, dim3(it->second.second), dim3(256), 0, s, it->second.first, d_gathered, d_rgb,
+        hipLaunchKernelGGL(k_unpack<T>, dim3(it->second.second), dim3(256), 0, s, it->second.first, d_gathered, d_rgb,
                            sc->info.width);
         HIP_TRY(hipGetLastError());
     }
+    return CRT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int crt_hip_unpack_shards(crt_hip_scene *sc, int shard_count, const float *d_gathered, float *d_rgb, void *stream) {
+    return unpack_shards_t<float>(sc, shard_count, d_gathered, d_rgb, stream);
+}
+
+int crt_hip_unpack_shards_rgb8(crt_hip_scene *sc, int shard_count, const uint8_t *d_gathered, uint8_t *d_rgb8,
+                               void *stream) {
+    return unpack_shards_t<uint8_t>(sc, shard_count, d_gathered, d_rgb8, stream);
+}
+
+int crt_hip_quantize_rgb8(const float *d_rgb, int64_t n, int32_t max_color_component, uint8_t *d_out, void *stream) {
+    if ((n > 0 && (!d_rgb || !d_out)) || n < 0) return set_error(CRT_E_INVALID, "bad argument");
+    if (max_color_component < 0 || max_color_component > 255)
+        return set_error(CRT_E_UNSUPPORTED, "8-bit output needs max_color_component in 0..255");
+    if (n == 0) return CRT_OK;
+    const int64_t threads = (n + 3) / 4;
+    hipLaunchKernelGGL(k_quantize, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), d_rgb, d_out, n, (float)max_color_component,
+                       max_color_component);
+    HIP_TRY(hipGetLastError());
     return CRT_OK;
 }
 

@@ -224,7 +224,13 @@ int  crt_hip_render(crt_hip_scene *scene, const crt_renderer_settings *settings,
                     float *rgb_out, crt_render_stats *stats);
 
 /* Asynchronous: render the whole frame into device memory d_rgb (W*H*3 fp32)
- * on `stream` (a hipStream_t, NULL = the scene's own stream). */
+ * on `stream` (a hipStream_t, NULL = the scene's own stream).
+ *
+ * Concurrency: a scene holds one set of per-frame scratch state (refill
+ * counter, wavefront queues, work counters, timing events).  At most one
+ * render of a scene may be in flight at a time: successive asynchronous calls
+ * on one scene must be issued on the same stream (or ordered by the caller
+ * with events).  Different scenes are independent. */
 int  crt_hip_render_device(crt_hip_scene *scene, const crt_renderer_settings *settings,
                            float *d_rgb, void *stream);
 
@@ -245,6 +251,18 @@ int64_t crt_shard_plan(int32_t width, int32_t height, int32_t bucket_size, int s
 /* d_gathered holds shard_count slots of crt_hip_shard_stride floats each. */
 int  crt_hip_unpack_shards(crt_hip_scene *scene, int shard_count, const float *d_gathered,
                            float *d_rgb, void *stream);
+/* Same for 8-bit shards (crt_hip_quantize_rgb8 of each packed shard):
+ * d_gathered holds shard_count slots of crt_hip_shard_stride BYTES each. */
+int  crt_hip_unpack_shards_rgb8(crt_hip_scene *scene, int shard_count, const uint8_t *d_gathered,
+                                uint8_t *d_rgb8, void *stream);
+
+/* write_ppm's per-component conversion on the device (crt_image_ppm.cpp:15-18):
+ * d_out[i] = clamp(static_cast<int>(d_rgb[i] * max), 0, max) for n floats
+ * (x86 cvttss2si semantics for the cast).  max_color_component <= 255.  Runs
+ * on `stream` (NULL = the null stream) of the current device.  Element order
+ * is kept, so it applies to whole frames and to packed shards alike. */
+int  crt_hip_quantize_rgb8(const float *d_rgb, int64_t n, int32_t max_color_component, uint8_t *d_out,
+                           void *stream);
 
 /* Test hook for the a1–a4 known-answer tests: closest hit of n rays
  * (rays = n * 6 floats: origin xyz, direction xyz), host buffers. */
@@ -312,6 +330,8 @@ int  crt_write_ppm(const char *path, const float *rgb, int32_t width, int32_t he
 
 const char *crt_hip_last_error(void);
 int  crt_hip_abi_version(void);
+/* Hash of the library's sources and build flags (measurements name the build). */
+const char *crt_hip_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""profiles/r02/pmc_<config>.json from rocprofv3 --pmc passes over
+scripts/render_loop.py (one pass per counter group, as MI355X_MICROARCH.md
+prescribes), read by bench.py's roofline when its build id equals the loaded
+library's.
+
+  pmc_record.py --config c2 --size 1920 1080 --dir gpurun_out/<tag>/pmc [--kernel k_render_tiles]
+
+Per-launch averages over the matching dispatches of each pass:
+  valu_insts_per_launch = SQ_INSTS_VALU (wave-instructions), salu = SQ_INSTS_SALU,
+  hbm_bytes_per_launch  = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes; FETCH_SIZE
+                          doubled per the gfx950 note), plus every other counter
+                          found (SQ_WAVE_CYCLES, SQ_WAIT_INST_ANY, TCC_HIT/MISS, ...).
+"""
+import argparse
+import collections
+import csv
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "chaos-ray-tracing-course-2025_amd"))
+
+
+def averages(root: Path, kernel: str) -> tuple[dict, int]:
+    out, ndisp = {}, 0
+    for f in sorted(root.rglob("*counter_collection.csv")):
+        agg = collections.defaultdict(float)
+        disp = set()
+        for r in csv.DictReader(open(f)):
+            if kernel not in r["Kernel_Name"]:
+                continue
+            agg[r["Counter_Name"]] += float(r["Counter_Value"])
+            disp.add(r["Dispatch_Id"])
+        if disp:
+            ndisp = max(ndisp, len(disp))
+            out.update({k: v / len(disp) for k, v in agg.items()})
+    return out, ndisp
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--config", required=True)
+    p.add_argument("--size", type=int, nargs=2, required=True)
+    p.add_argument("--dir", required=True)
+    p.add_argument("--kernel", default="k_render_tiles")
+    p.add_argument("--out", default=None)
+    p.add_argument("--command", default="")
+    a = p.parse_args()
+    from crt_amd import native as N
+    c, n = averages(Path(a.dir), a.kernel)
+    rec = {"config": a.config, "size": a.size, "kernel": a.kernel, "build_id": N.build_id(), "dispatches": n,
+           "counters_per_launch": c, "command": a.command,
+           "method": "rocprofv3 --pmc, one pass per counter group; per-dispatch averages of the kernel"}
+    if "SQ_INSTS_VALU" in c:
+        rec["valu_insts_per_launch"] = c["SQ_INSTS_VALU"]
+    if "SQ_INSTS_SALU" in c:
+        rec["salu_insts_per_launch"] = c["SQ_INSTS_SALU"]
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        rec["hbm_bytes_per_launch"] = int(round(2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024))
+    if "SQ_THREAD_CYCLES_VALU" in c and "SQ_INSTS_VALU" in c and c["SQ_INSTS_VALU"]:
+        rec["valu_lane_utilisation"] = c["SQ_THREAD_CYCLES_VALU"] / (64 * c["SQ_INSTS_VALU"])
+    if "SQ_WAIT_INST_ANY" in c and "SQ_WAVE_CYCLES" in c and c["SQ_WAVE_CYCLES"]:
+        rec["wait_inst_frac"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]
+    out = Path(a.out) if a.out else ROOT / "profiles" / "r02" / f"pmc_{a.config}.json"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    out.write_text(json.dumps(rec, indent=1) + "\n")
+    print(json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main()

@@ -42,6 +42,63 @@ def oracle():
     return pyoracle
 
 
+class DeviceBuffers:
+    """hipMalloc'd scratch through the HIP runtime libcrt_hip.so already loaded
+    (same SONAME), freed on close; for tests of the device-pointer entry points."""
+
+    def __init__(self):
+        import ctypes as C
+        self.C = C
+        self.hip = C.CDLL("libamdhip64.so.7")
+        self.hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+        self.hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        self.hip.hipFree.argtypes = [C.c_void_p]
+        self.hip.hipDeviceSynchronize.argtypes = []
+        self.ptrs = []
+
+    def alloc(self, nbytes: int) -> int:
+        p = self.C.c_void_p()
+        assert self.hip.hipMalloc(self.C.byref(p), max(int(nbytes), 1)) == 0
+        self.ptrs.append(p)
+        return p.value
+
+    def upload(self, a: np.ndarray) -> int:
+        a = np.ascontiguousarray(a)
+        p = self.alloc(a.nbytes)
+        assert self.hip.hipMemcpy(p, a.ctypes.data, a.nbytes, 1) == 0
+        return p
+
+    def download(self, p: int, shape, dtype) -> np.ndarray:
+        out = np.empty(shape, dtype)
+        assert self.hip.hipDeviceSynchronize() == 0
+        assert self.hip.hipMemcpy(out.ctypes.data, p, out.nbytes, 2) == 0
+        return out
+
+    def sync(self):
+        assert self.hip.hipDeviceSynchronize() == 0
+
+    def close(self):
+        for p in self.ptrs:
+            self.hip.hipFree(p)
+        self.ptrs = []
+
+
+@pytest.fixture
+def devbuf():
+    b = DeviceBuffers()
+    yield b
+    b.close()
+
+
+def ppm_quantize(rgb: np.ndarray, maxc: int = 255) -> np.ndarray:
+    """write_ppm's conversion (crt_image_ppm.cpp:15-18) in numpy:
+    clamp(static_cast<int>(c * max), 0, max) with x86 cvttss2si semantics."""
+    x = np.asarray(rgb, np.float32) * np.float32(maxc)
+    ok = (x >= np.float32(-2147483648.0)) & (x < np.float32(2147483648.0))
+    v = np.where(ok, np.trunc(np.where(ok, x, 0)).astype(np.int64), -2147483648)
+    return np.clip(v, 0, maxc).astype(np.uint8)
+
+
 def bits(a: np.ndarray) -> np.ndarray:
     a = np.ascontiguousarray(a)
     return a.view(np.uint32) if a.dtype == np.float32 else a

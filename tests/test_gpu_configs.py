@@ -1,0 +1,183 @@
+"""GPU parity at the BASELINE configs' own sizes, and against the reference's
+own per-ray records.
+
+  C3  11-01/scene8, 1920x1080, depth 8  — full frame against the oracle and the
+      committed full-resolution hash (tests/golden/image_hashes.json "C3")
+  C4  15-01/scene2 at its native 1080x1080 — work counts of the reference-order
+      walks equal the reference's (85,480,935 traversals, "C4_native"), the GI
+      frame's fp32 hash, and a 256x256 GI frame against the oracle
+  C5  the synthetic 1M-triangle mesh rendered at 64x36 and
+      160x90 against the oracle (device-built tree, pruned walks)
+  KAT the HIP trace hook against tests/golden/kat_*.npz — the Intersection
+      records the reference's own compiled ray_intersect_acceleration_tree
+      produced (crt_intersection.cpp:109-136), no oracle in between
+"""
+import hashlib
+import json
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, bits, hits_equal, ppm_quantize, scene_npz
+
+pytestmark = pytest.mark.gpu
+
+RMSE_TOL = 1e-4   # north_star: pixel RMSE < 1e-4 vs reference (fp32 RGB)
+HASHES = json.loads((GOLDEN / "image_hashes.json").read_text())
+
+
+@pytest.fixture(scope="module")
+def N():
+    from crt_amd import native
+    native.lib()
+    return native
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def compare(got, want):
+    rmse = float(np.sqrt(np.mean((got.astype(np.float64) - want) ** 2)))
+    nbad = int((bits(got) != bits(want)).sum())
+    return rmse, nbad
+
+
+def test_c3_full_frame(N, oracle):
+    """C3 at its own size: 1920x1080, max_ray_depth 8 (wavefront levels)."""
+    h = HASHES["C3"]
+    sc = scene_npz(h["scene"])
+    st = N.RendererSettings.default(**h["settings"])
+    gpu = N.HipScene(sc)
+    got = gpu.render(st)
+    assert got.shape == (1080, 1920, 3)
+    want = oracle.OracleScene(sc).render(st)
+    rmse, nbad = compare(got, want)
+    print(f"C3 1920x1080 depth 8: rmse {rmse:.3g}, {nbad} of {got.size} floats differ")
+    assert rmse < RMSE_TOL
+    assert nbad == 0, f"{nbad} floats differ (rmse {rmse})"
+    assert sha(got) == h["fp32_sha256"]
+    c = gpu.count_work(st)
+    assert c["traversals"] == h["traversals"] and c["hits"] == h["hits"]
+    r = N.HipScene(sc, traversal=7).count_work(st)
+    assert r == {k: h[k] for k in ("traversals", "node_tests", "triangle_tests", "hits")}
+
+
+def test_c4_native_counts_and_hash(N):
+    """C4's scene at its native 1080x1080 (GI on): the reference-order walks
+    execute exactly the reference's traversals / node / triangle tests, the
+    pruned default the same traversals and hits, and the frame's fp32 bits
+    equal the committed hash of the oracle's frame."""
+    h = HASHES["C4_native"]
+    sc = scene_npz(h["scene"]).set_resolution(h["width"], h["height"])
+    st = N.RendererSettings.default(**h["settings"])
+    ref = N.HipScene(sc, traversal=7).count_work(st)
+    assert ref == {k: h[k] for k in ("traversals", "node_tests", "triangle_tests", "hits")}
+    gpu = N.HipScene(sc)
+    c = gpu.count_work(st)
+    assert c["traversals"] == h["traversals"] and c["hits"] == h["hits"]
+    img = gpu.render(st)
+    assert sha(img) == h["fp32_sha256"]
+
+
+def test_c4_gi_256(N, oracle):
+    """A 256x256 GI frame of C4's scene against the oracle."""
+    sc = scene_npz("15-01-conclusion__scene2").set_resolution(256, 256)
+    st = N.RendererSettings.default()
+    got = N.HipScene(sc).render(st)
+    want = oracle.OracleScene(sc).render(st)
+    rmse, nbad = compare(got, want)
+    print(f"C4 scene 256x256 GI: rmse {rmse:.3g}, {nbad} floats differ")
+    assert rmse < RMSE_TOL and nbad == 0
+
+
+@pytest.fixture(scope="module")
+def c5_1m():
+    from crt_amd.synthetic import c5_scene
+    return c5_scene(1_000_000, 160, 90)
+
+
+@pytest.mark.parametrize("w,h", [(64, 36), (160, 90)])
+def test_c5_1m_triangles(N, oracle, c5_1m, w, h):
+    """C5's 1M-triangle mesh (880,933 nodes, device-built tree) rendered
+    through the pruned walks, bit for bit against the oracle."""
+    sc = c5_1m
+    sc.desc().camera.width, sc.desc().camera.height = w, h
+    st = N.RendererSettings.default()
+    gpu = N.HipScene(sc)
+    info = gpu.info()
+    assert info["tree_on_device"] == 1 and info["node_count"] == 880_933
+    got = gpu.render(st)
+    want = oracle.OracleScene(sc).render(st)
+    rmse, nbad = compare(got, want)
+    assert nbad == 0, f"{nbad} floats differ (rmse {rmse})"
+    c = gpu.count_work(st)
+    assert c["traversals"] == w * h
+
+
+@pytest.mark.parametrize("walk", [0, 1], ids=["reference-order", "pruned"])
+@pytest.mark.parametrize("name", sorted(p.stem[4:] for p in GOLDEN.glob("kat_*.npz")))
+def test_trace_matches_reference_records(N, name, walk):
+    """The HIP trace hook returns, for every ray, the Intersection the
+    reference's own ray_intersect_acceleration_tree returned (distance, point,
+    normal, uv, barycentrics, material; misses as misses), bit for bit."""
+    z = np.load(GOLDEN / f"kat_{name}.npz")
+    want = np.ascontiguousarray(z["hits"]).view(N.HIT_DTYPE).reshape(-1)
+    got = N.HipScene(scene_npz(name), trace_walk=walk).trace(z["rays"])
+    ok, first, nbad = hits_equal(got, want, with_tri=False)
+    assert ok, f"{name}: {nbad} rays differ (first {first}: gpu={got[first]} ref={want[first]})"
+    assert int(got["hit"].sum()) == int(want["hit"].sum()) > 0
+
+
+def test_deep_recursion_wavefront(N, oracle):
+    """max_ray_depth beyond the old fixed level cap (66) on a mirror scene:
+    the wavefront path traces every level up to the depth (no silent cut)."""
+    sc = scene_npz("09-03-reflective__scene5").set_resolution(48, 27)
+    st = N.RendererSettings.default(max_ray_depth=70)
+    got = N.HipScene(sc).render(st)
+    want = oracle.OracleScene(sc).render(st)
+    rmse, nbad = compare(got, want)
+    assert nbad == 0, f"{nbad} floats differ (rmse {rmse})"
+    with pytest.raises(N.CrtError):
+        N.HipScene(sc).render(N.RendererSettings.default(max_ray_depth=5000))
+
+
+def test_quantize_rgb8(N, devbuf):
+    """Device write_ppm conversion (crt_image_ppm.cpp:15-18) on ordinary and
+    special values, odd lengths and unaligned starts."""
+    rng = np.random.default_rng(3)
+    x = rng.uniform(-0.5, 1.5, 4099).astype(np.float32)
+    x[:12] = [np.nan, np.inf, -np.inf, -0.0, 0.0, 1.0, 255.0 / 255.0, 0.99999994, 1e30, -1e30, 8.5e6, 2.0 ** 31]
+    d_in = devbuf.upload(x)
+    d_out = devbuf.alloc(x.size + 8)
+    for off, n in [(0, x.size), (1, 4097), (3, 5), (0, 1)]:
+        N.quantize_rgb8(d_in + 4 * off, n, d_out + off, 255)
+        got = devbuf.download(d_out + off, n, np.uint8)
+        assert np.array_equal(got, ppm_quantize(x[off:off + n]))
+    N.quantize_rgb8(d_in, x.size, d_out, 7)
+    assert np.array_equal(devbuf.download(d_out, x.size, np.uint8), ppm_quantize(x, 7))
+    with pytest.raises(N.CrtError):
+        N.quantize_rgb8(d_in, x.size, d_out, 256)
+
+
+@pytest.mark.parametrize("shards", [1, 3, 8])
+def test_shard_rgb8_pack_and_unpack(N, devbuf, shards):
+    """tiles mode with the 8-bit payload: each packed shard quantised on the
+    device, gathered (here: side by side) and unpacked equals the quantised
+    full frame, i.e. the PPM components the reference writes."""
+    sc = scene_npz("14-01-acceleration-tree__scene1").set_resolution(333, 200)
+    gpu = N.HipScene(sc)
+    st = N.RendererSettings.default()
+    full = gpu.render(st)
+    stride = gpu.shard_stride(shards)
+    f32 = devbuf.alloc(4 * stride)
+    gathered = devbuf.alloc(stride * shards)
+    frame8 = devbuf.alloc(full.size)
+    for s in range(shards):
+        gpu.render_shard(st, s, shards, f32)
+        devbuf.sync()
+        N.quantize_rgb8(f32, stride, gathered + s * stride, 255)
+        devbuf.sync()
+    gpu.unpack_shards_rgb8(shards, gathered, frame8)
+    out = devbuf.download(frame8, full.shape, np.uint8)
+    assert np.array_equal(out, ppm_quantize(full))
