@@ -115,6 +115,9 @@ struct DeviceScene {
     /* GI angle tables: (cosf, sinf) pairs of pi*u and of 2*pi*u for the 2^23 values of u */
     const float *gi_pi;
     const float *gi_2pi;
+    /* powf(x, 5.0f) of the host's libm for every x = k * 2^-24 in [-1, 1]
+     * (2^25 + 1 floats, index k + 2^24): the Fresnel term's exact values */
+    const float *pow5;
     /* camera (crt_camera.cpp:7-35), per-frame constants precomputed on host */
     float cam_loc[3];
     float cam_rot[9];
@@ -124,7 +127,6 @@ struct DeviceScene {
     float tan_half_fov;     /* std::tan(fov_radians * 0.5f)     (crt_camera.cpp:26-27) */
     float background[3];
     int32_t gi_on, reflections_on, refractions_on;
-    int32_t oct_mask;       /* per-lane pruned walks: node order = octant(d) & oct_mask (7: the ray's own octant) */
 };
 
 /* Renderer settings as the kernels see them (crt_renderer.h:18-25). */

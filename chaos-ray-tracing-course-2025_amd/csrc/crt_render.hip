@@ -119,132 +119,6 @@ __device__ __forceinline__ int trace_closest(const DeviceScene &s, Vec o, Vec d,
     return best;
 }
 
-/* Same walk, "while-while" form (after Aila & Laine 2009, adapted to the
- * stackless order): a lane that reaches a passing leaf records it and keeps
- * walking speculatively while other lanes of the wave still search; the wave
- * then runs the triangle loop for every lane's pending leaf at once.  A lane
- * holds one pending leaf, so leaves are still tested in visit order and the
- * strict '<' keeps the reference's first-found winner.  A lane that meets a
- * second passing leaf parks on it (`parked`) and takes it without re-testing
- * its box in the next round. */
-template <bool COUNT>
-__device__ __forceinline__ int trace_closest_ww(const DeviceScene &s, Vec o, Vec d, float &best_t, LaneCounts &c) {
-    int best = -1;
-    best_t = 0.0f;
-    int i = 0;
-    const int n = s.node_count;
-    int lf = 0, lc = 0;          /* pending leaf: first slot, count */
-    bool parked = false;         /* node i is a passing leaf already counted */
-    if (COUNT) ++c.traversals;
-    for (;;) {
-        /* ---- traversal phase ---- */
-        while (i < n) {
-            const DNode nd = s.nodes[i];
-            bool pass;
-            if (parked) {
-                pass = true;
-                parked = false;
-            } else {
-                pass = box_hit(o, d, nd);
-                if (COUNT) ++c.nodes;
-            }
-            if (nd.b < 0) {
-                i = pass ? i + 1 : nd.a;
-            } else if (!pass) {
-                ++i;
-            } else if (lc == 0) {
-                lf = nd.b;
-                lc = node_leaf_count(nd);
-                ++i;
-            } else {
-                parked = true;   /* second leaf: wait here */
-                break;
-            }
-            if (__all(lc > 0 || i >= n)) break;
-        }
-        /* ---- intersection phase ---- */
-        for (int k = 0; k < lc; ++k) {
-            const int slot = lf + k;
-            float t;
-            if (COUNT) ++c.tris;
-            if (tri_hit(o, d, s.slots[slot], s.slot_cull + slot, t) && (best < 0 || t < best_t)) {
-                best_t = t;
-                best = slot;
-            }
-        }
-        lc = 0;
-        if (!__any(i < n)) break;
-    }
-    if (COUNT && best >= 0) ++c.hits;
-    return best;
-}
-
-/* While-while walk with software prefetch: while node i is tested, both
- * possible successors (i+1, and the skip target of an interior node) are
- * already in flight, and the next triangle record loads while the current one
- * is tested.  BF selects the branch-free box predicate. */
-template <bool COUNT, bool BF>
-__device__ __forceinline__ int trace_closest_wwp(const DeviceScene &s, Vec o, Vec d, float &best_t, LaneCounts &c) {
-    int best = -1;
-    best_t = 0.0f;
-    int i = 0;
-    const int n = s.node_count;
-    const int last = n - 1;
-    int lf = 0, lc = 0;
-    bool parked = false;
-    if (COUNT) ++c.traversals;
-    DNode nd = s.nodes[0];
-    for (;;) {
-        while (i < n) {
-            const int i1 = i + 1 < n ? i + 1 : last;
-            const int alt = nd.b < 0 ? (nd.a < n ? nd.a : last) : i1;
-            const DNode n1 = s.nodes[i1];
-            const DNode n2 = s.nodes[alt];
-            bool pass;
-            if (parked) {
-                pass = true;
-                parked = false;
-            } else {
-                pass = BF ? box_hit_bf(o, d, nd) : box_hit(o, d, nd);
-                if (COUNT) ++c.nodes;
-            }
-            if (nd.b < 0) {
-                if (pass) { i = i + 1; nd = n1; } else { i = nd.a; nd = n2; }
-            } else if (!pass) {
-                ++i;
-                nd = n1;
-            } else if (lc == 0) {
-                lf = nd.b;
-                lc = node_leaf_count(nd);
-                ++i;
-                nd = n1;
-            } else {
-                parked = true;
-                break;
-            }
-            if (__all(lc > 0 || i >= n)) break;
-        }
-        if (lc > 0) {
-            DTriGeo g = s.slots[lf];
-            for (int k = 0; k < lc; ++k) {
-                const int slot = lf + k;
-                const DTriGeo gn = s.slots[k + 1 < lc ? slot + 1 : slot];
-                float t;
-                if (COUNT) ++c.tris;
-                if (tri_hit(o, d, g, s.slot_cull + slot, t) && (best < 0 || t < best_t)) {
-                    best_t = t;
-                    best = slot;
-                }
-                g = gn;
-            }
-        }
-        lc = 0;
-        if (!__any(i < n)) break;
-    }
-    if (COUNT && best >= 0) ++c.hits;
-    return best;
-}
-
 /* ---------------------------------------------------------------------- */
 /* Wave-cooperative walk (TRAV 4)                                           */
 /* ---------------------------------------------------------------------- */
@@ -291,7 +165,7 @@ template <> struct WalkNode<false> {
 template <> struct WalkNode<true> {
     using T = PNode;
     static __device__ __forceinline__ const PNode *base(const DeviceScene &s, Vec d) {
-        return pnode_order(s.pnodes, s.node_count, ray_octant(d) & s.oct_mask);
+        return pnode_order(s.pnodes, s.node_count, ray_octant(d));
     }
     static __device__ __forceinline__ DNode cell(const PNode &n) { return cell_of(n); }
     static __device__ __forceinline__ bool alive(const PNode &n, const PruneRay &p, float lim) {
@@ -445,182 +319,8 @@ __device__ int trace_coop(const DeviceScene &s, CoopLds &L, bool active, Vec o, 
     return slot;
 }
 
-/* TRAV 5: the while-while walk with prefetch (TRAV 3) plus the piece sharing of
- * TRAV 4 at round granularity.  A round = traversal phase (until every lane
- * holds a leaf or is out of nodes) + triangle phase.  Lanes out of work at a
- * round start pop donated pieces; during the traversal phase a lane that
- * passes an interior node donates the rest of its piece while the wave's
- * demand (idle lanes at the round start) exceeds the banked pieces.  The
- * stack depth lives in LDS because donations happen under divergent control
- * flow.  PRUNE: pieces walk their ray's octant order and skip dead hulls
- * (TRAV 11). */
-template <bool COUNT, bool PRUNE>
-__device__ int trace_share(const DeviceScene &s, CoopLds &L, bool active, Vec o, Vec d, float &best_t,
-                           LaneCounts &c) {
-    using WN = WalkNode<PRUNE>;
-    using NT = typename WN::T;
-    const int lane = (int)(threadIdx.x & 63);
-    const int n = s.node_count;
-    const int last = n - 1;
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    volatile int *spp = &L.sp;
-    L.ray[lane][0] = o.x; L.ray[lane][1] = o.y; L.ray[lane][2] = o.z;
-    L.ray[lane][3] = d.x; L.ray[lane][4] = d.y; L.ray[lane][5] = d.z;
-    L.key[lane] = ~0ull;
-    if (lane == 0) *spp = 0;
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_wave_barrier();
-    if (COUNT && active) ++c.traversals;
-
-    int r = lane;
-    int i = active ? 0 : n, end = active ? n : 0;
-    bool live = active;                 /* holds a piece whose key is not merged yet */
-    int lf = 0, lc = 0;
-    bool parked = false;
-    Vec ro = o, rd = d;
-    const NT *nb = WN::base(s, d);
-    PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
-    float lim = INFINITY;
-    unsigned long long mine = ~0ull;
-    NT nd = nb[0];
-    for (;;) {
-        /* ---- merge finished pieces, refill idle lanes ---- */
-        if (live && !(i < end)) {
-            atomicMin(&L.key[r], mine);
-            mine = ~0ull;
-            live = false;
-        }
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __builtin_amdgcn_wave_barrier();
-        int sp = *spp;
-        const unsigned long long idle = __ballot(!(i < end));
-        int demand = 0;
-        if (idle != 0ull) {
-            const int nidle = __popcll(idle);
-            const int take = nidle < sp ? nidle : sp;
-            if (!(i < end)) {
-                const int rank = __popcll(idle & lt_mask);
-                if (rank < take) {
-                    const unsigned long long pc = L.stack[sp - 1 - rank];
-                    r = (int)(pc >> 58);
-                    i = (int)((pc >> 29) & 0x1fffffff);
-                    end = (int)(pc & 0x1fffffff);
-                    ro = vec(L.ray[r][0], L.ray[r][1], L.ray[r][2]);
-                    rd = vec(L.ray[r][3], L.ray[r][4], L.ray[r][5]);
-                    nb = WN::base(s, rd);
-                    if (PRUNE) {
-                        pr = make_prune_ray(ro, rd, s.prune_origin_max);
-                        lim = key_t(L.key[r]);
-                    }
-                    nd = nb[i];
-                    live = true;
-                }
-            }
-            sp -= take;
-            demand = nidle - take;
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            if (lane == __builtin_ctzll(__ballot(true))) *spp = sp;
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (!__any(i < end)) break;
-        /* ---- traversal phase ---- */
-        while (i < end) {
-            const int i1 = i + 1 < n ? i + 1 : last;
-            const int alt = nd.b < 0 ? (nd.a < n ? nd.a : last) : i1;
-            const NT n1 = nb[i1];
-            const NT n2 = nb[alt];
-            bool pass;
-            if (parked) {
-                pass = true;
-                parked = false;
-            } else {
-                pass = false;
-                if (WN::alive(nd, pr, lim)) {
-                    pass = box_hit_bf(ro, rd, WN::cell(nd));
-                    if (COUNT) ++c.nodes;
-                }
-            }
-            bool donate = false;
-            int rest = 0;
-            if (nd.b < 0) {
-                if (pass) {
-                    rest = n1.b < 0 ? n1.a : i + 2;
-                    donate = demand > 0 && rest < end;
-                    i = i + 1;
-                    nd = n1;
-                } else {
-                    i = nd.a;
-                    nd = n2;
-                }
-            } else if (!pass) {
-                ++i;
-                nd = n1;
-            } else if (lc == 0) {
-                lf = nd.b;
-                lc = nd.a & 0xffffff;
-                ++i;
-                nd = n1;
-            } else {
-                parked = true;
-                break;
-            }
-            if (demand > 0) {
-                const unsigned long long want = __ballot(donate);
-                if (want != 0ull) {
-                    const int sp0 = *spp;
-                    const int cap = kCoopStack - sp0;
-                    int g = __popcll(want);
-                    g = g < demand ? g : demand;
-                    g = g < cap ? g : cap;
-                    if (donate) {
-                        const int rank = __popcll(want & lt_mask);
-                        if (rank < g) {
-                            L.stack[sp0 + rank] = coop_piece(r, rest, end);
-                            end = rest;
-                        }
-                    }
-                    demand -= g;
-                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-                    if (lane == __builtin_ctzll(__ballot(true))) *spp = sp0 + g;
-                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-                    __builtin_amdgcn_wave_barrier();
-                }
-            }
-            if (__all(lc > 0 || i >= end)) break;
-        }
-        /* ---- triangle phase ---- */
-        if (lc > 0) {
-            DTriGeo g = s.slots[lf];
-            for (int k = 0; k < lc; ++k) {
-                const int slot = lf + k;
-                const DTriGeo gn = s.slots[k + 1 < lc ? slot + 1 : slot];
-                float t;
-                if (COUNT) ++c.tris;
-                if (tri_hit(ro, rd, g, s.slot_cull + slot, t)) {
-                    const unsigned long long kk = coop_key(t, slot);
-                    mine = kk < mine ? kk : mine;
-                    if (PRUNE) lim = fminf(lim, t);
-                }
-                g = gn;
-            }
-            lc = 0;
-        }
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_wave_barrier();
-    const unsigned long long kk = L.key[lane];
-    if (!active || kk == ~0ull) return -1;
-    const int slot = (int)(kk & 0xffffffffu);
-    float t = 0.0f;
-    (void)tri_hit(o, d, s.slots[slot], s.slot_cull + slot, t);
-    best_t = t;
-    if (COUNT) ++c.hits;
-    return slot;
-}
-
 /* ---------------------------------------------------------------------- */
-/* Masked packet walk (TRAV 6) — coherent rays (primary rays of a tile)     */
+/* Masked packet walk (TRAV 7) — coherent rays (primary rays of a tile)     */
 /* ---------------------------------------------------------------------- */
 /* The whole wave walks the traversal-ordered node array with ONE wave-uniform
  * index, so node and triangle records come through the scalar path (SGPRs)
@@ -659,7 +359,7 @@ __device__ __forceinline__ T load_scalar_at(const char *base, uint32_t byte_off)
 #endif
 }
 
-template <bool COUNT, bool EARLY>
+template <bool COUNT>
 __device__ int trace_packet(const DeviceScene &s, bool active, Vec o, Vec d, float &best_t, LaneCounts &c) {
     int best = -1;
     best_t = 0.0f;
@@ -695,23 +395,15 @@ __device__ int trace_packet(const DeviceScene &s, bool active, Vec o, Vec d, flo
                     float t;
                     if (COUNT && pass) ++c.tris;
                     if (COUNT) ++c.wave_tris;
-                    if (EARLY) {
-                        /* the edge tests only matter for a lane whose candidate
-                         * distance would replace its best: skip them when no lane
-                         * of the wave has one (same predicate, same arithmetic) */
-                        const bool pre = pass && tri_plane(o, d, g, cull, t) && (best < 0 || t < best_t);
-                        const bool any = __ballot(pre) != 0ull;
-                        if (COUNT && any) ++c.wave_edges;
-                        if (any && pre && tri_edges(o, d, g, t)) {
-                            best_t = t;
-                            best = slot;
-                        }
-                    } else {
-                        const bool h = tri_hit_bf(o, d, g, cull, t);
-                        if (pass && h && (best < 0 || t < best_t)) {
-                            best_t = t;
-                            best = slot;
-                        }
+                    /* the edge tests only matter for a lane whose candidate
+                     * distance would replace its best: skip them when no lane
+                     * of the wave has one (same predicate, same arithmetic) */
+                    const bool pre = pass && tri_plane(o, d, g, cull, t) && (best < 0 || t < best_t);
+                    const bool any = __ballot(pre) != 0ull;
+                    if (COUNT && any) ++c.wave_edges;
+                    if (any && pre && tri_edges(o, d, g, t)) {
+                        best_t = t;
+                        best = slot;
                     }
                 }
             }
@@ -723,7 +415,7 @@ __device__ int trace_packet(const DeviceScene &s, bool active, Vec o, Vec d, flo
 }
 
 /* ---------------------------------------------------------------------- */
-/* Pruned walks (TRAV 8 packet, TRAV 9 per lane) over the octant-ordered     */
+/* Pruned walks (TRAV 8/12 packet, per-lane for the trace hook) over the    */
 /* PNode arrays (crt_layout.h)                                               */
 /* ---------------------------------------------------------------------- */
 /* TRAV 8: the masked packet walk of TRAV 7 where a lane also drops a subtree
@@ -842,12 +534,6 @@ __device__ int trace_packet_pruned(const DeviceScene &s, bool active, Vec o, Vec
     return best;
 }
 
-#ifndef CRT_WIN_NEXT_PREFETCH
-#define CRT_WIN_NEXT_PREFETCH 0   /* A/B: no gain, costs 11 spilled VGPRs */
-#endif
-#ifndef CRT_WIN_TRI_PREFETCH
-#define CRT_WIN_TRI_PREFETCH 1
-#endif
 /* ---------------------------------------------------------------------- */
 /* Window walk (TRAV 13, small tiles of ≤ 16 camera rays)                    */
 /* ---------------------------------------------------------------------- */
@@ -931,11 +617,6 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
         const bool dead = valid & interior & (((E >> (sl * R)) & rmask) == 0ull);
         const int skip_to = wave_max_i(dead ? nd.a : 0);
         const int next = uniform_i(i + K > skip_to ? i + K : skip_to);
-        /* the next window's nodes are in flight while this window's leaves are tested */
-#if CRT_WIN_NEXT_PREFETCH
-        const int jn = next + sl;
-        const PNode nd_next = nodes[jn < n ? jn : n - 1];
-#endif
         /* triangles of the entered leaves, one leaf per lane (next triangle
          * prefetched), then a per-ray merge over the ray's K lanes */
         const bool leaf = enter & !interior;
@@ -948,16 +629,9 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
                 uint8_t cl = s.slot_cull[first];
                 for (int k = 0; k < cnt; ++k) {
                     const int slot = first + k;
-#if CRT_WIN_TRI_PREFETCH
                     const int sn = k + 1 < cnt ? slot + 1 : slot;
-                    const DTriGeo gn = s.slots[sn];
+                    const DTriGeo gn = s.slots[sn];           /* next triangle in flight */
                     const uint8_t cn = s.slot_cull[sn];
-#else
-                    g = s.slots[slot];
-                    cl = s.slot_cull[slot];
-                    const DTriGeo gn = g;
-                    const uint8_t cn = cl;
-#endif
                     float t;
                     if (COUNT) ++c.tris;
                     if (tri_plane(o, d, g, cl != 0, t) && key_better(t, slot, lt, ls) && tri_edges(o, d, g, t)) {
@@ -981,19 +655,15 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
             best = ls;
             lim = best >= 0 ? best_t : INFINITY;
         }
-#if CRT_WIN_NEXT_PREFETCH
-        nd = nd_next;
-#else
         nd = nodes[next + sl < n ? next + sl : n - 1];
-#endif
         i = next;
     }
     if (COUNT && best >= 0 && lead) ++c.hits;
     return best;
 }
 
-/* TRAV 9: per-lane pruned walk (crt_device.h walk_pruned) over the lane's own
- * octant order — scattered secondary rays. */
+/* Per-lane pruned walk (crt_device.h walk_pruned) over the lane's own octant
+ * order: crt_hip_trace_batch's pruned walk (arbitrary, unrelated rays). */
 template <bool COUNT>
 __device__ __forceinline__ int trace_lane_pruned(const DeviceScene &s, bool active, Vec o, Vec d, float &best_t,
                                                  LaneCounts &c) {
@@ -1014,25 +684,25 @@ __device__ __forceinline__ int trace_lane_pruned(const DeviceScene &s, bool acti
     return best;
 }
 
-/* TRAV: 0 per-lane walk | 1 while-while | 2 while-while + prefetch | 3 as 2 with branch-free boxes
- *       4 cooperative | 5 range sharing | 6/7 packet | 8 pruned packet | 9 pruned per lane
- *       10 / 11 pruned 4 / 5 */
+/* Walks (TRAV), all bit-identical in result:
+ *   7  packet walk in the reference's node order (work counters = the reference's)
+ *   8  pruned packet walk (exact t-pruning), any camera ray
+ *   12 8 for frames whose camera rays are all in the hoisted-division window
+ *   13 12 + window walk for the plan's split tiles (k_render_tiles)
+ *   4  cooperative walk in the reference's node order (scattered rays)
+ *   10 pruned cooperative walk */
+template <int TRAV>
+constexpr bool kIsCoop = TRAV == 4 || TRAV == 10;
+
 template <int TRAV, bool COUNT>
 __device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, bool active, Vec o, Vec d, float &best_t,
                                      LaneCounts &c) {
-    if (TRAV == 8) return trace_packet_pruned<COUNT, false>(s, active, o, d, best_t, c);
-    if (TRAV == 12 || TRAV == 13) return trace_packet_pruned<COUNT, true>(s, active, o, d, best_t, c);
-    if (TRAV == 9) return trace_lane_pruned<COUNT>(s, active, o, d, best_t, c);
-    if (TRAV == 4) return trace_coop<COUNT, false>(s, *L, active, o, d, best_t, c);
-    if (TRAV == 5) return trace_share<COUNT, false>(s, *L, active, o, d, best_t, c);
-    if (TRAV == 10) return trace_coop<COUNT, true>(s, *L, active, o, d, best_t, c);
-    if (TRAV == 11) return trace_share<COUNT, true>(s, *L, active, o, d, best_t, c);
-    if (TRAV == 6) return trace_packet<COUNT, false>(s, active, o, d, best_t, c);
-    if (TRAV == 7) return trace_packet<COUNT, true>(s, active, o, d, best_t, c);
-    if (TRAV == 1) return trace_closest_ww<COUNT>(s, o, d, best_t, c);
-    if (TRAV == 2) return trace_closest_wwp<COUNT, false>(s, o, d, best_t, c);
-    if (TRAV == 3) return trace_closest_wwp<COUNT, true>(s, o, d, best_t, c);
-    return trace_closest<COUNT>(s, o, d, best_t, c);
+    static_assert(TRAV == 4 || TRAV == 7 || TRAV == 8 || TRAV == 10 || TRAV == 12 || TRAV == 13, "no such walk");
+    if constexpr (TRAV == 8) return trace_packet_pruned<COUNT, false>(s, active, o, d, best_t, c);
+    else if constexpr (TRAV == 12 || TRAV == 13) return trace_packet_pruned<COUNT, true>(s, active, o, d, best_t, c);
+    else if constexpr (TRAV == 4) return trace_coop<COUNT, false>(s, *L, active, o, d, best_t, c);
+    else if constexpr (TRAV == 10) return trace_coop<COUNT, true>(s, *L, active, o, d, best_t, c);
+    else return trace_packet<COUNT>(s, active, o, d, best_t, c);
 }
 
 __device__ __forceinline__ void make_hit(const DeviceScene &s, Vec o, Vec d, float t, int slot, HitRec &h,
@@ -1090,13 +760,27 @@ __device__ __forceinline__ void gi_ray(const DeviceScene &s, const DSettings &st
     d = dir;
 }
 
-/* powf(x, 5.0f) (crt_renderer.cpp:130): x^5 in double, rounded once. */
-__device__ __forceinline__ float pow5(float x) {
+/* fresnel = 0.5f * std::pow(1.0f + dot, 5.0f) (crt_renderer.cpp:130), the
+ * host libm's powf bit for bit.  The normal is flipped so that dot <= 0
+ * (:117-121; |dot| <= 2 for any normal of length <= 2), and then
+ * x = fl(1 + dot) is a multiple of 2^-24 in [-1, 1]: for dot in (-0.5, 0]
+ * x rounds into [0.5, 1] where floats are multiples of 2^-24; for dot in
+ * [-2, -0.5] the exact sum 1 + dot is a multiple of ulp(dot) >= 2^-24 below 1
+ * in magnitude, hence representable.  So x * 2^24 is an exact integer and
+ * indexes a table of powf(x, 5) computed by the host's libm (crt_hip_scene:
+ * ensure_pow5_table).  Any other dot (NaN, or a smooth normal longer than 2)
+ * falls back to x^5 in double rounded once. */
+__device__ __forceinline__ float fresnel_of(const DeviceScene &s, float dot) {
+    const float x = 1.0f + dot;
+    if (s.pow5 != nullptr && dot >= -2.0f && dot <= 0.0f) {
+        const int k = (int)(x * 16777216.0f);
+        return 0.5f * load_global(s.pow5, k + 16777216);
+    }
     const double xd = x;
     double r = xd * xd;
     r = r * r;
     r = r * xd;
-    return (float)r;
+    return 0.5f * (float)r;
 }
 
 /* shade_ray of a camera ray whose closest hit is known, for frames without
@@ -1209,7 +893,7 @@ __device__ __forceinline__ bool shade_pass(const DeviceScene &s, const DSettings
                         f.a = vadd(h.p, vscale(vneg(n), 1e-2f));
                         f.b = rd;
                     }
-                    f.alb.x = 0.5f * pow5(1.0f + vdot(d, n));
+                    f.alb.x = fresnel_of(s, vdot(d, n));
                     o = vadd(h.p, vscale(n, st.reflection_bias));
                     d = vsub(d, vscale(vscale(n, 2.0f), vdot(d, n)));
                     depth = depth + 1;
@@ -1299,7 +983,7 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
 #define CRT_RENDER_BOUNDS __launch_bounds__(256)
 #endif
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT>
-__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 || TRAV == 14 ? CRT_WINDOW_WAVES : (FULL && MAXF == 4 ? CRT_GI_WAVES : 1)))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
+__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT_WINDOW_WAVES : (FULL && MAXF == 4 ? CRT_GI_WAVES : 1)))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
                                                   const Tile *__restrict__ tiles,
                                                       int ntiles, float *__restrict__ out,
                                                       unsigned long long *__restrict__ counters,
@@ -1318,7 +1002,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 || TR
      * dependent loads): they get issue priority over the light waves that
      * share their SIMD (s_setprio; scheduling only, results unchanged) */
     if (tl.prio) __builtin_amdgcn_s_setprio(3);
-    if constexpr ((TRAV == 13 || TRAV == 14) && !FULL) {
+    if constexpr (TRAV == 13 && !FULL) {
         /* tiles of <= 16 rays (the measured plan's splits of heavy tiles): window walk */
         const int tw = uniform_i(tl.w), th = uniform_i(tl.h);
         const int npx = tw * th;
@@ -1359,11 +1043,10 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 || TR
     const bool has_px = lx < tl.w && ly < tl.h;
     /* the sharing walks keep pixel-less lanes as helpers (they take donated node
      * ranges of the wave's rays); the other walks drop them */
-    constexpr bool kHelpers = (TRAV >= 4) && !FULL;   /* sharing walks use them; packet walks ignore them */
+    constexpr bool kHelpers = !FULL;   /* sharing walks use them; packet walks ignore them */
     if (!kHelpers && !has_px) return;
     LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    constexpr bool kCoop = TRAV == 4 || TRAV == 5 || TRAV == 10 || TRAV == 11 ||
-                           SEC == 4 || SEC == 5 || SEC == 10 || SEC == 11;   /* LDS only for the sharing walks */
+    constexpr bool kCoop = kIsCoop<TRAV> || kIsCoop<SEC>;   /* LDS only for the sharing walks */
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     const Vec c = shade_pixel<FULL, MAXF, TRAV, SEC, COUNT>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt,
                                                       &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px);
@@ -1505,11 +1188,11 @@ __global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restri
     Vec o, d;
     camera_ray(s, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), o, d);
     LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    constexpr bool kCoop = TRAV == 4 || TRAV == 5 || TRAV == 10 || TRAV == 11;
+    constexpr bool kCoop = kIsCoop<TRAV>;
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
     (void)trace<TRAV, true>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px, o, d, t, cnt);
-    constexpr bool kPacket = (TRAV >= 6 && TRAV <= 8) || TRAV == 12 || TRAV == 13;
+    constexpr bool kPacket = !kIsCoop<TRAV>;
     uint32_t c = kPacket ? cnt.wave_nodes + cnt.wave_tris + cnt.wave_edges : cnt.nodes + cnt.tris;
     for (int off = 32; off > 0; off >>= 1) {
         const uint32_t o2 = (uint32_t)__shfl_xor((int)c, off);
@@ -1555,7 +1238,6 @@ struct WLevel {
     WNode *nodes;            /* by ray id */
     DVec4 *cols;             /* by ray id */
     int32_t rpw;             /* levels >= 1: rays per wave (lanes rpw..63 start idle and take donated pieces) */
-    int32_t group;           /* child queue order: 1 = per wave, first children then second children */
 };
 
 template <int TRAV, bool LEVEL0, bool COUNT>
@@ -1596,7 +1278,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         }
     }
     LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    constexpr bool kCoop = TRAV == 4 || TRAV == 5 || TRAV == 10 || TRAV == 11;
+    constexpr bool kCoop = kIsCoop<TRAV>;
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
     const int slot = trace<TRAV, COUNT>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has, o, d, t, cnt);
@@ -1650,7 +1332,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
                         }
                     }
                     node.kind = has_refr ? wRefract2 : wRefract1;
-                    node.a0 = 0.5f * pow5(1.0f + vdot(d, n));
+                    node.a0 = fresnel_of(s, vdot(d, n));
                     co[0] = vadd(h.p, vscale(n, st.reflection_bias));
                     cd[0] = vsub(d, vscale(vscale(n, 2.0f), vdot(d, n)));
                     co[1] = vadd(h.p, vscale(vneg(n), 1e-2f));   /* refract_at's default bias (crt_ray.h:30-50) */
@@ -1671,11 +1353,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         int base = 0;
         if (lane == __ffsll((long long)(b1 | b2)) - 1) base = atomicAdd(lv.out_count, total);
         base = __shfl(base, __ffsll((long long)(b1 | b2)) - 1);
-        /* group 0: a lane's children side by side; group 1: the wave's first
-         * children (reflection rays) then its second children (refraction
-         * rays), so next-level waves hold rays of one kind */
-        const int k0 = lv.group ? base + __popcll(b1 & lt) : base + __popcll(b1 & lt) + __popcll(b2 & lt);
-        const int k1 = lv.group ? base + __popcll(b1) + __popcll(b2 & lt) : k0 + 1;
+        /* a lane's children side by side */
+        const int k0 = base + __popcll(b1 & lt) + __popcll(b2 & lt);
+        const int k1 = k0 + 1;
         for (int c = 0; c < nch; ++c) {
             const int k = c == 0 ? k0 : k1;
             WRay r;
@@ -1718,8 +1398,7 @@ __device__ __forceinline__ Vec wf_compose(const WNode &nd, const DVec4 *__restri
 
 /* Wavefront levels >= 1 (C3): own translation unit (crt_render_wf.hip) and
  * LLVM scheduling strategy, as for the GI refill kernels above. */
-#define CRT_WF_INSTANCES(X) X(4, false) X(4, true) X(5, false) X(5, true) X(9, false) X(9, true) \
-    X(10, false) X(10, true) X(11, false) X(11, true)
+#define CRT_WF_INSTANCES(X) X(4, false) X(4, true) X(10, false) X(10, true)
 #define CRT_WF_SIG(SEC, C) void k_wf_level<SEC, false, C>(const DeviceScene *__restrict__, DSettings, \
     const Tile *__restrict__, int, WLevel, unsigned long long *__restrict__);
 #ifdef CRT_WF_TU
@@ -1771,7 +1450,7 @@ __global__ __launch_bounds__(256) void k_trace_rays(DeviceScene s, const float *
     const Vec d = vec(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
     LaneCounts cnt;
     float t;
-    const int slot = walk == 1 ? trace_lane_pruned<false>(s, true, o, d, t, cnt) : trace_closest_ww<false>(s, o, d, t, cnt);
+    const int slot = walk == 1 ? trace_lane_pruned<false>(s, true, o, d, t, cnt) : trace_closest<false>(s, o, d, t, cnt);
     crt_hit r;
     r.distance = 0.f;
     r.point[0] = r.point[1] = r.point[2] = 0.f;
@@ -1863,10 +1542,6 @@ struct ShardPlan {
     std::vector<Tile> tiles;     /* host copy, dispatch order */
     std::vector<float> cost;     /* measured cost per tile (calibrated plans), else empty */
     bool has_small = false;      /* some tile has <= 16 pixels (walk 13 runs them with the window walk) */
-    /* the same tiles partitioned (cost order kept inside each part) for the
-     * two-kernel launch of walk 13: window-walk tiles, then 8x8 tiles */
-    Tile *d_split = nullptr;
-    int nsmall = 0, nbig = 0;
 };
 
 struct GiTables { float *d = nullptr; };   /* 4 * 2^23 floats on one device */
@@ -1922,6 +1597,7 @@ struct crt_hip_scene {
     crt_scene_info info{};
     bool has_secondary = false;    /* any reflective / refractive material */
     bool has_diffuse = false;
+    bool has_refractive = false;   /* Fresnel term: needs the powf table (fresnel_of) */
     DeviceScene ds{};
     DeviceScene ds_uploaded{};   /* what d_ds holds */
     DeviceScene *d_ds = nullptr;
@@ -1929,9 +1605,6 @@ struct crt_hip_scene {
     std::vector<void *> allocs;
     hipStream_t stream = nullptr;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
-    /* second stream + fork/join events of the two-kernel walk-13 launch */
-    hipStream_t stream2 = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     ShardPlan full;
     std::map<std::pair<int, int>, ShardPlan> shard_plans;
     std::map<int, std::pair<UnpackBucket *, int>> unpack_plans;
@@ -1939,18 +1612,18 @@ struct crt_hip_scene {
     unsigned long long *d_counters = nullptr;
     int32_t *d_next_px = nullptr;      /* pixel-refill list head (k_render_refill) */
     int gi_refill = 1;                 /* GI frames: persistent waves with pixel refill (env CRT_GI_REFILL, option "gi_refill") */
-    int refill_waves = 5120;           /* waves of the refill grid: CUs x 4 SIMDs x CRT_GI_WAVES (env CRT_REFILL_WAVES) */
+    int refill_waves = 5120;           /* waves of the refill grid: CUs x 4 SIMDs x CRT_GI_WAVES */
     bool grid_empty = false;
-    int traversal = 8;             /* kernel walk variant, see trace<> (env CRT_TRAVERSAL) */
+    int traversal = 8;             /* 7 reference order | 8 pruned (default), see trace<> (env CRT_TRAVERSAL) */
     int trace_walk = 1;            /* crt_hip_trace_batch: 0 reference-order walk, 1 pruned per-lane walk */
     bool camera_fast = false;      /* every camera ray takes the fast box path (camera_rays_fast) */
-    int tile_order = 1;            /* dispatch tiles by estimated work (env CRT_TILE_ORDER) */
-    /* a tile is split into 4x4 (2x2) pixel waves when its work estimate exceeds
-     * split4 (split16) times the mean work per resident wave slot, i.e. when it
-     * would run for several times the ideal makespan (env CRT_SPLIT="a,b") */
+    /* estimate plan (no calibration): a tile is split into 4x4 (2x2) pixel
+     * waves when its work estimate exceeds split4 (split16) times the mean work
+     * per resident wave slot, i.e. when it would run for several times the
+     * ideal makespan */
     float split4 = 4.5f, split16 = 9.0f;
     int wave_slots = 6144;   /* CUs x 4 SIMDs x 6 resident render waves */
-    int secondary = 0;       /* walk for secondary rays under TRAV 6/7 (0 = by scene, env CRT_SECONDARY) */
+    int secondary = 0;       /* walk for secondary rays: 0 = by frame, 4, 10 (env CRT_SECONDARY) */
     std::vector<float> tile_work;  /* per 8x8 tile of the full frame */
     /* measured-cost tile plan (calibrate_plan): per 8x8 tile of the full frame,
      * the sub-tiles it is split into and their probed costs */
@@ -1961,11 +1634,9 @@ struct crt_hip_scene {
     int window_walk = 1;           /* camera walk 12 -> 13 (window walk for split tiles), env CRT_WINDOW */
     int record_events = 1;         /* start/stop events around every render (crt_hip_last_kernel_ms), option "events" */
     bool events_valid = false;
-    int split_launch = 0;          /* walk 13 as two concurrent kernels (window tiles | 8x8 tiles), env CRT_SPLIT_LAUNCH; A/B: fork/join costs more than the 8x8 kernel gains (C2 0.226 vs 0.177 ms) */
     float calib_k = 4.0f;          /* split a wave whose cost exceeds k x (total cost / wave slots) (env CRT_CALIB_K) */
-    int calib_min = 2;             /* smallest sub-tile side (env CRT_CALIB_MIN: 1, 2, 4, 8) */
-    int calib_direct = 0;          /* split a heavy tile straight to calib_min-sided tiles (env CRT_CALIB_DIRECT) */
-    int prio_tiles = 1024;         /* heaviest tiles run at raised issue priority (env CRT_PRIO) */
+    int calib_min = 2;             /* smallest sub-tile side */
+    int prio_tiles = 1024;         /* heaviest tiles run at raised issue priority */
     float prio_min = 2.0f;         /* ... if they cost more than this x the mean per wave slot */
     std::vector<void *> plan_allocs;   /* tile lists of the current plans */
     /* the tree in the reference's numbering (crt_hip_scene_tree): host copies
@@ -1977,9 +1648,6 @@ struct crt_hip_scene {
     const int32_t *dt_ref_children = nullptr, *dt_ref_leaf_tris = nullptr;
     const int64_t *dt_ref_leaf_off = nullptr;
     int wavefront = 1;             /* level-by-level recursion when GI is off (env CRT_WAVEFRONT) */
-    int wf_group = 0;              /* child queue grouped by kind per wave (env CRT_WF_GROUP, option "wf_group"); C3 A/B: no gain (4.60 vs 4.56 ms at 32 rays/wave, worse at 64) */
-    int wf_oct_mask = 7;           /* node-order octant mask of wavefront levels >= 1 (env CRT_WF_OCT, option "wf_oct") */
-    int wf_oct_uploaded = -1;
     int wf_rays_per_wave = 32;     /* rays per wave of wavefront levels >= 1, coop walks (env CRT_WF_RPW, option "wf_rpw"); C3: 64 4.70, 32 4.53, 16 4.58 ms */
     WfBuffers wf;
 };
@@ -2084,7 +1752,7 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         const double slot_cost = csum / std::max(1, sc->wave_slots);
         for (size_t k = 0; k < tiles.size() && (int)k < sc->prio_tiles; ++k)
             tiles[k].prio = plan.cost[k] > sc->prio_min * slot_cost ? 1 : 0;
-    } else if (sc->tile_order && !tiles.empty() && !sc->tile_work.empty()) {
+    } else if (!tiles.empty() && !sc->tile_work.empty()) {
         /* dispatch the expensive tiles first so the longest waves start at t=0;
          * with a sharing walk, split the heaviest tiles so each of their waves
          * carries fewer rays and the rest of its lanes help (4x4 or 2x2 pixels) */
@@ -2094,7 +1762,7 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         for (const Tile &t : tiles) wsum += work(t);
         const float slot_work = (float)(wsum / sc->wave_slots);
         std::vector<Tile> split;
-        if (sc->traversal >= 4 && slot_work > 0.f && (sc->split4 > 0.f || sc->split16 > 0.f)) {
+        if (slot_work > 0.f && (sc->split4 > 0.f || sc->split16 > 0.f)) {
             for (const Tile &t : tiles) {
                 const float w = work(t) / slot_work;
                 const int sub = (sc->split16 > 0.f && w >= sc->split16) ? 2 : (sc->split4 > 0.f && w >= sc->split4) ? 4 : 8;
@@ -2123,23 +1791,6 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         sc->plan_allocs.push_back(p);
         plan.d_tiles = static_cast<Tile *>(p);
     }
-    plan.d_split = nullptr;
-    plan.nsmall = plan.nbig = 0;
-    if (plan.has_small) {
-        std::vector<Tile> part;
-        part.reserve(tiles.size());
-        for (const Tile &t : tiles)
-            if (t.w * t.h <= 16) part.push_back(t);
-        plan.nsmall = (int)part.size();
-        for (const Tile &t : tiles)
-            if (t.w * t.h > 16) part.push_back(t);
-        plan.nbig = (int)part.size() - plan.nsmall;
-        void *p = nullptr;
-        HIP_TRY(hipMalloc(&p, part.size() * sizeof(Tile)));
-        HIP_TRY(hipMemcpy(p, part.data(), part.size() * sizeof(Tile), hipMemcpyHostToDevice));
-        sc->plan_allocs.push_back(p);
-        plan.d_split = static_cast<Tile *>(p);
-    }
     return CRT_OK;
 }
 
@@ -2158,7 +1809,6 @@ int probe_tiles(crt_hip_scene *sc, const DeviceScene *d_scene, int walk, const s
         const Tile *t = static_cast<const Tile *>(dt);
         uint32_t *c = static_cast<uint32_t *>(dc);
         switch (walk) {
-        case 6: hipLaunchKernelGGL(k_probe_tiles<6>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         case 7: hipLaunchKernelGGL(k_probe_tiles<7>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         case 12: hipLaunchKernelGGL(k_probe_tiles<12>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         case 13: hipLaunchKernelGGL(k_probe_tiles<13>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
@@ -2207,7 +1857,7 @@ int calibrate_plan(crt_hip_scene *sc, const DeviceScene *d_scene, int walk, hipS
             thresh = sc->calib_k * sum / std::max(1, sc->wave_slots);
         }
         std::vector<Item> next;
-        const int half = sc->calib_direct ? sc->calib_min : side / 2;
+        const int half = side / 2;
         for (size_t i = 0; i < cur.size(); ++i) {
             const Item &it = cur[i];
             if ((double)cost[i] > thresh && half >= sc->calib_min && (it.w > half || it.h > half)) {
@@ -2233,6 +1883,48 @@ void free_plans(crt_hip_scene *sc) {
     sc->shard_plans.clear();
 }
 
+/* powf(x, 5.0f) for x = k * 2^-24, k = -2^24 .. 2^24 (fresnel_of), computed
+ * by this process's libm — the one the reference's std::pow resolves to on
+ * this host.  Called through a volatile pointer so the compiler cannot
+ * replace the libm call by its own expansion. */
+constexpr int64_t kPow5N = (int64_t(1) << 25) + 1;
+std::mutex g_pow5_mu;
+std::map<int, float *> g_pow5;             /* per device, process lifetime */
+std::vector<float> g_pow5_host;
+
+void build_pow5_host_table() {
+    if (!g_pow5_host.empty()) return;
+    g_pow5_host.resize((size_t)kPow5N);
+    float *t = g_pow5_host.data();
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> pool;
+    for (unsigned w = 0; w < nt; ++w) {
+        pool.emplace_back([=]() {
+            float (*volatile pw)(float, float) = ::powf;
+            for (int64_t k = w; k < kPow5N; k += nt) {
+                const float x = (float)(k - (int64_t(1) << 24)) * (1.0f / 16777216.0f);   /* exact */
+                t[k] = pw(x, 5.0f);
+            }
+        });
+    }
+    for (auto &th : pool) th.join();
+}
+
+int ensure_pow5_table(crt_hip_scene *sc) {
+    if (sc->ds.pow5) return CRT_OK;
+    std::lock_guard<std::mutex> g(g_pow5_mu);
+    float *&d = g_pow5[sc->device];
+    if (!d) {
+        build_pow5_host_table();
+        void *p = nullptr;
+        HIP_TRY(hipMalloc(&p, (size_t)kPow5N * sizeof(float)));
+        HIP_TRY(hipMemcpy(p, g_pow5_host.data(), (size_t)kPow5N * sizeof(float), hipMemcpyHostToDevice));
+        d = static_cast<float *>(p);
+    }
+    sc->ds.pow5 = d;
+    return CRT_OK;
+}
+
 int ensure_gi_tables(crt_hip_scene *sc) {
     if (sc->ds.gi_pi) return CRT_OK;
     std::lock_guard<std::mutex> g(g_gi_mu);
@@ -2253,21 +1945,16 @@ int ensure_gi_tables(crt_hip_scene *sc) {
  * host record changed (first GI frame, new resolution); kernels of earlier
  * frames may still read the old copy, so the device is drained first. */
 int sync_device_record(crt_hip_scene *sc, const DeviceScene **out) {
-    if (!sc->d_ds || std::memcmp(&sc->ds_uploaded, &sc->ds, sizeof(DeviceScene)) != 0 ||
-        sc->wf_oct_mask != sc->wf_oct_uploaded) {
-        sc->wf_oct_uploaded = sc->wf_oct_mask;
+    if (!sc->d_ds || std::memcmp(&sc->ds_uploaded, &sc->ds, sizeof(DeviceScene)) != 0) {
         if (!sc->d_ds) {
             void *p = nullptr;
-            HIP_TRY(hipMalloc(&p, 2 * sizeof(DeviceScene)));
+            HIP_TRY(hipMalloc(&p, sizeof(DeviceScene)));
             sc->allocs.push_back(p);
             sc->d_ds = static_cast<DeviceScene *>(p);
         } else {
             HIP_TRY(hipDeviceSynchronize());
         }
-        /* [0]: the frame's record; [1]: the same for wavefront levels >= 1 (secondary node order) */
-        DeviceScene two[2] = {sc->ds, sc->ds};
-        two[1].oct_mask = sc->wf_oct_mask;
-        HIP_TRY(hipMemcpy(sc->d_ds, two, sizeof two, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(sc->d_ds, &sc->ds, sizeof(DeviceScene), hipMemcpyHostToDevice));
         std::memcpy(&sc->ds_uploaded, &sc->ds, sizeof(DeviceScene));
     }
     *out = sc->d_ds;
@@ -2290,8 +1977,7 @@ int camera_walk(const crt_hip_scene *sc, int trav) {
 int plan_walk(const crt_hip_scene *sc, const crt_renderer_settings *st) {
     const bool gi = sc->info.gi_on && sc->has_diffuse && st->diffuse_reflection_ray_count > 0;
     const bool full = gi || sc->has_secondary;
-    const bool packet = sc->traversal >= 6 && sc->traversal <= 8;
-    if (gi || !packet) return -1;
+    if (gi) return -1;
     if (full) return sc->wavefront ? camera_walk(sc, sc->traversal == 8 ? 8 : 7) : -1;
     return camera_walk(sc, sc->traversal);
 }
@@ -2389,7 +2075,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
     if ((rc = wf_grow_ids(w, 3 * n0, 0, stream)) != CRT_OK) return rc;
     if ((rc = wf_grow_queue(w, 0, 2 * n0)) != CRT_OK) return rc;
     unsigned long long *cnt = sc->d_counters;
-    WLevel lv{nullptr, 0, 0, w.q[0], w.counts, (int32_t)n0, w.nodes, w.cols, 64, sc->wf_group};
+    WLevel lv{nullptr, 0, 0, w.q[0], w.counts, (int32_t)n0, w.nodes, w.cols, 64};
     const int blocks0 = (plan.ntiles + 3) / 4;
 #define CRT_WF0(T, COUNT)                                                                                   \
     hipLaunchKernelGGL((k_wf_level<T, true, COUNT>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,      \
@@ -2415,20 +2101,17 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
         if ((rc = wf_grow_ids(w, base + 3 * (int64_t)n, base, stream)) != CRT_OK) return rc;
         if ((rc = wf_grow_queue(w, cur ^ 1, 2 * (int64_t)n)) != CRT_OK) return rc;
         /* coop walks: fewer rays per wave put idle lanes on the long walks (donated pieces) */
-        const bool coop = sec == 4 || sec == 5 || sec == 10 || sec == 11;
-        const int rpw = coop ? std::min(64, std::max(1, sc->wf_rays_per_wave)) : 64;
-        WLevel l{w.q[cur], n, L, w.q[cur ^ 1], w.counts + L, (int32_t)(base + n), w.nodes, w.cols, rpw, sc->wf_group};
+        const int rpw = std::min(64, std::max(1, sc->wf_rays_per_wave));
+        WLevel l{w.q[cur], n, L, w.q[cur ^ 1], w.counts + L, (int32_t)(base + n), w.nodes, w.cols, rpw};
         const int64_t waves = ((int64_t)n + rpw - 1) / rpw;
         const int blocks = (int)((waves + 3) / 4);
 #define CRT_WF(SEC, COUNT)                                                                                  \
-    hipLaunchKernelGGL((k_wf_level<SEC, false, COUNT>), dim3(blocks), dim3(256), 0, stream, d_scene + 1, ds, \
+    hipLaunchKernelGGL((k_wf_level<SEC, false, COUNT>), dim3(blocks), dim3(256), 0, stream, d_scene, ds,     \
                        plan.d_tiles, plan.ntiles, l, cnt)
-        switch (sec) {
-        case 4: if (count) CRT_WF(4, true); else CRT_WF(4, false); break;
-        case 9: if (count) CRT_WF(9, true); else CRT_WF(9, false); break;
-        case 10: if (count) CRT_WF(10, true); else CRT_WF(10, false); break;
-        case 11: if (count) CRT_WF(11, true); else CRT_WF(11, false); break;
-        default: if (count) CRT_WF(5, true); else CRT_WF(5, false); break;
+        if (sec == 10) {
+            if (count) CRT_WF(10, true); else CRT_WF(10, false);
+        } else {
+            if (count) CRT_WF(4, true); else CRT_WF(4, false);
         }
 #undef CRT_WF
         HIP_TRY(hipGetLastError());
@@ -2454,6 +2137,10 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         const int rc = ensure_gi_tables(sc);
         if (rc != CRT_OK) return rc;
     }
+    if (sc->has_refractive && sc->info.refractions_on) {
+        const int rc = ensure_pow5_table(sc);
+        if (rc != CRT_OK) return rc;
+    }
     if (plan.ntiles == 0) return CRT_OK;
     const DeviceScene *d_scene = nullptr;
     {
@@ -2461,23 +2148,20 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         if (rc != CRT_OK) return rc;
     }
     const DSettings ds = to_dsettings(st);
-    /* Walks: camera rays of diffuse-only frames take the packet walk
-     * (traversal 7, or 8 pruned).  Secondary rays scatter and take a per-lane
-     * sharing walk: for reflect/refract levels range sharing (5) or, pruned,
-     * cooperative donation (10: 4.98 ms vs 5.75 for 11 and 7.0 for 5 on C3);
-     * for GI fan-out cooperative donation (4) — its pruned form (10) needs
-     * 134 VGPRs (3 waves/SIMD) and loses on C4 (378 vs 320 ms); with GI every
-     * ray of the per-lane frame-stack kernel takes that walk (the packet walk's
-     * registers would cost a wave per SIMD).  CRT_SECONDARY / "secondary"
-     * overrides the secondary walk. */
-    const bool pruned = sc->traversal >= 8;
+    /* Walks: camera rays take the packet walk (traversal 7, or 8 pruned).
+     * Secondary rays scatter and take the cooperative walk: pruned (10) for
+     * reflect/refract levels (C3), reference order (4) for GI fan-out — the
+     * pruned form needs 134 VGPRs (3 waves/SIMD) and loses on C4 (378 vs 320
+     * ms); with GI every ray of the per-lane frame-stack kernel takes that walk
+     * (the packet walk's registers would cost a wave per SIMD).
+     * CRT_SECONDARY / "secondary" overrides the secondary walk. */
+    const bool pruned = sc->traversal == 8;
     int sec = sc->secondary;
-    if (sec == 0) sec = gi ? 4 : (pruned ? 10 : 5);
-    const bool packet = sc->traversal >= 6 && sc->traversal <= 8;
-    if (full && !gi && sc->wavefront && packet && !stamps)
-        return render_wavefront(sc, ds, plan, d_out, stream, count, d_scene, sec, camera_walk(sc, pruned ? 8 : 7));
-    /* frame-stack kernel: one walk for every ray (packet walks hand over to sec) */
-    int trav = full ? (packet ? sec : sc->traversal) : camera_walk(sc, sc->traversal);
+    if (sec == 0) sec = (gi || !pruned) ? 4 : 10;
+    if (full && !gi && sc->wavefront && !stamps)
+        return render_wavefront(sc, ds, plan, d_out, stream, count, d_scene, sec, camera_walk(sc, sc->traversal));
+    /* frame-stack kernel: one walk for every ray */
+    int trav = full ? sec : camera_walk(sc, sc->traversal);
     if (trav == 13 && !plan.has_small) trav = 12;   /* no split tiles: the leaner packet-only kernel */
     const int blocks = (plan.ntiles + 3) / 4;
     const uint64_t frames = (uint64_t)st->max_ray_depth + 1;
@@ -2485,57 +2169,18 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
 #define CRT_LAUNCH_T(FULL, MAXF, TRAV, COUNT)                                                               \
     hipLaunchKernelGGL((k_render_tiles<FULL, MAXF, TRAV, TRAV, COUNT>), dim3(blocks), dim3(256), 0, stream,      \
                        d_scene, ds, plan.d_tiles, plan.ntiles, d_out, cnt, stamps)
-#define CRT_LAUNCH(FULL, MAXF, COUNT)                                                                       \
+#define CRT_LAUNCH(MAXF, COUNT)                                                                             \
     do {                                                                                                   \
-        switch (trav) {                                                                                    \
-        case 0: CRT_LAUNCH_T(FULL, MAXF, 0, COUNT); break;                                                 \
-        case 3: CRT_LAUNCH_T(FULL, MAXF, 3, COUNT); break;                                                 \
-        case 4: CRT_LAUNCH_T(FULL, MAXF, 4, COUNT); break;                                                 \
-        case 5: CRT_LAUNCH_T(FULL, MAXF, 5, COUNT); break;                                                 \
-        case 9: CRT_LAUNCH_T(FULL, MAXF, 9, COUNT); break;                                                 \
-        case 10: CRT_LAUNCH_T(FULL, MAXF, 10, COUNT); break;                                               \
-        case 11: CRT_LAUNCH_T(FULL, MAXF, 11, COUNT); break;                                               \
-        default: return set_error(CRT_E_INVALID, "no such walk for this kernel");                         \
-        }                                                                                                  \
+        if (trav == 10) CRT_LAUNCH_T(true, MAXF, 10, COUNT);                                               \
+        else CRT_LAUNCH_T(true, MAXF, 4, COUNT);                                                           \
     } while (0)
-    if (!full && trav == 13 && plan.d_split && sc->split_launch && !stamps) {
-        /* window-walk tiles (kernel 14, ~120 VGPRs) on a second stream, 8x8
-         * tiles (kernel 12, 75 VGPRs, 6 waves/SIMD) on the caller's stream,
-         * concurrently; the caller's stream waits for both */
-        if (!sc->stream2) {
-            HIP_TRY(hipStreamCreateWithFlags(&sc->stream2, hipStreamNonBlocking));
-            HIP_TRY(hipEventCreateWithFlags(&sc->ev_fork, hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&sc->ev_join, hipEventDisableTiming));
-        }
-        HIP_TRY(hipEventRecord(sc->ev_fork, stream));
-        HIP_TRY(hipStreamWaitEvent(sc->stream2, sc->ev_fork, 0));
-        const int bs = (plan.nsmall + 3) / 4, bb = (plan.nbig + 3) / 4;
-        if (count) {
-            hipLaunchKernelGGL((k_render_tiles<false, 0, 14, 14, true>), dim3(bs), dim3(256), 0, sc->stream2, d_scene, ds,
-                               plan.d_split, plan.nsmall, d_out, cnt, stamps);
-            if (bb > 0)
-                hipLaunchKernelGGL((k_render_tiles<false, 0, 12, 12, true>), dim3(bb), dim3(256), 0, stream, d_scene, ds,
-                                   plan.d_split + plan.nsmall, plan.nbig, d_out, cnt, stamps);
-        } else {
-            hipLaunchKernelGGL((k_render_tiles<false, 0, 14, 14, false>), dim3(bs), dim3(256), 0, sc->stream2, d_scene,
-                               ds, plan.d_split, plan.nsmall, d_out, cnt, stamps);
-            if (bb > 0)
-                hipLaunchKernelGGL((k_render_tiles<false, 0, 12, 12, false>), dim3(bb), dim3(256), 0, stream, d_scene,
-                                   ds, plan.d_split + plan.nsmall, plan.nbig, d_out, cnt, stamps);
-        }
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(sc->ev_join, sc->stream2));
-        HIP_TRY(hipStreamWaitEvent(stream, sc->ev_join, 0));
-        return CRT_OK;
-    }
     if (!full) {
         switch (trav) {
-        case 6: if (count) CRT_LAUNCH_T(false, 0, 6, true); else CRT_LAUNCH_T(false, 0, 6, false); break;
         case 7: if (count) CRT_LAUNCH_T(false, 0, 7, true); else CRT_LAUNCH_T(false, 0, 7, false); break;
         case 8: if (count) CRT_LAUNCH_T(false, 0, 8, true); else CRT_LAUNCH_T(false, 0, 8, false); break;
         case 12: if (count) CRT_LAUNCH_T(false, 0, 12, true); else CRT_LAUNCH_T(false, 0, 12, false); break;
         case 13: if (count) CRT_LAUNCH_T(false, 0, 13, true); else CRT_LAUNCH_T(false, 0, 13, false); break;
-        default: if (count) CRT_LAUNCH(false, 0, true); else CRT_LAUNCH(false, 0, false); break;
+        default: return set_error(CRT_E_INVALID, "no such camera walk");
         }
     } else if (gi && (trav == 4 || trav == 10) && sc->gi_refill && sc->d_next_px && !stamps && frames <= 64) {
         /* GI: persistent waves with pixel refill (k_render_refill) */
@@ -2558,11 +2203,11 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
 #undef CRT_REFILL
 #undef CRT_REFILL_T
     } else if (frames <= 4) {
-        if (count) CRT_LAUNCH(true, 4, true); else CRT_LAUNCH(true, 4, false);
+        if (count) CRT_LAUNCH(4, true); else CRT_LAUNCH(4, false);
     } else if (frames <= 16) {
-        if (count) CRT_LAUNCH(true, 16, true); else CRT_LAUNCH(true, 16, false);
+        if (count) CRT_LAUNCH(16, true); else CRT_LAUNCH(16, false);
     } else if (frames <= 64) {
-        if (count) CRT_LAUNCH(true, 64, true); else CRT_LAUNCH(true, 64, false);
+        if (count) CRT_LAUNCH(64, true); else CRT_LAUNCH(64, false);
     } else {
         return set_error(CRT_E_UNSUPPORTED, "max_ray_depth > 63 with recursive materials is not supported");
     }
@@ -2603,29 +2248,17 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     HIP_TRY(hipSetDevice(device));
     std::unique_ptr<crt_hip_scene> sc(new crt_hip_scene());
     sc->device = device;
-    if (const char *e = std::getenv("CRT_TRAVERSAL")) sc->traversal = std::atoi(e);
-    if (const char *e = std::getenv("CRT_TILE_ORDER")) sc->tile_order = std::atoi(e);
-    if (const char *e = std::getenv("CRT_SECONDARY")) sc->secondary = std::atoi(e);
-    if (const char *e = std::getenv("CRT_WAVEFRONT")) sc->wavefront = std::atoi(e);
-    if (const char *e = std::getenv("CRT_GI_REFILL")) sc->gi_refill = std::atoi(e) != 0;
-    if (const char *e = std::getenv("CRT_WF_GROUP")) sc->wf_group = std::atoi(e) != 0;
-    if (const char *e = std::getenv("CRT_WF_OCT")) sc->wf_oct_mask = std::atoi(e) & 7;
-    if (const char *e = std::getenv("CRT_WF_RPW")) sc->wf_rays_per_wave = std::min(64, std::max(1, std::atoi(e)));
-    if (const char *e = std::getenv("CRT_TRACE_WALK")) sc->trace_walk = std::atoi(e);
-    if (const char *e = std::getenv("CRT_CALIBRATE")) sc->calibrate = std::atoi(e);
-    if (const char *e = std::getenv("CRT_WINDOW")) sc->window_walk = std::atoi(e);
-    if (const char *e = std::getenv("CRT_SPLIT_LAUNCH")) sc->split_launch = std::atoi(e);
-    if (const char *e = std::getenv("CRT_EVENTS")) sc->record_events = std::atoi(e);
+    /* environment overrides of the options (crt_hip_scene_set_option names) */
+    static const char *const kEnv[][2] = {{"CRT_TRAVERSAL", "traversal"}, {"CRT_SECONDARY", "secondary"},
+                                           {"CRT_WAVEFRONT", "wavefront"}, {"CRT_GI_REFILL", "gi_refill"},
+                                           {"CRT_WF_RPW", "wf_rpw"},       {"CRT_TRACE_WALK", "trace_walk"},
+                                           {"CRT_CALIBRATE", "calibrate"}, {"CRT_WINDOW", "window"},
+                                           {"CRT_EVENTS", "events"}};
+    for (const auto &kv : kEnv)
+        if (const char *e = std::getenv(kv[0]))
+            if (crt_hip_scene_set_option(sc.get(), kv[1], std::atoi(e)) != CRT_OK) return CRT_E_INVALID;
     if (const char *e = std::getenv("CRT_CALIB_K")) sc->calib_k = (float)std::atof(e);
-    if (const char *e = std::getenv("CRT_CALIB_MIN")) sc->calib_min = std::max(1, std::atoi(e));
-    if (const char *e = std::getenv("CRT_CALIB_DIRECT")) sc->calib_direct = std::atoi(e);
-    if (const char *e = std::getenv("CRT_PRIO")) sc->prio_tiles = std::max(0, std::atoi(e));
-    if (const char *e = std::getenv("CRT_PRIO_MIN")) sc->prio_min = (float)std::atof(e);
-    if (const char *e = std::getenv("CRT_SPLIT")) {
-        float a = 0.f, b = 0.f;
-        if (std::sscanf(e, "%f,%f", &a, &b) >= 1) { sc->split4 = a; sc->split16 = b; }
-    }
-    if (sc->tile_order && hs.tree_on_host) sc->tile_work = tile_work_estimate(hs, (hs.width + 7) / 8, (hs.height + 7) / 8);
+    if (hs.tree_on_host) sc->tile_work = tile_work_estimate(hs, (hs.width + 7) / 8, (hs.height + 7) / 8);
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) {
@@ -2633,11 +2266,11 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
             sc->refill_waves = prop.multiProcessorCount * 4 * CRT_GI_WAVES;
         }
     }
-    if (const char *e = std::getenv("CRT_REFILL_WAVES")) sc->refill_waves = std::max(1, std::atoi(e));
     crt_host_scene_info(h, &sc->info);
     sc->info.device_bytes = 0;
     for (const DMaterial &m : hs.materials) {
         if (m.type == CRT_MATERIAL_REFLECTIVE || m.type == CRT_MATERIAL_REFRACTIVE) sc->has_secondary = true;
+        if (m.type == CRT_MATERIAL_REFRACTIVE) sc->has_refractive = true;
         if (m.type == CRT_MATERIAL_DIFFUSE) sc->has_diffuse = true;
     }
     DeviceScene &ds = sc->ds;
@@ -2695,7 +2328,6 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
                                  m * (int64_t)(sizeof(DTriGeo) + 4 + 1) + (m / 32 + 1) * 4;
     }
     sc->camera_fast = camera_rays_fast(hs, ds.planes_ok != 0);
-    if (const char *e = std::getenv("CRT_CAMERA_FAST")) sc->camera_fast = sc->camera_fast && std::atoi(e) != 0;
     if ((rc = upload(sc.get(), hs.tri_attr, &ds.tri_attr)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.vnormal, &ds.vnormal)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.vuv, &ds.vuv)) != CRT_OK) return rc;
@@ -2712,7 +2344,6 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     ds.tan_half_fov = hs.tan_half_fov;
     std::memcpy(ds.background, hs.background, sizeof ds.background);
     ds.gi_on = hs.gi_on;
-    ds.oct_mask = 7;
     ds.reflections_on = hs.reflections_on;
     ds.refractions_on = hs.refractions_on;
 
@@ -2799,10 +2430,6 @@ void crt_hip_scene_destroy(crt_hip_scene *sc) {
     for (auto &kv : sc->unpack_plans) (void)hipFree(kv.second.first);
     if (sc->ev_start) (void)hipEventDestroy(sc->ev_start);
     if (sc->ev_stop) (void)hipEventDestroy(sc->ev_stop);
-    if (sc->stream2) (void)hipStreamSynchronize(sc->stream2);
-    if (sc->ev_fork) (void)hipEventDestroy(sc->ev_fork);
-    if (sc->ev_join) (void)hipEventDestroy(sc->ev_join);
-    if (sc->stream2) (void)hipStreamDestroy(sc->stream2);
     if (sc->stream) (void)hipStreamDestroy(sc->stream);
     delete sc;
 }
@@ -3054,25 +2681,17 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
     if (!sc || !name) return set_error(CRT_E_INVALID, "null argument");
     const std::string k(name);
     if (k == "traversal") {
-        if (value < 0 || value > 11 || value == 1 || value == 2) return set_error(CRT_E_INVALID, "traversal must be 0, 3..11");
+        if (value != 7 && value != 8) return set_error(CRT_E_INVALID, "traversal must be 7 (reference order) or 8 (pruned)");
         sc->traversal = value;
     } else if (k == "secondary") {
-        if (value != 0 && value != 4 && value != 5 && value != 9 && value != 10 && value != 11)
-            return set_error(CRT_E_INVALID, "secondary must be 0, 4, 5, 9, 10 or 11");
+        if (value != 0 && value != 4 && value != 10) return set_error(CRT_E_INVALID, "secondary must be 0, 4 or 10");
         sc->secondary = value;
     } else if (k == "wavefront") {
         sc->wavefront = value != 0;
     } else if (k == "window") {
         sc->window_walk = value != 0;
-    } else if (k == "split_launch") {
-        sc->split_launch = value != 0;
     } else if (k == "gi_refill") {
         sc->gi_refill = value != 0;
-    } else if (k == "wf_group") {
-        sc->wf_group = value != 0;
-    } else if (k == "wf_oct") {
-        if (value < 0 || value > 7) return set_error(CRT_E_INVALID, "wf_oct must be 0..7");
-        sc->wf_oct_mask = value;
     } else if (k == "wf_rpw") {
         if (value < 1 || value > 64) return set_error(CRT_E_INVALID, "wf_rpw must be 1..64");
         sc->wf_rays_per_wave = value;

@@ -284,25 +284,24 @@ typedef struct crt_wave_counts {
 } crt_wave_counts;
 int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
 
-/* Walk selection (results are identical for every walk; work and speed
- * differ).  Names: "traversal" (primary-ray walk: 7 = reference-order packet
- * walk, whose work counters equal the reference's; 8 = pruned packet walk,
- * default; 0..6, 9 = other variants), "secondary" (0 = by walk, 4, 5, 9),
- * "wavefront" (0/1: level-by-level recursion when GI is off), "trace_walk"
- * (crt_hip_trace_batch: 0 = reference order, 1 = pruned per-ray walk),
- * "window" (0/1, default 1: the plan's split tiles of <= 16 camera rays take
- * the window walk), "split_launch" (0/1, default 0: window tiles and 8x8
- * tiles as two concurrent kernels), "calibrate" (0/1: measured-cost tile plan),
- * "events" (0/1: per-render start/stop events), "wf_rpw" (1..64, default 32:
- * rays per wave of wavefront levels >= 1 under the cooperative walks; the
- * other lanes start idle and take donated pieces), "wf_oct" (0..7, default 7:
- * node-order octant mask of those levels' pruned walks), "wf_group" (0/1,
- * default 0: queue each wave's first children before its second children),
- * "gi_refill" (0/1,
- * default 1: GI frames run persistent waves that refill finished lanes with
- * the next pixel of the tile list).
- * Environment variables CRT_TRAVERSAL, CRT_SECONDARY, CRT_WAVEFRONT,
- * CRT_TRACE_WALK, CRT_WF_RPW, CRT_WF_OCT and CRT_GI_REFILL set the initial values. */
+/* Options (results are identical for every setting; work and speed differ):
+ *   "traversal"  7 = packet walk in the reference's node order (work counters
+ *                equal the reference's) | 8 = exact t-pruned walks (default)
+ *   "secondary"  walk of secondary rays: 0 = by frame (default), 4 =
+ *                cooperative walk in the reference's order, 10 = pruned cooperative
+ *   "wavefront"  0/1 (default 1): level-by-level recursion when GI is off
+ *   "window"     0/1 (default 1): the plan's split tiles of <= 16 camera rays
+ *                take the window walk
+ *   "calibrate"  0/1 (default 1): measured-cost tile plan
+ *   "gi_refill"  0/1 (default 1): GI frames run persistent waves that refill
+ *                finished lanes with the next pixel of the tile list
+ *   "wf_rpw"     1..64 (default 32): rays per wave of wavefront levels >= 1 (the
+ *                other lanes start idle and take donated pieces)
+ *   "trace_walk" 0 = reference order, 1 = pruned per-ray walk (crt_hip_trace_batch)
+ *   "events"     0/1 (default 1): start/stop events around every render
+ * Environment variables CRT_TRAVERSAL, CRT_SECONDARY, CRT_WAVEFRONT, CRT_WINDOW,
+ * CRT_CALIBRATE, CRT_GI_REFILL, CRT_WF_RPW, CRT_TRACE_WALK and CRT_EVENTS set
+ * the initial values (an invalid value makes scene creation fail). */
 int  crt_hip_scene_set_option(crt_hip_scene *scene, const char *name, int value);
 
 /* Diagnostics: render one full frame with per-wave s_memrealtime stamps
