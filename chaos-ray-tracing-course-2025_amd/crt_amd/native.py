@@ -72,6 +72,30 @@ class SceneDesc(C.Structure):
                 ("lights", C.POINTER(LightDesc)), ("light_count", C.c_int32)]
 
 
+class TreeTriangle(C.Structure):
+    """crt_tree_triangle: one Triangle copy of a leaf (crt_triangle.h:19-23)."""
+    _fields_ = [("v", C.c_int32 * 3), ("face_normal", C.c_float * 3), ("material_index", C.c_int32),
+                ("flags", C.c_int32)]
+
+
+TREE_TRI_DTYPE = np.dtype([("v", "<i4", 3), ("face_normal", "<f4", 3), ("material_index", "<i4"), ("flags", "<i4")])
+assert TREE_TRI_DTYPE.itemsize == C.sizeof(TreeTriangle)
+
+
+class TreeSceneDesc(C.Structure):
+    """crt_tree_scene_desc: the reference's built crt::Scene (crt_scene.h:18-30)."""
+    _fields_ = [("background_color", Vec3), ("camera_location", Vec3), ("camera_rotation", C.c_float * 9),
+                ("width", C.c_int32), ("height", C.c_int32), ("fov_radians", C.c_float), ("bucket_size", C.c_int32),
+                ("gi_on", C.c_int32), ("reflections_on", C.c_int32), ("refractions_on", C.c_int32),
+                ("vertices", C.POINTER(C.c_float)), ("vertex_count", C.c_int64),
+                ("node_bounds", C.POINTER(C.c_float)), ("node_children", C.POINTER(C.c_int32)),
+                ("leaf_offsets", C.POINTER(C.c_int64)), ("leaf_triangles", C.POINTER(TreeTriangle)),
+                ("node_count", C.c_int64),
+                ("materials", C.POINTER(MaterialDesc)), ("material_count", C.c_int32),
+                ("textures", C.POINTER(TextureDesc)), ("texture_count", C.c_int32),
+                ("lights", C.POINTER(LightDesc)), ("light_count", C.c_int32)]
+
+
 class RendererSettings(C.Structure):
     """crt_renderer.h:18-25; defaults = crt_renderer.h:10-16."""
     _fields_ = [("max_ray_depth", C.c_uint32), ("diffuse_reflection_ray_count", C.c_uint32),
@@ -151,6 +175,8 @@ EXPORTS = [
     ("crt_host_scene_destroy", None, [_P]),
     ("crt_hip_scene_create", C.c_int, [C.POINTER(SceneDesc), C.c_int, C.POINTER(_P)]),
     ("crt_hip_scene_create_ex", C.c_int, [C.POINTER(SceneDesc), C.c_int, C.c_int, C.POINTER(_P)]),
+    ("crt_hip_scene_from_tree", C.c_int, [C.POINTER(TreeSceneDesc), C.c_int, C.POINTER(_P)]),
+    ("crt_host_scene_from_tree", C.c_int, [C.POINTER(TreeSceneDesc), C.POINTER(_P)]),
     ("crt_hip_scene_tree", C.c_int, [_P, _P, _P, _P, _P]),
     ("crt_hip_scene_upload", C.c_int, [_P, C.c_int, C.POINTER(_P)]),
     ("crt_hip_scene_info", C.c_int, [_P, C.POINTER(SceneInfo)]),
@@ -305,6 +331,39 @@ class SyntheticScene:
         return C.pointer(self._desc)
 
 
+class TreeScene:
+    """A crt_tree_scene_desc over numpy arrays: the reference's vertex array
+    (9 floats per vertex) and its built tree (bounds, children, leaf offsets,
+    leaf Triangle copies), plus materials / textures / lights / camera / flags
+    taken from a scene description (`shading`, e.g. an ArrayScene)."""
+
+    def __init__(self, shading, vertices, bounds, children, leaf_offsets, leaf_triangles):
+        d = shading.desc()
+        self._shading = shading
+        self.vertices = np.ascontiguousarray(vertices, np.float32).reshape(-1)
+        self.bounds = np.ascontiguousarray(bounds, np.float32).reshape(-1)
+        self.children = np.ascontiguousarray(children, np.int32).reshape(-1)
+        self.offsets = np.ascontiguousarray(leaf_offsets, np.int64).reshape(-1)
+        self.tris = np.ascontiguousarray(leaf_triangles).view(TREE_TRI_DTYPE).reshape(-1)
+        n = self.offsets.size - 1
+        # crt_camera.h:20: m_fov_radians = fov_degrees * pi_v<float> / 180.0f (float ops)
+        fov = np.float32(np.float32(d.camera.fov_degrees) * np.float32(np.pi)) / np.float32(180.0)
+        self._desc = TreeSceneDesc(
+            d.background_color, d.camera.location, d.camera.rotation, d.camera.width, d.camera.height,
+            float(fov), d.bucket_size, d.gi_on, d.reflections_on, d.refractions_on,
+            _fptr(self.vertices), self.vertices.size // 9, _fptr(self.bounds),
+            self.children.ctypes.data_as(C.POINTER(C.c_int32)), self.offsets.ctypes.data_as(C.POINTER(C.c_int64)),
+            self.tris.ctypes.data_as(C.POINTER(TreeTriangle)), n,
+            d.materials, d.material_count, d.textures, d.texture_count, d.lights, d.light_count)
+
+    def set_resolution(self, width: int, height: int) -> "TreeScene":
+        self._desc.width, self._desc.height = width, height
+        return self
+
+    def tree_desc_ptr(self):
+        return C.pointer(self._desc)
+
+
 def _desc_ptr(src):
     if hasattr(src, "desc_ptr"):
         return src.desc_ptr()
@@ -319,7 +378,10 @@ def _desc_ptr(src):
 class HostScene:
     def __init__(self, src):
         h = C.c_void_p()
-        _check(lib().crt_host_scene_create(_desc_ptr(src), C.byref(h)))
+        if hasattr(src, "tree_desc_ptr"):
+            _check(lib().crt_host_scene_from_tree(src.tree_desc_ptr(), C.byref(h)))
+        else:
+            _check(lib().crt_host_scene_create(_desc_ptr(src), C.byref(h)))
         self._h = h
         self._src = src
 
@@ -375,6 +437,8 @@ class HipScene:
         h = C.c_void_p()
         if isinstance(src, HostScene):
             _check(lib().crt_hip_scene_upload(src.handle, device, C.byref(h)))
+        elif hasattr(src, "tree_desc_ptr"):
+            _check(lib().crt_hip_scene_from_tree(src.tree_desc_ptr(), device, C.byref(h)))
         else:
             flag = {"auto": TREE_AUTO, "host": TREE_HOST, "device": TREE_DEVICE}[tree_build]
             _check(lib().crt_hip_scene_create_ex(_desc_ptr(src), device, flag, C.byref(h)))

@@ -98,6 +98,8 @@ struct HostScene {
 
 /* Mesh prep + (build_tree) the exact tree build and its flattening. */
 int prepare_scene(const crt_scene_desc *desc, HostScene &out, bool build_tree = true);
+/* The reference's built scene (vertices + tree) flattened as it is. */
+int prepare_scene_from_tree(const crt_tree_scene_desc *desc, HostScene &out);
 
 /* Screen-space work estimate: every leaf cell is projected through the camera
  * and its triangle count added to the 8x8 tiles its image overlaps.  Used only

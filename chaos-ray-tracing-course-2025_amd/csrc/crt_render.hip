@@ -2388,6 +2388,14 @@ int crt_hip_scene_create_ex(const crt_scene_desc *desc, int device, int flags, c
     return crt_hip_scene_upload(reinterpret_cast<crt_host_scene *>(hs.get()), device, out);
 }
 
+int crt_hip_scene_from_tree(const crt_tree_scene_desc *desc, int device, crt_hip_scene **out) {
+    if (!desc || !out) return set_error(CRT_E_INVALID, "null argument");
+    std::unique_ptr<HostScene> hs(new HostScene());
+    const int rc = prepare_scene_from_tree(desc, *hs);
+    if (rc != CRT_OK) return rc;
+    return crt_hip_scene_upload(reinterpret_cast<crt_host_scene *>(hs.get()), device, out);
+}
+
 int crt_hip_scene_create(const crt_scene_desc *desc, int device, crt_hip_scene **out) {
     return crt_hip_scene_create_ex(desc, device, CRT_SCENE_TREE_AUTO, out);
 }

@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstring>
 #include <limits>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -260,6 +261,141 @@ void build_pruned_nodes(const std::vector<BuildNode> &bn, HostScene &hs) {
     }
 }
 
+/* textures / materials / lights (crt_json.cpp:375-539, 220-247 as flattened
+ * into crt_scene_desc) */
+int add_shading(HostScene &hs, const crt_texture_desc *textures, int texture_count, const crt_material_desc *materials,
+                int material_count, const crt_light_desc *lights, int light_count) {
+    if ((texture_count > 0 && !textures) || (material_count > 0 && !materials) || (light_count > 0 && !lights))
+        return set_error(CRT_E_INVALID, "null shading arrays");
+    for (int i = 0; i < texture_count; ++i) {
+        const crt_texture_desc &t = textures[i];
+        DTexture x;
+        std::memset(&x, 0, sizeof x);
+        x.type = t.type;
+        x.c0x = t.color0.x; x.c0y = t.color0.y; x.c0z = t.color0.z;
+        x.c1x = t.color1.x; x.c1y = t.color1.y; x.c1z = t.color1.z;
+        x.scalar = t.scalar;
+        if (t.type < CRT_TEXTURE_ALBEDO || t.type > CRT_TEXTURE_BITMAP)
+            return set_error(CRT_E_INVALID, "unknown texture type");
+        if (t.type == CRT_TEXTURE_BITMAP) {
+            if (!t.bitmap_rgb || t.bitmap_width <= 0 || t.bitmap_height <= 0)
+                return set_error(CRT_E_INVALID, "bitmap texture without texels");
+            x.w = t.bitmap_width;
+            x.h = t.bitmap_height;
+            x.texel_offset = (int64_t)hs.texels.size();
+            for (int64_t k = 0; k < (int64_t)t.bitmap_width * t.bitmap_height; ++k)
+                hs.texels.push_back(DVec4{t.bitmap_rgb[3 * k], t.bitmap_rgb[3 * k + 1], t.bitmap_rgb[3 * k + 2], 0.f});
+        }
+        hs.textures.push_back(x);
+    }
+    for (int i = 0; i < material_count; ++i) {
+        const crt_material_desc &m = materials[i];
+        if (m.type < CRT_MATERIAL_DIFFUSE || m.type > CRT_MATERIAL_CONSTANT)
+            return set_error(CRT_E_INVALID, "unknown material type");
+        if (m.type != CRT_MATERIAL_REFRACTIVE && (m.albedo_texture_index < 0 || m.albedo_texture_index >= texture_count))
+            return set_error(CRT_E_INVALID, "material albedo texture index out of range");
+        hs.materials.push_back(DMaterial{m.type, m.albedo_texture_index, m.ior, 0});
+    }
+    for (int i = 0; i < light_count; ++i)
+        hs.lights.push_back(DLight{lights[i].intensity, lights[i].position.x, lights[i].position.y,
+                                   lights[i].position.z});
+
+    return CRT_OK;
+}
+
+/* The built tree (reference numbering) -> ref_* arrays, the traversal-ordered
+ * DNode array with its leaf slots, and the pruned walks' PNode orders. */
+int flatten_tree(const std::vector<BuildNode> &bn, HostScene &hs) {
+    const int32_t n = (int32_t)bn.size();
+
+    hs.ref_bounds.resize((size_t)n * 6);
+    hs.ref_children.resize((size_t)n * 2);
+    hs.ref_leaf_off.resize((size_t)n + 1);
+    hs.ref_depth.resize((size_t)n);
+    hs.ref_leaf_tris.clear();
+    hs.leaf_count = 0;
+    hs.max_depth = 0;
+    hs.max_leaf_size = 0;
+    for (int32_t i = 0; i < n; ++i) {
+        for (int k = 0; k < 3; ++k) {
+            hs.ref_bounds[6 * i + k] = bn[i].bounds.lo[k];
+            hs.ref_bounds[6 * i + 3 + k] = bn[i].bounds.hi[k];
+        }
+        hs.ref_children[2 * i] = bn[i].child[0];
+        hs.ref_children[2 * i + 1] = bn[i].child[1];
+        hs.ref_depth[i] = bn[i].depth;
+        hs.ref_leaf_off[i] = (int64_t)hs.ref_leaf_tris.size();
+        hs.ref_leaf_tris.insert(hs.ref_leaf_tris.end(), bn[i].tris.begin(), bn[i].tris.end());
+        if (!bn[i].tris.empty()) {
+            ++hs.leaf_count;
+            hs.max_leaf_size = std::max(hs.max_leaf_size, (int32_t)bn[i].tris.size());
+        }
+        hs.max_depth = std::max(hs.max_depth, bn[i].depth);
+    }
+    hs.ref_leaf_off[n] = (int64_t)hs.ref_leaf_tris.size();
+
+    /* ---- flatten to traversal order: preorder, child1 before child0 ---- */
+    std::vector<int32_t> order;
+    order.reserve(n);
+    {
+        std::vector<int32_t> st;
+        st.push_back(0);
+        while (!st.empty()) {
+            const int32_t x = st.back();
+            st.pop_back();
+            order.push_back(x);
+            if (bn[x].tris.empty()) {
+                if (bn[x].child[0] != -1) st.push_back(bn[x].child[0]);
+                if (bn[x].child[1] != -1) st.push_back(bn[x].child[1]);
+            }
+        }
+    }
+    std::vector<int32_t> pos(n), subtree(n, 1);
+    for (int32_t k = 0; k < n; ++k) pos[order[k]] = k;
+    for (int32_t k = n - 1; k >= 0; --k) {
+        const int32_t x = order[k];
+        if (bn[x].tris.empty())
+            for (int c = 0; c < 2; ++c)
+                if (bn[x].child[c] != -1) subtree[x] += subtree[bn[x].child[c]];
+    }
+    hs.nodes.resize(n);
+    hs.slots.clear();
+    hs.slot_tri.clear();
+    hs.slot_cull.clear();
+    hs.slots.reserve(hs.ref_leaf_tris.size());
+    for (int32_t k = 0; k < n; ++k) {
+        const int32_t x = order[k];
+        DNode &o = hs.nodes[k];
+        o.lo_x = bn[x].bounds.lo[0]; o.lo_y = bn[x].bounds.lo[1]; o.lo_z = bn[x].bounds.lo[2];
+        o.hi_x = bn[x].bounds.hi[0]; o.hi_y = bn[x].bounds.hi[1]; o.hi_z = bn[x].bounds.hi[2];
+        if (bn[x].tris.empty()) {
+            o.a = k + subtree[x];
+            o.b = -(bn[x].depth + 1);
+        } else {
+            if (bn[x].tris.size() >= (1u << 24) || bn[x].depth > 127)
+                return set_error(CRT_E_UNSUPPORTED, "leaf too large for the node record");
+            o.a = (int32_t)bn[x].tris.size() | (bn[x].depth << 24);
+            o.b = (int32_t)hs.slots.size();
+            for (int32_t t : bn[x].tris) {
+                const DTriAttr &at = hs.tri_attr[t];
+                DTriGeo g;
+                g.v0x = hs.vpos[3 * (size_t)at.i0]; g.v0y = hs.vpos[3 * (size_t)at.i0 + 1]; g.v0z = hs.vpos[3 * (size_t)at.i0 + 2];
+                g.v1x = hs.vpos[3 * (size_t)at.i1]; g.v1y = hs.vpos[3 * (size_t)at.i1 + 1]; g.v1z = hs.vpos[3 * (size_t)at.i1 + 2];
+                g.v2x = hs.vpos[3 * (size_t)at.i2]; g.v2y = hs.vpos[3 * (size_t)at.i2 + 1]; g.v2z = hs.vpos[3 * (size_t)at.i2 + 2];
+                g.nx = hs.face_normal[3 * (size_t)t]; g.ny = hs.face_normal[3 * (size_t)t + 1]; g.nz = hs.face_normal[3 * (size_t)t + 2];
+                hs.slots.push_back(g);
+                hs.slot_tri.push_back(t);
+                hs.slot_cull.push_back(hs.tri_cull[t]);
+            }
+        }
+    }
+    if (hs.slots.size() > (size_t)std::numeric_limits<int32_t>::max())
+        return set_error(CRT_E_UNSUPPORTED, "too many leaf triangle copies");
+    (void)pos;
+    build_pruned_nodes(bn, hs);
+    return CRT_OK;
+}
+
 }  // namespace
 
 int prepare_scene(const crt_scene_desc *d, HostScene &hs, bool build_tree_on_host) {
@@ -288,39 +424,9 @@ int prepare_scene(const crt_scene_desc *d, HostScene &hs, bool build_tree_on_hos
     hs.reflections_on = d->reflections_on != 0;
     hs.refractions_on = d->refractions_on != 0;
 
-    /* textures / materials / lights */
-    for (int i = 0; i < d->texture_count; ++i) {
-        const crt_texture_desc &t = d->textures[i];
-        DTexture x;
-        std::memset(&x, 0, sizeof x);
-        x.type = t.type;
-        x.c0x = t.color0.x; x.c0y = t.color0.y; x.c0z = t.color0.z;
-        x.c1x = t.color1.x; x.c1y = t.color1.y; x.c1z = t.color1.z;
-        x.scalar = t.scalar;
-        if (t.type < CRT_TEXTURE_ALBEDO || t.type > CRT_TEXTURE_BITMAP)
-            return set_error(CRT_E_INVALID, "unknown texture type");
-        if (t.type == CRT_TEXTURE_BITMAP) {
-            if (!t.bitmap_rgb || t.bitmap_width <= 0 || t.bitmap_height <= 0)
-                return set_error(CRT_E_INVALID, "bitmap texture without texels");
-            x.w = t.bitmap_width;
-            x.h = t.bitmap_height;
-            x.texel_offset = (int64_t)hs.texels.size();
-            for (int64_t k = 0; k < (int64_t)t.bitmap_width * t.bitmap_height; ++k)
-                hs.texels.push_back(DVec4{t.bitmap_rgb[3 * k], t.bitmap_rgb[3 * k + 1], t.bitmap_rgb[3 * k + 2], 0.f});
-        }
-        hs.textures.push_back(x);
-    }
-    for (int i = 0; i < d->material_count; ++i) {
-        const crt_material_desc &m = d->materials[i];
-        if (m.type < CRT_MATERIAL_DIFFUSE || m.type > CRT_MATERIAL_CONSTANT)
-            return set_error(CRT_E_INVALID, "unknown material type");
-        if (m.type != CRT_MATERIAL_REFRACTIVE && (m.albedo_texture_index < 0 || m.albedo_texture_index >= d->texture_count))
-            return set_error(CRT_E_INVALID, "material albedo texture index out of range");
-        hs.materials.push_back(DMaterial{m.type, m.albedo_texture_index, m.ior, 0});
-    }
-    for (int i = 0; i < d->light_count; ++i)
-        hs.lights.push_back(DLight{d->lights[i].intensity, d->lights[i].position.x, d->lights[i].position.y,
-                                   d->lights[i].position.z});
+    int rc = add_shading(hs, d->textures, d->texture_count, d->materials, d->material_count, d->lights,
+                         d->light_count);
+    if (rc != CRT_OK) return rc;
 
     /* ---- mesh prep (crt_mesh.cpp:10-73) ---- */
     int64_t nv = 0, nt = 0;
@@ -424,94 +530,120 @@ int prepare_scene(const crt_scene_desc *d, HostScene &hs, bool build_tree_on_hos
     }
     std::vector<BuildNode> bn;
     build_tree(tri_boxes, root, bn);
-    const int32_t n = (int32_t)bn.size();
+    return flatten_tree(bn, hs);
+}
 
-    hs.ref_bounds.resize((size_t)n * 6);
-    hs.ref_children.resize((size_t)n * 2);
-    hs.ref_leaf_off.resize((size_t)n + 1);
-    hs.ref_depth.resize((size_t)n);
-    hs.ref_leaf_tris.clear();
-    hs.leaf_count = 0;
-    hs.max_depth = 0;
-    hs.max_leaf_size = 0;
+/* The reference's built scene (crt_hip_scene_from_tree): vertices after
+ * vertex_array_extend and the tree after acceleration_tree::build are taken as
+ * they are.  Triangles get global ids in order of first appearance over the
+ * leaves in the tree's own numbering (the copies of one triangle share its
+ * vertex triple, material, flags and face normal — crt_acceleration_tree.cpp:
+ * 44-58 copies the Triangle). */
+int prepare_scene_from_tree(const crt_tree_scene_desc *d, HostScene &hs) {
+    if (!d) return set_error(CRT_E_INVALID, "null scene description");
+    if (d->width <= 0 || d->height <= 0) return set_error(CRT_E_INVALID, "image width/height must be positive");
+    if (d->bucket_size <= 0) return set_error(CRT_E_INVALID, "bucket_size must be positive");
+    if (d->material_count < 0 || d->texture_count < 0 || d->light_count < 0 || d->vertex_count < 0 ||
+        d->node_count < 1 || d->node_count >= (int64_t)std::numeric_limits<int32_t>::max())
+        return set_error(CRT_E_INVALID, "bad element count");
+    if ((d->vertex_count > 0 && !d->vertices) || !d->node_bounds || !d->node_children || !d->leaf_offsets)
+        return set_error(CRT_E_INVALID, "null scene arrays");
+    hs.background[0] = d->background_color.x;
+    hs.background[1] = d->background_color.y;
+    hs.background[2] = d->background_color.z;
+    hs.cam_loc[0] = d->camera_location.x;
+    hs.cam_loc[1] = d->camera_location.y;
+    hs.cam_loc[2] = d->camera_location.z;
+    std::memcpy(hs.cam_rot, d->camera_rotation, sizeof hs.cam_rot);
+    hs.width = d->width;
+    hs.height = d->height;
+    /* crt_camera.cpp:23,26-27 on the stored m_fov_radians */
+    hs.fov_radians = d->fov_radians;
+    hs.aspect = float(hs.width) / hs.height;
+    hs.tan_half_fov = std::tan(hs.fov_radians * 0.5f);
+    hs.bucket_size = d->bucket_size;
+    hs.gi_on = d->gi_on != 0;
+    hs.reflections_on = d->reflections_on != 0;
+    hs.refractions_on = d->refractions_on != 0;
+    int rc = add_shading(hs, d->textures, d->texture_count, d->materials, d->material_count, d->lights, d->light_count);
+    if (rc != CRT_OK) return rc;
+
+    const int64_t nv = d->vertex_count;
+    hs.vpos.resize((size_t)nv * 3);
+    hs.vnormal.resize((size_t)nv);
+    hs.vuv.resize((size_t)nv);
+    for (int64_t v = 0; v < nv; ++v) {
+        const float *x = d->vertices + 9 * v;
+        hs.vpos[3 * v] = x[0]; hs.vpos[3 * v + 1] = x[1]; hs.vpos[3 * v + 2] = x[2];
+        hs.vnormal[v] = DVec4{x[3], x[4], x[5], 0.f};
+        hs.vuv[v] = DVec4{x[6], x[7], x[8], 0.f};
+    }
+
+    const int32_t n = (int32_t)d->node_count;
+    if (d->leaf_offsets[0] != 0) return set_error(CRT_E_INVALID, "leaf_offsets[0] must be 0");
+    for (int32_t i = 0; i < n; ++i)
+        if (d->leaf_offsets[i + 1] < d->leaf_offsets[i]) return set_error(CRT_E_INVALID, "leaf_offsets not ascending");
+    const int64_t m = d->leaf_offsets[n];
+    if (m > 0 && !d->leaf_triangles) return set_error(CRT_E_INVALID, "null leaf triangles");
+    std::vector<BuildNode> bn((size_t)n);
+    std::vector<uint8_t> seen((size_t)n, 0);
+    seen[0] = 1;
+    struct Key {
+        int32_t v[3], mat, flags;
+        bool operator<(const Key &o) const {
+            return std::lexicographical_compare(&v[0], &v[0] + 5, &o.v[0], &o.v[0] + 5);
+        }
+    };
+    static_assert(sizeof(Key) == 5 * sizeof(int32_t), "Key must be packed");
+    std::map<Key, int32_t> ids;
     for (int32_t i = 0; i < n; ++i) {
+        BuildNode &b = bn[i];
         for (int k = 0; k < 3; ++k) {
-            hs.ref_bounds[6 * i + k] = bn[i].bounds.lo[k];
-            hs.ref_bounds[6 * i + 3 + k] = bn[i].bounds.hi[k];
+            b.bounds.lo[k] = d->node_bounds[6 * (size_t)i + k];
+            b.bounds.hi[k] = d->node_bounds[6 * (size_t)i + 3 + k];
         }
-        hs.ref_children[2 * i] = bn[i].child[0];
-        hs.ref_children[2 * i + 1] = bn[i].child[1];
-        hs.ref_depth[i] = bn[i].depth;
-        hs.ref_leaf_off[i] = (int64_t)hs.ref_leaf_tris.size();
-        hs.ref_leaf_tris.insert(hs.ref_leaf_tris.end(), bn[i].tris.begin(), bn[i].tris.end());
-        if (!bn[i].tris.empty()) {
-            ++hs.leaf_count;
-            hs.max_leaf_size = std::max(hs.max_leaf_size, (int32_t)bn[i].tris.size());
+        if (!seen[i]) return set_error(CRT_E_INVALID, "tree node unreachable from the root");
+        const int64_t f = d->leaf_offsets[i], e = d->leaf_offsets[i + 1];
+        for (int c = 0; c < 2; ++c) {
+            const int32_t ch = d->node_children[2 * (size_t)i + c];
+            if (ch == -1) continue;
+            if (ch <= i || ch >= n || seen[ch])
+                return set_error(CRT_E_INVALID, "tree children must be numbered after their parent, once");
+            if (f != e) return set_error(CRT_E_INVALID, "a leaf (node with triangles) has children");
+            seen[ch] = 1;
+            b.child[c] = ch;
+            bn[ch].depth = b.depth + 1;
         }
-        hs.max_depth = std::max(hs.max_depth, bn[i].depth);
-    }
-    hs.ref_leaf_off[n] = (int64_t)hs.ref_leaf_tris.size();
-
-    /* ---- flatten to traversal order: preorder, child1 before child0 ---- */
-    std::vector<int32_t> order;
-    order.reserve(n);
-    {
-        std::vector<int32_t> st;
-        st.push_back(0);
-        while (!st.empty()) {
-            const int32_t x = st.back();
-            st.pop_back();
-            order.push_back(x);
-            if (bn[x].tris.empty()) {
-                if (bn[x].child[0] != -1) st.push_back(bn[x].child[0]);
-                if (bn[x].child[1] != -1) st.push_back(bn[x].child[1]);
+        if (f == e && b.child[0] == -1 && b.child[1] == -1 && n > 1)
+            return set_error(CRT_E_INVALID, "interior node without children");
+        for (int64_t k = f; k < e; ++k) {
+            const crt_tree_triangle &t = d->leaf_triangles[k];
+            for (int j = 0; j < 3; ++j)
+                if (t.v[j] < 0 || t.v[j] >= nv) return set_error(CRT_E_INVALID, "triangle vertex index out of range");
+            if (t.material_index < 0 || t.material_index >= d->material_count)
+                return set_error(CRT_E_INVALID, "triangle material index out of range");
+            const Key key{{t.v[0], t.v[1], t.v[2]}, t.material_index, t.flags & 3};
+            auto it = ids.find(key);
+            int32_t id;
+            if (it == ids.end()) {
+                id = (int32_t)hs.tri_attr.size();
+                ids.emplace(key, id);
+                hs.tri_attr.push_back(DTriAttr{t.v[0], t.v[1], t.v[2],
+                                               t.material_index | ((t.flags & 1) ? (int32_t)0x80000000 : 0)});
+                hs.face_normal.insert(hs.face_normal.end(), t.face_normal, t.face_normal + 3);
+                hs.tri_cull.push_back((t.flags & 2) ? 1 : 0);
+            } else {
+                id = it->second;
             }
+            b.tris.push_back(id);
         }
     }
-    std::vector<int32_t> pos(n), subtree(n, 1);
-    for (int32_t k = 0; k < n; ++k) pos[order[k]] = k;
-    for (int32_t k = n - 1; k >= 0; --k) {
-        const int32_t x = order[k];
-        if (bn[x].tris.empty())
-            for (int c = 0; c < 2; ++c)
-                if (bn[x].child[c] != -1) subtree[x] += subtree[bn[x].child[c]];
+    set_prune_origin_max(hs);
+    for (int k = 0; k < 3; ++k) {
+        hs.root_box[k] = bn[0].bounds.lo[k];
+        hs.root_box[3 + k] = bn[0].bounds.hi[k];
     }
-    hs.nodes.resize(n);
-    hs.slots.clear();
-    hs.slot_tri.clear();
-    hs.slot_cull.clear();
-    hs.slots.reserve(hs.ref_leaf_tris.size());
-    for (int32_t k = 0; k < n; ++k) {
-        const int32_t x = order[k];
-        DNode &o = hs.nodes[k];
-        o.lo_x = bn[x].bounds.lo[0]; o.lo_y = bn[x].bounds.lo[1]; o.lo_z = bn[x].bounds.lo[2];
-        o.hi_x = bn[x].bounds.hi[0]; o.hi_y = bn[x].bounds.hi[1]; o.hi_z = bn[x].bounds.hi[2];
-        if (bn[x].tris.empty()) {
-            o.a = k + subtree[x];
-            o.b = -(bn[x].depth + 1);
-        } else {
-            if (bn[x].tris.size() >= (1u << 24) || bn[x].depth > 127)
-                return set_error(CRT_E_UNSUPPORTED, "leaf too large for the node record");
-            o.a = (int32_t)bn[x].tris.size() | (bn[x].depth << 24);
-            o.b = (int32_t)hs.slots.size();
-            for (int32_t t : bn[x].tris) {
-                const DTriAttr &at = hs.tri_attr[t];
-                DTriGeo g;
-                g.v0x = hs.vpos[3 * (size_t)at.i0]; g.v0y = hs.vpos[3 * (size_t)at.i0 + 1]; g.v0z = hs.vpos[3 * (size_t)at.i0 + 2];
-                g.v1x = hs.vpos[3 * (size_t)at.i1]; g.v1y = hs.vpos[3 * (size_t)at.i1 + 1]; g.v1z = hs.vpos[3 * (size_t)at.i1 + 2];
-                g.v2x = hs.vpos[3 * (size_t)at.i2]; g.v2y = hs.vpos[3 * (size_t)at.i2 + 1]; g.v2z = hs.vpos[3 * (size_t)at.i2 + 2];
-                g.nx = hs.face_normal[3 * (size_t)t]; g.ny = hs.face_normal[3 * (size_t)t + 1]; g.nz = hs.face_normal[3 * (size_t)t + 2];
-                hs.slots.push_back(g);
-                hs.slot_tri.push_back(t);
-                hs.slot_cull.push_back(hs.tri_cull[t]);
-            }
-        }
-    }
-    if (hs.slots.size() > (size_t)std::numeric_limits<int32_t>::max())
-        return set_error(CRT_E_UNSUPPORTED, "too many leaf triangle copies");
-    (void)pos;
-    build_pruned_nodes(bn, hs);
-    return CRT_OK;
+    return flatten_tree(bn, hs);
 }
 
 std::vector<float> tile_work_estimate(const HostScene &hs, int tiles_x, int tiles_y) {
@@ -648,6 +780,16 @@ int crt_host_scene_face_normals(const crt_host_scene *h, float *out) {
     if (!h || !out) return set_error(CRT_E_INVALID, "null argument");
     const HostScene &hs = *reinterpret_cast<const HostScene *>(h);
     std::memcpy(out, hs.face_normal.data(), hs.face_normal.size() * sizeof(float));
+    return CRT_OK;
+}
+
+int crt_host_scene_from_tree(const crt_tree_scene_desc *desc, crt_host_scene **out) {
+    if (!out) return set_error(CRT_E_INVALID, "null output");
+    *out = nullptr;
+    std::unique_ptr<HostScene> hs(new HostScene());
+    const int rc = prepare_scene_from_tree(desc, *hs);
+    if (rc != CRT_OK) return rc;
+    *out = reinterpret_cast<crt_host_scene *>(hs.release());
     return CRT_OK;
 }
 

@@ -209,6 +209,57 @@ int  crt_hip_scene_create(const crt_scene_desc *desc, int device, crt_hip_scene 
 #define CRT_SCENE_DEVICE_BUILD_MIN 65536
 int  crt_hip_scene_create_ex(const crt_scene_desc *desc, int device, int flags, crt_hip_scene **out);
 
+/* ---- device scene from the reference's already-built crt::Scene -------
+ * For a caller that holds the reference's own data structures (crt_scene.h:
+ * 18-30): the vertex array after vertex_array_extend (crt_mesh.cpp:32-73)
+ * and the acceleration tree after acceleration_tree::build
+ * (crt_acceleration_tree.cpp:87-106), node for node in its preorder
+ * numbering.  Nothing is rebuilt: the tree, its leaf triangle copies and
+ * their face normals are taken as given and flattened into the device
+ * layout.  Used by the crt::render_image shim (csrc/shim/). */
+
+/* One Triangle copy held by a leaf (crt_triangle.h:19-23): vertex indices
+ * into the vertex array (the reference's Vertex pointers minus the array's
+ * base), its face normal, material and TriangleFlags. */
+typedef struct crt_tree_triangle {
+    int32_t  v[3];
+    float    face_normal[3];
+    int32_t  material_index;
+    int32_t  flags;           /* bit 0 smooth_shading, bit 1 back_face_culling */
+} crt_tree_triangle;
+
+typedef struct crt_tree_scene_desc {
+    crt_vec3 background_color;
+    /* Camera (crt_camera.h:16-21): the stored m_fov_radians, m_transform */
+    crt_vec3 camera_location;
+    float    camera_rotation[9];      /* row-major, Matrix::data */
+    int32_t  width, height;
+    float    fov_radians;
+    int32_t  bucket_size;
+    int32_t  gi_on, reflections_on, refractions_on;
+    /* Scene::vertices: 9 floats per vertex — position, normal, uv (crt_vertex.h:7-11) */
+    const float *vertices;       int64_t vertex_count;
+    /* Scene::acceleration_tree in its own numbering: node_bounds n*6 (min xyz,
+     * max xyz), node_children n*2 (-1 = none), leaf_offsets n+1 into
+     * leaf_triangles (interior nodes: empty ranges) */
+    const float   *node_bounds;
+    const int32_t *node_children;
+    const int64_t *leaf_offsets;
+    const crt_tree_triangle *leaf_triangles;
+    int64_t node_count;
+    /* materials (smooth / culling fields ignored: flags are per triangle here),
+     * textures, lights as in crt_scene_desc */
+    const crt_material_desc *materials; int32_t material_count;
+    const crt_texture_desc  *textures;  int32_t texture_count;
+    const crt_light_desc    *lights;    int32_t light_count;
+} crt_tree_scene_desc;
+
+/* Validates the tree (children numbered after their parent, leaves hold
+ * triangles, interior nodes none; indices in range) and uploads it. */
+int  crt_hip_scene_from_tree(const crt_tree_scene_desc *desc, int device, crt_hip_scene **out);
+/* Host-only part of the same (tree flatten; no GPU). */
+int  crt_host_scene_from_tree(const crt_tree_scene_desc *desc, crt_host_scene **out);
+
 /* The scene's tree in the reference's preorder numbering, as
  * crt_host_scene_tree (sizes from crt_hip_scene_info). */
 int  crt_hip_scene_tree(const crt_hip_scene *scene, float *bounds, int32_t *children, int64_t *leaf_offsets,

@@ -110,6 +110,42 @@ int ref_tree_dump(ref_scene *s, float *bounds, int32_t *children, int64_t *leaf_
     return 0;
 }
 
+int64_t ref_vertex_count(ref_scene *s) { return (int64_t)s->vertices.size(); }
+
+/* Scene::vertices as the reference holds them after vertex_array_extend:
+ * position, normal, uv (crt_vertex.h:7-11), 9 floats per vertex. */
+int ref_vertex_dump(ref_scene *s, float *out) {
+    for (size_t i = 0; i < s->vertices.size(); ++i) {
+        const crt::Vertex &v = s->vertices[i];
+        const float x[9] = {v.position.x, v.position.y, v.position.z, v.normal.x, v.normal.y,
+                            v.normal.z, v.uv.x, v.uv.y, v.uv.z};
+        std::memcpy(out + 9 * i, x, sizeof x);
+    }
+    return 0;
+}
+
+/* The leaves' Triangle copies in tree order (ref_tree_dump's leaf_offsets):
+ * vertex indices = the Vertex pointers minus the array base, the copy's
+ * face_normal, material_index and TriangleFlags (crt_triangle.h:19-23). */
+int ref_leaf_triangles(ref_scene *s, crt_tree_triangle *out) {
+    int64_t k = 0;
+    const crt::Vertex *base = s->vertices.data();
+    for (const crt::AccelerationTreeNode &n : s->tree) {
+        for (const crt::Triangle &t : n.triangles) {
+            crt_tree_triangle &o = out[k++];
+            o.v[0] = (int32_t)(t.v0 - base);
+            o.v[1] = (int32_t)(t.v1 - base);
+            o.v[2] = (int32_t)(t.v2 - base);
+            o.face_normal[0] = t.face_normal.x;
+            o.face_normal[1] = t.face_normal.y;
+            o.face_normal[2] = t.face_normal.z;
+            o.material_index = t.material_index;
+            o.flags = (t.flags.smooth_shading ? 1 : 0) | (t.flags.back_face_culling ? 2 : 0);
+        }
+    }
+    return 0;
+}
+
 int ref_trace(ref_scene *s, const float *rays, int64_t n, crt_hit *hits) {
     for (int64_t i = 0; i < n; ++i) {
         crt::Ray r{};
