@@ -22,8 +22,12 @@ grid (crt_renderer.cpp:160-174) is dealt bucket k -> rank k mod N, each rank
 renders its buckets packed, the packed shards are gathered to rank 0 over RCCL
 (torch.distributed "nccl") and unpacked there, one frame per step; frame k's
 gather runs on RCCL's stream while frame k+1 renders (FramePipeline).
-`--payload u8` gathers write_ppm's 8-bit components (device quantise-and-pack,
-crt_image_ppm.cpp:9-23) instead of fp32 (4x fewer bytes into rank 0).  The
+By default only the LIVE 8x8 tiles travel (`--shards compact`): tiles with a
+pixel whose camera ray passes the reference's root-cell test — every other
+pixel is a miss, i.e. the background, written by the unpack on rank 0
+(lossless; 28% of C2's tiles are live).  `--payload u8` gathers write_ppm's
+8-bit components instead (device quantise-and-pack, crt_image_ppm.cpp:9-23;
+4x fewer bytes again, the PPM the CLI writes).  The
 frame-parallel mode (`frames`, weak scaling: every rank renders whole frames)
 is reported as a secondary field.
 
@@ -96,6 +100,9 @@ def parse(argv=None):
                         "frames = each GPU renders whole frames (weak scaling)")
     p.add_argument("--payload", choices=["f32", "u8"], default="f32",
                    help="tiles mode: gather fp32 RGB (the render_image image) or write_ppm's 8-bit components")
+    p.add_argument("--shards", choices=["compact", "full"], default="compact",
+                   help="tiles mode: gather only the live tiles (camera ray passes the root-cell test; the rest is "
+                        "background by construction — lossless) or every bucket")
     p.add_argument("--no-secondary", action="store_true", help="N>1: skip the secondary frames-mode measurement")
     p.add_argument("--event-every", type=int, default=5,
                    help="bracket every k-th render of the timed region with HIP events (kernel time sample; "
@@ -370,13 +377,15 @@ def main():
             timing["i"] += 1
 
     u8 = a.payload == "u8"
-    stride = gpu.shard_stride(world) if world > 1 else npx * 3
+    compact = a.shards == "compact"
+    stride = (gpu.compact_stride(world) if compact else gpu.shard_stride(world)) if world > 1 else npx * 3
     shard_f32 = torch.empty(stride, dtype=torch.float32, device="cuda")   # u8 payload / host staging scratch
 
     def render_shard(packed):
         # packed: this rank's slot of the gather (device, or host for gloo)
         dst = shard_f32 if (u8 or host_staged) else packed
-        timed(lambda: gpu.render_shard(settings, rank, world, dst.data_ptr(), sptr))
+        rs = gpu.render_shard_compact if compact else gpu.render_shard
+        timed(lambda: rs(settings, rank, world, dst.data_ptr(), sptr))
         if u8:
             tgt = packed if not host_staged else shard_u8
             N.quantize_rgb8(shard_f32.data_ptr(), stride, tgt.data_ptr(), 255, sptr)
@@ -391,9 +400,11 @@ def main():
             src = flat_dev_u8 if u8 else flat_dev
             src.copy_(flat)
         if u8:
-            gpu.unpack_shards_rgb8(world, src.data_ptr(), frame8.data_ptr(), sptr)
+            up = gpu.unpack_compact_rgb8 if compact else gpu.unpack_shards_rgb8
+            up(world, src.data_ptr(), frame8.data_ptr(), sptr)
         else:
-            gpu.unpack_shards(world, src.data_ptr(), frame.data_ptr(), sptr)
+            up = gpu.unpack_compact if compact else gpu.unpack_shards
+            up(world, src.data_ptr(), frame.data_ptr(), sptr)
 
     mode = a.mode if world > 1 else "single"
     if world > 1:
@@ -505,7 +516,7 @@ def main():
             note = "" if (cw, ch) == (W, H) else f" at {cw}x{ch} (same scene and settings; Mrays/s is per-ray work)"
             cpu = cpu_baseline(a.config, cw, ch, a.cpu_seconds, a.cpu_single_seconds, note)
         parallel = {"single": "single-gpu", "tiles": f"bucket-shard{world}+{'rccl' if dist_backend == 'nccl' else dist_backend}"
-                    f"-gather-{a.payload}", "frames": f"frame-parallel{world}"}[mode]
+                    f"-gather-{a.shards}-{a.payload}", "frames": f"frame-parallel{world}"}[mode]
         out = {
             "metric": ("Mrays/sec + frame ms, 1920x1080 scene 14-01" if a.config == "c2"
                        else f"Mrays/sec + frame ms, {W}x{H} {cfg['label']}"),
@@ -528,6 +539,8 @@ def main():
                        "triangle_tests_per_frame": counts["triangle_tests"],
                        "parallelism": parallel, "world_size_initialised": world,
                        "dist_backend": dist_backend, "payload": a.payload if mode == "tiles" else None,
+                       "shards": a.shards if mode == "tiles" else None,
+                       "gather_bytes_per_rank": (stride * (1 if u8 else 4)) if mode == "tiles" else None,
                        "frames_per_step": frames_per_step,
                        "frame_ms": round(ms_per_step, 5), "kernel_ms": round(kern_ms, 5),
                        "e2e_ms": round(e2e, 4) if e2e is not None else None,

@@ -189,6 +189,13 @@ EXPORTS = [
     ("crt_hip_unpack_shards", C.c_int, [_P, C.c_int, _P, _P, _P]),
     ("crt_hip_unpack_shards_rgb8", C.c_int, [_P, C.c_int, _P, _P, _P]),
     ("crt_hip_quantize_rgb8", C.c_int, [_P, C.c_int64, C.c_int32, _P, _P]),
+    ("crt_hip_live_mask", C.c_int, [_P, _P]),
+    ("crt_hip_compact_floats", C.c_int64, [_P, C.c_int, C.c_int]),
+    ("crt_hip_compact_stride", C.c_int64, [_P, C.c_int]),
+    ("crt_hip_render_shard_compact", C.c_int, [_P, C.POINTER(RendererSettings), C.c_int, C.c_int, _P, _P]),
+    ("crt_hip_unpack_compact", C.c_int, [_P, C.c_int, _P, _P, _P]),
+    ("crt_hip_unpack_compact_rgb8", C.c_int, [_P, C.c_int, _P, _P, _P]),
+    ("crt_shard_compact_plan", C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int, C.c_int, _P, _P, C.c_int64]),
     ("crt_shard_plan", C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int, C.c_int, _P, C.c_int64]),
     ("crt_hip_trace_batch", C.c_int, [_P, _P, C.c_int64, _P]),
     ("crt_hip_count_work", C.c_int, [_P, C.POINTER(RendererSettings), C.POINTER(WorkCounts)]),
@@ -515,6 +522,39 @@ class HipScene:
         _check(lib().crt_hip_unpack_shards(self._h, count, C.c_void_p(d_gathered), C.c_void_p(d_rgb),
                                            C.c_void_p(stream or 0)))
 
+    # compact shards: only live tiles (camera ray passes the root-cell test) are
+    # rendered / packed; unpacking writes the background into the others
+    def live_mask(self) -> np.ndarray:
+        info = self.info()
+        out = np.zeros((info["height"], info["width"]), np.uint8)
+        _check(lib().crt_hip_live_mask(self._h, out.ctypes.data))
+        return out
+
+    def compact_floats(self, shard: int, count: int) -> int:
+        v = lib().crt_hip_compact_floats(self._h, shard, count)
+        if v < 0:
+            _check(int(v))
+        return int(v)
+
+    def compact_stride(self, count: int) -> int:
+        v = lib().crt_hip_compact_stride(self._h, count)
+        if v < 0:
+            _check(int(v))
+        return int(v)
+
+    def render_shard_compact(self, settings: RendererSettings, shard: int, count: int, d_packed: int,
+                             stream: int | None = None) -> None:
+        _check(lib().crt_hip_render_shard_compact(self._h, C.byref(settings), shard, count, C.c_void_p(d_packed),
+                                                  C.c_void_p(stream or 0)))
+
+    def unpack_compact(self, count: int, d_gathered: int, d_rgb: int, stream: int | None = None) -> None:
+        _check(lib().crt_hip_unpack_compact(self._h, count, C.c_void_p(d_gathered), C.c_void_p(d_rgb),
+                                            C.c_void_p(stream or 0)))
+
+    def unpack_compact_rgb8(self, count: int, d_gathered: int, d_rgb8: int, stream: int | None = None) -> None:
+        _check(lib().crt_hip_unpack_compact_rgb8(self._h, count, C.c_void_p(d_gathered), C.c_void_p(d_rgb8),
+                                                 C.c_void_p(stream or 0)))
+
     def unpack_shards_rgb8(self, count: int, d_gathered: int, d_rgb8: int, stream: int | None = None) -> None:
         _check(lib().crt_hip_unpack_shards_rgb8(self._h, count, C.c_void_p(d_gathered), C.c_void_p(d_rgb8),
                                                 C.c_void_p(stream or 0)))
@@ -596,6 +636,24 @@ def quantize_rgb8(d_rgb: int, n: int, d_out: int, max_color_component: int = 255
     (crt_hip_quantize_rgb8, current device, `stream` or the null stream)."""
     _check(lib().crt_hip_quantize_rgb8(C.c_void_p(d_rgb), n, max_color_component, C.c_void_p(d_out),
                                        C.c_void_p(stream or 0)))
+
+
+def shard_compact_plan(width: int, height: int, bucket_size: int, shard: int, shard_count: int,
+                       live_mask: np.ndarray | None) -> np.ndarray:
+    """Live tiles of one shard for a live-pixel mask (H x W bytes; None = all
+    live): int64 [k, 5] = (x, y, w, h, packed_pixel_offset)."""
+    m = None
+    if live_mask is not None:
+        live_mask = np.ascontiguousarray(live_mask, np.uint8)
+        assert live_mask.shape == (height, width)
+        m = live_mask.ctypes.data
+    n = lib().crt_shard_compact_plan(width, height, bucket_size, shard, shard_count, m, None, 0)
+    if n < 0:
+        _check(int(n))
+    out = np.zeros((n, 5), np.int64)
+    if n:
+        lib().crt_shard_compact_plan(width, height, bucket_size, shard, shard_count, m, out.ctypes.data, n)
+    return out
 
 
 def write_ppm(path: str | os.PathLike, rgb: np.ndarray, max_color_component: int = 255) -> None:

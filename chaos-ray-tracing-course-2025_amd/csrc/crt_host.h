@@ -112,4 +112,10 @@ std::vector<float> tile_work_estimate(const HostScene &hs, int tiles_x, int tile
 std::vector<DBucket> shard_buckets(int32_t width, int32_t height, int32_t bucket_size, int shard,
                                    int shard_count, int64_t *packed_pixels);
 
+/* The shard's buckets cut into 8x8 tiles from each bucket origin, keeping the
+ * tiles with a live pixel (live: W*H bytes, null = all live), packed in order;
+ * the other tiles are appended to *dead (packed_offset -1) when given. */
+std::vector<DBucket> shard_live_tiles(int32_t width, int32_t height, int32_t bucket_size, int shard, int shard_count,
+                                      const uint8_t *live, int64_t *packed_pixels, std::vector<DBucket> *dead);
+
 }  // namespace crt_amd

@@ -1479,18 +1479,47 @@ __global__ __launch_bounds__(256) void k_trace_rays(DeviceScene s, const float *
 /* Scatter gathered shard buffers back into the row-major frame (fp32 RGB or
  * the quantised 8-bit RGB of k_quantize). */
 template <class T>
+struct Rgb { T c[3]; };
+
+template <class T>
 __global__ __launch_bounds__(256) void k_unpack(const UnpackBucket *__restrict__ buckets, const T *__restrict__ src,
-                                                T *__restrict__ dst, int width) {
+                                                T *__restrict__ dst, int width, Rgb<T> bg) {
     const UnpackBucket b = buckets[blockIdx.x];
     const int npx = b.w * b.h;
     for (int p = (int)threadIdx.x; p < npx; p += (int)blockDim.x) {
         const int lx = p % b.w, ly = p / b.w;
-        const T *s = src + b.src + 3 * (int64_t)p;
         T *d = dst + 3 * ((int64_t)(b.y + ly) * width + (b.x + lx));
-        d[0] = s[0];
-        d[1] = s[1];
-        d[2] = s[2];
+        if (b.src < 0) {   /* dead tile of a compact shard: the background (shade_ray's miss colour) */
+            d[0] = bg.c[0];
+            d[1] = bg.c[1];
+            d[2] = bg.c[2];
+        } else {
+            const T *s = src + b.src + 3 * (int64_t)p;
+            d[0] = s[0];
+            d[1] = s[1];
+            d[2] = s[2];
+        }
     }
+}
+
+/* Live pixels for the compact shards: the camera ray passes the reference's
+ * six-face test on the root cell (crt_intersection.cpp:14-45, node 0 popped
+ * first, :114-121).  A ray that fails it is a miss, i.e. shade_ray returns the
+ * background colour (crt_renderer.cpp:142-144) — so dead pixels need neither
+ * rendering nor transport. */
+__global__ __launch_bounds__(256) void k_live_pixels(const DeviceScene *__restrict__ scene, uint8_t *__restrict__ live) {
+    const DeviceScene &s = *scene;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)s.width * s.height) return;
+    const int x = (int)(i % s.width), y = (int)(i / s.width);
+    Vec o, d;
+    camera_ray(s, x, y, o, d);
+    bool hit = false;
+    if (s.node_count > 0) {
+        const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
+        hit = box_hit_r(o, d, rr, load_global(s.nodes, 0));
+    }
+    live[i] = hit ? 1 : 0;
 }
 
 /* write_ppm's per-component conversion (crt_image_ppm.cpp:15-18):
@@ -1608,6 +1637,11 @@ struct crt_hip_scene {
     ShardPlan full;
     std::map<std::pair<int, int>, ShardPlan> shard_plans;
     std::map<int, std::pair<UnpackBucket *, int>> unpack_plans;
+    /* compact shards (crt_hip_*_compact): live-pixel mask of the frame (host),
+     * per-(shard, count) render plans, per-count unpack lists */
+    std::vector<uint8_t> live_mask;
+    std::map<std::pair<int, int>, ShardPlan> compact_plans;
+    std::map<int, std::pair<UnpackBucket *, int>> compact_unpack;
     float *d_out = nullptr;
     unsigned long long *d_counters = nullptr;
     int32_t *d_next_px = nullptr;      /* pixel-refill list head (k_render_refill) */
@@ -1881,6 +1915,7 @@ void free_plans(crt_hip_scene *sc) {
     sc->plan_allocs.clear();
     sc->full = ShardPlan{};
     sc->shard_plans.clear();
+    sc->compact_plans.clear();
 }
 
 /* powf(x, 5.0f) for x = k * 2^-24, k = -2^24 .. 2^24 (fresnel_of), computed
@@ -2436,6 +2471,7 @@ void crt_hip_scene_destroy(crt_hip_scene *sc) {
     if (sc->d_out) (void)hipFree(sc->d_out);
     wf_free(sc->wf);
     for (auto &kv : sc->unpack_plans) (void)hipFree(kv.second.first);
+    for (auto &kv : sc->compact_unpack) (void)hipFree(kv.second.first);
     if (sc->ev_start) (void)hipEventDestroy(sc->ev_start);
     if (sc->ev_stop) (void)hipEventDestroy(sc->ev_stop);
     if (sc->stream) (void)hipStreamDestroy(sc->stream);
@@ -2501,8 +2537,38 @@ int64_t crt_hip_shard_stride(const crt_hip_scene *sc, int shard_count) {
     return (m + 63) / 64 * 64;
 }
 
-int crt_hip_render_shard(crt_hip_scene *sc, const crt_renderer_settings *st, int shard, int shard_count,
-                         float *d_packed, void *stream) {
+}  // extern "C"
+
+namespace {
+
+/* The frame's live-pixel mask (k_live_pixels), computed once per scene. */
+int ensure_live_mask(crt_hip_scene *sc) {
+    if (!sc->live_mask.empty() || sc->grid_empty) return CRT_OK;
+    const DeviceScene *d_scene = nullptr;
+    int rc = sync_device_record(sc, &d_scene);
+    if (rc != CRT_OK) return rc;
+    const int64_t npx = (int64_t)sc->info.width * sc->info.height;
+    uint8_t *d = nullptr;
+    HIP_TRY(hipMalloc(&d, (size_t)npx));
+    hipLaunchKernelGGL(k_live_pixels, dim3((unsigned)((npx + 255) / 256)), dim3(256), 0, sc->stream, d_scene, d);
+    hipError_t e = hipGetLastError();
+    std::vector<uint8_t> m((size_t)npx);
+    if (e == hipSuccess) e = hipMemcpyAsync(m.data(), d, (size_t)npx, hipMemcpyDeviceToHost, sc->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(sc->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return set_error(CRT_E_HIP, std::string("live mask: ") + hipGetErrorString(e));
+    sc->live_mask.swap(m);
+    return CRT_OK;
+}
+
+std::vector<DBucket> compact_tiles(crt_hip_scene *sc, int shard, int shard_count, int64_t *px,
+                                   std::vector<DBucket> *dead = nullptr) {
+    return shard_live_tiles(sc->info.width, sc->info.height, sc->info.bucket_size, shard, shard_count,
+                            sc->live_mask.empty() ? nullptr : sc->live_mask.data(), px, dead);
+}
+
+int render_shard_t(crt_hip_scene *sc, const crt_renderer_settings *st, int shard, int shard_count, float *d_packed,
+                   void *stream, bool compact) {
     if (!sc || !d_packed) return set_error(CRT_E_INVALID, "null argument");
     if (shard_count <= 0 || shard < 0 || shard >= shard_count) return set_error(CRT_E_INVALID, "bad shard");
     int rc = check_settings(st);
@@ -2510,15 +2576,18 @@ int crt_hip_render_shard(crt_hip_scene *sc, const crt_renderer_settings *st, int
     HIP_TRY(hipSetDevice(sc->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : sc->stream;
     if ((rc = ensure_plans(sc, st, s)) != CRT_OK) return rc;
+    if (compact && (rc = ensure_live_mask(sc)) != CRT_OK) return rc;
+    auto &plans = compact ? sc->compact_plans : sc->shard_plans;
     auto key = std::make_pair(shard, shard_count);
-    auto it = sc->shard_plans.find(key);
-    if (it == sc->shard_plans.end()) {
+    auto it = plans.find(key);
+    if (it == plans.end()) {
         int64_t px = 0;
-        const std::vector<DBucket> b = shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size, shard,
-                                                     shard_count, &px);
+        const std::vector<DBucket> b = compact ? compact_tiles(sc, shard, shard_count, &px)
+                                               : shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size,
+                                                               shard, shard_count, &px);
         ShardPlan plan;
         if ((rc = make_tile_plan(sc, b, false, plan)) != CRT_OK) return rc;
-        it = sc->shard_plans.emplace(key, plan).first;
+        it = plans.emplace(key, plan).first;
     }
     if (sc->record_events) HIP_TRY(hipEventRecord(sc->ev_start, s));
     rc = launch_render(sc, st, it->second, d_packed, s, false);
@@ -2528,36 +2597,54 @@ int crt_hip_render_shard(crt_hip_scene *sc, const crt_renderer_settings *st, int
     return CRT_OK;
 }
 
-}  // extern "C"
+/* write_ppm's conversion of one component on the host (k_quantize). */
+uint8_t quantize_host(float c) {
+    const float x = c * 255.0f;
+    int v = (x >= -2147483648.0f && x < 2147483648.0f) ? (int)x : (int)0x80000000;
+    return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
 
-namespace {
 template <class T>
-int unpack_shards_t(crt_hip_scene *sc, int shard_count, const T *d_gathered, T *d_rgb, void *stream) {
+int unpack_shards_t(crt_hip_scene *sc, int shard_count, const T *d_gathered, T *d_rgb, void *stream, bool compact) {
     if (!sc || !d_gathered || !d_rgb || shard_count <= 0) return set_error(CRT_E_INVALID, "bad argument");
     HIP_TRY(hipSetDevice(sc->device));
-    auto it = sc->unpack_plans.find(shard_count);
-    if (it == sc->unpack_plans.end()) {
-        const int64_t stride = crt_hip_shard_stride(sc, shard_count);
+    if (compact) {
+        const int rc = ensure_live_mask(sc);
+        if (rc != CRT_OK) return rc;
+    }
+    auto &plans = compact ? sc->compact_unpack : sc->unpack_plans;
+    auto it = plans.find(shard_count);
+    if (it == plans.end()) {
+        const int64_t stride = compact ? crt_hip_compact_stride(sc, shard_count) : crt_hip_shard_stride(sc, shard_count);
+        if (stride < 0) return (int)stride;
         std::vector<UnpackBucket> ub;
+        std::vector<DBucket> dead;
         for (int s = 0; s < shard_count; ++s) {
             int64_t px = 0;
-            for (const DBucket &b : shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size, s,
-                                                  shard_count, &px))
-                ub.push_back(UnpackBucket{b.x, b.y, b.w, b.h, s * stride + 3 * b.packed_offset, 0});
+            const std::vector<DBucket> b = compact ? compact_tiles(sc, s, shard_count, &px, &dead)
+                                                   : shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size,
+                                                                   s, shard_count, &px);
+            for (const DBucket &x : b) ub.push_back(UnpackBucket{x.x, x.y, x.w, x.h, s * stride + 3 * x.packed_offset, 0});
         }
+        for (const DBucket &x : dead) ub.push_back(UnpackBucket{x.x, x.y, x.w, x.h, -1, 0});
         UnpackBucket *d = nullptr;
         if (!ub.empty()) {
             HIP_TRY(hipMalloc(&d, ub.size() * sizeof(UnpackBucket)));
             HIP_TRY(hipMemcpy(d, ub.data(), ub.size() * sizeof(UnpackBucket), hipMemcpyHostToDevice));
         }
-        it = sc->unpack_plans.emplace(shard_count, std::make_pair(d, (int)ub.size())).first;
+        it = plans.emplace(shard_count, std::make_pair(d, (int)ub.size())).first;
     }
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : sc->stream;
     if (sc->grid_empty)
         HIP_TRY(hipMemsetAsync(d_rgb, 0, (size_t)sc->info.width * sc->info.height * 3 * sizeof(T), s));
     if (it->second.second > 0) {
+        Rgb<T> bg;
+        for (int k = 0; k < 3; ++k) {
+            if constexpr (sizeof(T) == 1) bg.c[k] = quantize_host(sc->ds.background[k]);
+            else bg.c[k] = sc->ds.background[k];
+        }
         hipLaunchKernelGGL(k_unpack<T>, dim3(it->second.second), dim3(256), 0, s, it->second.first, d_gathered, d_rgb,
-                           sc->info.width);
+                           sc->info.width, bg);
         HIP_TRY(hipGetLastError());
     }
     return CRT_OK;
@@ -2566,13 +2653,63 @@ int unpack_shards_t(crt_hip_scene *sc, int shard_count, const T *d_gathered, T *
 
 extern "C" {
 
+int crt_hip_render_shard(crt_hip_scene *sc, const crt_renderer_settings *st, int shard, int shard_count,
+                         float *d_packed, void *stream) {
+    return render_shard_t(sc, st, shard, shard_count, d_packed, stream, false);
+}
+
 int crt_hip_unpack_shards(crt_hip_scene *sc, int shard_count, const float *d_gathered, float *d_rgb, void *stream) {
-    return unpack_shards_t<float>(sc, shard_count, d_gathered, d_rgb, stream);
+    return unpack_shards_t<float>(sc, shard_count, d_gathered, d_rgb, stream, false);
 }
 
 int crt_hip_unpack_shards_rgb8(crt_hip_scene *sc, int shard_count, const uint8_t *d_gathered, uint8_t *d_rgb8,
                                void *stream) {
-    return unpack_shards_t<uint8_t>(sc, shard_count, d_gathered, d_rgb8, stream);
+    return unpack_shards_t<uint8_t>(sc, shard_count, d_gathered, d_rgb8, stream, false);
+}
+
+int crt_hip_live_mask(crt_hip_scene *sc, uint8_t *out) {
+    if (!sc) return set_error(CRT_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(sc->device));
+    const int rc = ensure_live_mask(sc);
+    if (rc != CRT_OK) return rc;
+    if (out && !sc->live_mask.empty()) std::memcpy(out, sc->live_mask.data(), sc->live_mask.size());
+    else if (out) std::memset(out, 0, (size_t)sc->info.width * sc->info.height);
+    return CRT_OK;
+}
+
+int64_t crt_hip_compact_floats(crt_hip_scene *sc, int shard, int shard_count) {
+    if (!sc || shard_count <= 0 || shard < 0 || shard >= shard_count) return set_error(CRT_E_INVALID, "bad shard");
+    HIP_TRY(hipSetDevice(sc->device));
+    const int rc = ensure_live_mask(sc);
+    if (rc != CRT_OK) return rc;
+    int64_t px = 0;
+    compact_tiles(sc, shard, shard_count, &px);
+    return 3 * px;
+}
+
+int64_t crt_hip_compact_stride(crt_hip_scene *sc, int shard_count) {
+    if (!sc || shard_count <= 0) return set_error(CRT_E_INVALID, "bad shard count");
+    int64_t m = 0;
+    for (int s = 0; s < shard_count; ++s) {
+        const int64_t f = crt_hip_compact_floats(sc, s, shard_count);
+        if (f < 0) return f;
+        m = std::max(m, f);
+    }
+    return std::max<int64_t>(64, (m + 63) / 64 * 64);
+}
+
+int crt_hip_render_shard_compact(crt_hip_scene *sc, const crt_renderer_settings *st, int shard, int shard_count,
+                                 float *d_packed, void *stream) {
+    return render_shard_t(sc, st, shard, shard_count, d_packed, stream, true);
+}
+
+int crt_hip_unpack_compact(crt_hip_scene *sc, int shard_count, const float *d_gathered, float *d_rgb, void *stream) {
+    return unpack_shards_t<float>(sc, shard_count, d_gathered, d_rgb, stream, true);
+}
+
+int crt_hip_unpack_compact_rgb8(crt_hip_scene *sc, int shard_count, const uint8_t *d_gathered, uint8_t *d_rgb8,
+                                void *stream) {
+    return unpack_shards_t<uint8_t>(sc, shard_count, d_gathered, d_rgb8, stream, true);
 }
 
 int crt_hip_quantize_rgb8(const float *d_rgb, int64_t n, int32_t max_color_component, uint8_t *d_out, void *stream) {

@@ -707,6 +707,33 @@ std::vector<DBucket> shard_buckets(int32_t width, int32_t height, int32_t bucket
     return out;
 }
 
+/* Live tiles of a shard: each bucket of the shard cut into 8x8 tiles from the
+ * bucket's origin (the render plan's own tiling), kept when some pixel of the
+ * tile is live (mask null: all live), packed back to back.  Dead tiles are the
+ * frame's background by construction (see crt_hip_compact_*). */
+std::vector<DBucket> shard_live_tiles(int32_t width, int32_t height, int32_t bucket_size, int shard, int shard_count,
+                                      const uint8_t *live, int64_t *packed_pixels, std::vector<DBucket> *dead) {
+    std::vector<DBucket> out;
+    int64_t px = 0, off = 0;
+    for (const DBucket &b : shard_buckets(width, height, bucket_size, shard, shard_count, &px)) {
+        for (int ty = 0; ty < b.h; ty += 8)
+            for (int tx = 0; tx < b.w; tx += 8) {
+                const int x = b.x + tx, y = b.y + ty, w = std::min(8, b.w - tx), h = std::min(8, b.h - ty);
+                bool any = live == nullptr;
+                for (int yy = 0; yy < h && !any; ++yy)
+                    for (int xx = 0; xx < w && !any; ++xx) any = live[(size_t)(y + yy) * width + x + xx] != 0;
+                if (any) {
+                    out.push_back(DBucket{x, y, w, h, off});
+                    off += (int64_t)w * h;
+                } else if (dead) {
+                    dead->push_back(DBucket{x, y, w, h, -1});
+                }
+            }
+    }
+    if (packed_pixels) *packed_pixels = off;
+    return out;
+}
+
 }  // namespace crt_amd
 
 using namespace crt_amd;
@@ -794,6 +821,20 @@ int crt_host_scene_from_tree(const crt_tree_scene_desc *desc, crt_host_scene **o
 }
 
 void crt_host_scene_destroy(crt_host_scene *h) { delete reinterpret_cast<HostScene *>(h); }
+
+int64_t crt_shard_compact_plan(int32_t width, int32_t height, int32_t bucket_size, int shard, int shard_count,
+                               const uint8_t *live_mask, int64_t *tiles_out, int64_t cap) {
+    if (width <= 0 || height <= 0 || bucket_size <= 0 || shard_count <= 0 || shard < 0 || shard >= shard_count)
+        return set_error(CRT_E_INVALID, "bad shard plan arguments");
+    int64_t px = 0;
+    const std::vector<DBucket> t = shard_live_tiles(width, height, bucket_size, shard, shard_count, live_mask, &px,
+                                                    nullptr);
+    for (size_t i = 0; i < t.size() && (int64_t)i < cap && tiles_out; ++i) {
+        int64_t *o = tiles_out + 5 * i;
+        o[0] = t[i].x; o[1] = t[i].y; o[2] = t[i].w; o[3] = t[i].h; o[4] = t[i].packed_offset;
+    }
+    return (int64_t)t.size();
+}
 
 int64_t crt_shard_plan(int32_t width, int32_t height, int32_t bucket_size, int shard, int shard_count,
                        int64_t *buckets_out, int64_t cap) {

@@ -139,3 +139,83 @@ def test_frame_pipeline_keeps_frames_apart(tmp_path, oracle):
     assert got.shape == (frames, H, W, 3)
     for k in range(frames):
         assert np.array_equal(bits(got[k]), bits(want * np.float32(k + 1)))
+
+
+def _compact_worker(rank, world, port, W, H, out_path):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path.insert(0, str(root / "chaos-ray-tracing-course-2025_amd"))
+    sys.path.insert(0, str(root))
+    import torch
+    import torch.distributed as dist
+    from crt_amd.distributed import FramePipeline, unpack_compact_numpy
+    from crt_amd.native import RendererSettings, shard_compact_plan
+    from crt_amd.scene_npz import load_npz
+    from oracle import pyoracle
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    sc = load_npz(root / "tests/golden/scenes/14-01-acceleration-tree__scene1.npz").set_resolution(W, H)
+    d = sc.desc()
+    bucket = d.bucket_size
+    orc = pyoracle.OracleScene(sc)
+    # any mask whose dead pixels are misses is lossless; on the GPU it is the
+    # root-cell test (crt_hip_live_mask), here the oracle's own hit/miss
+    ys, xs = np.mgrid[0:H, 0:W]
+    hits, _, _ = orc.trace(orc.camera_rays(np.stack([xs.ravel(), ys.ravel()], 1)))
+    mask = hits["hit"].reshape(H, W).astype(np.uint8)
+    plans = [shard_compact_plan(W, H, bucket, s, world, mask) for s in range(world)]
+    stride = max(64, max(3 * int((p[:, 2] * p[:, 3]).sum()) for p in plans))
+    st = RendererSettings.default()
+
+    def render(packed):
+        a = packed.numpy()
+        for x, y, w, h, off in plans[rank]:
+            for row in range(h):
+                a[3 * (off + row * w): 3 * (off + (row + 1) * w)] = orc.render_pixels(st, (y + row) * W + x, w).reshape(-1)
+
+    out = []
+    bg = (d.background_color.x, d.background_color.y, d.background_color.z)
+    pipe = FramePipeline(rank, world, stride, lambda n: torch.zeros(n, dtype=torch.float32), render,
+                         lambda flat: out.append(unpack_compact_numpy(flat.numpy(), W, H, bucket, world, stride, mask,
+                                                                      bg)), dist)
+    pipe.step()
+    pipe.drain()
+    if rank == 0:
+        np.save(out_path, out[0])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_compact_sharded_frame_equals_single_render(tmp_path, oracle):
+    """Compact shards over gloo (world 3): only live tiles are packed and
+    gathered, the unpack fills the rest with the background — the frame equals
+    the oracle's single render bit for bit, and the live plans partition the
+    live part of every shard's buckets."""
+    import torch.multiprocessing as mp
+    from crt_amd.native import RendererSettings
+    from conftest import bits, scene_npz
+    W, H, world = 150, 90, 3
+    out = tmp_path / "frame.npy"
+    mp.spawn(_compact_worker, args=(world, free_port(), W, H, str(out)), nprocs=world, join=True)
+    want = oracle.OracleScene(scene_npz("14-01-acceleration-tree__scene1").set_resolution(W, H)).render(
+        RendererSettings.default())
+    assert np.array_equal(bits(np.load(out)), bits(want))
+
+
+def test_compact_plan_covers_live_pixels():
+    from crt_amd.native import shard_compact_plan, shard_plan
+    rng = np.random.default_rng(5)
+    for W, H, b, world in [(333, 200, 24, 3), (100, 60, 20, 5), (64, 64, 24, 2)]:
+        mask = (rng.random((H, W)) < 0.02).astype(np.uint8)
+        cover = np.zeros((H, W), np.int32)
+        for s in range(world):
+            p = shard_compact_plan(W, H, b, s, world, mask)
+            packed = 0
+            for x, y, w, h, off in p:
+                assert off == packed and w <= 8 and h <= 8 and mask[y:y + h, x:x + w].any()
+                packed += w * h
+                cover[y:y + h, x:x + w] += 1
+            full = shard_compact_plan(W, H, b, s, world, None)          # no mask: every tile of the buckets
+            assert int((full[:, 2] * full[:, 3]).sum()) == int((shard_plan(W, H, b, s, world)[:, 2:4].prod(1)).sum())
+        assert (cover <= 1).all() and (cover[mask == 1] == 1).all()

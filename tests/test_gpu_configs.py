@@ -181,3 +181,50 @@ def test_shard_rgb8_pack_and_unpack(N, devbuf, shards):
     gpu.unpack_shards_rgb8(shards, gathered, frame8)
     out = devbuf.download(frame8, full.shape, np.uint8)
     assert np.array_equal(out, ppm_quantize(full))
+
+
+COMPACT_CASES = [
+    ("14-01-acceleration-tree__scene1", 1920, 1080, {}, None, [1, 2, 8]),
+    ("14-01-acceleration-tree__scene1", 333, 200, {}, 20, [3]),        # bucket grid off the 8x8 grid
+    ("11-01-refractive__scene8", 240, 135, {"max_ray_depth": 8}, None, [2, 3]),
+    ("15-01-conclusion__scene2", 70, 45, {}, None, [2]),                # GI, camera inside the root cell
+]
+
+
+@pytest.mark.parametrize("name,w,h,over,bucket,shards",
+                         [(n, w, h, o, b, k) for n, w, h, o, b, ks in COMPACT_CASES for k in ks])
+def test_compact_shards_lossless(N, devbuf, name, w, h, over, bucket, shards):
+    """Compact shards (only live tiles rendered and gathered; unpack writes the
+    background elsewhere) reproduce the full frame bit for bit, in fp32 and as
+    write_ppm bytes; the live mask only drops pixels whose ray misses."""
+    sc = scene_npz(name).set_resolution(w, h)
+    if bucket:
+        sc.set_settings(bucket_size=bucket)
+    gpu = N.HipScene(sc)
+    st = N.RendererSettings.default(**over)
+    full = gpu.render(st)
+    mask = gpu.live_mask()
+    stride = gpu.compact_stride(shards)
+    assert stride <= gpu.shard_stride(shards) + 64
+    gathered = devbuf.alloc(4 * stride * shards)
+    g8 = devbuf.alloc(stride * shards)
+    frame = devbuf.alloc(full.nbytes)
+    frame8 = devbuf.alloc(full.size)
+    for s in range(shards):
+        assert gpu.compact_floats(s, shards) <= stride
+        gpu.render_shard_compact(st, s, shards, gathered + 4 * s * stride)
+        devbuf.sync()
+        N.quantize_rgb8(gathered + 4 * s * stride, stride, g8 + s * stride, 255)
+        devbuf.sync()
+    gpu.unpack_compact(shards, gathered, frame)
+    gpu.unpack_compact_rgb8(shards, g8, frame8)
+    out = devbuf.download(frame, full.shape, np.float32)
+    assert np.array_equal(bits(out), bits(full))
+    assert np.array_equal(devbuf.download(frame8, full.shape, np.uint8), ppm_quantize(full))
+    # dead pixels are misses: exactly the background colour
+    bg = np.array([sc.desc().background_color.x, sc.desc().background_color.y, sc.desc().background_color.z],
+                  np.float32)
+    assert np.array_equal(bits(full[mask == 0]), bits(np.broadcast_to(bg, full[mask == 0].shape)))
+    if name.startswith("14-01") and w == 1920:
+        frac = float(mask.mean())
+        assert 0.15 < frac < 0.4, frac     # the dragon's root cell covers ~28% of the C2 frame
