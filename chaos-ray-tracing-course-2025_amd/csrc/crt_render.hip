@@ -82,6 +82,7 @@ struct LaneCounts {
     uint32_t traversals, nodes, tris, hits;
     /* wave-uniform steps of the packet walks (kept by every lane, added once per wave) */
     uint32_t wave_nodes, wave_tris, wave_edges;
+    uint32_t wave_box, wave_pass;   /* packet walks: node steps with a box test run / with a lane passing */
 };
 
 /* ---------------------------------------------------------------------- */
@@ -470,6 +471,7 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
         if (COUNT) ++c.wave_nodes;
         bool pass = false;
         if (__ballot(alive) != 0ull) {
+            if (COUNT) ++c.wave_box;
             pass = alive & box_hit_fast(o, d, rr, cell_of(cur));
             if (!FAST && __ballot(alive & !rr.fast) != 0ull) {
                 if (alive & !rr.fast) pass = box_hit_slow(o, d, cell_of(cur));
@@ -477,6 +479,7 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
             if (COUNT && alive) ++c.nodes;
         }
         const unsigned long long pm = __ballot(pass);
+        if (COUNT && pm != 0ull) ++c.wave_pass;
         if (interior) {
             if (pm != 0ull) {
                 const unsigned long long bit = 2ull << depth;
@@ -489,7 +492,11 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
             }
             continue;
         }
+#if defined(CRT_AB_NOTRI) && (CRT_AB_NOTRI & 2)   /* timing experiments only: no triangle phase (wrong image) */
+        if (false) {
+#else
         if (pm != 0ull) {
+#endif
             const int first = cur.b, cnt = pnode_leaf_count(cur);
             DTriGeo g = load_scalar(s.slots, first);
             uint32_t cw = load_scalar(s.slot_cull_bits, first >> 5);
@@ -609,7 +616,7 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
         }
         if (COUNT) {
             if (my_in & alive) ++c.nodes;
-            ++c.wave_nodes;
+            c.wave_nodes += (uint32_t)kk;     /* node records of the window */
         }
         const bool enter = my_in & pass;
         const unsigned long long E = __ballot(enter);
@@ -620,7 +627,11 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
         /* triangles of the entered leaves, one leaf per lane (next triangle
          * prefetched), then a per-ray merge over the ray's K lanes */
         const bool leaf = enter & !interior;
+#if defined(CRT_AB_NOTRI) && (CRT_AB_NOTRI & 1)   /* timing experiments only: no triangle phase (wrong image) */
+        if (false) {
+#else
         if (__ballot(leaf) != 0ull) {
+#endif
             float lt = best_t;
             int ls = best;
             if (leaf) {
@@ -788,6 +799,9 @@ __device__ __forceinline__ float fresnel_of(const DeviceScene &s, float dot) {
  * operations as shade_pixel<false>. */
 __device__ __forceinline__ Vec shade_primary(const DeviceScene &s, const DSettings &st, Vec o, Vec d, int slot, float t) {
     if (slot < 0) return vec(s.background[0], s.background[1], s.background[2]);
+#ifdef CRT_AB_NOSHADE   /* timing experiments only: the walk without the shading cost (wrong image) */
+    return vec(t, (float)slot, 0.0f);
+#endif
     HitRec h;
     make_hit(s, o, d, t, slot, h);
     const DMaterial m = s.materials[h.mat];
@@ -1006,6 +1020,9 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
         /* tiles of <= 16 rays (the measured plan's splits of heavy tiles): window walk */
         const int tw = uniform_i(tl.w), th = uniform_i(tl.h);
         const int npx = tw * th;
+#if defined(CRT_AB_ONLY)   /* timing experiments only: 1 = window tiles alone, 2 = 8x8 tiles alone */
+        if ((CRT_AB_ONLY == 1) != (npx <= 16)) return;
+#endif
         if (npx <= 16) {
             const int R = npx <= 4 ? 4 : 16;
             const int r = lane & (R - 1), sl = lane / R;
@@ -1013,7 +1030,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             const int px = act ? r % tw : 0, py = act ? r / tw : 0;
             Vec o, d;
             camera_ray(s, tl.x + px, tl.y + py, o, d);
-            LaneCounts cw = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+            LaneCounts cw = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
             float t;
             const int slot = trace_window<COUNT>(s, R, r, sl, act, o, d, t, cw);
             if (act && sl == 0) {
@@ -1034,18 +1051,24 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
                     atomicAdd(&counters[5], (unsigned long long)cw.wave_tris);
                     atomicAdd(&counters[6], (unsigned long long)cw.wave_edges);
                     atomicAdd(&counters[7], 1ull);
+                    atomicAdd(&counters[8], (unsigned long long)cw.wave_box);
+                    atomicAdd(&counters[9], (unsigned long long)cw.wave_pass);
+                    atomicAdd(&counters[10], 1ull);   /* window-walk waves */
                 }
             }
             return;
         }
     }
+#if defined(CRT_AB_ONLY) && CRT_AB_ONLY == 2   /* timing experiments only: 8x8 tiles alone under walk 12 too */
+    if (TRAV == 12 && uniform_i(tl.w) * uniform_i(tl.h) <= 16) return;
+#endif
     const int lx = lane & 7, ly = lane >> 3;
     const bool has_px = lx < tl.w && ly < tl.h;
     /* the sharing walks keep pixel-less lanes as helpers (they take donated node
      * ranges of the wave's rays); the other walks drop them */
     constexpr bool kHelpers = !FULL;   /* sharing walks use them; packet walks ignore them */
     if (!kHelpers && !has_px) return;
-    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     constexpr bool kCoop = kIsCoop<TRAV> || kIsCoop<SEC>;   /* LDS only for the sharing walks */
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     const Vec c = shade_pixel<FULL, MAXF, TRAV, SEC, COUNT>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt,
@@ -1067,6 +1090,8 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             atomicAdd(&counters[5], (unsigned long long)cnt.wave_tris);
             atomicAdd(&counters[6], (unsigned long long)cnt.wave_edges);
             atomicAdd(&counters[7], 1ull);
+            atomicAdd(&counters[8], (unsigned long long)cnt.wave_box);
+            atomicAdd(&counters[9], (unsigned long long)cnt.wave_pass);
         }
     }
 }
@@ -1094,7 +1119,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(MAXF == 4 ? (TRA
     const unsigned long long lt = (1ull << lane) - 1ull;
     __shared__ CoopLds coop[4];
     CoopLds *L = &coop[threadIdx.x >> 6];
-    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     bool has = false, dry = false;
     int64_t opx = 0;
     Vec o = vec(0.f, 0.f, 0.f), d = vec(0.f, 0.f, 1.f), col = vec(0.f, 0.f, 0.f);
@@ -1187,7 +1212,7 @@ __global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restri
     const bool has_px = lx < tl.w && ly < tl.h;
     Vec o, d;
     camera_ray(s, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), o, d);
-    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     constexpr bool kCoop = kIsCoop<TRAV>;
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
@@ -1277,7 +1302,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
             depth = r.depth;
         }
     }
-    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     constexpr bool kCoop = kIsCoop<TRAV>;
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
@@ -2386,7 +2411,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     HIP_TRY(hipEventCreate(&sc->ev_start));
     HIP_TRY(hipEventCreate(&sc->ev_stop));
     void *p = nullptr;
-    HIP_TRY(hipMalloc(&p, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&p, 16 * sizeof(unsigned long long)));
     sc->allocs.push_back(p);
     sc->d_counters = static_cast<unsigned long long *>(p);
     p = nullptr;
@@ -2805,10 +2830,10 @@ int crt_hip_count_work(crt_hip_scene *sc, const crt_renderer_settings *st, crt_w
     const size_t nfl = (size_t)sc->info.width * sc->info.height * 3;
     if (!sc->d_out) HIP_TRY(hipMalloc(&sc->d_out, nfl * sizeof(float)));
     if ((rc = ensure_plans(sc, st, sc->stream)) != CRT_OK) return rc;
-    HIP_TRY(hipMemsetAsync(sc->d_counters, 0, 8 * sizeof(unsigned long long), sc->stream));
+    HIP_TRY(hipMemsetAsync(sc->d_counters, 0, 16 * sizeof(unsigned long long), sc->stream));
     rc = launch_render(sc, st, sc->full, sc->d_out, sc->stream, true);
     if (rc != CRT_OK) return rc;
-    unsigned long long c[8];
+    unsigned long long c[16];
     HIP_TRY(hipMemcpyAsync(c, sc->d_counters, sizeof c, hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
     out->traversals = c[0];
@@ -2819,6 +2844,9 @@ int crt_hip_count_work(crt_hip_scene *sc, const crt_renderer_settings *st, crt_w
     sc->wave_counts.triangle_steps = c[5];
     sc->wave_counts.edge_steps = c[6];
     sc->wave_counts.waves = c[7];
+    sc->wave_counts.box_steps = c[8];
+    sc->wave_counts.pass_steps = c[9];
+    sc->wave_counts.window_waves = c[10];
     return CRT_OK;
 }
 

@@ -355,6 +355,9 @@ int  crt_hip_count_work(crt_hip_scene *scene, const crt_renderer_settings *setti
  * Zero for walks without wave-uniform steps. */
 typedef struct crt_wave_counts {
     uint64_t node_steps, triangle_steps, edge_steps, waves;
+    uint64_t box_steps;      /* packet walks: node steps where some lane ran the six-face test */
+    uint64_t pass_steps;     /* ... where some lane passed it */
+    uint64_t window_waves;   /* waves that ran the window walk (their node_steps count every window record) */
 } crt_wave_counts;
 int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
 
