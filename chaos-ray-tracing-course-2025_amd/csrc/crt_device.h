@@ -132,8 +132,8 @@ CRT_HD bool box_hit_bf(Vec o, Vec d, const DNode &n) {
  * the same bits as '/', i.e. the correctly rounded quotient.  Anything outside
  * that window takes the compiler's '/'. */
 struct RayRcp {
-    float y1[3];
-    float gate[3];   /* +inf where the axis' faces are tested, -1 where |d| < 1e-6 discards them */
+    float y1[3];     /* refined 1/d; NaN where |d| < 1e-6 discards the axis' faces (every quotient and
+                      * hit point of those faces is then NaN, and NaN fails each of the face's compares) */
     bool fast;       /* every box-face quotient of this ray is inside the exact window */
 };
 
@@ -169,12 +169,9 @@ CRT_HD RayRcp make_ray_rcp(Vec o, Vec d, bool planes_ok) {
     (void)planes_ok;
     r.fast = false;
 #endif
-    r.y1[0] = rcp_refined(d.x);
-    r.y1[1] = rcp_refined(d.y);
-    r.y1[2] = rcp_refined(d.z);
-    r.gate[0] = fabsf(d.x) < 1e-6f ? -1.0f : INFINITY;
-    r.gate[1] = fabsf(d.y) < 1e-6f ? -1.0f : INFINITY;
-    r.gate[2] = fabsf(d.z) < 1e-6f ? -1.0f : INFINITY;
+    r.y1[0] = fabsf(d.x) < 1e-6f ? NAN : rcp_refined(d.x);
+    r.y1[1] = fabsf(d.y) < 1e-6f ? NAN : rcp_refined(d.y);
+    r.y1[2] = fabsf(d.z) < 1e-6f ? NAN : rcp_refined(d.z);
     return r;
 }
 
@@ -191,15 +188,11 @@ CRT_HD bool face_ok(float t, float d_a, float o_u, float d_u, float o_w, float d
     return !(fabsf(d_a) < 1e-6f) & !(t < 0.0f) & (pu >= lo_u) & (pu <= hi_u) & (pw >= lo_w) & (pw <= hi_w);
 }
 
-/* Fast-ray form of the face test as a signed margin: a face passes iff its
- * margin is >= 0.  For a fast ray every term of a tested face is finite
- * (|t| <= 2^63 / 1e-6, |d| <= 2^20, |o|, |plane| <= 2^62), a rounded
- * difference has the sign of the exact one (denormals are on), and t = -0
- * passes like !(t < 0); an axis with |d| < 1e-6 is gated to <= -1 even when
- * its quotients are inf/NaN (minnum/maxnum return the non-NaN operand).  The
- * two faces of an axis share d and the refined reciprocal, so their quotients
- * and hit points are computed as float pairs (v_pk_mul/fma/add_f32); the
- * compares and mask ANDs of face_ok become subtracts and min/max. */
+/* Fast-ray form of the face test.  For a fast ray every term of a tested
+ * face is finite (|t| <= 2^63 / 1e-6, |d| <= 2^20, |o|, |plane| <= 2^62).
+ * The two faces of an axis share d and the refined reciprocal, so their
+ * quotients and hit points are computed as float pairs
+ * (v_pk_mul/fma/add_f32); each range check is one med3 and a compare. */
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 CRT_HD f2 div_fast2(f2 a, float b, float y1) {
@@ -209,46 +202,54 @@ CRT_HD f2 div_fast2(f2 a, float b, float y1) {
     return __builtin_elementwise_fma(__builtin_elementwise_fma(-B, q1, a), Y, q1);
 }
 
-CRT_HD float min3f(float a, float b, float c) { return fminf(fminf(a, b), c); }
+/* lo <= p <= hi for a finite p and ordered planes (lo <= hi: part of the
+ * planes_ok condition): a med3 returns one of its operands, so it equals p
+ * exactly when p lies in the closed range (-0 and +0 compare equal, as the
+ * reference's >= / <= do). */
+CRT_HD bool in_slab(float p, float lo, float hi) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_fmed3f(p, lo, hi) == p;
+#else
+    return (p >= lo) & (p <= hi);
+#endif
+}
 
-/* margin of an axis' two faces (planes pl = lo, hi) */
-CRT_HD float axis_margin(f2 pl, float o_a, float d_a, float y1, float gate, float o_u, float d_u, float o_w,
-                         float d_w, float lo_u, float hi_u, float lo_w, float hi_w) {
+/* The two faces of axis a (planes pl = lo, hi) for a fast ray: quotients and
+ * hit points as float pairs.  The face's t >= 0 test (!(t < 0): t of a fast
+ * ray is finite or, on a discarded axis, NaN) is folded into pu, which is
+ * NaN for a face that fails it, so the face passes iff both hit-point
+ * coordinates are in range (axis_pass). */
+CRT_HD void axis_points(f2 pl, float o_a, float d_a, float y1, float o_u, float d_u, float o_w, float d_w, f2 &pu,
+                        f2 &pw) {
     const f2 t = div_fast2(pl - o_a, d_a, y1);
-    const f2 pu = o_u + d_u * t;
-    const f2 pw = o_w + d_w * t;
-    const f2 u0 = pu - lo_u, u1 = hi_u - pu, w0 = pw - lo_w, w1 = hi_w - pw;
-    const float m_lo = min3f(min3f(u0.x, u1.x, w0.x), w1.x, t.x);
-    const float m_hi = min3f(min3f(u0.y, u1.y, w0.y), w1.y, t.y);
-    return fminf(fmaxf(m_lo, m_hi), gate);
+    pu = o_u + d_u * t;
+    pw = o_w + d_w * t;
+    pu.x = t.x >= 0.0f ? pu.x : NAN;
+    pu.y = t.y >= 0.0f ? pu.y : NAN;
+}
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"   /* no short-circuit: branch-free ORs */
+CRT_HD bool axis_pass(f2 pu, f2 pw, float lo_u, float hi_u, float lo_w, float hi_w) {
+    return (in_slab(pu.x, lo_u, hi_u) & in_slab(pw.x, lo_w, hi_w)) |
+           (in_slab(pu.y, lo_u, hi_u) & in_slab(pw.y, lo_w, hi_w));
 }
 
 /* ray_intersect_aabb_p (crt_intersection.cpp:14-45), branch-free over the six
  * faces, with the per-ray hoisted divisions (see coord_ok for when they are
  * exact; other rays take the compiler's '/' and the plain compares). */
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"   /* no short-circuit: one branch-free OR */
 /* The fast-ray form alone (caller guarantees r.fast for every lane it uses). */
 CRT_HD bool box_hit_fast(Vec o, Vec d, const RayRcp &r, const DNode n) {
-    const float mx = axis_margin((f2){n.lo_x, n.hi_x}, o.x, d.x, r.y1[0], r.gate[0], o.y, d.y, o.z, d.z, n.lo_y,
-                                 n.hi_y, n.lo_z, n.hi_z);
-    const float my = axis_margin((f2){n.lo_y, n.hi_y}, o.y, d.y, r.y1[1], r.gate[1], o.z, d.z, o.x, d.x, n.lo_z,
-                                 n.hi_z, n.lo_x, n.hi_x);
-    const float mz = axis_margin((f2){n.lo_z, n.hi_z}, o.z, d.z, r.y1[2], r.gate[2], o.x, d.x, o.y, d.y, n.lo_x,
-                                 n.hi_x, n.lo_y, n.hi_y);
-    return fmaxf(fmaxf(mx, my), mz) >= 0.0f;
+    f2 px, qx, py, qy, pz, qz;
+    axis_points((f2){n.lo_x, n.hi_x}, o.x, d.x, r.y1[0], o.y, d.y, o.z, d.z, px, qx);
+    axis_points((f2){n.lo_y, n.hi_y}, o.y, d.y, r.y1[1], o.z, d.z, o.x, d.x, py, qy);
+    axis_points((f2){n.lo_z, n.hi_z}, o.z, d.z, r.y1[2], o.x, d.x, o.y, d.y, pz, qz);
+    return axis_pass(px, qx, n.lo_y, n.hi_y, n.lo_z, n.hi_z) | axis_pass(py, qy, n.lo_z, n.hi_z, n.lo_x, n.hi_x) |
+           axis_pass(pz, qz, n.lo_x, n.hi_x, n.lo_y, n.hi_y);
 }
 
 CRT_HD bool box_hit_r(Vec o, Vec d, const RayRcp &r, const DNode n) {
-    if (r.fast) {
-        const float mx = axis_margin((f2){n.lo_x, n.hi_x}, o.x, d.x, r.y1[0], r.gate[0], o.y, d.y, o.z, d.z, n.lo_y,
-                                     n.hi_y, n.lo_z, n.hi_z);
-        const float my = axis_margin((f2){n.lo_y, n.hi_y}, o.y, d.y, r.y1[1], r.gate[1], o.z, d.z, o.x, d.x, n.lo_z,
-                                     n.hi_z, n.lo_x, n.hi_x);
-        const float mz = axis_margin((f2){n.lo_z, n.hi_z}, o.z, d.z, r.y1[2], r.gate[2], o.x, d.x, o.y, d.y, n.lo_x,
-                                     n.hi_x, n.lo_y, n.hi_y);
-        return fmaxf(fmaxf(mx, my), mz) >= 0.0f;
-    }
+    if (r.fast) return box_hit_fast(o, d, r, n);
     const float t0 = (n.lo_x - o.x) / d.x, t1 = (n.lo_y - o.y) / d.y, t2 = (n.lo_z - o.z) / d.z;
     const float t3 = (n.hi_x - o.x) / d.x, t4 = (n.hi_y - o.y) / d.y, t5 = (n.hi_z - o.z) / d.z;
     return face_ok(t0, d.x, o.y, d.y, o.z, d.z, n.lo_y, n.hi_y, n.lo_z, n.hi_z) |
@@ -262,18 +263,20 @@ CRT_HD bool box_hit_r(Vec o, Vec d, const RayRcp &r, const DNode n) {
 
 /* ---- pruned walks ------------------------------------------------------ */
 /* Hull slab test of a PNode (crt_layout.h).  The hull is conservative by a
- * margin (crt_scene_build.cpp) far above this test's own rounding (a
- * reciprocal with ~1 ulp error, one rounding per subtract and multiply), so
- * `alive` is false only when no triangle in the subtree can produce a hit
- * with t <= lim.  The slab distances are (plane - o) * (1/d): on an axis the
- * ray is parallel to (1/d = +-inf) they are correctly signed infinities, and
- * a NaN (0 * inf) only arises for an origin exactly on an expanded hull
- * plane, i.e. outside every triangle's box by the full margin, where the
- * subtree cannot hold a hit anyway.  The final tests are negated so a NaN
- * bound keeps the subtree. */
+ * margin (crt_scene_build.cpp) far above this test's own rounding, so `alive`
+ * is false only when no triangle in the subtree can produce a hit with
+ * t <= lim.  The slab distance of plane P on axis a is one fma,
+ * P * (1/d_a) + c_a with c_a = -o_a * (1/d_a) rounded once per ray: a
+ * reciprocal with ~1 ulp error and two roundings put it within a few ulps of
+ * |o_a| + |P - o_a| (over |d_a|) of the exact distance, the same order as the
+ * (P - o) * (1/d) form and far inside the margin's 2^-13 G.  An axis whose
+ * reciprocal is so large that a product could overflow (|1/d_a| G > 2^100,
+ * d_a = 0 included) gets 1/d_a = NaN: its slab distances are NaN, which
+ * fminf/fmaxf drop, so that axis stops restricting the test — the test stays
+ * conservative.  The final tests are negated so a NaN bound keeps the subtree. */
 struct PruneRay {
-    float ox, oy, oz;
-    float ix, iy, iz;      /* ~1/d */
+    float ix, iy, iz;      /* ~1/d, or NaN (see above) */
+    float cx, cy, cz;      /* -o * ix */
     bool on;               /* |o|_inf <= prune_origin_max: the margins hold for this ray */
 };
 
@@ -285,22 +288,27 @@ CRT_HD float rcp_any(float b) {
 #endif
 }
 
+CRT_HD float prune_rcp(float d, float omax) {
+    const float i = rcp_any(d);
+    return fabsf(i) * fmaxf(omax, 1.0f) <= 0x1p100f ? i : NAN;
+}
+
 CRT_HD PruneRay make_prune_ray(Vec o, Vec d, float omax) {
     PruneRay p;
-    p.ox = o.x;
-    p.oy = o.y;
-    p.oz = o.z;
-    p.ix = rcp_any(d.x);
-    p.iy = rcp_any(d.y);
-    p.iz = rcp_any(d.z);
+    p.ix = prune_rcp(d.x, omax);
+    p.iy = prune_rcp(d.y, omax);
+    p.iz = prune_rcp(d.z, omax);
+    p.cx = -o.x * p.ix;
+    p.cy = -o.y * p.iy;
+    p.cz = -o.z * p.iz;
     p.on = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z))) <= omax;
     return p;
 }
 
 CRT_HD bool hull_alive(const PNode &n, const PruneRay &p, float lim) {
-    const float t0x = (n.tlo_x - p.ox) * p.ix, t1x = (n.thi_x - p.ox) * p.ix;
-    const float t0y = (n.tlo_y - p.oy) * p.iy, t1y = (n.thi_y - p.oy) * p.iy;
-    const float t0z = (n.tlo_z - p.oz) * p.iz, t1z = (n.thi_z - p.oz) * p.iz;
+    const float t0x = fmaf(n.tlo_x, p.ix, p.cx), t1x = fmaf(n.thi_x, p.ix, p.cx);
+    const float t0y = fmaf(n.tlo_y, p.iy, p.cy), t1y = fmaf(n.thi_y, p.iy, p.cy);
+    const float t0z = fmaf(n.tlo_z, p.iz, p.cz), t1z = fmaf(n.thi_z, p.iz, p.cz);
     const float tin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
     const float tout = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
     return !p.on || (!(tin > lim) && !(tin > tout) && !(tout < 0.0f));

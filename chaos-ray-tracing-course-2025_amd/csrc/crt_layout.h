@@ -28,9 +28,11 @@
 
 namespace crt_amd {
 
+/* (lo, hi) of an axis sit in adjacent dwords: a scalar load puts each pair in
+ * an aligned SGPR pair, the direct operand of the box test's packed ops. */
 struct alignas(16) DNode {
-    float lo_x, lo_y, lo_z, hi_x;
-    float hi_y, hi_z;
+    float lo_x, hi_x, lo_y, hi_y;
+    float lo_z, hi_z;
     int32_t a;   /* interior: skip index (first node after the subtree) | leaf: count | depth << 24 */
     int32_t b;   /* interior: -(depth + 1)                               | leaf: first slot           */
 };
@@ -49,11 +51,11 @@ static_assert(sizeof(DNode) == 32, "DNode must be 32 B");
  * Leaf slot numbers are the reference's visit order in every copy, so ties in
  * t are broken exactly as the reference's first-found rule does. */
 struct alignas(16) PNode {
-    float lo_x, lo_y, lo_z, hi_x;
-    float hi_y, hi_z;
+    float lo_x, hi_x, lo_y, hi_y;   /* cell, (lo, hi) pairs as DNode */
+    float lo_z, hi_z;
     int32_t a, b;
-    float tlo_x, tlo_y, tlo_z, thi_x;
-    float thi_y, thi_z;
+    float tlo_x, thi_x, tlo_y, thi_y;   /* hull */
+    float tlo_z, thi_z;
     int32_t depth;   /* tree depth (indexes the packet walk's reach mask) */
     int32_t count;   /* leaf: triangle copies, interior: 0 */
 };

@@ -78,6 +78,21 @@ __device__ __forceinline__ T load_global(const T *p, int i) {
 #endif
 }
 
+/* timing experiments only (A/B builds with -DCRT_AB_PHASES): per-phase
+ * s_memtime sums of the walks, printed by crt_hip_render */
+#ifdef CRT_AB_PHASES
+__device__ unsigned long long g_phase[16];
+#define PH_DECL unsigned long long ph_t = __builtin_amdgcn_s_memtime(), ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PH(k) do { const unsigned long long ph_n = __builtin_amdgcn_s_memtime(); ph_acc[k] += ph_n - ph_t; ph_t = ph_n; } while (0)
+#define PH_COUNT(k) (++ph_acc[k])
+#define PH_FLUSH(base) do { if (__lane_id() == 0) for (int ph_k = 0; ph_k < 8; ++ph_k) atomicAdd(&g_phase[(base) + ph_k], ph_acc[ph_k]); } while (0)
+#else
+#define PH_DECL
+#define PH(k)
+#define PH_COUNT(k)
+#define PH_FLUSH(base)
+#endif
+
 struct LaneCounts {
     uint32_t traversals, nodes, tris, hits;
     /* wave-uniform steps of the packet walks (kept by every lane, added once per wave) */
@@ -435,6 +450,60 @@ __device__ __noinline__ bool box_hit_slow(Vec o, Vec d, const DNode n) {
     return box_hit_r(o, d, r, n);
 }
 
+/* Face cache of the fast packet walk.  A node's six-face test reads, per
+ * axis, the quotients and hit points of its two planes on that axis
+ * (axis_points) and then only compares them with the other axes' ranges
+ * (axis_pass).  Consecutive nodes of the walk share most planes — a child
+ * differs from its parent in one plane — so each lane keeps the hit points of
+ * the planes the wave last computed, and the wave recomputes an axis only
+ * when the node's (lo, hi) pair on it differs from the cached one (a uniform
+ * compare of the bit patterns).  Every lane of the wave updates the entries
+ * (they do not depend on the lane's reach or best hit), so an entry always
+ * holds exactly what box_hit_fast would compute for the cached planes. */
+struct FaceCache {
+    f2 pu[3], pw[3];
+    unsigned long long key[3];   /* bits of the cached (lo, hi) pair per axis: equal in every lane, kept in
+                                  * VGPRs (vgpr_u64) — the walk's SGPRs hold the prefetched node records */
+};
+
+/* the same value in every lane, in a VGPR pair (an asm result is divergent to the compiler) */
+__device__ __forceinline__ unsigned long long vgpr_u64(unsigned long long x) {
+    unsigned long long r;
+    asm volatile("v_mov_b64 %0, %1" : "=v"(r) : "s"(x));
+    return r;
+}
+
+__device__ __forceinline__ unsigned long long plane_key(float lo, float hi) {
+    return ((unsigned long long)__float_as_uint(hi) << 32) | (unsigned long long)__float_as_uint(lo);
+}
+
+__device__ __forceinline__ void face_cache_init(FaceCache &fc) {
+    for (int a = 0; a < 3; ++a) fc.key[a] = vgpr_u64(~0ull);   /* NaN planes: never a node of a planes_ok tree */
+}
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"   /* branch-free ORs */
+__device__ __forceinline__ bool face_cache_pass(FaceCache &fc, const PNode &n, Vec o, Vec d, const RayRcp &r) {
+    const unsigned long long kx = plane_key(n.lo_x, n.hi_x), ky = plane_key(n.lo_y, n.hi_y),
+                             kz = plane_key(n.lo_z, n.hi_z);
+    if (kx != fc.key[0]) {
+        axis_points((f2){n.lo_x, n.hi_x}, o.x, d.x, r.y1[0], o.y, d.y, o.z, d.z, fc.pu[0], fc.pw[0]);
+        fc.key[0] = vgpr_u64(kx);
+    }
+    if (ky != fc.key[1]) {
+        axis_points((f2){n.lo_y, n.hi_y}, o.y, d.y, r.y1[1], o.z, d.z, o.x, d.x, fc.pu[1], fc.pw[1]);
+        fc.key[1] = vgpr_u64(ky);
+    }
+    if (kz != fc.key[2]) {
+        axis_points((f2){n.lo_z, n.hi_z}, o.z, d.z, r.y1[2], o.x, d.x, o.y, d.y, fc.pu[2], fc.pw[2]);
+        fc.key[2] = vgpr_u64(kz);
+    }
+    return axis_pass(fc.pu[0], fc.pw[0], n.lo_y, n.hi_y, n.lo_z, n.hi_z) |
+           axis_pass(fc.pu[1], fc.pw[1], n.lo_z, n.hi_z, n.lo_x, n.hi_x) |
+           axis_pass(fc.pu[2], fc.pw[2], n.lo_x, n.hi_x, n.lo_y, n.hi_y);
+}
+#pragma clang diagnostic pop
+
 template <bool COUNT, bool FAST>
 __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool active, Vec o, Vec d,
                                                      const RayRcp &rr, float &best_t, LaneCounts &c) {
@@ -457,9 +526,13 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
      * it tests the current node; the whole 64-B record is read up front.
      * Predicates are combined without short-circuit so the only branches are
      * wave-uniform (no exec-mask save/restore). */
+    FaceCache fc;
+    face_cache_init(fc);
     int i = 0;
     PNode cur = load_scalar(nodes, 0);
+    PH_DECL
     while (i < n) {
+        PH_COUNT(7);
         const bool interior = cur.b < 0;
         const int i1 = i + 1 < n ? i + 1 : last;
         const int i2 = interior ? (cur.a < n ? cur.a : last) : i1;
@@ -472,13 +545,18 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
         bool pass = false;
         if (__ballot(alive) != 0ull) {
             if (COUNT) ++c.wave_box;
-            pass = alive & box_hit_fast(o, d, rr, cell_of(cur));
+            if constexpr (FAST) {
+                pass = alive & face_cache_pass(fc, cur, o, d, rr);
+            } else {
+                pass = alive & box_hit_fast(o, d, rr, cell_of(cur));
+            }
             if (!FAST && __ballot(alive & !rr.fast) != 0ull) {
                 if (alive & !rr.fast) pass = box_hit_slow(o, d, cell_of(cur));
             }
             if (COUNT && alive) ++c.nodes;
         }
         const unsigned long long pm = __ballot(pass);
+        PH(0);
         if (COUNT && pm != 0ull) ++c.wave_pass;
         if (interior) {
             if (pm != 0ull) {
@@ -522,10 +600,13 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
                 g = gn;
                 cw = cwn;
             }
+            PH(1);
+            PH_COUNT(6);
         }
         i = i + 1;
         cur = n1;
     }
+    PH_FLUSH(8);
     return best;
 }
 
@@ -591,14 +672,23 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
     const PNode *nodes = pnode_order(s.pnodes, n, uniform_i(oct));
     const unsigned long long rmask = (R >= 64) ? ~0ull : ((1ull << R) - 1ull);
     int i = 0;
-    PNode nd = nodes[sl < n ? sl : n - 1];
+    PNode nd = load_global(nodes, sl < n ? sl : n - 1);
+    PH_DECL
     while (i < n) {
+        PH_COUNT(7);
+#ifdef CRT_AB_WPREF
+        /* the window after this one, loaded while this one is tested; used
+         * unless a dead subtree moves the walk further (next > i + K) */
+        const int spec = i + K + sl;
+        const PNode nd_next = load_global(nodes, spec < n ? spec : n - 1);
+#endif
         const int j = i + sl;
         const bool valid = j < n;
         const bool interior = nd.count == 0;
         const bool alive = valid & active & hull_alive(nd, pr, lim);
         const bool pass = alive & box_hit_fast(o, d, rr, cell_of(nd));
         const unsigned long long P = __ballot(pass);
+        PH(0);
         /* replay the packet walk's reach update over the window, in order */
         const int meta = nd.depth | (interior ? 256 : 0);
         const int kk = n - i < K ? n - i : K;
@@ -614,18 +704,31 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
             }
             my_in = (a == sl) ? in : my_in;
         }
+        PH(1);
         if (COUNT) {
             if (my_in & alive) ++c.nodes;
             c.wave_nodes += (uint32_t)kk;     /* node records of the window */
         }
         const bool enter = my_in & pass;
         const unsigned long long E = __ballot(enter);
-        /* skip past the subtree of a window node no ray entered */
+        /* skip past the subtree of a window node no ray entered: the furthest
+         * skip index of the dead nodes, read from one lane per dead node */
         const bool dead = valid & interior & (((E >> (sl * R)) & rmask) == 0ull);
-        const int skip_to = wave_max_i(dead ? nd.a : 0);
+        unsigned long long D = __ballot(dead & (r == 0));
+        int skip_to = 0;
+        while (D != 0ull) {
+            const int l = __builtin_ctzll(D);
+            D &= D - 1ull;
+            const int v = __builtin_amdgcn_readlane(nd.a, l);
+            skip_to = v > skip_to ? v : skip_to;
+        }
         const int next = uniform_i(i + K > skip_to ? i + K : skip_to);
-        /* triangles of the entered leaves, one leaf per lane (next triangle
-         * prefetched), then a per-ray merge over the ray's K lanes */
+        PH(2);
+        /* triangles of the entered leaves, one leaf at a time over the whole
+         * wave: lane (sl, r) tests triangles sl, sl + K, ... of the leaf for
+         * its ray r if r entered it, so a leaf costs ceil(count / K) rounds
+         * (its triangles load as K consecutive records); then a per-ray merge
+         * of the candidates over the ray's K lanes by the key (t, slot). */
         const bool leaf = enter & !interior;
 #if defined(CRT_AB_NOTRI) && (CRT_AB_NOTRI & 1)   /* timing experiments only: no triangle phase (wrong image) */
         if (false) {
@@ -634,26 +737,30 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
 #endif
             float lt = best_t;
             int ls = best;
-            if (leaf) {
-                const int first = nd.b, cnt = nd.count;
-                DTriGeo g = s.slots[first];
-                uint8_t cl = s.slot_cull[first];
-                for (int k = 0; k < cnt; ++k) {
-                    const int slot = first + k;
-                    const int sn = k + 1 < cnt ? slot + 1 : slot;
-                    const DTriGeo gn = s.slots[sn];           /* next triangle in flight */
-                    const uint8_t cn = s.slot_cull[sn];
-                    float t;
-                    if (COUNT) ++c.tris;
-                    if (tri_plane(o, d, g, cl != 0, t) && key_better(t, slot, lt, ls) && tri_edges(o, d, g, t)) {
-                        lt = t;
-                        ls = slot;
+            unsigned long long Lm = __ballot(leaf);
+            while (Lm != 0ull) {
+                const int l0 = __builtin_ctzll(Lm);
+                const int s0 = l0 / R;
+                const unsigned long long sm = Lm & (rmask << (s0 * R));   /* the rays that entered leaf s0 */
+                Lm &= ~sm;
+                const int first = __builtin_amdgcn_readlane(nd.b, l0), cnt = __builtin_amdgcn_readlane(nd.count, l0);
+                if (COUNT) c.wave_tris += (uint32_t)((cnt + K - 1) / K);
+                if (((sm >> (s0 * R + r)) & 1ull) != 0ull) {
+                    for (int k = sl; k < cnt; k += K) {
+                        const int slot = first + k;
+                        const DTriGeo g = load_global(s.slots, slot);
+                        const uint8_t cl = load_global(s.slot_cull, slot);
+                        float t;
+                        if (COUNT) ++c.tris;
+                        if (tri_plane(o, d, g, cl != 0, t) && key_better(t, slot, lt, ls) && tri_edges(o, d, g, t)) {
+                            lt = t;
+                            ls = slot;
+                        }
                     }
-                    g = gn;
-                    cl = cn;
                 }
             }
-            if (COUNT) c.wave_tris += (uint32_t)wave_max_i(leaf ? nd.count : 0);
+            PH(3);
+            PH_COUNT(6);
             for (int off = R; off < 64; off <<= 1) {
                 const float ot = __shfl_xor(lt, off);
                 const int os = __shfl_xor(ls, off);
@@ -665,10 +772,19 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
             best_t = lt;
             best = ls;
             lim = best >= 0 ? best_t : INFINITY;
+            PH(4);
         }
-        nd = nodes[next + sl < n ? next + sl : n - 1];
+#ifdef CRT_AB_WPREF
+        if (next == i + K) {
+            nd = nd_next;
+        } else
+#endif
+        {
+            nd = load_global(nodes, next + sl < n ? next + sl : n - 1);
+        }
         i = next;
     }
+    PH_FLUSH(0);
     if (COUNT && best >= 0 && lead) ++c.hits;
     return best;
 }
@@ -2346,7 +2462,9 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
         };
         ds.planes_ok = 1;
         for (const DNode &n : hs.nodes)
-            if (!(ok(n.lo_x) && ok(n.lo_y) && ok(n.lo_z) && ok(n.hi_x) && ok(n.hi_y) && ok(n.hi_z))) ds.planes_ok = 0;
+            if (!(ok(n.lo_x) && ok(n.lo_y) && ok(n.lo_z) && ok(n.hi_x) && ok(n.hi_y) && ok(n.hi_z) &&
+                  n.lo_x <= n.hi_x && n.lo_y <= n.hi_y && n.lo_z <= n.hi_z))   /* ordered: crt_device.h in_slab */
+                ds.planes_ok = 0;
         if ((rc = upload(sc.get(), hs.slots, &ds.slots)) != CRT_OK) return rc;
         if ((rc = upload(sc.get(), hs.slot_tri, &ds.slot_tri)) != CRT_OK) return rc;
         if ((rc = upload(sc.get(), hs.slot_cull, &ds.slot_cull)) != CRT_OK) return rc;
@@ -2524,6 +2642,17 @@ int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rg
     if (rc != CRT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(rgb_out, sc->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
+#ifdef CRT_AB_PHASES
+    {
+        unsigned long long ph[16];
+        HIP_TRY(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof ph));
+        fprintf(stderr, "PHASES");
+        for (int k = 0; k < 16; ++k) fprintf(stderr, " %llu", ph[k]);
+        fprintf(stderr, "\n");
+        std::memset(ph, 0, sizeof ph);
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof ph));
+    }
+#endif
     if (stats) {
         std::memset(stats, 0, sizeof *stats);
         float ms = 0.f;

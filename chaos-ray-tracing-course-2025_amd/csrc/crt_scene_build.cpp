@@ -157,8 +157,8 @@ void build_tree(const std::vector<Box6> &tri_boxes, const Box6 &root_box, std::v
  * triangle's box, kappa = diam / inradius, c a small constant (< 100).  The
  * hull below uses 2^-14 * (diam * kappa + 2 G) for rays with |o|_inf <= G,
  * G = 4 max |vertex coordinate| — a margin of 2^10 over that bound — and the
- * device's slab test (rcp, one rounding per product) adds errors far below
- * it.  Triangles whose normal is not finite or whose area is 0 (no reliable
+ * device's slab test (rcp, one fma per plane: crt_device.h hull_alive) adds
+ * errors far below it.  Triangles whose normal is not finite or whose area is 0 (no reliable
  * bound) get an unbounded hull: their subtrees are never pruned. */
 /* round_down / round_up / HullD / triangle_hull: crt_device.h (shared with the
  * device build, crt_tree_build.hip, so both builds produce the same bits). */

@@ -449,6 +449,7 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs A) {
     const float cs[6] = {d.lo_x, d.lo_y, d.lo_z, d.hi_x, d.hi_y, d.hi_z};
     bool ok = true;
     for (int k = 0; k < 6; ++k) ok = ok && coord_ok(cs[k]);
+    ok = ok && d.lo_x <= d.hi_x && d.lo_y <= d.hi_y && d.lo_z <= d.hi_z;   /* ordered: crt_device.h in_slab */
     if (!ok) atomicAnd(A.planes_ok, 0);
 }
 

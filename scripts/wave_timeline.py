@@ -9,13 +9,14 @@ resident over time.
 """
 import argparse
 import json
+import os
 import sys
 from pathlib import Path
 
 import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
-sys.path.insert(0, str(ROOT / "chaos-ray-tracing-course-2025_amd"))
+sys.path.insert(0, os.environ.get("CRT_PKG") or str(ROOT / "chaos-ray-tracing-course-2025_amd"))   # CRT_PKG: another build
 from crt_amd import native as N  # noqa: E402
 from crt_amd.scene_npz import load_npz  # noqa: E402
 
