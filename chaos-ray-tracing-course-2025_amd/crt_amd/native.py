@@ -201,6 +201,7 @@ EXPORTS = [
     ("crt_hip_trace_batch", C.c_int, [_P, _P, C.c_int64, _P]),
     ("crt_hip_count_work", C.c_int, [_P, C.POINTER(RendererSettings), C.POINTER(WorkCounts)]),
     ("crt_hip_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_double)]),
+    ("crt_hip_plan_calib_k", C.c_double, [_P]),
     ("crt_hip_wave_counts", C.c_int, [_P, C.POINTER(WaveCounts)]),
     ("crt_hip_scene_set_option", C.c_int, [_P, C.c_char_p, C.c_int]),
     ("crt_hip_profile_waves", C.c_int, [_P, C.POINTER(RendererSettings), _P, C.c_int64, _P]),
@@ -559,6 +560,10 @@ class HipScene:
     def unpack_shards_rgb8(self, count: int, d_gathered: int, d_rgb8: int, stream: int | None = None) -> None:
         _check(lib().crt_hip_unpack_shards_rgb8(self._h, count, C.c_void_p(d_gathered), C.c_void_p(d_rgb8),
                                                 C.c_void_p(stream or 0)))
+
+    def plan_calib_k(self) -> float:
+        """Split threshold of the calibrated plan in use (0: none yet / estimate plan)."""
+        return float(lib().crt_hip_plan_calib_k(self._h))
 
     def last_kernel_ms(self) -> float:
         v = C.c_double()

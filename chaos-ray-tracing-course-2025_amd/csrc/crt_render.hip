@@ -504,6 +504,111 @@ __device__ __forceinline__ bool face_cache_pass(FaceCache &fc, const PNode &n, V
 }
 #pragma clang diagnostic pop
 
+/* Leaf phase of the fast packet walk when few rays entered the leaf (m of
+ * 64 lanes, m <= 32): instead of 64 lanes per triangle with 64 - m of them
+ * idle, the wave tests T = 64 / G triangles at once, G >= m lanes per
+ * triangle, lane (g, q) testing triangle g (+ T, + 2T, ...) for the q-th
+ * entering ray.  The rays' o, d and best keys pass through a per-wave LDS
+ * table indexed by rank; each lane filters its candidates by the ray's best
+ * key so far (key_better, as the packet loop does), the G-lane groups merge
+ * by the key (t, slot) — the reference's first-found rule in any order — and
+ * each entering lane takes its ray's result back.  Same tests, same result. */
+struct LeafRayLds {
+    float4 a[4][32];   /* (d.x, d.y, d.z, best_t) by rank, per wave of the 256-thread block */
+    float4 b[4][32];   /* (o.x, o.y, o.z, best as bits) */
+};
+
+template <bool COUNT>
+__device__ __forceinline__ void leaf_grouped(const DeviceScene &s, int first, int cnt, unsigned long long pm, bool pass,
+                                             Vec o, Vec d, float &best_t, int &best, float &lim, LaneCounts &c) {
+    __shared__ LeafRayLds L;
+    const int w = (int)(threadIdx.x >> 6);
+    const int lane = (int)__lane_id();
+    const int m = __popcll(pm);
+    const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+    if (pass) {
+        L.a[w][rank] = make_float4(d.x, d.y, d.z, best_t);
+        L.b[w][rank] = make_float4(o.x, o.y, o.z, __int_as_float(best));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int lg = m <= 1 ? 0 : 32 - __clz(m - 1);   /* G = 2^lg >= m */
+    const int G = 1 << lg, T = 64 >> lg;
+    const int q = lane & (G - 1), g = lane >> lg;
+    const bool qok = q < m;
+    const float4 ra = L.a[w][qok ? q : 0], rb = L.b[w][qok ? q : 0];
+    const Vec ro = vec(rb.x, rb.y, rb.z), rd = vec(ra.x, ra.y, ra.z);
+    float lt = ra.w;
+    int ls = __float_as_int(rb.w);
+#ifdef CRT_AB_GPREF
+    /* two rounds in flight: each buffer is refilled right after its test */
+    const int lst = first + cnt - 1;
+    int sa = first + g < lst ? first + g : lst, sb = first + g + T < lst ? first + g + T : lst;
+    DTriGeo ta = load_global(s.slots, sa), tb = load_global(s.slots, sb);
+    uint8_t ca = load_global(s.slot_cull, sa), cb = load_global(s.slot_cull, sb);
+    for (int k0 = 0; k0 < cnt; k0 += 2 * T) {
+        float t;
+        if (COUNT) ++c.wave_tris;
+        if (qok & (k0 + g < cnt)) {
+            if (COUNT) ++c.tris;
+            if (tri_plane(ro, rd, ta, ca != 0, t) && key_better(t, sa, lt, ls) && tri_edges(ro, rd, ta, t)) {
+                lt = t;
+                ls = sa;
+            }
+        }
+        sa = first + k0 + g + 2 * T < lst ? first + k0 + g + 2 * T : lst;
+        ta = load_global(s.slots, sa);
+        ca = load_global(s.slot_cull, sa);
+        if (k0 + T < cnt) {
+            if (COUNT) ++c.wave_tris;
+            if (qok & (k0 + T + g < cnt)) {
+                if (COUNT) ++c.tris;
+                if (tri_plane(ro, rd, tb, cb != 0, t) && key_better(t, sb, lt, ls) && tri_edges(ro, rd, tb, t)) {
+                    lt = t;
+                    ls = sb;
+                }
+            }
+        }
+        sb = first + k0 + g + 3 * T < lst ? first + k0 + g + 3 * T : lst;
+        tb = load_global(s.slots, sb);
+        cb = load_global(s.slot_cull, sb);
+    }
+#else
+    for (int k0 = 0; k0 < cnt; k0 += T) {
+        if (COUNT) ++c.wave_tris;
+        const int k = k0 + g;
+        if (qok & (k < cnt)) {
+            const int slot = first + k;
+            const DTriGeo tg = load_global(s.slots, slot);
+            const uint8_t cl = load_global(s.slot_cull, slot);
+            float t;
+            if (COUNT) ++c.tris;
+            if (tri_plane(ro, rd, tg, cl != 0, t) && key_better(t, slot, lt, ls) && tri_edges(ro, rd, tg, t)) {
+                lt = t;
+                ls = slot;
+            }
+        }
+    }
+#endif
+    for (int off = G; off < 64; off <<= 1) {
+        const float ot = __shfl_xor(lt, off);
+        const int os = __shfl_xor(ls, off);
+        if (os >= 0 && key_better(ot, os, lt, ls)) {
+            lt = ot;
+            ls = os;
+        }
+    }
+    const float nt = __shfl(lt, rank);
+    const int ns = __shfl(ls, rank);
+    if (pass) {
+        best_t = nt;
+        best = ns;
+        lim = ns >= 0 ? nt : lim;
+    }
+    __builtin_amdgcn_wave_barrier();   /* the table is rewritten by the next leaf */
+}
+
 template <bool COUNT, bool FAST>
 __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool active, Vec o, Vec d,
                                                      const RayRcp &rr, float &best_t, LaneCounts &c) {
@@ -576,6 +681,23 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
         if (pm != 0ull) {
 #endif
             const int first = cur.b, cnt = pnode_leaf_count(cur);
+#ifndef CRT_AB_NOGROUP
+#ifndef CRT_GROUP_MAX
+#define CRT_GROUP_MAX 32
+#endif
+            if (FAST && cnt >= 4 && __popcll(pm) <= CRT_GROUP_MAX) {
+                /* drop the face cache (its registers serve the grouped phase;
+                 * the next box test recomputes all three axes) */
+                for (int a = 0; a < 3; ++a) fc.pu[a] = fc.pw[a] = (f2){0.0f, 0.0f};
+                face_cache_init(fc);
+                leaf_grouped<COUNT>(s, first, cnt, pm, pass, o, d, best_t, best, lim, c);
+                PH(1);
+                PH_COUNT(6);
+                i = i + 1;
+                cur = n1;
+                continue;
+            }
+#endif
             DTriGeo g = load_scalar(s.slots, first);
             uint32_t cw = load_scalar(s.slot_cull_bits, first >> 5);
             for (int k = 0; k < cnt; ++k) {
@@ -1805,7 +1927,7 @@ struct crt_hip_scene {
     struct SubTile { int32_t dx, dy, w, h; float cost; };
     std::vector<std::vector<SubTile>> calib;
     int calib_walk = -1;           /* primary walk the calibration was measured with (-1: none) */
-    int calibrate = 1;             /* env CRT_CALIBRATE */
+    int calibrate = 1;             /* 0 estimate plan, 1 measured costs with a tuned k, 2 with calib_k (env CRT_CALIBRATE) */
     int window_walk = 1;           /* camera walk 12 -> 13 (window walk for split tiles), env CRT_WINDOW */
     int record_events = 1;         /* start/stop events around every render (crt_hip_last_kernel_ms), option "events" */
     bool events_valid = false;
@@ -2161,6 +2283,19 @@ int plan_walk(const crt_hip_scene *sc, const crt_renderer_settings *st) {
 /* Calibrate the tile plan for this frame's primary walk once (see
  * calibrate_plan), then rebuild the full-frame plan; shard plans are rebuilt
  * on their next use. */
+/* Split threshold of the calibrated plan (calibrate_plan: a tile whose
+ * measured cost exceeds k x mean cost per wave slot is split).  The best k
+ * depends on the scene and on how the walks' step counts relate to time (a
+ * split tile's window waves cost more per step than a packet wave), so by
+ * default it is tuned: each candidate's plan renders the frame (one untimed,
+ * two timed launches, min taken) and the fastest plan is kept.  Only the
+ * tiling changes with k; every plan produces the same image bits.
+ * calibrate = 2 (or env CRT_CALIB_K) keeps the given k instead. */
+static const float kCalibK[] = {1.5f, 2.0f, 2.5f, 3.0f, 4.0f, 6.0f};
+
+int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const ShardPlan &plan, float *d_out,
+                  hipStream_t stream, bool count, unsigned long long *stamps = nullptr);
+
 int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t stream) {
     if (!sc->calibrate || sc->grid_empty) return CRT_OK;
     const int walk = plan_walk(sc, st);
@@ -2169,10 +2304,54 @@ int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t
     int rc = sync_device_record(sc, &d_scene);
     if (rc != CRT_OK) return rc;
     HIP_TRY(hipDeviceSynchronize());   /* earlier frames may still read the old tile lists */
-    if ((rc = calibrate_plan(sc, d_scene, walk, stream)) != CRT_OK) return rc;
-    free_plans(sc);
     int64_t px = 0;
     const std::vector<DBucket> all = shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size, 0, 1, &px);
+    if (sc->calibrate == 2) {
+        if ((rc = calibrate_plan(sc, d_scene, walk, stream)) != CRT_OK) return rc;
+        free_plans(sc);
+        return make_tile_plan(sc, all, true, sc->full);
+    }
+    float *scratch = nullptr;
+    HIP_TRY(hipMalloc(&scratch, (size_t)sc->info.width * sc->info.height * 3 * sizeof(float)));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    float best_ms = INFINITY, best_k = kCalibK[0];
+    std::vector<std::vector<crt_hip_scene::SubTile>> best_cal;
+    auto tune = [&]() -> int {
+        HIP_TRY(hipEventCreate(&e0));
+        HIP_TRY(hipEventCreate(&e1));
+        for (const float k : kCalibK) {
+            sc->calib_k = k;
+            int r = calibrate_plan(sc, d_scene, walk, stream);
+            if (r != CRT_OK) return r;
+            free_plans(sc);
+            if ((r = make_tile_plan(sc, all, true, sc->full)) != CRT_OK) return r;
+            float ms = INFINITY;
+            for (int rep = 0; rep < 3; ++rep) {
+                HIP_TRY(hipEventRecord(e0, stream));
+                if ((r = launch_render(sc, st, sc->full, scratch, stream, false)) != CRT_OK) return r;
+                HIP_TRY(hipEventRecord(e1, stream));
+                HIP_TRY(hipEventSynchronize(e1));
+                float t = 0.f;
+                HIP_TRY(hipEventElapsedTime(&t, e0, e1));
+                if (rep > 0) ms = std::min(ms, t);
+            }
+            if (ms < best_ms) {
+                best_ms = ms;
+                best_k = k;
+                best_cal = sc->calib;
+            }
+        }
+        return CRT_OK;
+    };
+    rc = tune();
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(scratch);
+    if (rc != CRT_OK) return rc;
+    sc->calib_k = best_k;
+    sc->calib.swap(best_cal);
+    sc->calib_walk = walk;
+    free_plans(sc);
     return make_tile_plan(sc, all, true, sc->full);
 }
 
@@ -2306,7 +2485,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
 
 /* Pick and launch the kernel variant for this scene + settings. */
 int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const ShardPlan &plan, float *d_out,
-                  hipStream_t stream, bool count, unsigned long long *stamps = nullptr) {
+                  hipStream_t stream, bool count, unsigned long long *stamps) {
     const bool gi = sc->info.gi_on && sc->has_diffuse && st->diffuse_reflection_ray_count > 0;
     const bool full = gi || sc->has_secondary;
     if (gi) {
@@ -2433,7 +2612,10 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     for (const auto &kv : kEnv)
         if (const char *e = std::getenv(kv[0]))
             if (crt_hip_scene_set_option(sc.get(), kv[1], std::atoi(e)) != CRT_OK) return CRT_E_INVALID;
-    if (const char *e = std::getenv("CRT_CALIB_K")) sc->calib_k = (float)std::atof(e);
+    if (const char *e = std::getenv("CRT_CALIB_K")) {   /* a fixed split threshold instead of the tuned one */
+        sc->calib_k = (float)std::atof(e);
+        if (sc->calibrate) sc->calibrate = 2;
+    }
     if (hs.tree_on_host) sc->tile_work = tile_work_estimate(hs, (hs.width + 7) / 8, (hs.height + 7) / 8);
     {
         hipDeviceProp_t prop;
@@ -2664,6 +2846,10 @@ int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rg
         stats->height = sc->info.height;
     }
     return CRT_OK;
+}
+
+double crt_hip_plan_calib_k(const crt_hip_scene *sc) {
+    return (sc && sc->calib_walk >= 0) ? (double)sc->calib_k : 0.0;
 }
 
 int crt_hip_last_kernel_ms(crt_hip_scene *sc, double *ms) {
@@ -3000,8 +3186,10 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
     } else if (k == "events") {
         sc->record_events = value != 0;
     } else if (k == "calibrate") {
-        sc->calibrate = value != 0;
-        if (!sc->calibrate && sc->calib_walk >= 0) {   /* back to the estimate plan */
+        if (value < 0 || value > 2) return set_error(CRT_E_INVALID, "calibrate must be 0 (estimate plan), 1 (tuned) or 2 (fixed k)");
+        if (value != sc->calibrate) sc->calib_walk = sc->calibrate ? -1 : sc->calib_walk;   /* re-plan on next use */
+        sc->calibrate = value;
+        if (!sc->calibrate && !sc->calib.empty()) {   /* back to the estimate plan */
             HIP_TRY(hipDeviceSynchronize());
             sc->calib.clear();
             sc->calib_walk = -1;

@@ -369,7 +369,9 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  *   "wavefront"  0/1 (default 1): level-by-level recursion when GI is off
  *   "window"     0/1 (default 1): the plan's split tiles of <= 16 camera rays
  *                take the window walk
- *   "calibrate"  0/1 (default 1): measured-cost tile plan
+ *   "calibrate"  0 = estimate plan | 1 = measured-cost tile plan, split
+ *                threshold tuned by timing candidate plans (default) | 2 = the
+ *                threshold of env CRT_CALIB_K (default 4)
  *   "gi_refill"  0/1 (default 1): GI frames run persistent waves that refill
  *                finished lanes with the next pixel of the tile list
  *   "wf_rpw"     1..64 (default 32): rays per wave of wavefront levels >= 1 (the
@@ -381,14 +383,21 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  * the initial values (an invalid value makes scene creation fail). */
 int  crt_hip_scene_set_option(crt_hip_scene *scene, const char *name, int value);
 
-/* Diagnostics: render one full frame with per-wave s_memrealtime stamps
- * (100 MHz ticks; stamps = 2 per 8x8 tile: start, end; tile_xy = tile origin,
- * in dispatch order).  With NULL buffers returns the tile count. */
 /* Diagnostics: the full-frame tile plan in dispatch order (x, y, w, h per
  * tile) and each tile's measured walk cost (wave steps; 0 without a
  * calibrated plan).  With NULL xywh returns the tile count. */
 int  crt_hip_plan_tiles(crt_hip_scene *scene, const crt_renderer_settings *settings, int32_t *xywh, float *cost,
                         int64_t cap);
+
+/* Split threshold k of the calibrated tile plan in use (a tile is split
+ * while its measured cost exceeds k x the mean cost per wave slot; tuned per
+ * scene by timing the candidate plans' frames, or the given k with
+ * "calibrate" 2 / env CRT_CALIB_K); 0 when no calibrated plan is in use. */
+double crt_hip_plan_calib_k(const crt_hip_scene *scene);
+
+/* Diagnostics: render one full frame with per-wave s_memrealtime stamps
+ * (100 MHz ticks; stamps = 2 per 8x8 tile: start, end; tile_xy = tile origin,
+ * in dispatch order).  With NULL buffers returns the tile count. */
 
 int  crt_hip_profile_waves(crt_hip_scene *scene, const crt_renderer_settings *settings, uint64_t *stamps,
                            int64_t cap, int32_t *tile_xy);

@@ -10,7 +10,7 @@ SCN=${SCN:---frames 30}
 for r in $(seq 1 ${ROUNDS:-3}); do
   for b in $BUILDS; do
     timeout -k 10 200 env CRT_PKG=abtest/$b python3 scripts/render_loop.py $SCN > "$OUT/${b}_$r.json" 2>&1 || { echo "$b failed"; tail -5 "$OUT/${b}_$r.json"; exit 1; }
-    echo "r$r $b $(tail -1 $OUT/${b}_$r.json | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); k=d["kernel"]["default"]; print(round(k["median_ms"],4), round(k["min_ms"],4))')"
+    echo "r$r $(python3 scripts/ab_summary.py $OUT/${b}_$r.json)"
   done
 done
 if [ -n "${COUNTS:-}" ]; then
