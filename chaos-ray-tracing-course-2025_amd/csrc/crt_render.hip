@@ -783,9 +783,13 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
     int best = -1;
     best_t = 0.0f;
     float lim = INFINITY;
-    unsigned long long reach = active ? 1ull : 0ull;
     const int n = s.node_count;
     const int K = 64 / R;
+    /* reach state per depth as ray masks: lane dd of `vreach` holds the R-bit
+     * mask of the rays that entered the window's last node at depth dd - 1
+     * (bit r: ray r), i.e. the packet walk's reach bit dd of every ray */
+    const uint32_t amask = (uint32_t)__ballot(active && lead);   /* lanes 0..R-1 are (slot 0, ray r) */
+    uint32_t vreach = __lane_id() == 0 ? amask : 0u;
     const int na = __popcll(__ballot(active && lead));
     int oct = 0;
     if (2 * __popcll(__ballot(active && lead && d.x < 0.0f)) > na) oct |= 1;
@@ -811,21 +815,24 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
         const bool pass = alive & box_hit_fast(o, d, rr, cell_of(nd));
         const unsigned long long P = __ballot(pass);
         PH(0);
-        /* replay the packet walk's reach update over the window, in order */
+        /* replay the packet walk's reach update over the window, in order, on
+         * wave-uniform ray masks: node a's rays in = reach mask of its depth;
+         * an interior node sets the mask of depth + 1 to the rays that entered
+         * it (in & pass) */
         const int meta = nd.depth | (interior ? 256 : 0);
         const int kk = n - i < K ? n - i : K;
-        bool my_in = false;
+        unsigned long long IN = 0ull;   /* bit a * R + r: ray r reaches window node a */
         for (int a = 0; a < kk; ++a) {
             const int m = __builtin_amdgcn_readlane(meta, a * R);
             const int dd = m & 255;
-            const bool in = ((reach >> dd) & 1ull) != 0ull;
-            const bool e = in & (((P >> (a * R + r)) & 1ull) != 0ull);
+            const uint32_t in_m = (uint32_t)__builtin_amdgcn_readlane((int)vreach, dd);
             if (m & 256) {
-                const unsigned long long bit = 2ull << dd;
-                reach = e ? (reach | bit) : (reach & ~bit);
+                const uint32_t e_m = in_m & (uint32_t)(P >> (a * R)) & (uint32_t)rmask;
+                vreach = (int)__lane_id() == dd + 1 ? e_m : vreach;
             }
-            my_in = (a == sl) ? in : my_in;
+            IN |= (unsigned long long)in_m << (a * R);
         }
+        const bool my_in = ((IN >> __lane_id()) & 1ull) != 0ull;
         PH(1);
         if (COUNT) {
             if (my_in & alive) ++c.nodes;

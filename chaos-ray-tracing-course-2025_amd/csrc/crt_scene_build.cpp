@@ -613,6 +613,8 @@ int prepare_scene_from_tree(const crt_tree_scene_desc *d, HostScene &hs) {
             seen[ch] = 1;
             b.child[c] = ch;
             bn[ch].depth = b.depth + 1;
+            if (bn[ch].depth > 62)   /* the walks keep one reach bit per depth in 64-bit masks */
+                return set_error(CRT_E_UNSUPPORTED, "tree deeper than 62 levels (the reference builds at most 40)");
         }
         if (f == e && b.child[0] == -1 && b.child[1] == -1 && n > 1)
             return set_error(CRT_E_INVALID, "interior node without children");
