@@ -17,7 +17,7 @@ PKG_DIR = Path(__file__).resolve().parent.parent          # chaos-ray-tracing-co
 LIB_PATH = PKG_DIR / "lib" / "libcrt_hip.so"
 
 CRT_OK = 0
-CRT_E_INVALID, CRT_E_PARSE, CRT_E_UNSUPPORTED, CRT_E_HIP, CRT_E_NOMEM, CRT_E_IO = -1, -2, -3, -4, -5, -6
+CRT_E_INVALID, CRT_E_PARSE, CRT_E_UNSUPPORTED, CRT_E_HIP, CRT_E_NOMEM, CRT_E_IO, CRT_E_STATE = -1, -2, -3, -4, -5, -6, -7
 
 MATERIAL_DIFFUSE, MATERIAL_REFLECTIVE, MATERIAL_REFRACTIVE, MATERIAL_CONSTANT = 0, 1, 2, 3
 TEXTURE_ALBEDO, TEXTURE_EDGES, TEXTURE_CHECKER, TEXTURE_BITMAP = 0, 1, 2, 3

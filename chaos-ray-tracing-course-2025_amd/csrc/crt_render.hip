@@ -1508,6 +1508,8 @@ struct WLevel {
     WNode *nodes;            /* by ray id */
     DVec4 *cols;             /* by ray id */
     int32_t rpw;             /* levels >= 1: rays per wave (lanes rpw..63 start idle and take donated pieces) */
+    int32_t out_cap;         /* children this level may queue (recorded level sizes: exactly the next level) */
+    int32_t *overflow;       /* set when a level queued more children than out_cap (none written) */
 };
 
 template <int TRAV, bool LEVEL0, bool COUNT>
@@ -1621,8 +1623,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
     const int total = __popcll(b1) + __popcll(b2);
     if (total > 0) {
         int base = 0;
-        if (lane == __ffsll((long long)(b1 | b2)) - 1) base = atomicAdd(lv.out_count, total);
+        if (lane == __ffsll((long long)(b1 | b2)) - 1) {
+            base = atomicAdd(lv.out_count, total);
+            if (base + total > lv.out_cap) atomicOr(lv.overflow, 1);
+        }
         base = __shfl(base, __ffsll((long long)(b1 | b2)) - 1);
+        if (base + total > lv.out_cap) nch = 0;   /* never past the queue (the frame is then reported, not used) */
         /* a lane's children side by side */
         const int k0 = base + __popcll(b1 & lt) + __popcll(b2 & lt);
         const int k1 = k0 + 1;
@@ -1884,9 +1890,41 @@ struct WfBuffers {
     int64_t cap = 0;             /* ray ids */
     crt_amd::WRay *q[2] = {nullptr, nullptr};
     int64_t qcap[2] = {0, 0};
-    int32_t *counts = nullptr;   /* children queued per level */
+    int32_t *counts = nullptr;   /* children queued per level; counts[count_cap - 1]: overflow flag */
     int count_cap = 0;
+    /* Level sizes of the last frame traced with host read-backs, and what they
+     * depend on (settings, tile list): a frame's level sizes are a function of
+     * its rays alone, so later frames with the same key launch every level
+     * with these sizes and no host sync (render_wavefront). */
+    struct Rec {
+        std::vector<int32_t> sizes;   /* rays of levels 1, 2, ... */
+        crt_renderer_settings st{};
+        int ntiles = 0;
+    };
+    std::map<const void *, Rec> recs;   /* by tile list (device pointer; cleared when plans are freed) */
+    /* overflow flag of recorded-size frames: device word, copied into pinned
+     * host memory behind each such frame and read once that copy is done */
+    int32_t *d_flag = nullptr;
+    int32_t *h_flag = nullptr;
+    hipEvent_t flag_ev = nullptr;
+    bool flag_pending = false;
+    /* recorded-size frames captured as HIP graphs, by everything their
+     * launches bake in (cleared whenever a buffer, tile list or record changes) */
+    struct Graph {
+        const void *tiles;
+        crt_renderer_settings st;
+        const float *out;
+        hipStream_t stream;
+        const void *scene;
+        hipGraphExec_t exec;
+    };
+    std::vector<Graph> graphs;
 };
+
+void wf_graphs_clear(WfBuffers &w) {
+    for (auto &g : w.graphs) (void)hipGraphExecDestroy(g.exec);
+    w.graphs.clear();
+}
 
 /* Deepest recursion the wavefront path accepts (levels are launched one by one). */
 constexpr int kWfMaxDepth = 4096;
@@ -1952,6 +1990,9 @@ struct crt_hip_scene {
     const int32_t *dt_ref_children = nullptr, *dt_ref_leaf_tris = nullptr;
     const int64_t *dt_ref_leaf_off = nullptr;
     int wavefront = 1;             /* level-by-level recursion when GI is off (env CRT_WAVEFRONT) */
+    int wf_graph = 1;              /* recorded-size wavefront frames replayed from captured HIP graphs (option "wf_graph") */
+    int wf_replay = 1;             /* wavefront frames after the first: 1 recorded level sizes, 0 read back every level,
+                                    * 2 recorded sizes minus one (tests: forces the overflow path) (option "wf_replay") */
     int wf_rays_per_wave = 32;     /* rays per wave of wavefront levels >= 1, coop walks (env CRT_WF_RPW, option "wf_rpw"); C3: 64 4.70, 32 4.53, 16 4.58 ms */
     WfBuffers wf;
 };
@@ -2183,6 +2224,8 @@ int calibrate_plan(crt_hip_scene *sc, const DeviceScene *d_scene, int walk, hipS
 void free_plans(crt_hip_scene *sc) {
     for (void *p : sc->plan_allocs) (void)hipFree(p);
     sc->plan_allocs.clear();
+    sc->wf.recs.clear();   /* keyed by the tile lists' device pointers */
+    wf_graphs_clear(sc->wf);
     sc->full = ShardPlan{};
     sc->shard_plans.clear();
     sc->compact_plans.clear();
@@ -2302,6 +2345,7 @@ static const float kCalibK[] = {1.5f, 2.0f, 2.5f, 3.0f, 4.0f, 6.0f};
 
 int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const ShardPlan &plan, float *d_out,
                   hipStream_t stream, bool count, unsigned long long *stamps = nullptr);
+bool wf_overflowed(WfBuffers &w, bool wait);
 
 int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t stream) {
     if (!sc->calibrate || sc->grid_empty) return CRT_OK;
@@ -2338,6 +2382,7 @@ int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t
                 if ((r = launch_render(sc, st, sc->full, scratch, stream, false)) != CRT_OK) return r;
                 HIP_TRY(hipEventRecord(e1, stream));
                 HIP_TRY(hipEventSynchronize(e1));
+                (void)wf_overflowed(sc->wf, true);   /* a wrong trial frame only drops the recorded level sizes */
                 float t = 0.f;
                 HIP_TRY(hipEventElapsedTime(&t, e0, e1));
                 if (rep > 0) ms = std::min(ms, t);
@@ -2375,6 +2420,7 @@ DSettings to_dsettings(const crt_renderer_settings *st) {
 
 int wf_grow_ids(WfBuffers &w, int64_t need, int64_t used, hipStream_t stream) {
     if (need <= w.cap) return CRT_OK;
+    wf_graphs_clear(w);
     const int64_t cap = std::max<int64_t>(need, 2 * w.cap);
     void *pn = nullptr, *pc = nullptr;
     HIP_TRY(hipMalloc(&pn, (size_t)cap * sizeof(WNode)));
@@ -2394,6 +2440,7 @@ int wf_grow_ids(WfBuffers &w, int64_t need, int64_t used, hipStream_t stream) {
 
 int wf_grow_queue(WfBuffers &w, int k, int64_t need) {
     if (need <= w.qcap[k]) return CRT_OK;
+    wf_graphs_clear(w);
     const int64_t cap = std::max<int64_t>(need, 2 * w.qcap[k]);
     if (w.q[k]) (void)hipFree(w.q[k]);
     w.q[k] = nullptr;
@@ -2405,16 +2452,44 @@ int wf_grow_queue(WfBuffers &w, int k, int64_t need) {
 }
 
 void wf_free(WfBuffers &w) {
-    for (void *p : {(void *)w.nodes, (void *)w.cols, (void *)w.q[0], (void *)w.q[1], (void *)w.counts})
+    wf_graphs_clear(w);
+    for (void *p : {(void *)w.nodes, (void *)w.cols, (void *)w.q[0], (void *)w.q[1], (void *)w.counts, (void *)w.d_flag})
         if (p) (void)hipFree(p);
+    if (w.h_flag) (void)hipHostFree(w.h_flag);
+    if (w.flag_ev) (void)hipEventDestroy(w.flag_ev);
     w = WfBuffers{};
 }
 
-/* One frame of the wavefront path (see k_wf_level).  The host reads each
- * level's queue length before launching the next level, so the call returns
- * after the last level has been traced (composition is left enqueued). */
-int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &plan, float *d_out,
-                     hipStream_t stream, bool count, const DeviceScene *d_scene, int sec, int primary) {
+/* The last recorded-size frame's overflow flag, if its copy has landed
+ * (wait: block until it has).  Returns true when that frame overflowed; the
+ * recorded sizes are then dropped, so the next frame reads its sizes back. */
+bool wf_overflowed(WfBuffers &w, bool wait) {
+    if (!w.flag_pending) return false;
+    if (wait) {
+        if (hipEventSynchronize(w.flag_ev) != hipSuccess) return false;
+    } else if (hipEventQuery(w.flag_ev) != hipSuccess) {
+        return false;
+    }
+    w.flag_pending = false;
+    if (*w.h_flag == 0) return false;
+    *w.h_flag = 0;
+    w.recs.clear();
+    wf_graphs_clear(w);
+    return true;
+}
+
+/* One frame of the wavefront path (see k_wf_level).  A level's size is
+ * known only once the level before it has run, so the first frame of a
+ * (settings, tile list) reads each level's queue length back before launching
+ * the next level (one host sync per level) and records the sizes.  The sizes
+ * are a function of the frame's rays alone, so every later frame with the same
+ * key launches all levels back to back with the recorded sizes, no host sync:
+ * each level may queue exactly the recorded size of the next, and a level
+ * that would queue more sets an overflow flag instead (checked behind the
+ * frame: crt_hip_render re-renders that frame with read-backs, the device-side
+ * entry points report it on the next call). */
+int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_settings *st, const ShardPlan &plan,
+                     float *d_out, hipStream_t stream, bool count, const DeviceScene *d_scene, int sec, int primary) {
     WfBuffers &w = sc->wf;
     /* levels 0..max_ray_depth are traced (a child deeper than max_ray_depth is
      * never queued, crt_renderer.cpp:47-48), so the loop below always drains
@@ -2422,6 +2497,9 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
     if (ds.max_ray_depth > (uint32_t)kWfMaxDepth)
         return set_error(CRT_E_UNSUPPORTED, "max_ray_depth > " + std::to_string(kWfMaxDepth) +
                                                 " with reflective/refractive materials is not supported");
+    if (wf_overflowed(w, false))
+        return set_error(CRT_E_STATE, "a wavefront level outgrew its recorded size in the previous frame; "
+                                         "that frame is wrong (sizes are now read back again)");
     const int kMaxLevels = (int)ds.max_ray_depth + 2;
     if (!w.counts || w.count_cap < kMaxLevels) {
         if (w.counts) (void)hipFree(w.counts);
@@ -2430,14 +2508,59 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
         HIP_TRY(hipMalloc(&p, (size_t)kMaxLevels * sizeof(int32_t)));
         w.counts = static_cast<int32_t *>(p);
         w.count_cap = kMaxLevels;
+        wf_graphs_clear(w);
     }
-    HIP_TRY(hipMemsetAsync(w.counts, 0, kMaxLevels * sizeof(int32_t), stream));
+    if (!w.d_flag) {
+        void *p = nullptr;
+        HIP_TRY(hipMalloc(&p, sizeof(int32_t)));
+        w.d_flag = static_cast<int32_t *>(p);
+        HIP_TRY(hipMemsetAsync(w.d_flag, 0, sizeof(int32_t), stream));
+        HIP_TRY(hipHostMalloc(&p, sizeof(int32_t), hipHostMallocDefault));
+        w.h_flag = static_cast<int32_t *>(p);
+        *w.h_flag = 0;
+        HIP_TRY(hipEventCreateWithFlags(&w.flag_ev, hipEventDisableTiming));
+    }
     const int64_t n0 = (int64_t)plan.ntiles * 64;
+    const auto rit = w.recs.find((const void *)plan.d_tiles);
+    const bool replay = !count && sc->wf_replay && rit != w.recs.end() && rit->second.ntiles == plan.ntiles &&
+                        std::memcmp(&rit->second.st, st, sizeof *st) == 0;
+    static const std::vector<int32_t> kNone;
+    const std::vector<int32_t> &rec = replay ? rit->second.sizes : kNone;
     int rc;
-    if ((rc = wf_grow_ids(w, 3 * n0, 0, stream)) != CRT_OK) return rc;
-    if ((rc = wf_grow_queue(w, 0, 2 * n0)) != CRT_OK) return rc;
+    int64_t qneed = 2 * n0, ids = 3 * n0;
+    if (replay) {
+        int64_t tot = n0, mx = 0;
+        for (int32_t n : rec) {
+            tot += n;
+            mx = std::max<int64_t>(mx, n);
+        }
+        qneed = std::max<int64_t>(mx, 1);
+        ids = tot;
+    }
+    if ((rc = wf_grow_ids(w, ids, 0, stream)) != CRT_OK) return rc;
+    if ((rc = wf_grow_queue(w, 0, qneed)) != CRT_OK) return rc;
+    if (replay && (rc = wf_grow_queue(w, 1, qneed)) != CRT_OK) return rc;
+    /* a recorded-size frame is a fixed launch sequence: replayed from a HIP
+     * graph captured the first time (one launch instead of ~2 per level) */
+    if (replay && sc->wf_graph) {
+        for (const auto &g : w.graphs)
+            if (g.tiles == (const void *)plan.d_tiles && g.out == d_out && g.stream == stream &&
+                g.scene == (const void *)d_scene && std::memcmp(&g.st, st, sizeof *st) == 0) {
+                HIP_TRY(hipGraphLaunch(g.exec, stream));
+                HIP_TRY(hipEventRecord(w.flag_ev, stream));
+                w.flag_pending = true;
+                return CRT_OK;
+            }
+    }
+    const bool capture = replay && sc->wf_graph;
+    if (capture) HIP_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
+    auto cap_of = [](int64_t c) { return (int32_t)std::min<int64_t>(c, INT32_MAX); };
+    std::vector<int32_t> sizes;
+    auto enqueue = [&]() -> int {
+    HIP_TRY(hipMemsetAsync(w.counts, 0, kMaxLevels * sizeof(int32_t), stream));
     unsigned long long *cnt = sc->d_counters;
-    WLevel lv{nullptr, 0, 0, w.q[0], w.counts, (int32_t)n0, w.nodes, w.cols, 64};
+    WLevel lv{nullptr, 0, 0, w.q[0], w.counts, (int32_t)n0, w.nodes, w.cols, 64,
+              replay ? (rec.empty() ? 0 : rec[0]) : cap_of(w.qcap[0]), w.d_flag};
     const int blocks0 = (plan.ntiles + 3) / 4;
 #define CRT_WF0(T, COUNT)                                                                                   \
     hipLaunchKernelGGL((k_wf_level<T, true, COUNT>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,      \
@@ -2454,17 +2577,26 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
     std::vector<std::pair<int64_t, int64_t>> levels;   /* (first id, count) of levels >= 1 */
     int64_t base = n0;
     int cur = 0;
+    const int rpw = std::min(64, std::max(1, sc->wf_rays_per_wave));   /* coop walks: idle lanes take donated pieces */
     for (int L = 1; L < kMaxLevels; ++L) {
         int32_t n = 0;
-        HIP_TRY(hipMemcpyAsync(&n, w.counts + (L - 1), sizeof n, hipMemcpyDeviceToHost, stream));
-        HIP_TRY(hipStreamSynchronize(stream));
-        if (n == 0) break;
-        if (base + 3 * (int64_t)n > INT32_MAX) return set_error(CRT_E_UNSUPPORTED, "wavefront ray ids exceed 2^31");
-        if ((rc = wf_grow_ids(w, base + 3 * (int64_t)n, base, stream)) != CRT_OK) return rc;
-        if ((rc = wf_grow_queue(w, cur ^ 1, 2 * (int64_t)n)) != CRT_OK) return rc;
-        /* coop walks: fewer rays per wave put idle lanes on the long walks (donated pieces) */
-        const int rpw = std::min(64, std::max(1, sc->wf_rays_per_wave));
-        WLevel l{w.q[cur], n, L, w.q[cur ^ 1], w.counts + L, (int32_t)(base + n), w.nodes, w.cols, rpw};
+        int32_t out_cap = 0;
+        if (replay) {
+            if (L - 1 >= (int)rec.size()) break;
+            n = rec[L - 1];
+            out_cap = L < (int)rec.size() ? rec[L] : 0;
+        } else {
+            HIP_TRY(hipMemcpyAsync(&n, w.counts + (L - 1), sizeof n, hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+            if (n == 0) break;
+            if (base + 3 * (int64_t)n > INT32_MAX) return set_error(CRT_E_UNSUPPORTED, "wavefront ray ids exceed 2^31");
+            if ((rc = wf_grow_ids(w, base + 3 * (int64_t)n, base, stream)) != CRT_OK) return rc;
+            if ((rc = wf_grow_queue(w, cur ^ 1, 2 * (int64_t)n)) != CRT_OK) return rc;
+            out_cap = cap_of(w.qcap[cur ^ 1]);
+            sizes.push_back(n);
+        }
+        WLevel l{w.q[cur], n, L, w.q[cur ^ 1], w.counts + L, (int32_t)(base + n), w.nodes, w.cols, rpw, out_cap,
+                 w.d_flag};
         const int64_t waves = ((int64_t)n + rpw - 1) / rpw;
         const int blocks = (int)((waves + 3) / 4);
 #define CRT_WF(SEC, COUNT)                                                                                  \
@@ -2487,6 +2619,41 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const ShardPlan &pl
     hipLaunchKernelGGL(k_wf_pixels, dim3(blocks0), dim3(256), 0, stream, w.nodes, w.cols, plan.d_tiles,
                        plan.ntiles, d_out);
     HIP_TRY(hipGetLastError());
+    if (replay) {
+        HIP_TRY(hipMemcpyAsync(w.h_flag, w.d_flag, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipMemsetAsync(w.d_flag, 0, sizeof(int32_t), stream));
+    }
+    return CRT_OK;
+    };
+    rc = enqueue();
+    if (capture) {
+        hipGraph_t graph = nullptr;
+        const hipError_t e = hipStreamEndCapture(stream, &graph);
+        if (rc != CRT_OK) {
+            if (graph) (void)hipGraphDestroy(graph);
+            return rc;
+        }
+        if (e != hipSuccess) return set_error(CRT_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+        hipGraphExec_t exec = nullptr;
+        const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (ei != hipSuccess) return set_error(CRT_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
+        w.graphs.push_back(WfBuffers::Graph{(const void *)plan.d_tiles, *st, d_out, stream, (const void *)d_scene, exec});
+        HIP_TRY(hipGraphLaunch(exec, stream));
+    } else if (rc != CRT_OK) {
+        return rc;
+    }
+    if (replay) {
+        HIP_TRY(hipEventRecord(w.flag_ev, stream));
+        w.flag_pending = true;
+    } else if (!count && sc->wf_replay) {
+        WfBuffers::Rec &r = w.recs[(const void *)plan.d_tiles];
+        if (sc->wf_replay == 2)
+            for (int32_t &n : sizes) n = n > 1 ? n - 1 : n;
+        r.sizes.swap(sizes);
+        r.st = *st;
+        r.ntiles = plan.ntiles;
+    }
     return CRT_OK;
 }
 
@@ -2521,7 +2688,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     int sec = sc->secondary;
     if (sec == 0) sec = (gi || !pruned) ? 4 : 10;
     if (full && !gi && sc->wavefront && !stamps)
-        return render_wavefront(sc, ds, plan, d_out, stream, count, d_scene, sec, camera_walk(sc, sc->traversal));
+        return render_wavefront(sc, ds, st, plan, d_out, stream, count, d_scene, sec, camera_walk(sc, sc->traversal));
     /* frame-stack kernel: one walk for every ray */
     int trav = full ? sec : camera_walk(sc, sc->traversal);
     if (trav == 13 && !plan.has_small) trav = 12;   /* no split tiles: the leaner packet-only kernel */
@@ -2831,6 +2998,11 @@ int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rg
     if (rc != CRT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(rgb_out, sc->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
+    if (wf_overflowed(sc->wf, true)) {   /* recorded level sizes did not hold: render again with read-backs */
+        if ((rc = render_into(sc, st, sc->d_out, sc->stream, false)) != CRT_OK) return rc;
+        HIP_TRY(hipMemcpyAsync(rgb_out, sc->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
+        HIP_TRY(hipStreamSynchronize(sc->stream));
+    }
 #ifdef CRT_AB_PHASES
     {
         unsigned long long ph[16];
@@ -3187,6 +3359,14 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         sc->window_walk = value != 0;
     } else if (k == "gi_refill") {
         sc->gi_refill = value != 0;
+    } else if (k == "wf_graph") {
+        sc->wf_graph = value != 0;
+        wf_graphs_clear(sc->wf);
+    } else if (k == "wf_replay") {
+        if (value < 0 || value > 2) return set_error(CRT_E_INVALID, "wf_replay must be 0, 1 or 2");
+        sc->wf_replay = value;
+        sc->wf.recs.clear();
+        wf_graphs_clear(sc->wf);
     } else if (k == "wf_rpw") {
         if (value < 1 || value > 64) return set_error(CRT_E_INVALID, "wf_rpw must be 1..64");
         sc->wf_rays_per_wave = value;

@@ -35,6 +35,7 @@ extern "C" {
 #define CRT_E_HIP         (-4)   /* HIP runtime error                         */
 #define CRT_E_NOMEM       (-5)
 #define CRT_E_IO          (-6)
+#define CRT_E_STATE       (-7)   /* an earlier asynchronous frame was rendered wrongly (see the message) */
 
 /* ---- scene description (the reference's crt::Scene inputs, flat) ---- */
 typedef struct crt_vec3 { float x, y, z; } crt_vec3;
@@ -376,6 +377,12 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  *                finished lanes with the next pixel of the tile list
  *   "wf_rpw"     1..64 (default 32): rays per wave of wavefront levels >= 1 (the
  *                other lanes start idle and take donated pieces)
+ *   "wf_replay"  1 (default): a wavefront frame whose settings and tile list
+ *                were rendered before launches every level with the recorded
+ *                level sizes, no host read-back | 0: read every level's size
+ *                back | 2: tests only, recorded sizes minus one (overflow path)
+ *   "wf_graph"   0/1 (default 1): such frames run as a HIP graph captured on
+ *                their first replay (per tile list, settings, output, stream)
  *   "trace_walk" 0 = reference order, 1 = pruned per-ray walk (crt_hip_trace_batch)
  *   "events"     0/1 (default 1): start/stop events around every render
  * Environment variables CRT_TRAVERSAL, CRT_SECONDARY, CRT_WAVEFRONT, CRT_WINDOW,

@@ -228,3 +228,49 @@ def test_compact_shards_lossless(N, devbuf, name, w, h, over, bucket, shards):
     if name.startswith("14-01") and w == 1920:
         frac = float(mask.mean())
         assert 0.15 < frac < 0.4, frac     # the dragon's root cell covers ~28% of the C2 frame
+
+
+@pytest.mark.parametrize("graph", [1, 0], ids=["graph", "no-graph"])
+def test_c3_recorded_level_sizes(N, devbuf, graph):
+    """Wavefront frames after the first launch every level with the recorded
+    level sizes and no host read-back (as a captured HIP graph, or launch by
+    launch): the same bits as the read-back frame, through the host and the
+    device entry points, and for a second tile list (a shard) next to the
+    full frame's."""
+    sc = scene_npz("11-01-refractive__scene8").set_resolution(320, 180)
+    st = N.RendererSettings.default(max_ray_depth=8)
+    ref = N.HipScene(sc, wf_replay=0).render(st)
+    g = N.HipScene(sc, wf_graph=graph)
+    for _ in range(3):
+        assert np.array_equal(bits(g.render(st)), bits(ref))
+    d = devbuf.alloc(ref.nbytes)
+    for _ in range(2):
+        g.render_device(st, d)
+        devbuf.sync()
+        assert np.array_equal(bits(devbuf.download(d, ref.shape, np.float32)), bits(ref))
+    stride = g.shard_stride(2)
+    packed = devbuf.alloc(4 * stride)
+    outs = []
+    for _ in range(2):
+        g.render_shard(st, 1, 2, packed)
+        devbuf.sync()
+        outs.append(devbuf.download(packed, (stride,), np.float32))
+        assert np.array_equal(bits(g.render(st)), bits(ref))
+    assert np.array_equal(bits(outs[0]), bits(outs[1]))
+
+
+def test_c3_recorded_sizes_overflow(N, devbuf):
+    """A frame whose levels outgrow the recorded sizes (forced: wf_replay 2
+    records every size one short) is detected: crt_hip_render renders it again
+    with read-backs, a device-side render reports it on the next call."""
+    sc = scene_npz("11-01-refractive__scene8").set_resolution(160, 90)
+    st = N.RendererSettings.default(max_ray_depth=8)
+    ref = N.HipScene(sc, wf_replay=0).render(st)
+    g = N.HipScene(sc, wf_replay=2)
+    assert np.array_equal(bits(g.render(st)), bits(ref))      # read-back frame, sizes recorded one short
+    assert np.array_equal(bits(g.render(st)), bits(ref))      # replay overflows: rendered again (and re-recorded)
+    d = devbuf.alloc(ref.nbytes)
+    g.render_device(st, d)                                    # replay overflows (reported on the next call)
+    devbuf.sync()
+    with pytest.raises(N.CrtError):
+        g.render_device(st, d)
