@@ -547,7 +547,7 @@ def main():
                        "e2e_note": ("crt_hip_render into a pinned host buffer: render + D2H of the fp32 image, "
                                     "the reference's render_image call (main.cpp:37-43)") if e2e is not None else None,
                        "check": check, "build_id": build_id,
-                       "plan_calib_k": round(gpu.plan_calib_k(), 3)},
+                       "plan": gpu.plan_info()},
             "roofline": roof,
             "secondary": secondary,
             "cpu_baseline": cpu,

@@ -201,7 +201,7 @@ EXPORTS = [
     ("crt_hip_trace_batch", C.c_int, [_P, _P, C.c_int64, _P]),
     ("crt_hip_count_work", C.c_int, [_P, C.POINTER(RendererSettings), C.POINTER(WorkCounts)]),
     ("crt_hip_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_double)]),
-    ("crt_hip_plan_calib_k", C.c_double, [_P]),
+    ("crt_hip_plan_info", C.c_int, [_P, _P]),
     ("crt_hip_wave_counts", C.c_int, [_P, C.POINTER(WaveCounts)]),
     ("crt_hip_scene_set_option", C.c_int, [_P, C.c_char_p, C.c_int]),
     ("crt_hip_profile_waves", C.c_int, [_P, C.POINTER(RendererSettings), _P, C.c_int64, _P]),
@@ -439,6 +439,10 @@ class HostScene:
 # --------------------------------------------------------------------------
 #  device scene (HBM-resident) and rendering
 # --------------------------------------------------------------------------
+class PlanInfo(C.Structure):
+    _fields_ = [("calib_k", C.c_double), ("tiles", C.c_int32), ("small_tiles", C.c_int32)]
+
+
 class HipScene:
     def __init__(self, src, device: int = 0, tree_build: str = "auto", **options):
         """tree_build: "auto" | "host" | "device" — where the acceleration tree is
@@ -561,9 +565,11 @@ class HipScene:
         _check(lib().crt_hip_unpack_shards_rgb8(self._h, count, C.c_void_p(d_gathered), C.c_void_p(d_rgb8),
                                                 C.c_void_p(stream or 0)))
 
-    def plan_calib_k(self) -> float:
-        """Split threshold of the calibrated plan in use (0: none yet / estimate plan)."""
-        return float(lib().crt_hip_plan_calib_k(self._h))
+    def plan_info(self) -> dict:
+        """The full-frame plan in use (crt_hip_plan_info): calib_k, tiles, small_tiles."""
+        out = PlanInfo()
+        _check(lib().crt_hip_plan_info(self._h, C.byref(out)))
+        return {f: getattr(out, f) for f, _ in PlanInfo._fields_}
 
     def last_kernel_ms(self) -> float:
         v = C.c_double()

@@ -3027,8 +3027,13 @@ int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rg
     return CRT_OK;
 }
 
-double crt_hip_plan_calib_k(const crt_hip_scene *sc) {
-    return (sc && sc->calib_walk >= 0) ? (double)sc->calib_k : 0.0;
+int crt_hip_plan_info(const crt_hip_scene *sc, crt_plan_info *out) {
+    if (!sc || !out) return set_error(CRT_E_INVALID, "null argument");
+    std::memset(out, 0, sizeof *out);
+    out->calib_k = (sc->calib_walk >= 0 && !sc->calib.empty()) ? (double)sc->calib_k : 0.0;
+    out->tiles = sc->full.ntiles;
+    for (const Tile &t : sc->full.tiles) out->small_tiles += t.w * t.h <= 16 ? 1 : 0;
+    return CRT_OK;
 }
 
 int crt_hip_last_kernel_ms(crt_hip_scene *sc, double *ms) {
@@ -3359,6 +3364,11 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         sc->window_walk = value != 0;
     } else if (k == "gi_refill") {
         sc->gi_refill = value != 0;
+    } else if (k == "calib_k_milli") {   /* a fixed split threshold k = value / 1000 (calibrate 2) */
+        if (value <= 0) return set_error(CRT_E_INVALID, "calib_k_milli must be > 0");
+        sc->calib_k = (float)value / 1000.0f;
+        sc->calibrate = 2;
+        sc->calib_walk = -1;
     } else if (k == "wf_graph") {
         sc->wf_graph = value != 0;
         wf_graphs_clear(sc->wf);

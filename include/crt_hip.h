@@ -383,6 +383,7 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  *                back | 2: tests only, recorded sizes minus one (overflow path)
  *   "wf_graph"   0/1 (default 1): such frames run as a HIP graph captured on
  *                their first replay (per tile list, settings, output, stream)
+ *   "calib_k_milli" k x 1000: a fixed split threshold (sets "calibrate" 2)
  *   "trace_walk" 0 = reference order, 1 = pruned per-ray walk (crt_hip_trace_batch)
  *   "events"     0/1 (default 1): start/stop events around every render
  * Environment variables CRT_TRAVERSAL, CRT_SECONDARY, CRT_WAVEFRONT, CRT_WINDOW,
@@ -396,11 +397,16 @@ int  crt_hip_scene_set_option(crt_hip_scene *scene, const char *name, int value)
 int  crt_hip_plan_tiles(crt_hip_scene *scene, const crt_renderer_settings *settings, int32_t *xywh, float *cost,
                         int64_t cap);
 
-/* Split threshold k of the calibrated tile plan in use (a tile is split
- * while its measured cost exceeds k x the mean cost per wave slot; tuned per
- * scene by timing the candidate plans' frames, or the given k with
- * "calibrate" 2 / env CRT_CALIB_K); 0 when no calibrated plan is in use. */
-double crt_hip_plan_calib_k(const crt_hip_scene *scene);
+/* The full-frame tile plan in use.  A calibrated plan splits a tile whose
+ * measured cost exceeds calib_k x the mean cost per wave slot into 4x4 / 2x2
+ * tiles (window walk); k is tuned per scene by timing the candidate plans'
+ * frames (or fixed: "calibrate" 2 with env CRT_CALIB_K / "calib_k_milli"). */
+typedef struct crt_plan_info {
+    double  calib_k;       /* 0: no calibrated plan */
+    int32_t tiles;         /* waves of the full-frame plan */
+    int32_t small_tiles;   /* split tiles of <= 16 pixels */
+} crt_plan_info;
+int  crt_hip_plan_info(const crt_hip_scene *scene, crt_plan_info *out);
 
 /* Diagnostics: render one full frame with per-wave s_memrealtime stamps
  * (100 MHz ticks; stamps = 2 per 8x8 tile: start, end; tile_xy = tile origin,
