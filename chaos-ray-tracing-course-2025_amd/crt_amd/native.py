@@ -152,7 +152,8 @@ class WorkCounts(C.Structure):
 class WaveCounts(C.Structure):
     _fields_ = [("node_steps", C.c_uint64), ("triangle_steps", C.c_uint64), ("edge_steps", C.c_uint64),
                 ("waves", C.c_uint64), ("box_steps", C.c_uint64), ("pass_steps", C.c_uint64),
-                ("window_waves", C.c_uint64)]
+                ("window_waves", C.c_uint64), ("window_steps", C.c_uint64), ("window_slots", C.c_uint64),
+                ("window_reached", C.c_uint64), ("window_tri_rounds", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: int(getattr(self, k)) for k, _ in self._fields_}

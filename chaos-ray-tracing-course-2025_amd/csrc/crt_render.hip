@@ -78,26 +78,13 @@ __device__ __forceinline__ T load_global(const T *p, int i) {
 #endif
 }
 
-/* timing experiments only (A/B builds with -DCRT_AB_PHASES): per-phase
- * s_memtime sums of the walks, printed by crt_hip_render */
-#ifdef CRT_AB_PHASES
-__device__ unsigned long long g_phase[16];
-#define PH_DECL unsigned long long ph_t = __builtin_amdgcn_s_memtime(), ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define PH(k) do { const unsigned long long ph_n = __builtin_amdgcn_s_memtime(); ph_acc[k] += ph_n - ph_t; ph_t = ph_n; } while (0)
-#define PH_COUNT(k) (++ph_acc[k])
-#define PH_FLUSH(base) do { if (__lane_id() == 0) for (int ph_k = 0; ph_k < 8; ++ph_k) atomicAdd(&g_phase[(base) + ph_k], ph_acc[ph_k]); } while (0)
-#else
-#define PH_DECL
-#define PH(k)
-#define PH_COUNT(k)
-#define PH_FLUSH(base)
-#endif
 
 struct LaneCounts {
     uint32_t traversals, nodes, tris, hits;
     /* wave-uniform steps of the packet walks (kept by every lane, added once per wave) */
     uint32_t wave_nodes, wave_tris, wave_edges;
     uint32_t wave_box, wave_pass;   /* packet walks: node steps with a box test run / with a lane passing */
+    uint32_t win_steps, win_slots, win_reached, win_rounds;   /* window walk (crt_wave_counts) */
 };
 
 /* ---------------------------------------------------------------------- */
@@ -541,40 +528,6 @@ __device__ __forceinline__ void leaf_grouped(const DeviceScene &s, int first, in
     const Vec ro = vec(rb.x, rb.y, rb.z), rd = vec(ra.x, ra.y, ra.z);
     float lt = ra.w;
     int ls = __float_as_int(rb.w);
-#ifdef CRT_AB_GPREF
-    /* two rounds in flight: each buffer is refilled right after its test */
-    const int lst = first + cnt - 1;
-    int sa = first + g < lst ? first + g : lst, sb = first + g + T < lst ? first + g + T : lst;
-    DTriGeo ta = load_global(s.slots, sa), tb = load_global(s.slots, sb);
-    uint8_t ca = load_global(s.slot_cull, sa), cb = load_global(s.slot_cull, sb);
-    for (int k0 = 0; k0 < cnt; k0 += 2 * T) {
-        float t;
-        if (COUNT) ++c.wave_tris;
-        if (qok & (k0 + g < cnt)) {
-            if (COUNT) ++c.tris;
-            if (tri_plane(ro, rd, ta, ca != 0, t) && key_better(t, sa, lt, ls) && tri_edges(ro, rd, ta, t)) {
-                lt = t;
-                ls = sa;
-            }
-        }
-        sa = first + k0 + g + 2 * T < lst ? first + k0 + g + 2 * T : lst;
-        ta = load_global(s.slots, sa);
-        ca = load_global(s.slot_cull, sa);
-        if (k0 + T < cnt) {
-            if (COUNT) ++c.wave_tris;
-            if (qok & (k0 + T + g < cnt)) {
-                if (COUNT) ++c.tris;
-                if (tri_plane(ro, rd, tb, cb != 0, t) && key_better(t, sb, lt, ls) && tri_edges(ro, rd, tb, t)) {
-                    lt = t;
-                    ls = sb;
-                }
-            }
-        }
-        sb = first + k0 + g + 3 * T < lst ? first + k0 + g + 3 * T : lst;
-        tb = load_global(s.slots, sb);
-        cb = load_global(s.slot_cull, sb);
-    }
-#else
     for (int k0 = 0; k0 < cnt; k0 += T) {
         if (COUNT) ++c.wave_tris;
         const int k = k0 + g;
@@ -590,7 +543,6 @@ __device__ __forceinline__ void leaf_grouped(const DeviceScene &s, int first, in
             }
         }
     }
-#endif
     for (int off = G; off < 64; off <<= 1) {
         const float ot = __shfl_xor(lt, off);
         const int os = __shfl_xor(ls, off);
@@ -635,9 +587,7 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
     face_cache_init(fc);
     int i = 0;
     PNode cur = load_scalar(nodes, 0);
-    PH_DECL
     while (i < n) {
-        PH_COUNT(7);
         const bool interior = cur.b < 0;
         const int i1 = i + 1 < n ? i + 1 : last;
         const int i2 = interior ? (cur.a < n ? cur.a : last) : i1;
@@ -661,7 +611,6 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
             if (COUNT && alive) ++c.nodes;
         }
         const unsigned long long pm = __ballot(pass);
-        PH(0);
         if (COUNT && pm != 0ull) ++c.wave_pass;
         if (interior) {
             if (pm != 0ull) {
@@ -675,13 +624,8 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
             }
             continue;
         }
-#if defined(CRT_AB_NOTRI) && (CRT_AB_NOTRI & 2)   /* timing experiments only: no triangle phase (wrong image) */
-        if (false) {
-#else
         if (pm != 0ull) {
-#endif
             const int first = cur.b, cnt = pnode_leaf_count(cur);
-#ifndef CRT_AB_NOGROUP
 #ifndef CRT_GROUP_MAX
 #define CRT_GROUP_MAX 32
 #endif
@@ -691,13 +635,10 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
                 for (int a = 0; a < 3; ++a) fc.pu[a] = fc.pw[a] = (f2){0.0f, 0.0f};
                 face_cache_init(fc);
                 leaf_grouped<COUNT>(s, first, cnt, pm, pass, o, d, best_t, best, lim, c);
-                PH(1);
-                PH_COUNT(6);
                 i = i + 1;
                 cur = n1;
                 continue;
             }
-#endif
             DTriGeo g = load_scalar(s.slots, first);
             uint32_t cw = load_scalar(s.slot_cull_bits, first >> 5);
             for (int k = 0; k < cnt; ++k) {
@@ -722,13 +663,10 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
                 g = gn;
                 cw = cwn;
             }
-            PH(1);
-            PH_COUNT(6);
         }
         i = i + 1;
         cur = n1;
     }
-    PH_FLUSH(8);
     return best;
 }
 
@@ -799,22 +737,13 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
     const unsigned long long rmask = (R >= 64) ? ~0ull : ((1ull << R) - 1ull);
     int i = 0;
     PNode nd = load_global(nodes, sl < n ? sl : n - 1);
-    PH_DECL
     while (i < n) {
-        PH_COUNT(7);
-#ifdef CRT_AB_WPREF
-        /* the window after this one, loaded while this one is tested; used
-         * unless a dead subtree moves the walk further (next > i + K) */
-        const int spec = i + K + sl;
-        const PNode nd_next = load_global(nodes, spec < n ? spec : n - 1);
-#endif
         const int j = i + sl;
         const bool valid = j < n;
         const bool interior = nd.count == 0;
         const bool alive = valid & active & hull_alive(nd, pr, lim);
         const bool pass = alive & box_hit_fast(o, d, rr, cell_of(nd));
         const unsigned long long P = __ballot(pass);
-        PH(0);
         /* replay the packet walk's reach update over the window, in order, on
          * wave-uniform ray masks: node a's rays in = reach mask of its depth;
          * an interior node sets the mask of depth + 1 to the rays that entered
@@ -833,10 +762,12 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
             IN |= (unsigned long long)in_m << (a * R);
         }
         const bool my_in = ((IN >> __lane_id()) & 1ull) != 0ull;
-        PH(1);
         if (COUNT) {
             if (my_in & alive) ++c.nodes;
             c.wave_nodes += (uint32_t)kk;     /* node records of the window */
+            ++c.win_steps;
+            if (sl < kk && r < __popcll(__ballot(active && lead))) ++c.win_slots;
+            if (my_in & alive) ++c.win_reached;
         }
         const bool enter = my_in & pass;
         const unsigned long long E = __ballot(enter);
@@ -852,18 +783,13 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
             skip_to = v > skip_to ? v : skip_to;
         }
         const int next = uniform_i(i + K > skip_to ? i + K : skip_to);
-        PH(2);
         /* triangles of the entered leaves, one leaf at a time over the whole
          * wave: lane (sl, r) tests triangles sl, sl + K, ... of the leaf for
          * its ray r if r entered it, so a leaf costs ceil(count / K) rounds
          * (its triangles load as K consecutive records); then a per-ray merge
          * of the candidates over the ray's K lanes by the key (t, slot). */
         const bool leaf = enter & !interior;
-#if defined(CRT_AB_NOTRI) && (CRT_AB_NOTRI & 1)   /* timing experiments only: no triangle phase (wrong image) */
-        if (false) {
-#else
         if (__ballot(leaf) != 0ull) {
-#endif
             float lt = best_t;
             int ls = best;
             unsigned long long Lm = __ballot(leaf);
@@ -873,7 +799,10 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
                 const unsigned long long sm = Lm & (rmask << (s0 * R));   /* the rays that entered leaf s0 */
                 Lm &= ~sm;
                 const int first = __builtin_amdgcn_readlane(nd.b, l0), cnt = __builtin_amdgcn_readlane(nd.count, l0);
-                if (COUNT) c.wave_tris += (uint32_t)((cnt + K - 1) / K);
+                if (COUNT) {
+                    c.wave_tris += (uint32_t)((cnt + K - 1) / K);
+                    c.win_rounds += (uint32_t)((cnt + K - 1) / K);
+                }
                 if (((sm >> (s0 * R + r)) & 1ull) != 0ull) {
                     for (int k = sl; k < cnt; k += K) {
                         const int slot = first + k;
@@ -888,8 +817,6 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
                     }
                 }
             }
-            PH(3);
-            PH_COUNT(6);
             for (int off = R; off < 64; off <<= 1) {
                 const float ot = __shfl_xor(lt, off);
                 const int os = __shfl_xor(ls, off);
@@ -901,19 +828,12 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
             best_t = lt;
             best = ls;
             lim = best >= 0 ? best_t : INFINITY;
-            PH(4);
         }
-#ifdef CRT_AB_WPREF
-        if (next == i + K) {
-            nd = nd_next;
-        } else
-#endif
         {
             nd = load_global(nodes, next + sl < n ? next + sl : n - 1);
         }
         i = next;
     }
-    PH_FLUSH(0);
     if (COUNT && best >= 0 && lead) ++c.hits;
     return best;
 }
@@ -1044,9 +964,6 @@ __device__ __forceinline__ float fresnel_of(const DeviceScene &s, float dot) {
  * operations as shade_pixel<false>. */
 __device__ __forceinline__ Vec shade_primary(const DeviceScene &s, const DSettings &st, Vec o, Vec d, int slot, float t) {
     if (slot < 0) return vec(s.background[0], s.background[1], s.background[2]);
-#ifdef CRT_AB_NOSHADE   /* timing experiments only: the walk without the shading cost (wrong image) */
-    return vec(t, (float)slot, 0.0f);
-#endif
     HitRec h;
     make_hit(s, o, d, t, slot, h);
     const DMaterial m = s.materials[h.mat];
@@ -1265,9 +1182,6 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
         /* tiles of <= 16 rays (the measured plan's splits of heavy tiles): window walk */
         const int tw = uniform_i(tl.w), th = uniform_i(tl.h);
         const int npx = tw * th;
-#if defined(CRT_AB_ONLY)   /* timing experiments only: 1 = window tiles alone, 2 = 8x8 tiles alone */
-        if ((CRT_AB_ONLY == 1) != (npx <= 16)) return;
-#endif
         if (npx <= 16) {
             const int R = npx <= 4 ? 4 : 16;
             const int r = lane & (R - 1), sl = lane / R;
@@ -1275,7 +1189,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             const int px = act ? r % tw : 0, py = act ? r / tw : 0;
             Vec o, d;
             camera_ray(s, tl.x + px, tl.y + py, o, d);
-            LaneCounts cw = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+            LaneCounts cw = {};
             float t;
             const int slot = trace_window<COUNT>(s, R, r, sl, act, o, d, t, cw);
             if (act && sl == 0) {
@@ -1299,21 +1213,22 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
                     atomicAdd(&counters[8], (unsigned long long)cw.wave_box);
                     atomicAdd(&counters[9], (unsigned long long)cw.wave_pass);
                     atomicAdd(&counters[10], 1ull);   /* window-walk waves */
+                    atomicAdd(&counters[11], (unsigned long long)cw.win_steps);
+                    atomicAdd(&counters[14], (unsigned long long)cw.win_rounds);
                 }
+                atomicAdd(&counters[12], (unsigned long long)cw.win_slots);
+                atomicAdd(&counters[13], (unsigned long long)cw.win_reached);
             }
             return;
         }
     }
-#if defined(CRT_AB_ONLY) && CRT_AB_ONLY == 2   /* timing experiments only: 8x8 tiles alone under walk 12 too */
-    if (TRAV == 12 && uniform_i(tl.w) * uniform_i(tl.h) <= 16) return;
-#endif
     const int lx = lane & 7, ly = lane >> 3;
     const bool has_px = lx < tl.w && ly < tl.h;
     /* the sharing walks keep pixel-less lanes as helpers (they take donated node
      * ranges of the wave's rays); the other walks drop them */
     constexpr bool kHelpers = !FULL;   /* sharing walks use them; packet walks ignore them */
     if (!kHelpers && !has_px) return;
-    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    LaneCounts cnt = {};
     constexpr bool kCoop = kIsCoop<TRAV> || kIsCoop<SEC>;   /* LDS only for the sharing walks */
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     const Vec c = shade_pixel<FULL, MAXF, TRAV, SEC, COUNT>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt,
@@ -1364,7 +1279,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(MAXF == 4 ? (TRA
     const unsigned long long lt = (1ull << lane) - 1ull;
     __shared__ CoopLds coop[4];
     CoopLds *L = &coop[threadIdx.x >> 6];
-    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    LaneCounts cnt = {};
     bool has = false, dry = false;
     int64_t opx = 0;
     Vec o = vec(0.f, 0.f, 0.f), d = vec(0.f, 0.f, 1.f), col = vec(0.f, 0.f, 0.f);
@@ -1457,7 +1372,7 @@ __global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restri
     const bool has_px = lx < tl.w && ly < tl.h;
     Vec o, d;
     camera_ray(s, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), o, d);
-    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    LaneCounts cnt = {};
     constexpr bool kCoop = kIsCoop<TRAV>;
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
@@ -1549,7 +1464,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
             depth = r.depth;
         }
     }
-    LaneCounts cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    LaneCounts cnt = {};
     constexpr bool kCoop = kIsCoop<TRAV>;
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
@@ -3003,17 +2918,6 @@ int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rg
         HIP_TRY(hipMemcpyAsync(rgb_out, sc->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
         HIP_TRY(hipStreamSynchronize(sc->stream));
     }
-#ifdef CRT_AB_PHASES
-    {
-        unsigned long long ph[16];
-        HIP_TRY(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof ph));
-        fprintf(stderr, "PHASES");
-        for (int k = 0; k < 16; ++k) fprintf(stderr, " %llu", ph[k]);
-        fprintf(stderr, "\n");
-        std::memset(ph, 0, sizeof ph);
-        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof ph));
-    }
-#endif
     if (stats) {
         std::memset(stats, 0, sizeof *stats);
         float ms = 0.f;
@@ -3346,6 +3250,10 @@ int crt_hip_count_work(crt_hip_scene *sc, const crt_renderer_settings *st, crt_w
     sc->wave_counts.box_steps = c[8];
     sc->wave_counts.pass_steps = c[9];
     sc->wave_counts.window_waves = c[10];
+    sc->wave_counts.window_steps = c[11];
+    sc->wave_counts.window_slots = c[12];
+    sc->wave_counts.window_reached = c[13];
+    sc->wave_counts.window_tri_rounds = c[14];
     return CRT_OK;
 }
 

@@ -359,6 +359,10 @@ typedef struct crt_wave_counts {
     uint64_t box_steps;      /* packet walks: node steps where some lane ran the six-face test */
     uint64_t pass_steps;     /* ... where some lane passed it */
     uint64_t window_waves;   /* waves that ran the window walk (their node_steps count every window record) */
+    uint64_t window_steps;   /* window walk: windows evaluated */
+    uint64_t window_slots;   /* ... lane slots of those windows (records x rays) */
+    uint64_t window_reached; /* ... slots whose ray reached the record and kept it alive (hull) */
+    uint64_t window_tri_rounds; /* ... rounds of the leaf phase (one triangle per lane group each) */
 } crt_wave_counts;
 int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
 
