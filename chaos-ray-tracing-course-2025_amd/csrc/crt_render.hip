@@ -2253,7 +2253,7 @@ int plan_walk(const crt_hip_scene *sc, const crt_renderer_settings *st) {
  * depends on the scene and on how the walks' step counts relate to time (a
  * split tile's window waves cost more per step than a packet wave), so by
  * default it is tuned: each candidate's plan renders the frame (one untimed,
- * two timed launches, min taken) and the fastest plan is kept.  Only the
+ * five timed launches, median taken) and the fastest plan is kept.  Only the
  * tiling changes with k; every plan produces the same image bits.
  * calibrate = 2 (or env CRT_CALIB_K) keeps the given k instead. */
 static const float kCalibK[] = {1.5f, 2.0f, 2.5f, 3.0f, 4.0f, 6.0f};
@@ -2291,8 +2291,8 @@ int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t
             if (r != CRT_OK) return r;
             free_plans(sc);
             if ((r = make_tile_plan(sc, all, true, sc->full)) != CRT_OK) return r;
-            float ms = INFINITY;
-            for (int rep = 0; rep < 3; ++rep) {
+            std::vector<float> reps;
+            for (int rep = 0; rep < 6; ++rep) {
                 HIP_TRY(hipEventRecord(e0, stream));
                 if ((r = launch_render(sc, st, sc->full, scratch, stream, false)) != CRT_OK) return r;
                 HIP_TRY(hipEventRecord(e1, stream));
@@ -2300,8 +2300,10 @@ int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t
                 (void)wf_overflowed(sc->wf, true);   /* a wrong trial frame only drops the recorded level sizes */
                 float t = 0.f;
                 HIP_TRY(hipEventElapsedTime(&t, e0, e1));
-                if (rep > 0) ms = std::min(ms, t);
+                if (rep > 0) reps.push_back(t);
             }
+            std::sort(reps.begin(), reps.end());
+            const float ms = reps[reps.size() / 2];   /* median of 5 timed frames */
             if (ms < best_ms) {
                 best_ms = ms;
                 best_k = k;
