@@ -630,10 +630,6 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
 #define CRT_GROUP_MAX 32
 #endif
             if (FAST && cnt >= 4 && __popcll(pm) <= CRT_GROUP_MAX) {
-                /* drop the face cache (its registers serve the grouped phase;
-                 * the next box test recomputes all three axes) */
-                for (int a = 0; a < 3; ++a) fc.pu[a] = fc.pw[a] = (f2){0.0f, 0.0f};
-                face_cache_init(fc);
                 leaf_grouped<COUNT>(s, first, cnt, pm, pass, o, d, best_t, best, lim, c);
                 i = i + 1;
                 cur = n1;
