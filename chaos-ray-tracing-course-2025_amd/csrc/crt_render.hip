@@ -800,6 +800,34 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
                     c.win_rounds += (uint32_t)((cnt + K - 1) / K);
                 }
                 if (((sm >> (s0 * R + r)) & 1ull) != 0ull) {
+#ifdef CRT_WIN_TRI_PF
+                    /* two rounds in flight: each buffer is refilled right after its test */
+                    const int lst = first + cnt - 1;
+                    int sa = first + sl, sb = first + sl + K;
+                    DTriGeo ga = load_global(s.slots, sa < lst ? sa : lst), gb = load_global(s.slots, sb < lst ? sb : lst);
+                    uint8_t ca = load_global(s.slot_cull, sa < lst ? sa : lst), cb = load_global(s.slot_cull, sb < lst ? sb : lst);
+                    for (int k = sl; k < cnt; k += 2 * K) {
+                        float t;
+                        if (COUNT) ++c.tris;
+                        if (tri_plane(o, d, ga, ca != 0, t) && key_better(t, sa, lt, ls) && tri_edges(o, d, ga, t)) {
+                            lt = t;
+                            ls = sa;
+                        }
+                        sa = first + k + 2 * K;
+                        ga = load_global(s.slots, sa < lst ? sa : lst);
+                        ca = load_global(s.slot_cull, sa < lst ? sa : lst);
+                        if (k + K < cnt) {
+                            if (COUNT) ++c.tris;
+                            if (tri_plane(o, d, gb, cb != 0, t) && key_better(t, sb, lt, ls) && tri_edges(o, d, gb, t)) {
+                                lt = t;
+                                ls = sb;
+                            }
+                        }
+                        sb = first + k + 3 * K;
+                        gb = load_global(s.slots, sb < lst ? sb : lst);
+                        cb = load_global(s.slot_cull, sb < lst ? sb : lst);
+                    }
+#else
                     for (int k = sl; k < cnt; k += K) {
                         const int slot = first + k;
                         const DTriGeo g = load_global(s.slots, slot);
@@ -811,6 +839,7 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
                             ls = slot;
                         }
                     }
+#endif
                 }
             }
             for (int off = R; off < 64; off <<= 1) {
@@ -1149,13 +1178,17 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
                                 * 80 VGPRs at 6 waves (116.6 ms) in same-box A/B */
 #endif
 #ifndef CRT_WINDOW_WAVES
-#define CRT_WINDOW_WAVES 4   /* min waves/SIMD asked of the walk-13 kernel (A/B: 4 beats 1, 5, 6 on C2 and C5) */
+#define CRT_WINDOW_WAVES 5   /* min waves/SIMD asked of the walk-13 kernel: 96 VGPRs (1 spilled); C2 0.1233 ms at
+                              * its best plan vs 0.127-0.130 at 4 waves (profiles/r02/w5tune) */
 #endif
 #ifndef CRT_RENDER_BOUNDS
 #define CRT_RENDER_BOUNDS __launch_bounds__(256)
 #endif
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT>
-__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT_WINDOW_WAVES : (FULL && MAXF == 4 ? CRT_GI_WAVES : 1)))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
+#ifndef CRT_PACKET_WAVES
+#define CRT_PACKET_WAVES 5   /* min waves/SIMD asked of the walk-12 kernel (as walk 13) */
+#endif
+__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT_WINDOW_WAVES : TRAV == 12 ? CRT_PACKET_WAVES : (FULL && MAXF == 4 ? CRT_GI_WAVES : 1)))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
                                                   const Tile *__restrict__ tiles,
                                                       int ntiles, float *__restrict__ out,
                                                       unsigned long long *__restrict__ counters,
@@ -2251,8 +2284,9 @@ int plan_walk(const crt_hip_scene *sc, const crt_renderer_settings *st) {
  * default it is tuned: each candidate's plan renders the frame (one untimed,
  * five timed launches, median taken) and the fastest plan is kept.  Only the
  * tiling changes with k; every plan produces the same image bits.
- * calibrate = 2 (or env CRT_CALIB_K) keeps the given k instead. */
-static const float kCalibK[] = {1.5f, 2.0f, 2.5f, 3.0f, 4.0f, 6.0f};
+ * calibrate = 2 (or env CRT_CALIB_K) keeps the given k instead.  The grid
+ * is fine around 2-3: C2's frame moves by 5-10 % between neighbouring k. */
+static const float kCalibK[] = {1.5f, 1.75f, 2.0f, 2.25f, 2.5f, 2.75f, 3.0f, 3.5f, 4.0f, 6.0f};
 
 int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const ShardPlan &plan, float *d_out,
                   hipStream_t stream, bool count, unsigned long long *stamps = nullptr);
