@@ -800,34 +800,6 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
                     c.win_rounds += (uint32_t)((cnt + K - 1) / K);
                 }
                 if (((sm >> (s0 * R + r)) & 1ull) != 0ull) {
-#ifdef CRT_WIN_TRI_PF
-                    /* two rounds in flight: each buffer is refilled right after its test */
-                    const int lst = first + cnt - 1;
-                    int sa = first + sl, sb = first + sl + K;
-                    DTriGeo ga = load_global(s.slots, sa < lst ? sa : lst), gb = load_global(s.slots, sb < lst ? sb : lst);
-                    uint8_t ca = load_global(s.slot_cull, sa < lst ? sa : lst), cb = load_global(s.slot_cull, sb < lst ? sb : lst);
-                    for (int k = sl; k < cnt; k += 2 * K) {
-                        float t;
-                        if (COUNT) ++c.tris;
-                        if (tri_plane(o, d, ga, ca != 0, t) && key_better(t, sa, lt, ls) && tri_edges(o, d, ga, t)) {
-                            lt = t;
-                            ls = sa;
-                        }
-                        sa = first + k + 2 * K;
-                        ga = load_global(s.slots, sa < lst ? sa : lst);
-                        ca = load_global(s.slot_cull, sa < lst ? sa : lst);
-                        if (k + K < cnt) {
-                            if (COUNT) ++c.tris;
-                            if (tri_plane(o, d, gb, cb != 0, t) && key_better(t, sb, lt, ls) && tri_edges(o, d, gb, t)) {
-                                lt = t;
-                                ls = sb;
-                            }
-                        }
-                        sb = first + k + 3 * K;
-                        gb = load_global(s.slots, sb < lst ? sb : lst);
-                        cb = load_global(s.slot_cull, sb < lst ? sb : lst);
-                    }
-#else
                     for (int k = sl; k < cnt; k += K) {
                         const int slot = first + k;
                         const DTriGeo g = load_global(s.slots, slot);
@@ -839,7 +811,6 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
                             ls = slot;
                         }
                     }
-#endif
                 }
             }
             for (int off = R; off < 64; off <<= 1) {
