@@ -103,6 +103,9 @@ def parse(argv=None):
     p.add_argument("--shards", choices=["compact", "full"], default="compact",
                    help="tiles mode: gather only the live tiles (camera ray passes the root-cell test; the rest is "
                         "background by construction — lossless) or every bucket")
+    p.add_argument("--shadows", action="store_true",
+                   help="trace the shadow rays (option \"shadows\": the course's earlier renderer, dead code at HEAD; "
+                        "a separate report, never the HEAD-parity headline): rays = camera + shadow rays")
     p.add_argument("--no-secondary", action="store_true", help="N>1: skip the secondary frames-mode measurement")
     p.add_argument("--event-every", type=int, default=5,
                    help="bracket every k-th render of the timed region with HIP events (kernel time sample; "
@@ -160,7 +163,7 @@ def cpu_worker(spec: dict) -> dict:
     cfg = CONFIGS[spec["config"]]
     scene = make_scene(cfg, spec["w"], spec["h"])
     st = RendererSettings.default(**cfg["settings"])
-    orc = pyoracle.OracleScene(scene)
+    orc = pyoracle.OracleScene(scene).set_shadows(bool(spec.get("shadows")))
     wc = WorkCounts()
     orc.render(st, nthreads=spec["threads"], counts=wc)      # warm-up frame, and the frame's ray count
     rays = int(wc.traversals)
@@ -199,14 +202,15 @@ def cpu_info() -> dict:
     return {"model": model or "host CPU", "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": quota}
 
 
-def cpu_baseline(config: str, w: int, h: int, seconds: float, single_seconds: float, size_note: str) -> dict:
+def cpu_baseline(config: str, w: int, h: int, seconds: float, single_seconds: float, size_note: str,
+                 shadows: bool = False) -> dict:
     info = cpu_info()
     threads = info["affinity_cpus"]          # hardware_concurrency() of this process (crt_renderer.cpp:178)
     multi = run_cpu_worker({"config": config, "w": w, "h": h, "threads": threads, "pin": None,
-                            "seconds": seconds, "min_frames": 5})
+                            "seconds": seconds, "min_frames": 5, "shadows": shadows})
     pin = sorted(os.sched_getaffinity(0))[0]
     single = run_cpu_worker({"config": config, "w": w, "h": h, "threads": 1, "pin": pin,
-                             "seconds": single_seconds, "min_frames": 2})
+                             "seconds": single_seconds, "min_frames": 2, "shadows": shadows})
     rays = multi["rays_per_frame"]
     return {
         "value": round(rays / multi["median_s"] / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
@@ -351,7 +355,7 @@ def main():
     settings = N.RendererSettings.default(**cfg["settings"])
     # the library's own start/stop events (crt_hip_last_kernel_ms) would sit inside
     # this script's timing events and add ~8 us per frame: timing here uses torch's
-    gpu = N.HipScene(scene, device=local, events=0)
+    gpu = N.HipScene(scene, device=local, events=0, shadows=int(a.shadows))
     build_id = N.build_id()
     # an explicit stream: the render kernel, the gather and the timing events
     # all go on it (handle 0 would mean "the scene's own stream" to the C-ABI)
@@ -514,12 +518,13 @@ def main():
         if world == 1 and not a.no_cpu_baseline:
             cw, ch = cfg["cpu_size"] if (W, H) == cfg["size"] else (W, H)
             note = "" if (cw, ch) == (W, H) else f" at {cw}x{ch} (same scene and settings; Mrays/s is per-ray work)"
-            cpu = cpu_baseline(a.config, cw, ch, a.cpu_seconds, a.cpu_single_seconds, note)
+            cpu = cpu_baseline(a.config, cw, ch, a.cpu_seconds, a.cpu_single_seconds, note, a.shadows)
         parallel = {"single": "single-gpu", "tiles": f"bucket-shard{world}+{'rccl' if dist_backend == 'nccl' else dist_backend}"
                     f"-gather-{a.shards}-{a.payload}", "frames": f"frame-parallel{world}"}[mode]
         out = {
             "metric": ("Mrays/sec + frame ms, 1920x1080 scene 14-01" if a.config == "c2"
-                       else f"Mrays/sec + frame ms, {W}x{H} {cfg['label']}"),
+                       else f"Mrays/sec + frame ms, {W}x{H} {cfg['label']}")
+                      + (" (primary + shadow rays)" if a.shadows else ""),
             "value": round(mrays, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -533,7 +538,8 @@ def main():
             "data": (f"scene file scenes/{cfg['label']}.crtscene (parsed fixture tests/golden/scenes)" if "scene" in cfg
                      else "synthetic mesh (crt_amd.synthetic.c5_scene, SURVEY §8(d) C5 spec)"),
             "config": {"workload": f"{cfg['label']} {W}x{H}, RendererSettings defaults "
-                                   f"(max_ray_depth {settings.max_ray_depth}), {cfg['note']}",
+                                   f"(max_ray_depth {settings.max_ray_depth}), "
+                                   + ("shadow rays traced (option shadows; HEAD traces none)" if a.shadows else cfg["note"]),
                        "config": a.config,
                        "rays_per_frame": rays_per_frame, "node_tests_per_frame": counts["node_tests"],
                        "triangle_tests_per_frame": counts["triangle_tests"],

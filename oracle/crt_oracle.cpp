@@ -110,6 +110,9 @@ struct Scene {
     std::vector<Texture> textures;
     std::vector<Material> materials;
     std::vector<Light> lights;
+    /* oracle_set_shadows: trace each light's shadow ray (the course's earlier
+     * renderer; dead code at HEAD, crt_renderer.cpp:29-44) */
+    bool shadows = false;
 };
 
 struct Counters { uint64_t traversals = 0, nodes = 0, tris = 0, hits = 0; };
@@ -445,7 +448,17 @@ static V3 shade(const Scene &sc, const Ray &ray, const crt_renderer_settings &st
             const float cos_law = (0.0f < dn) ? dn : 0.0f;       /* std::max(0.0f, dn) */
             const float area = 4 * 3.14159265358979323846f * r2;
             /* shadow ray: trace_ray_with_refractions never loops (crt_renderer.cpp:29-44),
-             * so every light counts as unoccluded. */
+             * so at HEAD every light counts as unoccluded.  With sc.shadows the loop
+             * body runs: it always intersects the unchanged shadow ray, so the
+             * result is that ray's closest hit (:90-92). */
+            if (sc.shadows) {
+                Ray sr;
+                sr.o = add(h.p, scale(n, st.shadow_bias));
+                sr.d = ld;
+                sr.depth = 0;
+                Hit sh;
+                if (closest_hit(sc, sr, sh, cnt) && !(sh.t * sh.t > r2)) continue;
+            }
             const V3 term = scale(divs(scale(alb, L.intensity), area), cos_law);
             acc.x += term.x; acc.y += term.y; acc.z += term.z;
         }
@@ -611,6 +624,8 @@ oracle_scene *oracle_scene_create(const crt_scene_desc *d) {
     o->sc = make_scene(d);
     return o;
 }
+
+void oracle_set_shadows(oracle_scene *o, int shadows) { o->sc->shadows = shadows != 0; }
 
 void oracle_scene_destroy(oracle_scene *o) {
     if (!o) return;

@@ -48,6 +48,7 @@ def oracle_lib() -> C.CDLL:
         L.oracle_scene_create.restype = _P
         L.oracle_scene_create.argtypes = [_P]
         L.oracle_scene_destroy.argtypes = [_P]
+        L.oracle_set_shadows.argtypes = [_P, C.c_int]
         L.oracle_render.argtypes = [_P, _P, _P, C.c_int, _P]
         L.oracle_render_pixels.argtypes = [_P, _P, C.c_int64, C.c_int64, _P, _P]
         L.oracle_trace.argtypes = [_P, _P, C.c_int64, _P, _P, _P]
@@ -104,6 +105,13 @@ class OracleScene:
         self._keep = desc_src
         self.width = desc_src.desc().camera.width
         self.height = desc_src.desc().camera.height
+
+    def set_shadows(self, on: bool = True) -> "OracleScene":
+        """Trace the shadow rays (the course's earlier renderer; dead code at
+        HEAD, crt_renderer.cpp:29-44,90-92): a light counts only when the shadow
+        ray's closest hit is absent or farther than the light."""
+        self._L.oracle_set_shadows(self._h, int(bool(on)))
+        return self
 
     def render(self, settings, nthreads: int = 0, counts=None) -> np.ndarray:
         out = np.zeros((self.height, self.width, 3), np.float32)
