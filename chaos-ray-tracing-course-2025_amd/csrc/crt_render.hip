@@ -1148,6 +1148,53 @@ __device__ __forceinline__ bool shade_pass(const DeviceScene &s, const DSettings
     return called;
 }
 
+/* Camera ray + shading with shadow rays for frames without recursion
+ * (FULL=false, option "shadows"): the same operations as diffuse_finish<true>,
+ * but each light's shadow rays are traced by the whole wave at once with the
+ * pruned packet walk — a tile's shadow rays towards one light are coherent —
+ * instead of one per-lane walk per lane. */
+template <int TRAV, bool COUNT>
+__device__ Vec shade_shadowed(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt, CoopLds *L,
+                              bool has_px) {
+    Vec o, d;
+    camera_ray(s, x, y, o, d);
+    float t;
+    const int slot = trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
+    Vec col = vec(s.background[0], s.background[1], s.background[2]);
+    bool diffuse = false;
+    HitRec h;
+    h.p = vec(0.f, 0.f, 0.f);
+    h.n = vec(0.f, 0.f, 1.f);
+    Vec alb = vec(0.f, 0.f, 0.f);
+    if (has_px && slot >= 0) {
+        make_hit(s, o, d, t, slot, h);
+        const DMaterial m = s.materials[h.mat];
+        alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+        if (m.type == CRT_MATERIAL_DIFFUSE) diffuse = true;
+        else col = alb;                                               /* Constant :137-139 */
+    }
+    Vec acc = vec(0.f, 0.f, 0.f);
+    const int nl = s.light_count;
+    for (int l = 0; l < nl; ++l) {                                    /* :81-96 */
+        const DLight Lt = s.lights[l];
+        Vec ld = vsub(vec(Lt.px, Lt.py, Lt.pz), h.p);
+        const float r2 = vlen_sq(ld);
+        ld = vnormalize(ld);
+        const float dn = vdot(ld, h.n);
+        const float cos_law = (0.0f < dn) ? dn : 0.0f;
+        const float area = 4 * kPi * r2;
+        bool lit = true;
+        if (__ballot(diffuse) != 0ull) {
+            float ts;
+            const int ss = trace<8, COUNT>(s, L, diffuse, vadd(h.p, vscale(h.n, st.shadow_bias)), ld, ts, cnt);
+            lit = !(ss >= 0 && !(ts * ts > r2));
+        }
+        if (diffuse && lit) acc = vadd(acc, vscale(vdiv(vscale(alb, Lt.intensity), area), cos_law));
+    }
+    if (diffuse) col = vdiv(acc, (float)(st.diffuse_reflection_ray_count + 1));
+    return col;
+}
+
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW = false>
 __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt, CoopLds *L,
                            bool has_px) {
@@ -1281,8 +1328,13 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
     LaneCounts cnt = {};
     constexpr bool kCoop = kIsCoop<TRAV> || kIsCoop<SEC>;   /* LDS only for the sharing walks */
     __shared__ CoopLds coop[kCoop ? 4 : 1];
-    const Vec c = shade_pixel<FULL, MAXF, TRAV, SEC, COUNT, SHADOW>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt,
-                                                      &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px);
+    Vec c;
+    if constexpr (SHADOW && !FULL)
+        c = shade_shadowed<TRAV, COUNT>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt,
+                                        &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px);
+    else
+        c = shade_pixel<FULL, MAXF, TRAV, SEC, COUNT, SHADOW>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0),
+                                                              cnt, &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px);
     if (has_px) {
         float *px = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
         px[0] = c.x;
@@ -2671,6 +2723,16 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         const uint64_t nf = (uint64_t)st->max_ray_depth + 1;
         const int nb = (plan.ntiles + 3) / 4;
         unsigned long long *cn = sc->d_counters;
+        if (!full) {   /* no recursion: packet walks for camera and shadow rays (shade_shadowed) */
+            if (count)
+                hipLaunchKernelGGL((k_render_tiles<false, 0, 8, 8, true, true>), dim3(nb), dim3(256), 0, stream, d_scene, ds,
+                                   plan.d_tiles, plan.ntiles, d_out, cn, nullptr);
+            else
+                hipLaunchKernelGGL((k_render_tiles<false, 0, 8, 8, false, true>), dim3(nb), dim3(256), 0, stream, d_scene,
+                                   ds, plan.d_tiles, plan.ntiles, d_out, cn, nullptr);
+            HIP_TRY(hipGetLastError());
+            return CRT_OK;
+        }
 #define CRT_LAUNCH_S(MAXF, COUNT)                                                                           \
     hipLaunchKernelGGL((k_render_tiles<true, MAXF, 10, 10, COUNT, true>), dim3(nb), dim3(256), 0, stream,      \
                        d_scene, ds, plan.d_tiles, plan.ntiles, d_out, cn, nullptr)

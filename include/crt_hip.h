@@ -390,6 +390,18 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  *   "calib_k_milli" k x 1000: a fixed split threshold (sets "calibrate" 2)
  *   "trace_walk" 0 = reference order, 1 = pruned per-ray walk (crt_hip_trace_batch)
  *   "events"     0/1 (default 1): start/stop events around every render
+ *   "lane_tiles" 0/1 (default 0): the calibrated plan's split tiles run as one
+ *                wave per 8x8 tile with a per-lane walk instead of window walks
+ *   "shadows"    0/1 (default 0): trace the shadow rays — NOT HEAD's image.
+ *                At HEAD trace_ray_with_refractions never runs its loop
+ *                (crt_renderer.cpp:29-44) and every light is unoccluded; the
+ *                course's earlier renderer traced them (:90-92: a light counts
+ *                when the shadow ray's closest hit is absent or farther than
+ *                the light), which its committed renders 09-02/scene3 and
+ *                09-03/scene5 show at every pixel.  A separate report
+ *                (bench.py --shadows), never the HEAD-parity headline; the
+ *                frame runs the frame-stack kernel with per-lane shadow walks,
+ *                and crt_hip_count_work counts the shadow rays as traversals.
  * Environment variables CRT_TRAVERSAL, CRT_SECONDARY, CRT_WAVEFRONT, CRT_WINDOW,
  * CRT_CALIBRATE, CRT_GI_REFILL, CRT_WF_RPW, CRT_TRACE_WALK and CRT_EVENTS set
  * the initial values (an invalid value makes scene creation fail). */
