@@ -45,10 +45,8 @@ struct alignas(16) Tile {
     int32_t x, y, w, h;        /* pixel rectangle, w,h <= 8 */
     int64_t out_base;          /* output pixel index of (x, y) */
     int32_t out_stride;        /* output pixels per row */
-    int32_t prio;              /* bit 0: one of the frame's heaviest waves — raised issue priority;
-                                * bit 1: walk 13 traces this tile's rays with the per-lane walk (kLaneTile) */
+    int32_t prio;              /* 1: one of the frame's heaviest waves — raised issue priority */
 };
-constexpr int32_t kLaneTile = 2;
 
 struct alignas(16) UnpackBucket {
     int32_t x, y, w, h;
@@ -1245,37 +1243,8 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
     /* the heaviest tiles set the frame length (their walks are long chains of
      * dependent loads): they get issue priority over the light waves that
      * share their SIMD (s_setprio; scheduling only, results unchanged) */
-    if (tl.prio & 1) __builtin_amdgcn_s_setprio(3);
+    if (tl.prio) __builtin_amdgcn_s_setprio(3);
     if constexpr (TRAV == 13 && !FULL) {
-        if (tl.prio & kLaneTile) {
-            /* a heavy 8x8 tile whose rays diverge (option "lane_tiles"): every
-             * lane walks its own ray (per-lane pruned walk over its octant
-             * order), so the wave pays for its longest ray, not for the union
-             * of the 64 rays' visit sets */
-            const int lx = lane & 7, ly = lane >> 3;
-            const bool act = lx < tl.w && ly < tl.h;
-            Vec o, d;
-            camera_ray(s, tl.x + (act ? lx : 0), tl.y + (act ? ly : 0), o, d);
-            LaneCounts cl = {};
-            float t;
-            const int slot = trace_lane_pruned<COUNT>(s, act, o, d, t, cl);
-            if (act) {
-                const Vec c = shade_primary(s, st, o, d, slot, t);
-                float *pxo = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
-                pxo[0] = c.x;
-                pxo[1] = c.y;
-                pxo[2] = c.z;
-            }
-            if (stamps && lane == 0) stamps[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
-            if (COUNT) {
-                atomicAdd(&counters[0], (unsigned long long)cl.traversals);
-                atomicAdd(&counters[1], (unsigned long long)cl.nodes);
-                atomicAdd(&counters[2], (unsigned long long)cl.tris);
-                atomicAdd(&counters[3], (unsigned long long)cl.hits);
-                if (lane == 0) atomicAdd(&counters[7], 1ull);
-            }
-            return;
-        }
         /* tiles of <= 16 rays (the measured plan's splits of heavy tiles): window walk */
         const int tw = uniform_i(tl.w), th = uniform_i(tl.h);
         const int npx = tw * th;
@@ -1549,7 +1518,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         const int wave = gid >> 6;
         if (wave >= ntiles) return;
         const Tile tl = tiles[wave];
-        if (tl.prio & 1) __builtin_amdgcn_s_setprio(3);
+        if (tl.prio) __builtin_amdgcn_s_setprio(3);
         const int lx = lane & 7, ly = lane >> 3;
         has = lx < tl.w && ly < tl.h;
         if (has) camera_ray(s, tl.x + lx, tl.y + ly, o, d);
@@ -1863,7 +1832,7 @@ struct ShardPlan {
     int64_t packed_pixels = 0;
     std::vector<Tile> tiles;     /* host copy, dispatch order */
     std::vector<float> cost;     /* measured cost per tile (calibrated plans), else empty */
-    bool has_small = false;      /* some tile has <= 16 pixels or kLaneTile (walk 13 runs them: window / per-lane walk) */
+    bool has_small = false;      /* some tile has <= 16 pixels (walk 13 runs them with the window walk) */
 };
 
 struct GiTables { float *d = nullptr; };   /* 4 * 2^23 floats on one device */
@@ -1974,7 +1943,6 @@ struct crt_hip_scene {
     int refill_waves = 5120;           /* waves of the refill grid: CUs x 4 SIMDs x CRT_GI_WAVES */
     bool grid_empty = false;
     int traversal = 8;             /* 7 reference order | 8 pruned (default), see trace<> (env CRT_TRAVERSAL) */
-    int lane_tiles = 0;            /* option "lane_tiles": the calibrated plan's split tiles run as one per-lane-walk wave */
     int shadows = 0;               /* option "shadows": trace the shadow rays (k_render_tiles<..., SHADOW>) */
     int trace_walk = 1;            /* crt_hip_trace_batch: 0 reference-order walk, 1 pruned per-lane walk */
     bool camera_fast = false;      /* every camera ray takes the fast box path (camera_rays_fast) */
@@ -2091,14 +2059,7 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
             const auto &cal = sc->calib[k];
             const bool aligned = t.x % 8 == 0 && t.y % 8 == 0 && t.w == std::min(8, W - t.x) &&
                                  t.h == std::min(8, sc->info.height - t.y);
-            if (aligned && sc->lane_tiles && cal.size() > 1) {
-                /* a split tile: one wave, per-lane walk, at the cost of its parts */
-                float c = 0.f;
-                for (const auto &st : cal) c += st.cost;
-                Tile lt = t;
-                lt.prio = kLaneTile;
-                out.push_back({c, lt});
-            } else if (aligned) {
+            if (aligned) {
                 for (const auto &st : cal)
                     out.push_back({st.cost, Tile{t.x + st.dx, t.y + st.dy, st.w, st.h,
                                                  t.out_base + (int64_t)st.dy * t.out_stride + st.dx, t.out_stride, 0}});
@@ -2122,7 +2083,7 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         for (float c : plan.cost) csum += c;
         const double slot_cost = csum / std::max(1, sc->wave_slots);
         for (size_t k = 0; k < tiles.size() && (int)k < sc->prio_tiles; ++k)
-            tiles[k].prio |= plan.cost[k] > sc->prio_min * slot_cost ? 1 : 0;
+            tiles[k].prio = plan.cost[k] > sc->prio_min * slot_cost ? 1 : 0;
     } else if (!tiles.empty() && !sc->tile_work.empty()) {
         /* dispatch the expensive tiles first so the longest waves start at t=0;
          * with a sharing walk, split the heaviest tiles so each of their waves
@@ -2153,7 +2114,7 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
     }
     plan.ntiles = (int)tiles.size();
     plan.has_small = false;
-    for (const Tile &t : tiles) plan.has_small = plan.has_small || t.w * t.h <= 16 || (t.prio & kLaneTile);
+    for (const Tile &t : tiles) plan.has_small = plan.has_small || t.w * t.h <= 16;
     plan.tiles = tiles;
     if (!tiles.empty()) {
         void *p = nullptr;
@@ -3451,9 +3412,6 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
                                           true, sc->full);
             if (rc != CRT_OK) return rc;
         }
-    } else if (k == "lane_tiles") {
-        sc->lane_tiles = value != 0;
-        sc->calib_walk = -1;   /* re-plan (and re-tune k) on next use */
     } else if (k == "shadows") {
         sc->shadows = value != 0;
     } else if (k == "trace_walk") {

@@ -25,11 +25,9 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("scene", nargs="?", default="14-01-acceleration-tree__scene1")
     p.add_argument("--window", type=int, default=1)
-    p.add_argument("--lane-tiles", type=int, default=0)
     p.add_argument("--out", default=None)
     a = p.parse_args()
-    g = N.HipScene(load_npz(ROOT / "tests/golden/scenes" / f"{a.scene}.npz"), window=a.window,
-                   lane_tiles=a.lane_tiles)
+    g = N.HipScene(load_npz(ROOT / "tests/golden/scenes" / f"{a.scene}.npz"), window=a.window)
     st = N.RendererSettings.default()
     g.render(st)
     xywh, cost = g.plan_tiles(st)
@@ -41,8 +39,7 @@ def main():
     dur = e - s
     npx = xywh[:, 2] * xywh[:, 3]
     out = {"scene": a.scene, "window": a.window, "span_us": float(e.max()), "waves": int(len(s))}
-    lane = (N.plan_tile_flags(g, st) & 2) != 0 if hasattr(N, "plan_tile_flags") else np.zeros(len(npx), bool)
-    for name, sel in [("small_le16", npx <= 16), ("tile_gt16", (npx > 16) & ~lane), ("lane_tiles", lane)]:
+    for name, sel in [("small_le16", npx <= 16), ("tile_gt16", npx > 16)]:
         if not sel.any():
             continue
         d, ee = dur[sel], e[sel]

@@ -91,14 +91,12 @@ def test_render_matches_oracle(N, oracle, name, w, h, over, exact):
         assert nbad == 0, f"{name}: {nbad} floats differ (rmse {rmse})"
 
 
-@pytest.mark.parametrize("lane_tiles", [0, 1], ids=["window-walk", "lane-tiles"])
-def test_c2_full_frame_bit_exact(N, oracle, lane_tiles):
-    """Config C2: 14-01/scene1 at 1920x1080, default settings; heavy tiles on the
-    window walk or (option lane_tiles) on per-lane walks."""
+def test_c2_full_frame_bit_exact(N, oracle):
+    """Config C2: 14-01/scene1 at 1920x1080, default settings."""
     sc = scene_npz("14-01-acceleration-tree__scene1")
     st = N.RendererSettings.default()
     want = oracle.OracleScene(sc).render(st)
-    gpu = N.HipScene(sc, lane_tiles=lane_tiles)
+    gpu = N.HipScene(sc)
     got = gpu.render(st)
     assert got.shape == (1080, 1920, 3)
     assert np.array_equal(bits(got), bits(want))
