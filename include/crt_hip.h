@@ -390,8 +390,6 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  *   "calib_k_milli" k x 1000: a fixed split threshold (sets "calibrate" 2)
  *   "trace_walk" 0 = reference order, 1 = pruned per-ray walk (crt_hip_trace_batch)
  *   "events"     0/1 (default 1): start/stop events around every render
- *   "lane_tiles" 0/1 (default 0): the calibrated plan's split tiles run as one
- *                wave per 8x8 tile with a per-lane walk instead of window walks
  *   "shadows"    0/1 (default 0): trace the shadow rays — NOT HEAD's image.
  *                At HEAD trace_ray_with_refractions never runs its loop
  *                (crt_renderer.cpp:29-44) and every light is unoccluded; the

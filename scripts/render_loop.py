@@ -4,6 +4,7 @@ kernel traces / PMC passes and for in-process A/B of kernel variants.
 
   render_loop.py [--scene NAME] [--width W --height H] [--frames K] [--depth D]
                  [--ab VAR=a,b]   # A/B: one scene per env value, interleaved rounds
+                 [--opt OPTION=a,b]   # A/B: one scene per set_option value
 """
 import argparse
 import json
@@ -29,6 +30,7 @@ def main():
     p.add_argument("--depth", type=int, default=3)
     p.add_argument("--gi", type=int, default=4, help="diffuse_reflection_ray_count")
     p.add_argument("--ab", default=None, help="ENVVAR=v1,v2,... — build one scene per value")
+    p.add_argument("--opt", default=None, help="OPTION=v1,v2,... — one scene per crt_hip_scene_set_option value")
     p.add_argument("--counts", action="store_true", help="print per-ray and per-wave work counts per variant")
     p.add_argument("--synthetic", type=int, default=0, help="C5: synthetic mesh of N triangles instead of --scene")
     a = p.parse_args()
@@ -44,8 +46,14 @@ def main():
         var, vals = a.ab.split("=", 1)
         sep = ";" if ";" in vals else ","
         variants = [(f"{var}={v}", (var, v)) for v in vals.split(sep)]
+    if a.opt:
+        opt, vals = a.opt.split("=", 1)
+        variants = [(f"{opt}={v}", ("opt", opt, int(v))) for v in vals.split(",")]
     scenes = []
     for name, kv in variants:
+        if kv and kv[0] == "opt":
+            scenes.append((name, N.HipScene(sc).set_option(kv[1], kv[2])))
+            continue
         if kv:
             os.environ[kv[0]] = kv[1]
         scenes.append((name, N.HipScene(sc)))
