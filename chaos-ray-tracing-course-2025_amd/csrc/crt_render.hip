@@ -1209,51 +1209,6 @@ __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int
     return col;
 }
 
-/* One split tile of <= 16 camera rays (the measured plan's splits of heavy
- * tiles) on the window walk: shading, output and counters of the wave. */
-template <bool COUNT>
-__device__ __forceinline__ void window_tile(const DeviceScene &s, const DSettings &st, const Tile &tl, int tw, int npx,
-                                            int wave, int lane, float *__restrict__ out,
-                                            unsigned long long *__restrict__ counters,
-                                            unsigned long long *__restrict__ stamps) {
-    const int R = npx <= 4 ? 4 : 16;
-    const int r = lane & (R - 1), sl = lane / R;
-    const bool act = r < npx;
-    const int px = act ? r % tw : 0, py = act ? r / tw : 0;
-    Vec o, d;
-    camera_ray(s, tl.x + px, tl.y + py, o, d);
-    LaneCounts cw = {};
-    float t;
-    const int slot = trace_window<COUNT>(s, R, r, sl, act, o, d, t, cw);
-    if (act && sl == 0) {
-        const Vec c = shade_primary(s, st, o, d, slot, t);
-        float *pxo = out + 3 * (tl.out_base + (int64_t)py * tl.out_stride + px);
-        pxo[0] = c.x;
-        pxo[1] = c.y;
-        pxo[2] = c.z;
-    }
-    if (stamps && lane == 0) stamps[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
-    if (COUNT) {
-        atomicAdd(&counters[0], (unsigned long long)cw.traversals);
-        atomicAdd(&counters[1], (unsigned long long)cw.nodes);
-        atomicAdd(&counters[2], (unsigned long long)cw.tris);
-        atomicAdd(&counters[3], (unsigned long long)cw.hits);
-        if (lane == 0) {
-            atomicAdd(&counters[4], (unsigned long long)cw.wave_nodes);
-            atomicAdd(&counters[5], (unsigned long long)cw.wave_tris);
-            atomicAdd(&counters[6], (unsigned long long)cw.wave_edges);
-            atomicAdd(&counters[7], 1ull);
-            atomicAdd(&counters[8], (unsigned long long)cw.wave_box);
-            atomicAdd(&counters[9], (unsigned long long)cw.wave_pass);
-            atomicAdd(&counters[10], 1ull);   /* window-walk waves */
-            atomicAdd(&counters[11], (unsigned long long)cw.win_steps);
-            atomicAdd(&counters[14], (unsigned long long)cw.win_rounds);
-        }
-        atomicAdd(&counters[12], (unsigned long long)cw.win_slots);
-        atomicAdd(&counters[13], (unsigned long long)cw.win_reached);
-    }
-}
-
 #ifndef CRT_GI_WAVES
 #define CRT_GI_WAVES 5       /* min waves/SIMD asked of the depth<=3 frame-stack (GI) kernels: 96 VGPRs
                                 * + 17 spilled beat 114 VGPRs at 4 waves (C4 1080^2: 102.8 vs 111.7 ms) and
@@ -1294,7 +1249,42 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
         const int tw = uniform_i(tl.w), th = uniform_i(tl.h);
         const int npx = tw * th;
         if (npx <= 16) {
-            window_tile<COUNT>(s, st, tl, tw, npx, wave, lane, out, counters, stamps);
+            const int R = npx <= 4 ? 4 : 16;
+            const int r = lane & (R - 1), sl = lane / R;
+            const bool act = r < npx;
+            const int px = act ? r % tw : 0, py = act ? r / tw : 0;
+            Vec o, d;
+            camera_ray(s, tl.x + px, tl.y + py, o, d);
+            LaneCounts cw = {};
+            float t;
+            const int slot = trace_window<COUNT>(s, R, r, sl, act, o, d, t, cw);
+            if (act && sl == 0) {
+                const Vec c = shade_primary(s, st, o, d, slot, t);
+                float *pxo = out + 3 * (tl.out_base + (int64_t)py * tl.out_stride + px);
+                pxo[0] = c.x;
+                pxo[1] = c.y;
+                pxo[2] = c.z;
+            }
+            if (stamps && lane == 0) stamps[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
+            if (COUNT) {
+                atomicAdd(&counters[0], (unsigned long long)cw.traversals);
+                atomicAdd(&counters[1], (unsigned long long)cw.nodes);
+                atomicAdd(&counters[2], (unsigned long long)cw.tris);
+                atomicAdd(&counters[3], (unsigned long long)cw.hits);
+                if (lane == 0) {
+                    atomicAdd(&counters[4], (unsigned long long)cw.wave_nodes);
+                    atomicAdd(&counters[5], (unsigned long long)cw.wave_tris);
+                    atomicAdd(&counters[6], (unsigned long long)cw.wave_edges);
+                    atomicAdd(&counters[7], 1ull);
+                    atomicAdd(&counters[8], (unsigned long long)cw.wave_box);
+                    atomicAdd(&counters[9], (unsigned long long)cw.wave_pass);
+                    atomicAdd(&counters[10], 1ull);   /* window-walk waves */
+                    atomicAdd(&counters[11], (unsigned long long)cw.win_steps);
+                    atomicAdd(&counters[14], (unsigned long long)cw.win_rounds);
+                }
+                atomicAdd(&counters[12], (unsigned long long)cw.win_slots);
+                atomicAdd(&counters[13], (unsigned long long)cw.win_reached);
+            }
             return;
         }
     }
@@ -1335,27 +1325,6 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             atomicAdd(&counters[9], (unsigned long long)cnt.wave_pass);
         }
     }
-}
-
-/* The split tiles alone (window walk), for frames whose plan runs them
- * beside the packet tiles on a second stream (launch_render): without the
- * packet walk's registers this kernel fits more waves per SIMD, so the
- * latency-bound window waves hide more of each other's memory round trips. */
-#ifndef CRT_WINDOW_ONLY_WAVES
-#define CRT_WINDOW_ONLY_WAVES 8
-#endif
-template <bool COUNT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRT_WINDOW_ONLY_WAVES))) void k_render_window(
-    const DeviceScene *__restrict__ scene, DSettings st, const Tile *__restrict__ tiles, int ntiles,
-    float *__restrict__ out, unsigned long long *__restrict__ counters) {
-    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    const int lane = (int)(threadIdx.x & 63);
-    if (wave >= ntiles) return;
-    const DeviceScene &s = *scene;
-    const Tile tl = tiles[wave];
-    if (tl.prio) __builtin_amdgcn_s_setprio(3);
-    const int tw = uniform_i(tl.w), th = uniform_i(tl.h);
-    window_tile<COUNT>(s, st, tl, tw, tw * th, wave, lane, out, counters, nullptr);
 }
 
 /* Frame-stack kernel with pixel refill (GI frames, cooperative walk).  A
@@ -1864,10 +1833,6 @@ struct ShardPlan {
     std::vector<Tile> tiles;     /* host copy, dispatch order */
     std::vector<float> cost;     /* measured cost per tile (calibrated plans), else empty */
     bool has_small = false;      /* some tile has <= 16 pixels (walk 13 runs them with the window walk) */
-    /* the same tiles in two lists (dispatch order kept): packet tiles (> 16
-     * pixels) and split tiles (<= 16), for the two-stream launch */
-    Tile *d_big = nullptr, *d_small = nullptr;
-    int nbig = 0, nsmall = 0;
 };
 
 struct GiTables { float *d = nullptr; };   /* 4 * 2^23 floats on one device */
@@ -1963,11 +1928,6 @@ struct crt_hip_scene {
     std::vector<void *> allocs;
     hipStream_t stream = nullptr;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
-    /* two-stream launch of walk-13 frames (option "window_stream"): the split
-     * tiles' window kernel on stream2, joined back by events */
-    hipStream_t stream2 = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    int window_stream = 1;
     ShardPlan full;
     std::map<std::pair<int, int>, ShardPlan> shard_plans;
     std::map<int, std::pair<UnpackBucket *, int>> unpack_plans;
@@ -2162,22 +2122,6 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         HIP_TRY(hipMemcpy(p, tiles.data(), tiles.size() * sizeof(Tile), hipMemcpyHostToDevice));
         sc->plan_allocs.push_back(p);
         plan.d_tiles = static_cast<Tile *>(p);
-    }
-    plan.d_big = plan.d_small = nullptr;
-    plan.nbig = plan.nsmall = 0;
-    if (plan.has_small) {
-        std::vector<Tile> two;
-        two.reserve(tiles.size());
-        for (const Tile &t : tiles) if (t.w * t.h > 16) two.push_back(t);
-        plan.nbig = (int)two.size();
-        for (const Tile &t : tiles) if (t.w * t.h <= 16) two.push_back(t);
-        plan.nsmall = (int)two.size() - plan.nbig;
-        void *p = nullptr;
-        HIP_TRY(hipMalloc(&p, two.size() * sizeof(Tile)));
-        HIP_TRY(hipMemcpy(p, two.data(), two.size() * sizeof(Tile), hipMemcpyHostToDevice));
-        sc->plan_allocs.push_back(p);
-        plan.d_big = static_cast<Tile *>(p);
-        plan.d_small = plan.d_big + plan.nbig;
     }
     return CRT_OK;
 }
@@ -2782,24 +2726,6 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         if (trav == 10) CRT_LAUNCH_T(true, MAXF, 10, COUNT);                                               \
         else CRT_LAUNCH_T(true, MAXF, 4, COUNT);                                                           \
     } while (0)
-    if (!full && trav == 13 && sc->window_stream && !count && !stamps && plan.nsmall > 0) {
-        /* split tiles on stream2 (window kernel, more waves per SIMD), packet
-         * tiles on `stream` (walk 12 kernel), joined before anything later on
-         * `stream`; both write disjoint pixels of d_out */
-        HIP_TRY(hipEventRecord(sc->ev_fork, stream));
-        HIP_TRY(hipStreamWaitEvent(sc->stream2, sc->ev_fork, 0));
-        hipLaunchKernelGGL(k_render_window<false>, dim3((unsigned)((plan.nsmall + 3) / 4)), dim3(256), 0, sc->stream2,
-                           d_scene, ds, plan.d_small, plan.nsmall, d_out, cnt);
-        HIP_TRY(hipGetLastError());
-        if (plan.nbig > 0) {
-            hipLaunchKernelGGL((k_render_tiles<false, 0, 12, 12, false>), dim3((unsigned)((plan.nbig + 3) / 4)), dim3(256),
-                               0, stream, d_scene, ds, plan.d_big, plan.nbig, d_out, cnt, nullptr);
-            HIP_TRY(hipGetLastError());
-        }
-        HIP_TRY(hipEventRecord(sc->ev_join, sc->stream2));
-        HIP_TRY(hipStreamWaitEvent(stream, sc->ev_join, 0));
-        return CRT_OK;
-    }
     if (!full) {
         switch (trav) {
         case 7: if (count) CRT_LAUNCH_T(false, 0, 7, true); else CRT_LAUNCH_T(false, 0, 7, false); break;
@@ -2979,9 +2905,6 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     ds.refractions_on = hs.refractions_on;
 
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&sc->stream2, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&sc->ev_fork, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&sc->ev_join, hipEventDisableTiming));
     HIP_TRY(hipEventCreate(&sc->ev_start));
     HIP_TRY(hipEventCreate(&sc->ev_stop));
     void *p = nullptr;
@@ -3074,9 +2997,6 @@ void crt_hip_scene_destroy(crt_hip_scene *sc) {
     if (sc->ev_start) (void)hipEventDestroy(sc->ev_start);
     if (sc->ev_stop) (void)hipEventDestroy(sc->ev_stop);
     if (sc->stream) (void)hipStreamDestroy(sc->stream);
-    if (sc->stream2) (void)hipStreamDestroy(sc->stream2);
-    if (sc->ev_fork) (void)hipEventDestroy(sc->ev_fork);
-    if (sc->ev_join) (void)hipEventDestroy(sc->ev_join);
     delete sc;
 }
 
@@ -3492,8 +3412,6 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
                                           true, sc->full);
             if (rc != CRT_OK) return rc;
         }
-    } else if (k == "window_stream") {
-        sc->window_stream = value != 0;
     } else if (k == "shadows") {
         sc->shadows = value != 0;
     } else if (k == "trace_walk") {

@@ -91,14 +91,12 @@ def test_render_matches_oracle(N, oracle, name, w, h, over, exact):
         assert nbad == 0, f"{name}: {nbad} floats differ (rmse {rmse})"
 
 
-@pytest.mark.parametrize("window_stream", [1, 0], ids=["two-stream", "one-kernel"])
-def test_c2_full_frame_bit_exact(N, oracle, window_stream):
-    """Config C2: 14-01/scene1 at 1920x1080, default settings; split tiles in
-    their own kernel on a second stream (default) or in the walk-13 kernel."""
+def test_c2_full_frame_bit_exact(N, oracle):
+    """Config C2: 14-01/scene1 at 1920x1080, default settings."""
     sc = scene_npz("14-01-acceleration-tree__scene1")
     st = N.RendererSettings.default()
     want = oracle.OracleScene(sc).render(st)
-    gpu = N.HipScene(sc, window_stream=window_stream)
+    gpu = N.HipScene(sc)
     got = gpu.render(st)
     assert got.shape == (1080, 1920, 3)
     assert np.array_equal(bits(got), bits(want))
