@@ -3412,6 +3412,10 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
                                           true, sc->full);
             if (rc != CRT_OK) return rc;
         }
+    } else if (k == "calib_min") {   /* smallest side the calibrated plan splits tiles down to */
+        if (value != 1 && value != 2 && value != 4 && value != 8) return set_error(CRT_E_INVALID, "calib_min must be 1, 2, 4 or 8");
+        sc->calib_min = value;
+        sc->calib_walk = -1;
     } else if (k == "shadows") {
         sc->shadows = value != 0;
     } else if (k == "trace_walk") {
