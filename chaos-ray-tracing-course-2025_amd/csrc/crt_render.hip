@@ -1249,7 +1249,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
         const int tw = uniform_i(tl.w), th = uniform_i(tl.h);
         const int npx = tw * th;
         if (npx <= 16) {
-            const int R = npx == 1 ? 1 : npx <= 4 ? 4 : 16;   /* rays per wave; K = 64 / R window slots */
+            const int R = npx <= 4 ? 4 : 16;
             const int r = lane & (R - 1), sl = lane / R;
             const bool act = r < npx;
             const int px = act ? r % tw : 0, py = act ? r / tw : 0;
