@@ -707,7 +707,7 @@ __device__ __forceinline__ int wave_max_i(int v) {
     return v;
 }
 
-template <bool COUNT, bool ANY = false>
+template <bool COUNT>
 __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool active, Vec o, Vec d, float &best_t,
                             LaneCounts &c) {
     const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
@@ -738,10 +738,7 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
         const bool valid = j < n;
         const bool interior = nd.count == 0;
         const bool alive = valid & active & hull_alive(nd, pr, lim);
-        bool pass = alive & box_hit_fast(o, d, rr, cell_of(nd));
-        if (ANY && __ballot(alive & !rr.fast) != 0ull) {   /* secondary rays: exact division off the fast window */
-            if (alive & !rr.fast) pass = box_hit_slow(o, d, cell_of(nd));
-        }
+        const bool pass = alive & box_hit_fast(o, d, rr, cell_of(nd));
         const unsigned long long P = __ballot(pass);
         /* replay the packet walk's reach update over the window, in order, on
          * wave-uniform ray masks: node a's rays in = reach mask of its depth;
@@ -868,12 +865,6 @@ __device__ __forceinline__ int trace_lane_pruned(const DeviceScene &s, bool acti
  *   10 pruned cooperative walk */
 template <int TRAV>
 constexpr bool kIsCoop = TRAV == 4 || TRAV == 10;
-/* wavefront levels >= 1 on the window walk: 14 = 16 rays x 4 window slots
- * per wave, 15 = 4 rays x 16 slots (secondary rays, exact box fallback) */
-template <int TRAV>
-constexpr bool kIsWfWindow = TRAV == 14 || TRAV == 15;
-template <int TRAV>
-constexpr int kWfWindowRays = TRAV == 15 ? 4 : 16;
 
 template <int TRAV, bool COUNT>
 __device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, bool active, Vec o, Vec d, float &best_t,
@@ -1531,21 +1522,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         const int lx = lane & 7, ly = lane >> 3;
         has = lx < tl.w && ly < tl.h;
         if (has) camera_ray(s, tl.x + lx, tl.y + ly, o, d);
-    } else if constexpr (kIsWfWindow<TRAV>) {
-        /* window walk (secondary 14 / 15): R rays per wave, each on K = 64 / R
-         * lanes; the ray's lane with slot 0 shades it */
-        constexpr int R = kWfWindowRays<TRAV>;
-        const int ray0 = (gid >> 6) * R;
-        if (ray0 >= lv.n) return;
-        const int ray = ray0 + (lane & (R - 1));
-        has = ray < lv.n;
-        if (has) {
-            const WRay r = lv.in[ray];
-            o = vec(r.ox, r.oy, r.oz);
-            d = vec(r.dx, r.dy, r.dz);
-            id = r.id;
-            depth = r.depth;
-        }
     } else {
         const int ray0 = (gid >> 6) * lv.rpw;
         if (ray0 >= lv.n) return;          /* whole wave past the queue */
@@ -1563,14 +1539,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
     constexpr bool kCoop = kIsCoop<TRAV>;
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
-    int slot;
-    if constexpr (!LEVEL0 && kIsWfWindow<TRAV>) {
-        constexpr int R = kWfWindowRays<TRAV>;
-        slot = trace_window<COUNT, true>(s, R, lane & (R - 1), lane / R, has, o, d, t, cnt);
-        has = has && lane < R;    /* one shading lane per ray */
-    } else {
-        slot = trace<kIsWfWindow<TRAV> ? 12 : TRAV, COUNT>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has, o, d, t, cnt);
-    }
+    const int slot = trace<TRAV, COUNT>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has, o, d, t, cnt);
 
     WNode node = {wFinal, -1, -1, 0, 0.f, 0.f, 0.f, 0.f};
     Vec col = vec(0.f, 0.f, 0.f);
@@ -1691,8 +1660,7 @@ __device__ __forceinline__ Vec wf_compose(const WNode &nd, const DVec4 *__restri
 
 /* Wavefront levels >= 1 (C3): own translation unit (crt_render_wf.hip) and
  * LLVM scheduling strategy, as for the GI refill kernels above. */
-#define CRT_WF_INSTANCES(X) X(4, false) X(4, true) X(10, false) X(10, true) X(14, false) X(14, true) X(15, false) \
-    X(15, true)
+#define CRT_WF_INSTANCES(X) X(4, false) X(4, true) X(10, false) X(10, true)
 #define CRT_WF_SIG(SEC, C) void k_wf_level<SEC, false, C>(const DeviceScene *__restrict__, DSettings, \
     const Tile *__restrict__, int, WLevel, unsigned long long *__restrict__);
 #ifdef CRT_WF_TU
@@ -1984,7 +1952,7 @@ struct crt_hip_scene {
      * ideal makespan */
     float split4 = 4.5f, split16 = 9.0f;
     int wave_slots = 6144;   /* CUs x 4 SIMDs x 6 resident render waves */
-    int secondary = 0;       /* walk for secondary rays: 0 = by frame, 4, 10, 14/15 (window walks of wavefront levels) (env CRT_SECONDARY) */
+    int secondary = 0;       /* walk for secondary rays: 0 = by frame, 4, 10 (env CRT_SECONDARY) */
     std::vector<float> tile_work;  /* per 8x8 tile of the full frame */
     /* measured-cost tile plan (calibrate_plan): per 8x8 tile of the full frame,
      * the sub-tiles it is split into and their probed costs */
@@ -2599,7 +2567,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
     std::vector<std::pair<int64_t, int64_t>> levels;   /* (first id, count) of levels >= 1 */
     int64_t base = n0;
     int cur = 0;
-    const int rpw = sec == 14 ? 16 : sec == 15 ? 4 : std::min(64, std::max(1, sc->wf_rays_per_wave));   /* coop walks: idle lanes take donated pieces */
+    const int rpw = std::min(64, std::max(1, sc->wf_rays_per_wave));   /* coop walks: idle lanes take donated pieces */
     for (int L = 1; L < kMaxLevels; ++L) {
         int32_t n = 0;
         int32_t out_cap = 0;
@@ -2626,10 +2594,6 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
                        plan.d_tiles, plan.ntiles, l, cnt)
         if (sec == 10) {
             if (count) CRT_WF(10, true); else CRT_WF(10, false);
-        } else if (sec == 14) {
-            if (count) CRT_WF(14, true); else CRT_WF(14, false);
-        } else if (sec == 15) {
-            if (count) CRT_WF(15, true); else CRT_WF(15, false);
         } else {
             if (count) CRT_WF(4, true); else CRT_WF(4, false);
         }
@@ -2713,8 +2677,6 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     const bool pruned = sc->traversal == 8;
     int sec = sc->secondary;
     if (sec == 0) sec = (gi || !pruned) ? 4 : 10;
-    const int sec_wf = sec;                      /* 14 / 15: window walks, wavefront levels only */
-    if (sec == 14 || sec == 15) sec = 10;
     if (sc->shadows) {
         /* shadow-ray frames (option "shadows"): frame-stack kernel, pruned
          * cooperative walk for every traced ray, per-lane shadow walks */
@@ -2749,7 +2711,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         return CRT_OK;
     }
     if (full && !gi && sc->wavefront && !stamps)
-        return render_wavefront(sc, ds, st, plan, d_out, stream, count, d_scene, sec_wf, camera_walk(sc, sc->traversal));
+        return render_wavefront(sc, ds, st, plan, d_out, stream, count, d_scene, sec, camera_walk(sc, sc->traversal));
     /* frame-stack kernel: one walk for every ray */
     int trav = full ? sec : camera_walk(sc, sc->traversal);
     if (trav == 13 && !plan.has_small) trav = 12;   /* no split tiles: the leaner packet-only kernel */
@@ -3410,8 +3372,7 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         if (value != 7 && value != 8) return set_error(CRT_E_INVALID, "traversal must be 7 (reference order) or 8 (pruned)");
         sc->traversal = value;
     } else if (k == "secondary") {
-        if (value != 0 && value != 4 && value != 10 && value != 14 && value != 15)
-            return set_error(CRT_E_INVALID, "secondary must be 0, 4, 10, 14 or 15");
+        if (value != 0 && value != 4 && value != 10) return set_error(CRT_E_INVALID, "secondary must be 0, 4 or 10");
         sc->secondary = value;
     } else if (k == "wavefront") {
         sc->wavefront = value != 0;

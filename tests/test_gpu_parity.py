@@ -258,19 +258,3 @@ def test_gi_pixel_refill_bit_identical(N, oracle, w, h):
     ca = N.HipScene(sc).set_option("gi_refill", 1).count_work(st)
     cb = N.HipScene(sc).set_option("gi_refill", 0).count_work(st)
     assert ca == cb
-
-
-@pytest.mark.parametrize("secondary", [14, 15], ids=["window-r16", "window-r4"])
-@pytest.mark.parametrize("name,w,h,depth", [("11-01-refractive__scene8", 320, 180, 8),
-                                            ("09-03-reflective__scene5", 160, 90, 3),
-                                            ("11-01-refractive__scene3", 160, 90, 8)])
-def test_wavefront_window_walks_match_oracle(N, oracle, name, w, h, depth, secondary):
-    """Wavefront levels >= 1 on the window walk (secondary 14 / 15): secondary
-    rays leave the fast-division window, so the exact box fallback runs too."""
-    sc = scene_npz(name).set_resolution(w, h)
-    st = N.RendererSettings.default(max_ray_depth=depth)
-    want = oracle.OracleScene(sc).render(st)
-    gpu = N.HipScene(sc, secondary=secondary)
-    for _ in range(2):    # first frame reads level sizes back, the second replays them
-        got = gpu.render(st)
-        assert np.array_equal(bits(got), bits(want)), f"{name}: {int((bits(got) != bits(want)).sum())} floats differ"
