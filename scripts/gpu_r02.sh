@@ -36,6 +36,6 @@ if [[ $STEPS == *pmc* ]]; then
   run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc/fetch" -o run --output-format csv -- $CMD
   run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc/write" -o run --output-format csv -- $CMD
   run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$OUT/pmc/tcc" -o run --output-format csv -- $CMD
-  run pmc_record 120 python3 scripts/pmc_record.py --config c2 --size 1920 1080 --dir "$OUT/pmc" --out "$OUT/pmc_c2.json" --command "$CMD"
+  run pmc_record 120 python3 scripts/pmc_record.py --config c2 --size 1920 1080 --dir "$OUT/pmc" --out "$OUT/pmc_c2.json" --last 3 --command "$CMD"
 fi
 exit 0

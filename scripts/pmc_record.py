@@ -23,19 +23,27 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "chaos-ray-tracing-course-2025_amd"))
 
 
-def averages(root: Path, kernel: str) -> tuple[dict, int]:
+def averages(root: Path, kernel: str, last: int = 0) -> tuple[dict, int]:
+    """Per-dispatch averages of each counter over the kernel's dispatches of
+    each pass; last > 0 keeps only the pass's `last` latest dispatches (the
+    timed frames, after the plan tuning's trial frames)."""
     out, ndisp = {}, 0
     for f in sorted(root.rglob("*counter_collection.csv")):
-        agg = collections.defaultdict(float)
-        disp = set()
+        per = collections.defaultdict(lambda: collections.defaultdict(float))
         for r in csv.DictReader(open(f)):
             if kernel not in r["Kernel_Name"]:
                 continue
-            agg[r["Counter_Name"]] += float(r["Counter_Value"])
-            disp.add(r["Dispatch_Id"])
-        if disp:
-            ndisp = max(ndisp, len(disp))
-            out.update({k: v / len(disp) for k, v in agg.items()})
+            per[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+        ids = sorted(per)
+        if last > 0:
+            ids = ids[-last:]
+        if ids:
+            ndisp = max(ndisp, len(ids))
+            agg = collections.defaultdict(float)
+            for i in ids:
+                for k, v in per[i].items():
+                    agg[k] += v
+            out.update({k: v / len(ids) for k, v in agg.items()})
     return out, ndisp
 
 
@@ -47,12 +55,14 @@ def main():
     p.add_argument("--kernel", default="k_render_tiles")
     p.add_argument("--out", default=None)
     p.add_argument("--command", default="")
+    p.add_argument("--last", type=int, default=0, help="average only the latest N dispatches of each pass")
     a = p.parse_args()
     from crt_amd import native as N
-    c, n = averages(Path(a.dir), a.kernel)
+    c, n = averages(Path(a.dir), a.kernel, a.last)
     rec = {"config": a.config, "size": a.size, "kernel": a.kernel, "build_id": N.build_id(), "dispatches": n,
            "counters_per_launch": c, "command": a.command,
-           "method": "rocprofv3 --pmc, one pass per counter group; per-dispatch averages of the kernel"}
+           "method": "rocprofv3 --pmc, one pass per counter group; per-dispatch averages of the kernel"
+                     + (f" over each pass's last {a.last} dispatches (the timed frames)" if a.last else "")}
     if "SQ_INSTS_VALU" in c:
         rec["valu_insts_per_launch"] = c["SQ_INSTS_VALU"]
     if "SQ_INSTS_SALU" in c:
