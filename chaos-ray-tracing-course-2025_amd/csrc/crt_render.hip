@@ -707,8 +707,8 @@ __device__ __forceinline__ int wave_max_i(int v) {
     return v;
 }
 
-template <bool COUNT>
-__device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool active, Vec o, Vec d, float &best_t,
+template <bool COUNT, int R>
+__device__ int trace_window(const DeviceScene &s, int r, int sl, bool active, Vec o, Vec d, float &best_t,
                             LaneCounts &c) {
     const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
     const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
@@ -718,7 +718,7 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
     best_t = 0.0f;
     float lim = INFINITY;
     const int n = s.node_count;
-    const int K = 64 / R;
+    constexpr int K = 64 / R;
     /* reach state per depth as ray masks: lane dd of `vreach` holds the R-bit
      * mask of the rays that entered the window's last node at depth dd - 1
      * (bit r: ray r), i.e. the packet walk's reach bit dd of every ray */
@@ -730,7 +730,7 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
     if (2 * __popcll(__ballot(active && lead && d.y < 0.0f)) > na) oct |= 2;
     if (2 * __popcll(__ballot(active && lead && d.z < 0.0f)) > na) oct |= 4;
     const PNode *nodes = pnode_order(s.pnodes, n, uniform_i(oct));
-    const unsigned long long rmask = (R >= 64) ? ~0ull : ((1ull << R) - 1ull);
+    constexpr unsigned long long rmask = (R >= 64) ? ~0ull : ((1ull << R) - 1ull);
     int i = 0;
     PNode nd = load_global(nodes, sl < n ? sl : n - 1);
     while (i < n) {
@@ -744,20 +744,24 @@ __device__ int trace_window(const DeviceScene &s, int R, int r, int sl, bool act
          * wave-uniform ray masks: node a's rays in = reach mask of its depth;
          * an interior node sets the mask of depth + 1 to the rays that entered
          * it (in & pass) */
-        const int meta = nd.depth | (interior ? 256 : 0);
-        const int kk = n - i < K ? n - i : K;
+        /* the K window nodes in order, unrolled and branch-free: a node past
+         * the array end (meta 0) reads depth 0 and writes nothing; its IN
+         * bits are never used (the node is not valid) */
+        const int meta = valid ? (nd.depth | (interior ? 256 : 0)) : 0;
         unsigned long long IN = 0ull;   /* bit a * R + r: ray r reaches window node a */
-        for (int a = 0; a < kk; ++a) {
-            const int m = __builtin_amdgcn_readlane(meta, a * R);
-            const int dd = m & 255;
+        int ms[K];
+#pragma unroll
+        for (int a = 0; a < K; ++a) ms[a] = __builtin_amdgcn_readlane(meta, a * R);
+#pragma unroll
+        for (int a = 0; a < K; ++a) {
+            const int dd = ms[a] & 255;
             const uint32_t in_m = (uint32_t)__builtin_amdgcn_readlane((int)vreach, dd);
-            if (m & 256) {
-                const uint32_t e_m = in_m & (uint32_t)(P >> (a * R)) & (uint32_t)rmask;
-                vreach = (int)__lane_id() == dd + 1 ? e_m : vreach;
-            }
+            const uint32_t e_m = in_m & (uint32_t)(P >> (a * R)) & (uint32_t)rmask;
+            vreach = ((ms[a] & 256) != 0) & ((int)__lane_id() == dd + 1) ? e_m : vreach;
             IN |= (unsigned long long)in_m << (a * R);
         }
         const bool my_in = ((IN >> __lane_id()) & 1ull) != 0ull;
+        const int kk = n - i < K ? n - i : K;   /* valid nodes of the window */
         if (COUNT) {
             if (my_in & alive) ++c.nodes;
             c.wave_nodes += (uint32_t)kk;     /* node records of the window */
@@ -1257,7 +1261,8 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             camera_ray(s, tl.x + px, tl.y + py, o, d);
             LaneCounts cw = {};
             float t;
-            const int slot = trace_window<COUNT>(s, R, r, sl, act, o, d, t, cw);
+            const int slot = R == 4 ? trace_window<COUNT, 4>(s, r, sl, act, o, d, t, cw)
+                                    : trace_window<COUNT, 16>(s, r, sl, act, o, d, t, cw);
             if (act && sl == 0) {
                 const Vec c = shade_primary(s, st, o, d, slot, t);
                 float *pxo = out + 3 * (tl.out_base + (int64_t)py * tl.out_stride + px);
