@@ -1,9 +1,9 @@
 #!/bin/bash
 # Round-2 GPU session: tests, smoke, bench (N=1), N=2 tiles rehearsal on the one
 # GPU (gloo, f32 and u8 payloads, --check), rocprofv3 kernel trace of the bench
-# command, PMC passes of the C2 render kernel -> profiles/r02/pmc_c2.json.
+# command, per-wave timeline, shadow-ray bench, PMC passes of the C2 render kernel -> profiles/r02/pmc_c2.json.
 # Each GPU step has its own time limit; a fault / abort / timeout ends the session.
-#   TAG=x STEPS=tests,smoke,bench,rehearse,prof,pmc bash scripts/gpu_r02.sh
+#   TAG=x STEPS=tests,smoke,bench,timeline,shadow,rehearse,prof,pmc bash scripts/gpu_r02.sh
 set -u
 cd "$(dirname "$0")/.."
 TAG=${TAG:-r02}
@@ -19,7 +19,7 @@ run() {
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-STEPS=${STEPS:-tests,smoke,bench,rehearse,prof,pmc}
+STEPS=${STEPS:-tests,smoke,bench,timeline,shadow,rehearse,prof,pmc}
 PYTEST_ARGS=${PYTEST_ARGS:-tests}
 [[ $STEPS == *tests* ]] && run pytest_gpu 900 python -u -m pytest $PYTEST_ARGS -m gpu -v -rf --timeout 300 --timeout-method thread
 [[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
@@ -28,6 +28,8 @@ if [[ $STEPS == *rehearse* ]]; then
   run rehearse2_f32 300 python bench.py --gpus 2 --steps 20 --warmup 3 --backend gloo --check
   run rehearse2_u8 300 python bench.py --gpus 2 --steps 20 --warmup 3 --backend gloo --check --payload u8 --no-secondary
 fi
+[[ $STEPS == *timeline* ]] && run timeline 300 python scripts/wave_timeline.py --out "$OUT/timeline_c2.json"
+[[ $STEPS == *shadow* ]] && run bench_shadows 600 python bench.py --shadows --steps 20 --warmup 5
 [[ $STEPS == *prof* ]] && run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-e2e
 if [[ $STEPS == *pmc* ]]; then
   CMD="python3 scripts/render_loop.py --frames 3"
