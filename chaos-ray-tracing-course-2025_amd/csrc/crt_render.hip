@@ -561,12 +561,16 @@ __device__ __forceinline__ void leaf_grouped(const DeviceScene &s, int first, in
     __builtin_amdgcn_wave_barrier();   /* the table is rewritten by the next leaf */
 }
 
-template <bool COUNT, bool FAST>
+/* ANY (shadow rays): only whether a hit lies within the light matters — the
+ * walk starts with lim0 (a bound past the light, so subtrees beyond it are
+ * pruned) and a lane leaves as soon as it holds a hit with t * t <= r2. */
+template <bool COUNT, bool FAST, bool ANY = false>
 __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool active, Vec o, Vec d,
-                                                     const RayRcp &rr, float &best_t, LaneCounts &c) {
+                                                     const RayRcp &rr, float &best_t, LaneCounts &c,
+                                                     float lim0 = INFINITY, float r2 = 0.0f) {
     int best = -1;
     best_t = 0.0f;
-    float lim = INFINITY;
+    float lim = ANY ? lim0 : INFINITY;
     const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
     unsigned long long reach = active ? 1ull : 0ull;
     const int n = s.node_count;
@@ -588,6 +592,7 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
     int i = 0;
     PNode cur = load_scalar(nodes, 0);
     while (i < n) {
+        if (ANY && __ballot(reach != 0ull) == 0ull) break;   /* every lane settled */
         const bool interior = cur.b < 0;
         const int i1 = i + 1 < n ? i + 1 : last;
         const int i2 = interior ? (cur.a < n ? cur.a : last) : i1;
@@ -654,7 +659,12 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
                     const bool hit = pre & tri_edges(o, d, g, t);
                     best_t = hit ? t : best_t;
                     best = hit ? slot : best;
-                    lim = hit ? t : lim;
+                    if constexpr (ANY) {
+                        lim = hit ? fminf(t, lim) : lim;
+                        if (hit && !(t * t > r2)) reach = 0ull;   /* occluded: this lane is done */
+                    } else {
+                        lim = hit ? t : lim;
+                    }
                 }
                 g = gn;
                 cw = cwn;
@@ -1150,6 +1160,21 @@ __device__ __forceinline__ bool shade_pass(const DeviceScene &s, const DSettings
     return called;
 }
 
+/* Shadow ray of shade_shadowed: true iff its closest hit is within the light
+ * (crt_renderer.cpp:92, distance^2 <= |light - p|^2).  Any hit with
+ * fl(t * t) <= r2 has t <= sqrt(r2) (1 + 2^-24) < lim0, so pruning past lim0
+ * and stopping at the first such hit give the same answer as the closest hit. */
+template <bool COUNT>
+__device__ __forceinline__ bool shadow_occluded_packet(const DeviceScene &s, bool active, Vec o, Vec d, float r2,
+                                                       LaneCounts &c) {
+    const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
+    if (COUNT && active) ++c.traversals;
+    const float lim0 = sqrtf(r2) * (1.0f + 0x1p-20f);
+    float t;
+    const int best = trace_packet_pruned_t<COUNT, false, true>(s, active, o, d, rr, t, c, lim0, r2);
+    return best >= 0 && !(t * t > r2);
+}
+
 /* Camera ray + shading with shadow rays for frames without recursion
  * (FULL=false, option "shadows"): the same operations as diffuse_finish<true>,
  * but each light's shadow rays are traced by the whole wave at once with the
@@ -1186,11 +1211,8 @@ __device__ Vec shade_shadowed(const DeviceScene &s, const DSettings &st, int x, 
         const float cos_law = (0.0f < dn) ? dn : 0.0f;
         const float area = 4 * kPi * r2;
         bool lit = true;
-        if (__ballot(diffuse) != 0ull) {
-            float ts;
-            const int ss = trace<8, COUNT>(s, L, diffuse, vadd(h.p, vscale(h.n, st.shadow_bias)), ld, ts, cnt);
-            lit = !(ss >= 0 && !(ts * ts > r2));
-        }
+        if (__ballot(diffuse) != 0ull)
+            lit = !shadow_occluded_packet<COUNT>(s, diffuse, vadd(h.p, vscale(h.n, st.shadow_bias)), ld, r2, cnt);
         if (diffuse && lit) acc = vadd(acc, vscale(vdiv(vscale(alb, Lt.intensity), area), cos_law));
     }
     if (diffuse) col = vdiv(acc, (float)(st.diffuse_reflection_ray_count + 1));
