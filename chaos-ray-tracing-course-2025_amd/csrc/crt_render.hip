@@ -1180,13 +1180,9 @@ __device__ __forceinline__ bool shadow_occluded_packet(const DeviceScene &s, boo
  * but each light's shadow rays are traced by the whole wave at once with the
  * pruned packet walk — a tile's shadow rays towards one light are coherent —
  * instead of one per-lane walk per lane. */
-template <int TRAV, bool COUNT>
-__device__ Vec shade_shadowed(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt, CoopLds *L,
-                              bool has_px) {
-    Vec o, d;
-    camera_ray(s, x, y, o, d);
-    float t;
-    const int slot = trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
+template <bool COUNT>
+__device__ Vec shade_hit_shadowed(const DeviceScene &s, const DSettings &st, bool has_px, Vec o, Vec d, int slot,
+                                  float t, LaneCounts &cnt) {
     Vec col = vec(s.background[0], s.background[1], s.background[2]);
     bool diffuse = false;
     HitRec h;
@@ -1217,6 +1213,16 @@ __device__ Vec shade_shadowed(const DeviceScene &s, const DSettings &st, int x, 
     }
     if (diffuse) col = vdiv(acc, (float)(st.diffuse_reflection_ray_count + 1));
     return col;
+}
+
+template <int TRAV, bool COUNT>
+__device__ Vec shade_shadowed(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt, CoopLds *L,
+                              bool has_px) {
+    Vec o, d;
+    camera_ray(s, x, y, o, d);
+    float t;
+    const int slot = trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
+    return shade_hit_shadowed<COUNT>(s, st, has_px, o, d, slot, t, cnt);
 }
 
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW = false>
@@ -1285,8 +1291,10 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             float t;
             const int slot = R == 4 ? trace_window<COUNT, 4>(s, r, sl, act, o, d, t, cw)
                                     : trace_window<COUNT, 16>(s, r, sl, act, o, d, t, cw);
+            Vec c;
+            if constexpr (SHADOW) c = shade_hit_shadowed<COUNT>(s, st, act && sl == 0, o, d, slot, t, cw);   /* wave-wide */
             if (act && sl == 0) {
-                const Vec c = shade_primary(s, st, o, d, slot, t);
+                if constexpr (!SHADOW) c = shade_primary(s, st, o, d, slot, t);
                 float *pxo = out + 3 * (tl.out_base + (int64_t)py * tl.out_stride + px);
                 pxo[0] = c.x;
                 pxo[1] = c.y;
@@ -2711,13 +2719,20 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         const uint64_t nf = (uint64_t)st->max_ray_depth + 1;
         const int nb = (plan.ntiles + 3) / 4;
         unsigned long long *cn = sc->d_counters;
-        if (!full) {   /* no recursion: packet walks for camera and shadow rays (shade_shadowed) */
-            if (count)
-                hipLaunchKernelGGL((k_render_tiles<false, 0, 8, 8, true, true>), dim3(nb), dim3(256), 0, stream, d_scene, ds,
-                                   plan.d_tiles, plan.ntiles, d_out, cn, nullptr);
-            else
-                hipLaunchKernelGGL((k_render_tiles<false, 0, 8, 8, false, true>), dim3(nb), dim3(256), 0, stream, d_scene,
-                                   ds, plan.d_tiles, plan.ntiles, d_out, cn, nullptr);
+        if (!full) {   /* no recursion: the frame's camera walk, packet walks for shadow rays (shade_hit_shadowed) */
+            int tr = camera_walk(sc, sc->traversal);
+            if (tr == 13 && !plan.has_small) tr = 12;
+#define CRT_LAUNCH_SH(TR, COUNT)                                                                            \
+    hipLaunchKernelGGL((k_render_tiles<false, 0, TR, TR, COUNT, true>), dim3(nb), dim3(256), 0, stream, d_scene, ds, \
+                       plan.d_tiles, plan.ntiles, d_out, cn, nullptr)
+            if (tr == 13) {
+                if (count) CRT_LAUNCH_SH(13, true); else CRT_LAUNCH_SH(13, false);
+            } else if (tr == 12) {
+                if (count) CRT_LAUNCH_SH(12, true); else CRT_LAUNCH_SH(12, false);
+            } else {
+                if (count) CRT_LAUNCH_SH(8, true); else CRT_LAUNCH_SH(8, false);
+            }
+#undef CRT_LAUNCH_SH
             HIP_TRY(hipGetLastError());
             return CRT_OK;
         }
