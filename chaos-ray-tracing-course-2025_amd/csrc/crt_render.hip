@@ -2015,7 +2015,8 @@ struct crt_hip_scene {
     int wf_graph = 1;              /* recorded-size wavefront frames replayed from captured HIP graphs (option "wf_graph") */
     int wf_replay = 1;             /* wavefront frames after the first: 1 recorded level sizes, 0 read back every level,
                                     * 2 recorded sizes minus one (tests: forces the overflow path) (option "wf_replay") */
-    int wf_rays_per_wave = 32;     /* rays per wave of wavefront levels >= 1, coop walks (env CRT_WF_RPW, option "wf_rpw"); C3: 64 4.70, 32 4.53, 16 4.58 ms */
+    int wf_rays_per_wave = 48;     /* rays per wave of wavefront levels >= 1, coop walks (env CRT_WF_RPW, option "wf_rpw");
+                                    * C3 (profiles/r02/ab_wf_rpw): 48 3.55, 32 3.64, 16 3.62, 64 3.68 ms */
     WfBuffers wf;
 };
 
