@@ -827,13 +827,28 @@ __device__ int trace_window(const DeviceScene &s, int r, int sl, bool active, Ve
                     }
                 }
             }
-            for (int off = R; off < 64; off <<= 1) {
-                const float ot = __shfl_xor(lt, off);
-                const int os = __shfl_xor(ls, off);
-                if (os >= 0 && key_better(ot, os, lt, ls)) {
-                    lt = ot;
-                    ls = os;
-                }
+            /* branch-free merge of the ray's K candidates as one 64-bit key:
+             * (t bits, slot), +-0 as 0 with the sign of a zero t kept in slot
+             * bit 31 (ignored by the order), no hit = all ones; the in-row
+             * steps (R < 16) rotate by DPP instead of LDS permutes */
+            unsigned hi = ls < 0 ? 0xffffffffu : (lt == 0.0f ? 0u : __float_as_uint(lt));
+            unsigned lo = ls < 0 ? 0xffffffffu : ((unsigned)ls | (__float_as_uint(lt) == 0x80000000u ? 0x80000000u : 0u));
+            auto keep_min = [&](unsigned ohi, unsigned olo) {
+                const unsigned long long a = ((unsigned long long)hi << 32) | (lo & 0x7fffffffu);
+                const unsigned long long b = ((unsigned long long)ohi << 32) | (olo & 0x7fffffffu);
+                const bool take = b < a;
+                hi = take ? ohi : hi;
+                lo = take ? olo : lo;
+            };
+            if constexpr (R < 8) keep_min((unsigned)__builtin_amdgcn_update_dpp((int)hi, (int)hi, 0x124, 0xf, 0xf, false),
+                                          (unsigned)__builtin_amdgcn_update_dpp((int)lo, (int)lo, 0x124, 0xf, 0xf, false));
+            if constexpr (R < 16) keep_min((unsigned)__builtin_amdgcn_update_dpp((int)hi, (int)hi, 0x128, 0xf, 0xf, false),
+                                           (unsigned)__builtin_amdgcn_update_dpp((int)lo, (int)lo, 0x128, 0xf, 0xf, false));
+#pragma unroll
+            for (int off = 16; off < 64; off <<= 1) keep_min((unsigned)__shfl_xor((int)hi, off), (unsigned)__shfl_xor((int)lo, off));
+            if (hi != 0xffffffffu) {
+                ls = (int)(lo & 0x7fffffffu);
+                lt = hi != 0u ? __uint_as_float(hi) : ((lo & 0x80000000u) ? -0.0f : 0.0f);
             }
             best_t = lt;
             best = ls;

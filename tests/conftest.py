@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
-PKG = ROOT / "chaos-ray-tracing-course-2025_amd"
+PKG = Path(os.environ["CRT_PKG"]).resolve() if os.environ.get("CRT_PKG") else ROOT / "chaos-ray-tracing-course-2025_amd"   # CRT_PKG: a variant build
 for p in (str(PKG), str(ROOT)):
     if p not in sys.path:
         sys.path.insert(0, p)
