@@ -491,6 +491,47 @@ __device__ __forceinline__ bool face_cache_pass(FaceCache &fc, const PNode &n, V
 }
 #pragma clang diagnostic pop
 
+/* Closest-hit candidates of one ray spread over lanes congruent mod G (G a
+ * power of two), merged branch-free as one 64-bit key: (t bits, slot) with
+ * +-0 as 0 and a zero t's sign kept in slot bit 31 outside the order; no
+ * hit = all ones.  Steps below 16 lanes rotate within the row by DPP
+ * (row_ror, a multiple of G, so within the class), wider ones use LDS
+ * permutes; every lane of a class ends with the class minimum — the
+ * reference's first-found choice (key_better) whatever the lane order. */
+struct HitKey { unsigned hi, lo; };
+__device__ __forceinline__ HitKey hit_key(float t, int slot) {
+    if (slot < 0) return HitKey{0xffffffffu, 0xffffffffu};
+    return HitKey{t == 0.0f ? 0u : __float_as_uint(t),
+                  (unsigned)slot | (__float_as_uint(t) == 0x80000000u ? 0x80000000u : 0u)};
+}
+__device__ __forceinline__ void hit_key_min(HitKey &k, unsigned ohi, unsigned olo) {
+    const unsigned long long a = ((unsigned long long)k.hi << 32) | (k.lo & 0x7fffffffu);
+    const unsigned long long b = ((unsigned long long)ohi << 32) | (olo & 0x7fffffffu);
+    const bool take = b < a;
+    k.hi = take ? ohi : k.hi;
+    k.lo = take ? olo : k.lo;
+}
+template <int CTRL>
+__device__ __forceinline__ void hit_key_dpp(HitKey &k) {
+    hit_key_min(k, (unsigned)__builtin_amdgcn_update_dpp((int)k.hi, (int)k.hi, CTRL, 0xf, 0xf, false),
+                (unsigned)__builtin_amdgcn_update_dpp((int)k.lo, (int)k.lo, CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ void hit_key_allmin(HitKey &k, int G) {   /* G wave-uniform */
+    if (G <= 1) hit_key_dpp<0x121>(k);   /* row_ror:1 */
+    if (G <= 2) hit_key_dpp<0x122>(k);
+    if (G <= 4) hit_key_dpp<0x124>(k);
+    if (G <= 8) hit_key_dpp<0x128>(k);
+    for (int off = G > 16 ? G : 16; off < 64; off <<= 1)
+        hit_key_min(k, (unsigned)__shfl_xor((int)k.hi, off), (unsigned)__shfl_xor((int)k.lo, off));
+}
+/* decode into (t, slot) when the key holds a hit */
+__device__ __forceinline__ void hit_key_get(const HitKey &k, float &t, int &slot) {
+    if (k.hi != 0xffffffffu) {
+        slot = (int)(k.lo & 0x7fffffffu);
+        t = k.hi != 0u ? __uint_as_float(k.hi) : ((k.lo & 0x80000000u) ? -0.0f : 0.0f);
+    }
+}
+
 /* Leaf phase of the fast packet walk when few rays entered the leaf (m of
  * 64 lanes, m <= 32): instead of 64 lanes per triangle with 64 - m of them
  * idle, the wave tests T = 64 / G triangles at once, G >= m lanes per
@@ -543,16 +584,13 @@ __device__ __forceinline__ void leaf_grouped(const DeviceScene &s, int first, in
             }
         }
     }
-    for (int off = G; off < 64; off <<= 1) {
-        const float ot = __shfl_xor(lt, off);
-        const int os = __shfl_xor(ls, off);
-        if (os >= 0 && key_better(ot, os, lt, ls)) {
-            lt = ot;
-            ls = os;
-        }
-    }
-    const float nt = __shfl(lt, rank);
-    const int ns = __shfl(ls, rank);
+    HitKey key = hit_key(lt, ls);
+    hit_key_allmin(key, G);
+    key.hi = (unsigned)__shfl((int)key.hi, rank);
+    key.lo = (unsigned)__shfl((int)key.lo, rank);
+    float nt = 0.0f;
+    int ns = -1;
+    hit_key_get(key, nt, ns);
     if (pass) {
         best_t = nt;
         best = ns;
@@ -827,29 +865,9 @@ __device__ int trace_window(const DeviceScene &s, int r, int sl, bool active, Ve
                     }
                 }
             }
-            /* branch-free merge of the ray's K candidates as one 64-bit key:
-             * (t bits, slot), +-0 as 0 with the sign of a zero t kept in slot
-             * bit 31 (ignored by the order), no hit = all ones; the in-row
-             * steps (R < 16) rotate by DPP instead of LDS permutes */
-            unsigned hi = ls < 0 ? 0xffffffffu : (lt == 0.0f ? 0u : __float_as_uint(lt));
-            unsigned lo = ls < 0 ? 0xffffffffu : ((unsigned)ls | (__float_as_uint(lt) == 0x80000000u ? 0x80000000u : 0u));
-            auto keep_min = [&](unsigned ohi, unsigned olo) {
-                const unsigned long long a = ((unsigned long long)hi << 32) | (lo & 0x7fffffffu);
-                const unsigned long long b = ((unsigned long long)ohi << 32) | (olo & 0x7fffffffu);
-                const bool take = b < a;
-                hi = take ? ohi : hi;
-                lo = take ? olo : lo;
-            };
-            if constexpr (R < 8) keep_min((unsigned)__builtin_amdgcn_update_dpp((int)hi, (int)hi, 0x124, 0xf, 0xf, false),
-                                          (unsigned)__builtin_amdgcn_update_dpp((int)lo, (int)lo, 0x124, 0xf, 0xf, false));
-            if constexpr (R < 16) keep_min((unsigned)__builtin_amdgcn_update_dpp((int)hi, (int)hi, 0x128, 0xf, 0xf, false),
-                                           (unsigned)__builtin_amdgcn_update_dpp((int)lo, (int)lo, 0x128, 0xf, 0xf, false));
-#pragma unroll
-            for (int off = 16; off < 64; off <<= 1) keep_min((unsigned)__shfl_xor((int)hi, off), (unsigned)__shfl_xor((int)lo, off));
-            if (hi != 0xffffffffu) {
-                ls = (int)(lo & 0x7fffffffu);
-                lt = hi != 0u ? __uint_as_float(hi) : ((lo & 0x80000000u) ? -0.0f : 0.0f);
-            }
+            HitKey key = hit_key(lt, ls);   /* merge over the ray's K lanes */
+            hit_key_allmin(key, R);
+            hit_key_get(key, lt, ls);
             best_t = lt;
             best = ls;
             lim = best >= 0 ? best_t : INFINITY;
