@@ -45,10 +45,8 @@ struct alignas(16) Tile {
     int32_t x, y, w, h;        /* pixel rectangle, w,h <= 8 */
     int64_t out_base;          /* output pixel index of (x, y) */
     int32_t out_stride;        /* output pixels per row */
-    int32_t prio;              /* bit 0: one of the frame's heaviest waves — raised issue priority;
-                                * bit 2 (kPartTile): part (bits 4-5) of a tile split over a block's 4 waves */
+    int32_t prio;              /* 1: one of the frame's heaviest waves — raised issue priority */
 };
-constexpr int32_t kPartTile = 4;
 
 struct alignas(16) UnpackBucket {
     int32_t x, y, w, h;
@@ -494,9 +492,9 @@ __device__ __forceinline__ bool face_cache_pass(FaceCache &fc, const PNode &n, V
 #pragma clang diagnostic pop
 
 /* Closest-hit candidates of one ray spread over lanes congruent mod G (G a
- * power of two), merged branch-free as one 64-bit key: (t bits, 2 slot + s)
- * with +-0 as 0 and s the sign of a zero t (a slot belongs to one triangle
- * copy, so s never decides between two candidates); no hit = all ones.  Steps below 16 lanes rotate within the row by DPP
+ * power of two), merged branch-free as one 64-bit key: (t bits, slot) with
+ * +-0 as 0 and a zero t's sign kept in slot bit 31 outside the order; no
+ * hit = all ones.  Steps below 16 lanes rotate within the row by DPP
  * (row_ror, a multiple of G, so within the class), wider ones use LDS
  * permutes; every lane of a class ends with the class minimum — the
  * reference's first-found choice (key_better) whatever the lane order. */
@@ -504,14 +502,11 @@ struct HitKey { unsigned hi, lo; };
 __device__ __forceinline__ HitKey hit_key(float t, int slot) {
     if (slot < 0) return HitKey{0xffffffffu, 0xffffffffu};
     return HitKey{t == 0.0f ? 0u : __float_as_uint(t),
-                  ((unsigned)slot << 1) | (__float_as_uint(t) == 0x80000000u ? 1u : 0u)};
-}
-__device__ __forceinline__ unsigned long long hit_key_u64(const HitKey &k) {
-    return ((unsigned long long)k.hi << 32) | k.lo;
+                  (unsigned)slot | (__float_as_uint(t) == 0x80000000u ? 0x80000000u : 0u)};
 }
 __device__ __forceinline__ void hit_key_min(HitKey &k, unsigned ohi, unsigned olo) {
-    const unsigned long long a = ((unsigned long long)k.hi << 32) | k.lo;
-    const unsigned long long b = ((unsigned long long)ohi << 32) | olo;
+    const unsigned long long a = ((unsigned long long)k.hi << 32) | (k.lo & 0x7fffffffu);
+    const unsigned long long b = ((unsigned long long)ohi << 32) | (olo & 0x7fffffffu);
     const bool take = b < a;
     k.hi = take ? ohi : k.hi;
     k.lo = take ? olo : k.lo;
@@ -532,8 +527,8 @@ __device__ __forceinline__ void hit_key_allmin(HitKey &k, int G) {   /* G wave-u
 /* decode into (t, slot) when the key holds a hit */
 __device__ __forceinline__ void hit_key_get(const HitKey &k, float &t, int &slot) {
     if (k.hi != 0xffffffffu) {
-        slot = (int)(k.lo >> 1);
-        t = k.hi != 0u ? __uint_as_float(k.hi) : ((k.lo & 1u) ? -0.0f : 0.0f);
+        slot = (int)(k.lo & 0x7fffffffu);
+        t = k.hi != 0u ? __uint_as_float(k.hi) : ((k.lo & 0x80000000u) ? -0.0f : 0.0f);
     }
 }
 
@@ -760,14 +755,9 @@ __device__ __forceinline__ int wave_max_i(int v) {
     return v;
 }
 
-/* PART (tile parts, option "tile_parts"): the wave walks one of the four
- * depth-2 subtrees of the octant order (part 0..3; the two nodes above it are
- * tested first to seed the reach masks), and the four waves of the block
- * share each ray's best key through `keys` (LDS): a wave prunes with the best
- * hit any part has found so far, which never removes a better candidate. */
-template <bool COUNT, int R, bool PART = false>
+template <bool COUNT, int R>
 __device__ int trace_window(const DeviceScene &s, int r, int sl, bool active, Vec o, Vec d, float &best_t,
-                            LaneCounts &c, int part = 0, unsigned long long *keys = nullptr) {
+                            LaneCounts &c) {
     const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
     const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
     const bool lead = sl == 0;                       /* one lane per ray for votes and counters */
@@ -789,43 +779,11 @@ __device__ int trace_window(const DeviceScene &s, int r, int sl, bool active, Ve
     if (2 * __popcll(__ballot(active && lead && d.z < 0.0f)) > na) oct |= 4;
     const PNode *nodes = pnode_order(s.pnodes, n, uniform_i(oct));
     constexpr unsigned long long rmask = (R >= 64) ? ~0ull : ((1ull << R) - 1ull);
-    int lo = 0, hi = n;
-    if constexpr (PART) {
-        /* root 0, children A = 1 and B = skip(1); A's children 2 and
-         * skip(2), B's B + 1 and skip(B + 1) (preorder of this octant) */
-        const PNode r0 = load_scalar(nodes, 0);
-        const PNode na = load_scalar(nodes, 1);
-        const int b = na.a;
-        bool ok = r0.b < 0 && na.b < 0 && b > 2 && b < n;
-        const PNode nb = load_scalar(nodes, ok ? b : 0);
-        ok = ok && nb.b < 0 && b + 1 < n;
-        const PNode a1 = load_scalar(nodes, 2);
-        const PNode b1 = load_scalar(nodes, ok ? b + 1 : 0);
-        if (ok) {
-            const int ranges[5] = {2, a1.a, b, b1.a, nb.a};   /* part p: nodes [lo, hi) */
-            lo = part == 0 ? ranges[0] : part == 1 ? ranges[1] : part == 2 ? b + 1 : ranges[3];
-            hi = part == 0 ? ranges[1] : part == 1 ? ranges[2] : part == 2 ? ranges[3] : ranges[4];
-            const PNode anc = part < 2 ? na : nb;
-            const bool p0 = active & hull_alive(r0, pr, INFINITY) & box_hit_fast(o, d, rr, cell_of(r0));
-            const bool p1 = p0 & hull_alive(anc, pr, INFINITY) & box_hit_fast(o, d, rr, cell_of(anc));
-            const uint32_t m1 = (uint32_t)__ballot(p0 && lead), m2 = (uint32_t)__ballot(p1 && lead);
-            vreach = __lane_id() == 1 ? m1 : __lane_id() == 2 ? m2 : vreach;
-        } else if (part != 0) {
-            lo = hi = 0;   /* a shallow tree: part 0 walks it whole */
-        }
-    }
-    int i = lo;
-    PNode nd = load_global(nodes, lo + sl < hi ? lo + sl : (hi > 0 ? hi - 1 : 0));
-    while (i < hi) {
-        if constexpr (PART) {   /* the best hit any part of this ray holds bounds the hull test */
-            const unsigned long long gk = keys[r];
-            if (gk != ~0ull) {
-                const unsigned ghi = (unsigned)(gk >> 32);
-                lim = fminf(lim, ghi != 0u ? __uint_as_float(ghi) : 0.0f);
-            }
-        }
+    int i = 0;
+    PNode nd = load_global(nodes, sl < n ? sl : n - 1);
+    while (i < n) {
         const int j = i + sl;
-        const bool valid = j < hi;
+        const bool valid = j < n;
         const bool interior = nd.count == 0;
         const bool alive = valid & active & hull_alive(nd, pr, lim);
         const bool pass = alive & box_hit_fast(o, d, rr, cell_of(nd));
@@ -851,7 +809,7 @@ __device__ int trace_window(const DeviceScene &s, int r, int sl, bool active, Ve
             IN |= (unsigned long long)in_m << (a * R);
         }
         const bool my_in = ((IN >> __lane_id()) & 1ull) != 0ull;
-        const int kk = hi - i < K ? hi - i : K;   /* valid nodes of the window */
+        const int kk = n - i < K ? n - i : K;   /* valid nodes of the window */
         if (COUNT) {
             if (my_in & alive) ++c.nodes;
             c.wave_nodes += (uint32_t)kk;     /* node records of the window */
@@ -913,12 +871,9 @@ __device__ int trace_window(const DeviceScene &s, int r, int sl, bool active, Ve
             best_t = lt;
             best = ls;
             lim = best >= 0 ? best_t : INFINITY;
-            if constexpr (PART) {
-                if (lead && active && best >= 0) atomicMin(&keys[r], hit_key_u64(hit_key(best_t, best)));
-            }
         }
         {
-            nd = load_global(nodes, next + sl < hi ? next + sl : hi - 1);
+            nd = load_global(nodes, next + sl < n ? next + sl : n - 1);
         }
         i = next;
     }
@@ -1353,7 +1308,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
     /* the heaviest tiles set the frame length (their walks are long chains of
      * dependent loads): they get issue priority over the light waves that
      * share their SIMD (s_setprio; scheduling only, results unchanged) */
-    if (tl.prio & 1) __builtin_amdgcn_s_setprio(3);
+    if (tl.prio) __builtin_amdgcn_s_setprio(3);
     if constexpr (TRAV == 13 && !FULL) {
         /* tiles of <= 16 rays (the measured plan's splits of heavy tiles): window walk */
         const int tw = uniform_i(tl.w), th = uniform_i(tl.h);
@@ -1367,35 +1322,8 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             camera_ray(s, tl.x + px, tl.y + py, o, d);
             LaneCounts cw = {};
             float t;
-            int slot;
-            if (tl.prio & kPartTile) {
-                /* tile parts: the block's four waves are parts 0..3 of one
-                 * <= 4-ray tile (plan: aligned groups), each walking one
-                 * depth-2 subtree; part 0 shades the block's merged result */
-                __shared__ unsigned long long part_keys[4];
-                const int part = (tl.prio >> 4) & 3;
-                if (part == 0 && lane < 4) part_keys[lane] = ~0ull;
-                __syncthreads();
-                slot = trace_window<COUNT, 4, true>(s, r, sl, act, o, d, t, cw, part, part_keys);
-                __syncthreads();
-                if (part != 0) slot = -1;   /* only part 0 writes the pixels */
-                else {
-                    const unsigned long long k = part_keys[r];
-                    HitKey hk{(unsigned)(k >> 32), (unsigned)k};
-                    slot = -1;
-                    hit_key_get(hk, t, slot);
-                }
-                if (part != 0) {
-                    if (COUNT) {
-                        atomicAdd(&counters[1], (unsigned long long)cw.nodes);
-                        atomicAdd(&counters[2], (unsigned long long)cw.tris);
-                    }
-                    return;
-                }
-            } else {
-                slot = R == 4 ? trace_window<COUNT, 4>(s, r, sl, act, o, d, t, cw)
-                              : trace_window<COUNT, 16>(s, r, sl, act, o, d, t, cw);
-            }
+            const int slot = R == 4 ? trace_window<COUNT, 4>(s, r, sl, act, o, d, t, cw)
+                                    : trace_window<COUNT, 16>(s, r, sl, act, o, d, t, cw);
             Vec c;
             if constexpr (SHADOW) c = shade_hit_shadowed<COUNT>(s, st, act && sl == 0, o, d, slot, t, cw);   /* wave-wide */
             if (act && sl == 0) {
@@ -1658,7 +1586,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         const int wave = gid >> 6;
         if (wave >= ntiles) return;
         const Tile tl = tiles[wave];
-        if (tl.prio & 1) __builtin_amdgcn_s_setprio(3);
+        if (tl.prio) __builtin_amdgcn_s_setprio(3);
         const int lx = lane & 7, ly = lane >> 3;
         has = lx < tl.w && ly < tl.h;
         if (has) camera_ray(s, tl.x + lx, tl.y + ly, o, d);
@@ -2083,7 +2011,6 @@ struct crt_hip_scene {
     int refill_waves = 5120;           /* waves of the refill grid: CUs x 4 SIMDs x CRT_GI_WAVES */
     bool grid_empty = false;
     int traversal = 8;             /* 7 reference order | 8 pruned (default), see trace<> (env CRT_TRAVERSAL) */
-    int tile_parts = 1;            /* option "tile_parts": split tiles of <= 4 rays walked by 4 waves (see use_tile_parts) */
     int shadows = 0;               /* option "shadows": trace the shadow rays (k_render_tiles<..., SHADOW>) */
     int trace_walk = 1;            /* crt_hip_trace_batch: 0 reference-order walk, 1 pruned per-lane walk */
     bool camera_fast = false;      /* every camera ray takes the fast box path (camera_rays_fast) */
@@ -2171,17 +2098,7 @@ bool camera_rays_fast(const HostScene &hs, bool planes_ok) {
     return smin > 0x1p-50 && smin > 1e-4 * (2.0 + aa + ta) * mx;
 }
 
-/* Tile parts (option "tile_parts": 0 off, 1 shard plans of >= 2 shards,
- * 2 every plan): only for scenes whose frames run no recursion and no GI, the
- * frames whose kernels know part tiles (k_render_tiles; the other tile-list
- * kernels would render a part group's tile four times). */
-bool use_tile_parts(const crt_hip_scene *sc, int shard_count) {
-    if (sc->has_secondary || sc->info.gi_on) return false;
-    return sc->tile_parts == 2 || (sc->tile_parts == 1 && shard_count >= 2);
-}
-
-int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool full_frame, ShardPlan &plan,
-                   bool parts = false) {
+int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool full_frame, ShardPlan &plan) {
     std::vector<Tile> tiles;
     const int W = sc->info.width;
     if (full_frame) {
@@ -2225,22 +2142,7 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
                          [](const std::pair<float, Tile> &a, const std::pair<float, Tile> &b) { return a.first > b.first; });
         tiles.clear();
         plan.cost.clear();
-        if (parts) {
-            /* tile parts (walk 13): every split tile of <= 4 rays becomes a
-             * group of four waves, parts 0..3, at the front of the list so
-             * each group fills one 256-thread block (4-aligned indices) */
-            for (const auto &e : out) {
-                if (e.second.w * e.second.h > 4) continue;
-                for (int p = 0; p < 4; ++p) {
-                    Tile t = e.second;
-                    t.prio = kPartTile | (p << 4);
-                    tiles.push_back(t);
-                    plan.cost.push_back(e.first);
-                }
-            }
-        }
         for (const auto &e : out) {
-            if (parts && e.second.w * e.second.h <= 4) continue;
             tiles.push_back(e.second);
             plan.cost.push_back(e.first);
         }
@@ -2515,7 +2417,7 @@ int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t
     if (sc->calibrate == 2) {
         if ((rc = calibrate_plan(sc, d_scene, walk, stream)) != CRT_OK) return rc;
         free_plans(sc);
-        return make_tile_plan(sc, all, true, sc->full, use_tile_parts(sc, 0));
+        return make_tile_plan(sc, all, true, sc->full);
     }
     float *scratch = nullptr;
     HIP_TRY(hipMalloc(&scratch, (size_t)sc->info.width * sc->info.height * 3 * sizeof(float)));
@@ -2530,7 +2432,7 @@ int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t
             int r = calibrate_plan(sc, d_scene, walk, stream);
             if (r != CRT_OK) return r;
             free_plans(sc);
-            if ((r = make_tile_plan(sc, all, true, sc->full, use_tile_parts(sc, 0))) != CRT_OK) return r;
+            if ((r = make_tile_plan(sc, all, true, sc->full)) != CRT_OK) return r;
             std::vector<float> reps;
             for (int rep = 0; rep < 6; ++rep) {
                 HIP_TRY(hipEventRecord(e0, stream));
@@ -2561,7 +2463,7 @@ int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t
     sc->calib.swap(best_cal);
     sc->calib_walk = walk;
     free_plans(sc);
-    return make_tile_plan(sc, all, true, sc->full, use_tile_parts(sc, 0));
+    return make_tile_plan(sc, all, true, sc->full);
 }
 
 DSettings to_dsettings(const crt_renderer_settings *st) {
@@ -3296,7 +3198,7 @@ int render_shard_t(crt_hip_scene *sc, const crt_renderer_settings *st, int shard
                                                : shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size,
                                                                shard, shard_count, &px);
         ShardPlan plan;
-        if ((rc = make_tile_plan(sc, b, false, plan, use_tile_parts(sc, shard_count))) != CRT_OK) return rc;
+        if ((rc = make_tile_plan(sc, b, false, plan)) != CRT_OK) return rc;
         it = plans.emplace(key, plan).first;
     }
     if (sc->record_events) HIP_TRY(hipEventRecord(sc->ev_start, s));
@@ -3590,12 +3492,6 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         if (value != 1 && value != 2 && value != 4 && value != 8) return set_error(CRT_E_INVALID, "calib_min must be 1, 2, 4 or 8");
         sc->calib_min = value;
         sc->calib_walk = -1;
-    } else if (k == "tile_parts") {
-        if (value < 0 || value > 2) return set_error(CRT_E_INVALID, "tile_parts must be 0, 1 or 2");
-        sc->tile_parts = value;
-        HIP_TRY(hipDeviceSynchronize());
-        sc->calib_walk = -1;   /* rebuild the plans */
-        free_plans(sc);
     } else if (k == "shadows") {
         sc->shadows = value != 0;
     } else if (k == "trace_walk") {

@@ -258,21 +258,3 @@ def test_gi_pixel_refill_bit_identical(N, oracle, w, h):
     ca = N.HipScene(sc).set_option("gi_refill", 1).count_work(st)
     cb = N.HipScene(sc).set_option("gi_refill", 0).count_work(st)
     assert ca == cb
-
-
-@pytest.mark.parametrize("calib_k", [None, "1.5"])
-def test_tile_parts_bit_exact(N, oracle, monkeypatch, calib_k):
-    """Tile parts (option tile_parts 2: every split tile of <= 4 rays walked by
-    four waves, one depth-2 subtree each, sharing best keys in LDS) give the
-    oracle's frame bit for bit; calib_k 1.5 splits many more tiles."""
-    if calib_k:
-        monkeypatch.setenv("CRT_CALIB_K", calib_k)
-        monkeypatch.setenv("CRT_CALIBRATE", "2")
-    sc = scene_npz("14-01-acceleration-tree__scene1")
-    st = N.RendererSettings.default()
-    want = oracle.OracleScene(sc).render(st)
-    gpu = N.HipScene(sc, tile_parts=2)
-    got = gpu.render(st)
-    assert gpu.plan_info()["small_tiles"] > 0
-    nbad = int((bits(got) != bits(want)).sum())
-    assert nbad == 0, f"{nbad} floats differ"
