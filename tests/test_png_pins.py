@@ -114,3 +114,25 @@ def test_gpu_shadow_rays_match_oracle(oracle, name, w, h, over):
         gc = gpu.count_work(st)
         assert gc["traversals"] == wc.traversals > w * h   # shadow rays stop at their first occluder, so
                                                             # hits are not compared
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards", [3, 8])
+def test_gpu_shadow_shards_reassemble(devbuf, shards):
+    """Shadow-ray frames sharded by the reference's bucket grid (compact shards,
+    as bench.py --gpus N --shadows would run them) reassemble into the
+    single-GPU shadow frame bit for bit."""
+    from crt_amd import native as N
+    sc = scene_npz("14-01-acceleration-tree__scene1").set_resolution(640, 360)
+    st = N.RendererSettings.default()
+    gpu = N.HipScene(sc, shadows=1)
+    full = gpu.render(st)
+    stride = gpu.compact_stride(shards)
+    gathered = devbuf.alloc(4 * stride * shards)
+    frame = devbuf.alloc(full.nbytes)
+    for s in range(shards):
+        gpu.render_shard_compact(st, s, shards, gathered + 4 * s * stride)
+        devbuf.sync()
+    gpu.unpack_compact(shards, gathered, frame)
+    out = devbuf.download(frame, full.shape, np.float32)
+    assert np.array_equal(bits(out), bits(full))
