@@ -2048,8 +2048,9 @@ struct crt_hip_scene {
     int wf_graph = 1;              /* recorded-size wavefront frames replayed from captured HIP graphs (option "wf_graph") */
     int wf_replay = 1;             /* wavefront frames after the first: 1 recorded level sizes, 0 read back every level,
                                     * 2 recorded sizes minus one (tests: forces the overflow path) (option "wf_replay") */
-    int wf_rays_per_wave = 48;     /* rays per wave of wavefront levels >= 1, coop walks (env CRT_WF_RPW, option "wf_rpw");
-                                    * C3 (profiles/r02/ab_wf_rpw): 48 3.55, 32 3.64, 16 3.62, 64 3.68 ms */
+    int wf_rays_per_wave = 48;     /* cap on the rays per wave of wavefront levels >= 1 (each level takes
+                                    * min(cap, max(8, n / 4096)), render_wavefront), coop walks (env CRT_WF_RPW,
+                                    * option "wf_rpw"); fixed 48 / 32 / 16 / 64: 3.55 / 3.64 / 3.62 / 3.68 ms */
     WfBuffers wf;
 };
 
@@ -2654,9 +2655,14 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
             out_cap = cap_of(w.qcap[cur ^ 1]);
             sizes.push_back(n);
         }
-        WLevel l{w.q[cur], n, L, w.q[cur ^ 1], w.counts + L, (int32_t)(base + n), w.nodes, w.cols, rpw, out_cap,
+        /* rays per wave of this level: fewer (more helper lanes per ray) when
+         * the level has fewer rays than ~4096 waves' worth, at least 8, at most
+         * the wf_rpw cap — a level's time is its slowest waves'
+         * (C3 3.60 -> 3.33 ms, profiles/r02/ab_c3_rpw) */
+        const int rpw_l = std::min(rpw, std::max(8, (int)((n + 4095) / 4096)));
+        WLevel l{w.q[cur], n, L, w.q[cur ^ 1], w.counts + L, (int32_t)(base + n), w.nodes, w.cols, rpw_l, out_cap,
                  w.d_flag};
-        const int64_t waves = ((int64_t)n + rpw - 1) / rpw;
+        const int64_t waves = ((int64_t)n + rpw_l - 1) / rpw_l;
         const int blocks = (int)((waves + 3) / 4);
 #define CRT_WF(SEC, COUNT)                                                                                  \
     hipLaunchKernelGGL((k_wf_level<SEC, false, COUNT>), dim3(blocks), dim3(256), 0, stream, d_scene, ds,     \

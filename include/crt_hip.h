@@ -379,8 +379,9 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  *                threshold of env CRT_CALIB_K (default 4)
  *   "gi_refill"  0/1 (default 1): GI frames run persistent waves that refill
  *                finished lanes with the next pixel of the tile list
- *   "wf_rpw"     1..64 (default 48): rays per wave of wavefront levels >= 1 (the
- *                other lanes start idle and take donated pieces)
+ *   "wf_rpw"     1..64 (default 48): cap on the rays per wave of wavefront
+ *                levels >= 1; a level of n rays takes min(cap, max(8, n / 4096))
+ *                and the other lanes start idle and take donated pieces
  *   "wf_replay"  1 (default): a wavefront frame whose settings and tile list
  *                were rendered before launches every level with the recorded
  *                level sizes, no host read-back | 0: read every level's size
