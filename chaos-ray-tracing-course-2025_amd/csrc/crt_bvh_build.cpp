@@ -1,0 +1,248 @@
+/*
+ * crt_bvh_build.cpp — host build of the secondary-ray BVH (crt_bvh.h,
+ * crt_layout.h BNode).
+ *
+ * The BVH is an acceleration structure of our own, next to the reference's
+ * tree, not a replacement of it: scattered rays find their closest triangle
+ * through it and then prove on the reference's tree that the reference
+ * reaches that triangle (crt_bvh.h).  So its shape is free and only its
+ * boxes carry the exactness argument: every box is the union, rounded
+ * outwards, of the conservative hulls of the triangles below it
+ * (crt_device.h triangle_hull, the same hulls as the pruned kd walks'), so a
+ * box the ray misses before `lim` holds no triangle the reference's test
+ * could accept at t <= lim.
+ *
+ * Shape: binned SAH (16 bins over triangle centroids, surface areas of the
+ * triangles' own boxes), leaves of at most kLeafMax triangles; every triangle
+ * once.  Stored once per direction octant (8 orders) in preorder with the
+ * near child first along the node's split axis, with skip links, so the walk
+ * is stackless.
+ */
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <vector>
+
+#include "crt_device.h"
+#include "crt_host.h"
+
+namespace crt_amd {
+
+namespace {
+
+constexpr int kLeafMax = 2;     /* triangles per leaf (15-01/scene2 GI rays: ~15 box + ~3.3 triangle tests) */
+constexpr int kBins = 16;
+constexpr int kMaxDepth = 48;   /* deeper subtrees are split at the median index */
+
+struct Aabb {
+    float lo[3], hi[3];
+};
+
+Aabb aabb_empty() {
+    const float inf = std::numeric_limits<float>::infinity();
+    return Aabb{{inf, inf, inf}, {-inf, -inf, -inf}};
+}
+
+void grow(Aabb &a, const Aabb &b) {
+    for (int k = 0; k < 3; ++k) {
+        a.lo[k] = std::min(a.lo[k], b.lo[k]);
+        a.hi[k] = std::max(a.hi[k], b.hi[k]);
+    }
+}
+
+double area(const Aabb &a) {
+    const double dx = (double)a.hi[0] - a.lo[0], dy = (double)a.hi[1] - a.lo[1], dz = (double)a.hi[2] - a.lo[2];
+    if (!(dx >= 0.0) || !(dy >= 0.0) || !(dz >= 0.0)) return 0.0;
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+}
+
+struct Build {
+    int32_t left = -1, right = -1;   /* children (build numbering) */
+    int32_t axis = 0;
+    int32_t first = 0, count = 0;    /* leaf: range of `order` */
+    HullD hull;
+};
+
+}  // namespace
+
+int build_bvh(HostScene &hs) {
+    hs.bnodes.clear();
+    hs.btri.clear();
+    hs.btri_id.clear();
+    const int32_t nt = (int32_t)hs.tri_attr.size();
+    if (nt == 0) return CRT_OK;
+    const double G = hs.prune_G;
+
+    std::vector<Aabb> box((size_t)nt);
+    std::vector<float> cen((size_t)nt * 3);
+    std::vector<HullD> hull((size_t)nt);
+    for (int32_t t = 0; t < nt; ++t) {
+        const DTriAttr &at = hs.tri_attr[t];
+        const float *v[3] = {&hs.vpos[3 * (size_t)at.i0], &hs.vpos[3 * (size_t)at.i1], &hs.vpos[3 * (size_t)at.i2]};
+        Aabb b = aabb_empty();
+        bool finite = true;
+        for (int k = 0; k < 3; ++k)
+            for (int j = 0; j < 3; ++j) {
+                finite = finite && std::isfinite(v[j][k]);
+                b.lo[k] = std::min(b.lo[k], v[j][k]);
+                b.hi[k] = std::max(b.hi[k], v[j][k]);
+            }
+        if (!finite) b = Aabb{{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};   /* shape only; its hull is unbounded */
+        box[t] = b;
+        for (int k = 0; k < 3; ++k) cen[3 * (size_t)t + k] = 0.5f * (b.lo[k] + b.hi[k]);
+        hull[t] = triangle_hull(v[0], v[1], v[2], &hs.face_normal[3 * (size_t)t], G);
+    }
+
+    std::vector<int32_t> order((size_t)nt);
+    for (int32_t t = 0; t < nt; ++t) order[t] = t;
+    std::vector<Build> nodes;
+    nodes.reserve((size_t)nt * 2 / kLeafMax + 2);
+    struct Work { int32_t node, lo, hi, depth; };
+    std::vector<Work> st;
+    nodes.push_back(Build{});
+    st.push_back(Work{0, 0, nt, 0});
+    while (!st.empty()) {
+        const Work w = st.back();
+        st.pop_back();
+        const int32_t cnt = w.hi - w.lo;
+        Aabb cb = aabb_empty();
+        for (int32_t i = w.lo; i < w.hi; ++i) {
+            const int32_t t = order[i];
+            Aabb c{{cen[3 * t], cen[3 * t + 1], cen[3 * t + 2]}, {cen[3 * t], cen[3 * t + 1], cen[3 * t + 2]}};
+            grow(cb, c);
+        }
+        if (cnt <= kLeafMax) {
+            nodes[w.node].first = w.lo;
+            nodes[w.node].count = cnt;
+            continue;
+        }
+        int best_axis = -1, best_split = -1;
+        double best_cost = std::numeric_limits<double>::infinity();
+        if (w.depth < kMaxDepth) {
+            for (int ax = 0; ax < 3; ++ax) {
+                const float ext = cb.hi[ax] - cb.lo[ax];
+                if (!(ext > 0.f)) continue;
+                Aabb bins[kBins];
+                int32_t bc[kBins] = {0};
+                for (auto &b : bins) b = aabb_empty();
+                for (int32_t i = w.lo; i < w.hi; ++i) {
+                    const int32_t t = order[i];
+                    const int k = std::min(kBins - 1, (int)((cen[3 * t + ax] - cb.lo[ax]) / ext * kBins));
+                    ++bc[k];
+                    grow(bins[k], box[t]);
+                }
+                for (int s = 1; s < kBins; ++s) {
+                    Aabb l = aabb_empty(), r = aabb_empty();
+                    int32_t nl = 0, nr = 0;
+                    for (int k = 0; k < s; ++k) { grow(l, bins[k]); nl += bc[k]; }
+                    for (int k = s; k < kBins; ++k) { grow(r, bins[k]); nr += bc[k]; }
+                    if (nl == 0 || nr == 0) continue;
+                    const double c = area(l) * nl + area(r) * nr;
+                    if (c < best_cost) {
+                        best_cost = c;
+                        best_axis = ax;
+                        best_split = s;
+                    }
+                }
+            }
+        }
+        int32_t mid;
+        int axis = 0;
+        if (best_axis >= 0) {
+            axis = best_axis;
+            const float ext = cb.hi[axis] - cb.lo[axis];
+            const auto it = std::stable_partition(order.begin() + w.lo, order.begin() + w.hi, [&](int32_t t) {
+                return std::min(kBins - 1, (int)((cen[3 * t + axis] - cb.lo[axis]) / ext * kBins)) < best_split;
+            });
+            mid = (int32_t)(it - order.begin());
+        } else {
+            /* coincident centroids (or too deep): halves by index along the widest axis */
+            for (int k = 1; k < 3; ++k)
+                if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
+            mid = w.lo + cnt / 2;
+            std::stable_sort(order.begin() + w.lo, order.begin() + w.hi,
+                             [&](int32_t a, int32_t b) { return cen[3 * a + axis] < cen[3 * b + axis]; });
+        }
+        if (mid <= w.lo || mid >= w.hi) mid = w.lo + cnt / 2;
+        const int32_t l = (int32_t)nodes.size(), r = l + 1;
+        nodes.push_back(Build{});
+        nodes.push_back(Build{});
+        nodes[w.node].left = l;
+        nodes[w.node].right = r;
+        nodes[w.node].axis = axis;
+        st.push_back(Work{r, mid, w.hi, w.depth + 1});
+        st.push_back(Work{l, w.lo, mid, w.depth + 1});
+    }
+    const int32_t n = (int32_t)nodes.size();
+    if ((int64_t)nt * 16 >= (int64_t)std::numeric_limits<int32_t>::max())
+        return set_error(CRT_E_UNSUPPORTED, "too many triangles for the BVH leaf record");
+
+    /* hulls bottom up: children are numbered after their parent */
+    const double inf = std::numeric_limits<double>::infinity();
+    for (int32_t x = n - 1; x >= 0; --x) {
+        HullD h{{inf, inf, inf}, {-inf, -inf, -inf}};
+        auto merge = [&](const HullD &o) {
+            for (int k = 0; k < 3; ++k) {
+                h.lo[k] = std::min(h.lo[k], o.lo[k]);
+                h.hi[k] = std::max(h.hi[k], o.hi[k]);
+            }
+        };
+        if (nodes[x].left < 0) {
+            for (int32_t i = 0; i < nodes[x].count; ++i) merge(hull[order[nodes[x].first + i]]);
+        } else {
+            merge(nodes[nodes[x].left].hull);
+            merge(nodes[nodes[x].right].hull);
+        }
+        nodes[x].hull = h;
+    }
+    std::vector<int32_t> subtree((size_t)n, 1);
+    for (int32_t x = n - 1; x >= 0; --x)
+        if (nodes[x].left >= 0) subtree[x] += subtree[nodes[x].left] + subtree[nodes[x].right];
+
+    /* triangles in leaf order, geometry exactly as the leaf slots hold it */
+    hs.btri.resize((size_t)nt);
+    hs.btri_id.resize((size_t)nt);
+    for (int32_t i = 0; i < nt; ++i) {
+        const int32_t t = order[i];
+        const DTriAttr &at = hs.tri_attr[t];
+        DTriGeo g;
+        g.v0x = hs.vpos[3 * (size_t)at.i0]; g.v0y = hs.vpos[3 * (size_t)at.i0 + 1]; g.v0z = hs.vpos[3 * (size_t)at.i0 + 2];
+        g.v1x = hs.vpos[3 * (size_t)at.i1]; g.v1y = hs.vpos[3 * (size_t)at.i1 + 1]; g.v1z = hs.vpos[3 * (size_t)at.i1 + 2];
+        g.v2x = hs.vpos[3 * (size_t)at.i2]; g.v2y = hs.vpos[3 * (size_t)at.i2 + 1]; g.v2z = hs.vpos[3 * (size_t)at.i2 + 2];
+        g.nx = hs.face_normal[3 * (size_t)t]; g.ny = hs.face_normal[3 * (size_t)t + 1]; g.nz = hs.face_normal[3 * (size_t)t + 2];
+        hs.btri[i] = g;
+        hs.btri_id[i] = t | (hs.tri_cull[t] ? (int32_t)0x80000000 : 0);
+    }
+
+    hs.bnodes.assign((size_t)8 * (n + 1), BNode{});   /* + one zero record per order */
+    std::vector<int32_t> st2;
+    for (int oct = 0; oct < 8; ++oct) {
+        BNode *out = hs.bnodes.data() + (size_t)oct * (n + 1);
+        int32_t k = 0;
+        st2.assign(1, 0);
+        while (!st2.empty()) {
+            const int32_t x = st2.back();
+            st2.pop_back();
+            const Build &b = nodes[x];
+            BNode &o = out[k];
+            o.lo_x = round_down(b.hull.lo[0]); o.lo_y = round_down(b.hull.lo[1]); o.lo_z = round_down(b.hull.lo[2]);
+            o.hi_x = round_up(b.hull.hi[0]); o.hi_y = round_up(b.hull.hi[1]); o.hi_z = round_up(b.hull.hi[2]);
+            o.skip = k + subtree[x];
+            if (b.left < 0) {
+                o.leaf = b.first * 16 + b.count;
+            } else {
+                o.leaf = 0;
+                /* near child first: the right child holds the larger centroids
+                 * along the split axis, entered first by a ray going down it */
+                const bool neg = ((oct >> b.axis) & 1) != 0;
+                st2.push_back(neg ? b.left : b.right);
+                st2.push_back(neg ? b.right : b.left);
+            }
+            ++k;
+        }
+    }
+    hs.bnode_count = n;
+    return CRT_OK;
+}
+
+}  // namespace crt_amd

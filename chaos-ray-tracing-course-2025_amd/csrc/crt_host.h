@@ -79,6 +79,13 @@ struct HostScene {
     float prune_origin_max = 0.f;
     double prune_G = 0.0;           /* the G of the hull margins (crt_scene_build.cpp) */
 
+    /* secondary-ray BVH (crt_bvh_build.cpp, crt_layout.h BNode): 8 octant
+     * orders x (bnode_count + 1) nodes, triangles in leaf order */
+    std::vector<BNode> bnodes;
+    int32_t bnode_count = 0;
+    std::vector<DTriGeo> btri;
+    std::vector<int32_t> btri_id;   /* triangle id | back_face_culling << 31 */
+
     /* root cell (crt_acceleration_tree.cpp:89-94); tree_on_host = false when
      * prepare_scene skipped the tree (built on the device, crt_tree_build.h) */
     float root_box[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -95,6 +102,10 @@ struct HostScene {
     int32_t max_depth = 0;
     int32_t max_leaf_size = 0;
 };
+
+/* The secondary-ray BVH over hs's triangles (crt_bvh_build.cpp); needs the
+ * mesh prep and prune_G. */
+int build_bvh(HostScene &hs);
 
 /* Mesh prep + (build_tree) the exact tree build and its flattening. */
 int prepare_scene(const crt_scene_desc *desc, HostScene &out, bool build_tree = true);

@@ -61,6 +61,22 @@ struct alignas(16) PNode {
 };
 static_assert(sizeof(PNode) == 64, "PNode must be 64 B");
 
+/* Node of the secondary-ray BVH (crt_bvh.h): a bounding volume hierarchy
+ * over the scene's triangles (each triangle once, not the tree's duplicated
+ * leaf copies), whose boxes are unions of the triangles' hulls (the same
+ * conservative hulls as PNode's), stored like PNode once per direction octant
+ * in preorder with the near child first.  `skip` is the first node after the
+ * subtree in that order; `leaf` = first * 16 + count for a leaf (count 1..15,
+ * triangles first .. first + count - 1 of the BVH triangle array), 0 for an
+ * interior node. */
+struct alignas(16) BNode {
+    float lo_x, hi_x, lo_y, hi_y;
+    float lo_z, hi_z;
+    int32_t skip;
+    int32_t leaf;
+};
+static_assert(sizeof(BNode) == 32, "BNode must be 32 B");
+
 struct alignas(16) DTriGeo {
     float v0x, v0y, v0z, v1x;
     float v1y, v1z, v2x, v2y;
@@ -106,6 +122,13 @@ struct DeviceScene {
     const int32_t *slot_tri;
     const uint8_t *slot_cull;
     const uint32_t *slot_cull_bits;   /* same flags, 1 bit per slot (scalar-path reads) */
+    /* secondary-ray BVH (crt_bvh.h): 8 octant orders x (bnode_count + 1) nodes,
+     * its triangles in leaf order (geometry as the slots hold it, and the
+     * global triangle id | back_face_culling << 31); null when not built */
+    const BNode *bnodes;
+    int32_t bnode_count;
+    const DTriGeo *btri;
+    const int32_t *btri_id;
     const DTriAttr *tri_attr;
     const DVec4 *vnormal;
     const DVec4 *vuv;

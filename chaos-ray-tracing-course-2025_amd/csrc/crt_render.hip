@@ -33,6 +33,7 @@
 #include <thread>
 #include <vector>
 
+#include "crt_bvh.h"
 #include "crt_device.h"
 #include "crt_host.h"
 #include "crt_tree_build.h"
@@ -903,24 +904,48 @@ __device__ __forceinline__ int trace_lane_pruned(const DeviceScene &s, bool acti
     return best;
 }
 
+/* Per-lane BVH walk with its proof on the reference's tree (crt_bvh.h):
+ * scattered rays (GI bounces, reflections, refractions) of the frame-stack,
+ * refill and wavefront kernels when the scene has its BVH. */
+template <bool COUNT>
+__device__ __forceinline__ int trace_lane_bvh(const DeviceScene &s, bool active, Vec o, Vec d, float &best_t,
+                                              LaneCounts &c) {
+    best_t = 0.0f;
+    if (!active) return -1;
+    if (COUNT) ++c.traversals;
+    WalkCounts wc = {0u, 0u};
+    const int best = trace_bvh_exact<COUNT>(s.bnodes, s.bnode_count, s.btri, s.btri_id, s.nodes, s.pnodes,
+                                            s.node_count, s.slots, s.slot_cull, s.slot_tri, s.prune_origin_max,
+                                            s.planes_ok != 0, o, d, best_t, wc);
+    if (COUNT) {
+        c.nodes += wc.nodes;
+        c.tris += wc.tris;
+        if (best >= 0) ++c.hits;
+    }
+    return best;
+}
+
 /* Walks (TRAV), all bit-identical in result:
  *   7  packet walk in the reference's node order (work counters = the reference's)
  *   8  pruned packet walk (exact t-pruning), any camera ray
  *   12 8 for frames whose camera rays are all in the hoisted-division window
  *   13 12 + window walk for the plan's split tiles (k_render_tiles)
  *   4  cooperative walk in the reference's node order (scattered rays)
- *   10 pruned cooperative walk */
+ *   10 pruned cooperative walk
+ *   14 per-lane BVH walk + proof on the reference's tree (scattered rays, crt_bvh.h) */
 template <int TRAV>
 constexpr bool kIsCoop = TRAV == 4 || TRAV == 10;
 
 template <int TRAV, bool COUNT>
 __device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, bool active, Vec o, Vec d, float &best_t,
                                      LaneCounts &c) {
-    static_assert(TRAV == 4 || TRAV == 7 || TRAV == 8 || TRAV == 10 || TRAV == 12 || TRAV == 13, "no such walk");
+    static_assert(TRAV == 4 || TRAV == 7 || TRAV == 8 || TRAV == 10 || TRAV == 12 || TRAV == 13 || TRAV == 14,
+                  "no such walk");
     if constexpr (TRAV == 8) return trace_packet_pruned<COUNT, false>(s, active, o, d, best_t, c);
     else if constexpr (TRAV == 12 || TRAV == 13) return trace_packet_pruned<COUNT, true>(s, active, o, d, best_t, c);
     else if constexpr (TRAV == 4) return trace_coop<COUNT, false>(s, *L, active, o, d, best_t, c);
     else if constexpr (TRAV == 10) return trace_coop<COUNT, true>(s, *L, active, o, d, best_t, c);
+    else if constexpr (TRAV == 14) return trace_lane_bvh<COUNT>(s, active, o, d, best_t, c);
     else return trace_packet<COUNT>(s, active, o, d, best_t, c);
 }
 
@@ -1409,15 +1434,18 @@ template <int MAXF, int TRAV, bool COUNT>
 #ifndef CRT_GI10_WAVES
 #define CRT_GI10_WAVES 4     /* min waves/SIMD of the refill kernel with the pruned walk (TRAV 10) */
 #endif
-__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(MAXF == 4 ? (TRAV == 10 ? CRT_GI10_WAVES : CRT_GI_WAVES) : 1))) void k_render_refill(
+#ifndef CRT_GI14_WAVES
+#define CRT_GI14_WAVES 1     /* ... with the per-lane BVH walk (TRAV 14): no minimum */
+#endif
+__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(MAXF == 4 ? (TRAV == 10 ? CRT_GI10_WAVES : TRAV == 14 ? CRT_GI14_WAVES : CRT_GI_WAVES) : 1))) void k_render_refill(
     const DeviceScene *__restrict__ scene, DSettings st, const Tile *__restrict__ tiles, int ntiles,
     float *__restrict__ out, int32_t *__restrict__ next_px, unsigned long long *__restrict__ counters) {
     const int lane = (int)(threadIdx.x & 63);
     const DeviceScene &s = *scene;
     const int total = ntiles * 64;   /* pixel slots: tile k, lane j -> (j & 7, j >> 3) inside tile k */
     const unsigned long long lt = (1ull << lane) - 1ull;
-    __shared__ CoopLds coop[4];
-    CoopLds *L = &coop[threadIdx.x >> 6];
+    __shared__ CoopLds coop[kIsCoop<TRAV> ? 4 : 1];
+    CoopLds *L = &coop[kIsCoop<TRAV> ? (threadIdx.x >> 6) : 0];
     LaneCounts cnt = {};
     bool has = false, dry = false;
     int64_t opx = 0;
@@ -1480,7 +1508,8 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(MAXF == 4 ? (TRA
  * 1080^2 77.3 -> 75.3 ms, profiles/r01/ab_wf_waves_sched_strategy.log) while
  * the C2 camera kernel keeps the default one. */
 #define CRT_REFILL_INSTANCES(X) X(4, 4, false) X(4, 4, true) X(4, 10, false) X(4, 10, true) \
-    X(16, 4, false) X(16, 4, true) X(64, 4, false) X(64, 4, true)
+    X(16, 4, false) X(16, 4, true) X(64, 4, false) X(64, 4, true) X(4, 14, false) X(4, 14, true) \
+    X(16, 14, false) X(16, 14, true) X(64, 14, false) X(64, 14, true)
 #define CRT_REFILL_SIG(MAXF, T, C) void k_render_refill<MAXF, T, C>(const DeviceScene *__restrict__, DSettings, \
     const Tile *__restrict__, int, float *__restrict__, int32_t *__restrict__, unsigned long long *__restrict__);
 #ifdef CRT_GI_TU
@@ -1728,7 +1757,7 @@ __device__ __forceinline__ Vec wf_compose(const WNode &nd, const DVec4 *__restri
 
 /* Wavefront levels >= 1 (C3): own translation unit (crt_render_wf.hip) and
  * LLVM scheduling strategy, as for the GI refill kernels above. */
-#define CRT_WF_INSTANCES(X) X(4, false) X(4, true) X(10, false) X(10, true)
+#define CRT_WF_INSTANCES(X) X(4, false) X(4, true) X(10, false) X(10, true) X(14, false) X(14, true)
 #define CRT_WF_SIG(SEC, C) void k_wf_level<SEC, false, C>(const DeviceScene *__restrict__, DSettings, \
     const Tile *__restrict__, int, WLevel, unsigned long long *__restrict__);
 #ifdef CRT_WF_TU
@@ -1780,7 +1809,8 @@ __global__ __launch_bounds__(256) void k_trace_rays(DeviceScene s, const float *
     const Vec d = vec(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
     LaneCounts cnt;
     float t;
-    const int slot = walk == 1 ? trace_lane_pruned<false>(s, true, o, d, t, cnt) : trace_closest<false>(s, o, d, t, cnt);
+    const int slot = walk == 2 && s.bnodes ? trace_lane_bvh<false>(s, true, o, d, t, cnt)
+                     : walk >= 1 ? trace_lane_pruned<false>(s, true, o, d, t, cnt) : trace_closest<false>(s, o, d, t, cnt);
     crt_hit r;
     r.distance = 0.f;
     r.point[0] = r.point[1] = r.point[2] = 0.f;
@@ -2659,7 +2689,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
          * the level has fewer rays than ~4096 waves' worth, at least 8, at most
          * the wf_rpw cap — a level's time is its slowest waves'
          * (C3 3.60 -> 3.33 ms, profiles/r02/ab_c3_rpw) */
-        const int rpw_l = std::min(rpw, std::max(8, (int)((n + 4095) / 4096)));
+        const int rpw_l = sec == 14 ? 64 : std::min(rpw, std::max(8, (int)((n + 4095) / 4096)));
         WLevel l{w.q[cur], n, L, w.q[cur ^ 1], w.counts + L, (int32_t)(base + n), w.nodes, w.cols, rpw_l, out_cap,
                  w.d_flag};
         const int64_t waves = ((int64_t)n + rpw_l - 1) / rpw_l;
@@ -2667,7 +2697,9 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
 #define CRT_WF(SEC, COUNT)                                                                                  \
     hipLaunchKernelGGL((k_wf_level<SEC, false, COUNT>), dim3(blocks), dim3(256), 0, stream, d_scene, ds,     \
                        plan.d_tiles, plan.ntiles, l, cnt)
-        if (sec == 10) {
+        if (sec == 14) {
+            if (count) CRT_WF(14, true); else CRT_WF(14, false);
+        } else if (sec == 10) {
             if (count) CRT_WF(10, true); else CRT_WF(10, false);
         } else {
             if (count) CRT_WF(4, true); else CRT_WF(4, false);
@@ -2751,7 +2783,8 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
      * CRT_SECONDARY / "secondary" overrides the secondary walk. */
     const bool pruned = sc->traversal == 8;
     int sec = sc->secondary;
-    if (sec == 0) sec = (gi || !pruned) ? 4 : 10;
+    if (sec == 14 && !sc->ds.bnodes) sec = 10;   /* no BVH (device-built tree) */
+    if (sec == 0) sec = !pruned ? 4 : sc->ds.bnodes ? 14 : gi ? 4 : 10;
     if (sc->shadows) {
         /* shadow-ray frames (option "shadows"): frame-stack kernel, pruned
          * cooperative walk for every traced ray, per-lane shadow walks */
@@ -2805,7 +2838,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
                        d_scene, ds, plan.d_tiles, plan.ntiles, d_out, cnt, stamps)
 #define CRT_LAUNCH(MAXF, COUNT)                                                                             \
     do {                                                                                                   \
-        if (trav == 10) CRT_LAUNCH_T(true, MAXF, 10, COUNT);                                               \
+        if (trav == 10 || trav == 14) CRT_LAUNCH_T(true, MAXF, 10, COUNT);                                  \
         else CRT_LAUNCH_T(true, MAXF, 4, COUNT);                                                           \
     } while (0)
     if (!full) {
@@ -2816,7 +2849,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         case 13: if (count) CRT_LAUNCH_T(false, 0, 13, true); else CRT_LAUNCH_T(false, 0, 13, false); break;
         default: return set_error(CRT_E_INVALID, "no such camera walk");
         }
-    } else if (gi && (trav == 4 || trav == 10) && sc->gi_refill && sc->d_next_px && !stamps && frames <= 64) {
+    } else if (gi && (trav == 4 || trav == 10 || trav == 14) && sc->gi_refill && sc->d_next_px && !stamps && frames <= 64) {
         /* GI: persistent waves with pixel refill (k_render_refill) */
         HIP_TRY(hipMemsetAsync(sc->d_next_px, 0, sizeof(int32_t), stream));
         const int nw = std::max(1, std::min(plan.ntiles, sc->refill_waves));
@@ -2825,7 +2858,15 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     hipLaunchKernelGGL((k_render_refill<MAXF, T, COUNT>), dim3(rb), dim3(256), 0, stream, d_scene, ds,       \
                        plan.d_tiles, plan.ntiles, d_out, sc->d_next_px, cnt)
 #define CRT_REFILL(MAXF, COUNT) CRT_REFILL_T(MAXF, 4, COUNT)
-        if (frames <= 4 && trav == 10) {   /* pruned cooperative walk for GI (secondary = 10) */
+        if (trav == 14) {                   /* per-lane BVH walk (crt_bvh.h) */
+            if (frames <= 4) {
+                if (count) CRT_REFILL_T(4, 14, true); else CRT_REFILL_T(4, 14, false);
+            } else if (frames <= 16) {
+                if (count) CRT_REFILL_T(16, 14, true); else CRT_REFILL_T(16, 14, false);
+            } else {
+                if (count) CRT_REFILL_T(64, 14, true); else CRT_REFILL_T(64, 14, false);
+            }
+        } else if (frames <= 4 && trav == 10) {   /* pruned cooperative walk for GI (secondary = 10) */
             if (count) CRT_REFILL_T(4, 10, true); else CRT_REFILL_T(4, 10, false);
         } else if (frames <= 4) {
             if (count) CRT_REFILL(4, true); else CRT_REFILL(4, false);
@@ -2965,6 +3006,12 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
         const int64_t n = dt.node_count, m = dt.slot_count;
         sc->info.device_bytes += n * (int64_t)sizeof(DNode) + 8 * (n + 1) * (int64_t)sizeof(PNode) +
                                  m * (int64_t)(sizeof(DTriGeo) + 4 + 1) + (m / 32 + 1) * 4;
+    }
+    if (hs.bnode_count > 0) {   /* secondary-ray BVH (crt_bvh.h) */
+        if ((rc = upload(sc.get(), hs.bnodes, &ds.bnodes)) != CRT_OK) return rc;
+        if ((rc = upload(sc.get(), hs.btri, &ds.btri)) != CRT_OK) return rc;
+        if ((rc = upload(sc.get(), hs.btri_id, &ds.btri_id)) != CRT_OK) return rc;
+        ds.bnode_count = hs.bnode_count;
     }
     sc->camera_fast = camera_rays_fast(hs, ds.planes_ok != 0);
     if ((rc = upload(sc.get(), hs.tri_attr, &ds.tri_attr)) != CRT_OK) return rc;
@@ -3454,7 +3501,8 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         if (value != 7 && value != 8) return set_error(CRT_E_INVALID, "traversal must be 7 (reference order) or 8 (pruned)");
         sc->traversal = value;
     } else if (k == "secondary") {
-        if (value != 0 && value != 4 && value != 10) return set_error(CRT_E_INVALID, "secondary must be 0, 4 or 10");
+        if (value != 0 && value != 4 && value != 10 && value != 14)
+            return set_error(CRT_E_INVALID, "secondary must be 0, 4, 10 or 14");
         sc->secondary = value;
     } else if (k == "wavefront") {
         sc->wavefront = value != 0;
@@ -3501,7 +3549,7 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
     } else if (k == "shadows") {
         sc->shadows = value != 0;
     } else if (k == "trace_walk") {
-        if (value != 0 && value != 1) return set_error(CRT_E_INVALID, "trace_walk must be 0 or 1");
+        if (value < 0 || value > 2) return set_error(CRT_E_INVALID, "trace_walk must be 0, 1 or 2 (BVH)");
         sc->trace_walk = value;
     } else {
         return set_error(CRT_E_INVALID, "unknown option: " + k);

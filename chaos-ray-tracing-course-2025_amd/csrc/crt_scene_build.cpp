@@ -396,6 +396,17 @@ int flatten_tree(const std::vector<BuildNode> &bn, HostScene &hs) {
     return CRT_OK;
 }
 
+/* The secondary-ray BVH (crt_bvh.h) serves scattered rays only: built when
+ * the scene makes any (GI with a diffuse material, reflective or refractive
+ * materials). */
+int maybe_build_bvh(HostScene &hs) {
+    bool need = false;
+    for (const DMaterial &m : hs.materials)
+        need = need || m.type == CRT_MATERIAL_REFLECTIVE || m.type == CRT_MATERIAL_REFRACTIVE ||
+               (hs.gi_on && m.type == CRT_MATERIAL_DIFFUSE);
+    return need ? build_bvh(hs) : CRT_OK;
+}
+
 }  // namespace
 
 int prepare_scene(const crt_scene_desc *d, HostScene &hs, bool build_tree_on_host) {
@@ -507,7 +518,7 @@ int prepare_scene(const crt_scene_desc *d, HostScene &hs, bool build_tree_on_hos
             hs.root_box[3 + k] = root.hi[k];
         }
         hs.tree_on_host = false;
-        return CRT_OK;
+        return maybe_build_bvh(hs);
     }
     std::vector<Box6> tri_boxes((size_t)nt);
     for (int64_t t = 0; t < nt; ++t) {
@@ -530,7 +541,8 @@ int prepare_scene(const crt_scene_desc *d, HostScene &hs, bool build_tree_on_hos
     }
     std::vector<BuildNode> bn;
     build_tree(tri_boxes, root, bn);
-    return flatten_tree(bn, hs);
+    if ((rc = flatten_tree(bn, hs)) != CRT_OK) return rc;
+    return maybe_build_bvh(hs);
 }
 
 /* The reference's built scene (crt_hip_scene_from_tree): vertices after
@@ -645,7 +657,8 @@ int prepare_scene_from_tree(const crt_tree_scene_desc *d, HostScene &hs) {
         hs.root_box[k] = bn[0].bounds.lo[k];
         hs.root_box[3 + k] = bn[0].bounds.hi[k];
     }
-    return flatten_tree(bn, hs);
+    if ((rc = flatten_tree(bn, hs)) != CRT_OK) return rc;
+    return maybe_build_bvh(hs);
 }
 
 std::vector<float> tile_work_estimate(const HostScene &hs, int tiles_x, int tiles_y) {

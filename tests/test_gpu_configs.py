@@ -115,7 +115,7 @@ def test_c5_1m_triangles(N, oracle, c5_1m, w, h):
     assert c["traversals"] == w * h
 
 
-@pytest.mark.parametrize("walk", [0, 1], ids=["reference-order", "pruned"])
+@pytest.mark.parametrize("walk", [0, 1, 2], ids=["reference-order", "pruned", "bvh"])
 @pytest.mark.parametrize("name", sorted(p.stem[4:] for p in GOLDEN.glob("kat_*.npz")))
 def test_trace_matches_reference_records(N, name, walk):
     """The HIP trace hook returns, for every ray, the Intersection the

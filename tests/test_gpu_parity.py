@@ -218,7 +218,7 @@ def test_window_walk_equals_packet_walk(N, oracle, monkeypatch, calib_k):
     assert ca["traversals"] == cb["traversals"] == 1920 * 1080 and ca["hits"] == cb["hits"]
 
 
-@pytest.mark.parametrize("opt,values", [("wf_rpw", [64, 32, 5, 1]), ("secondary", [4, 10])])
+@pytest.mark.parametrize("opt,values", [("wf_rpw", [64, 32, 5, 1]), ("secondary", [4, 10, 14])])
 def test_wavefront_level_layouts_bit_identical(N, oracle, opt, values):
     """Wavefront levels >= 1 (reflect/refract recursion, C3 scene at depth 8):
     rays per wave (idle lanes take donated pieces) and the secondary walk
@@ -241,6 +241,33 @@ def test_wavefront_level_layouts_bit_identical(N, oracle, opt, values):
         N.HipScene(sc).set_option(opt, 99)
 
 
+@pytest.mark.parametrize("name,w,h,over", [
+    ("11-01-refractive__scene8", 240, 135, {"max_ray_depth": 8}),
+    ("15-01-conclusion__scene2", 64, 64, {}),
+    ("15-01-conclusion__scene1", 64, 64, {}),
+    ("09-03-reflective__scene5", 96, 54, {"max_ray_depth": 5}),
+])
+def test_bvh_walk_equals_reference_walks(N, oracle, name, w, h, over):
+    """Scattered rays through the BVH with its proof on the reference's tree
+    (secondary walk 14, crt_bvh.h, the default) vs the reference-order walks:
+    same image bits and the same traversal and hit counts as the oracle's,
+    far fewer triangle tests."""
+    from crt_amd.native import WorkCounts
+    sc = scene_npz(name).set_resolution(w, h)
+    st = N.RendererSettings.default(**over)
+    fast = N.HipScene(sc, secondary=14)
+    ref = N.HipScene(sc, traversal=7)
+    a, b = fast.render(st), ref.render(st)
+    assert np.array_equal(bits(a), bits(b))
+    assert np.array_equal(bits(a), bits(oracle.OracleScene(sc).render(st)))
+    ca, cb = fast.count_work(st), ref.count_work(st)
+    wc = WorkCounts()
+    oracle.OracleScene(sc).render(st, counts=wc)
+    assert cb == wc.as_dict()
+    assert ca["traversals"] == cb["traversals"] and ca["hits"] == cb["hits"]
+    assert ca["triangle_tests"] < cb["triangle_tests"]
+
+
 @pytest.mark.parametrize("w,h", [(70, 45), (96, 96)])
 def test_gi_pixel_refill_bit_identical(N, oracle, w, h):
     """GI frames (15-01/scene2): persistent waves refilling finished lanes with
@@ -257,4 +284,9 @@ def test_gi_pixel_refill_bit_identical(N, oracle, w, h):
     assert np.array_equal(bits(got), bits(want))
     ca = N.HipScene(sc).set_option("gi_refill", 1).count_work(st)
     cb = N.HipScene(sc).set_option("gi_refill", 0).count_work(st)
-    assert ca == cb
+    # the tile kernel takes the cooperative walk, refill the BVH walk: same rays
+    assert ca["traversals"] == cb["traversals"] and ca["hits"] == cb["hits"]
+    for walk in (4, 10, 14):
+        g = N.HipScene(sc, secondary=walk)
+        assert g.count_work(st) == g.count_work(st)
+        assert np.array_equal(bits(g.render(st)), bits(want)), walk

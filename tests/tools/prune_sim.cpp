@@ -11,9 +11,11 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <vector>
 
 #include "../../chaos-ray-tracing-course-2025_amd/csrc/crt_host.h"
 #include "../../chaos-ray-tracing-course-2025_amd/csrc/crt_device.h"
+#include "../../chaos-ray-tracing-course-2025_amd/csrc/crt_bvh.h"
 
 using namespace crt_amd;
 
@@ -82,6 +84,91 @@ int prune_sim_trace(const crt_scene_desc *desc, const float *rays, int64_t n, in
     counts[2] = pn;
     counts[3] = pt;
     return CRT_OK;
+}
+
+/* The BVH walk with its kd verification (crt_bvh.h trace_bvh_exact), from
+ * the product's sources, next to the reference-order walk.  A BVH answer is
+ * equal to the reference's when its t bits match and its slot holds the same
+ * triangle (copies of a triangle give the same record; the slot numbers may
+ * differ).  counts[0..4] = reference nodes, reference triangles, BVH walk +
+ * verification node tests, BVH triangle tests, rays that took the fallback. */
+int bvh_sim_trace(const crt_scene_desc *desc, const float *rays, int64_t n, int32_t *ref_tri, float *ref_t,
+                  int32_t *bvh_tri, float *bvh_t, uint64_t *counts) {
+    HostScene hs;
+    int rc = prepare_scene(desc, hs);
+    if (rc != CRT_OK) return rc;
+    if (hs.bnode_count == 0 && (rc = build_bvh(hs)) != CRT_OK) return rc;   /* scenes without scattered rays */
+    const int nn = (int)hs.nodes.size();
+    uint64_t rn = 0, rt = 0, fbn = 0;
+    WalkCounts c = {0u, 0u};
+    for (int64_t i = 0; i < n; ++i) {
+        const Vec o = vec(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+        const Vec d = vec(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+        float t = 0.f;
+        const int rs = walk_reference(hs, o, d, t, rn, rt);
+        ref_tri[i] = rs >= 0 ? hs.slot_tri[rs] : -1;
+        ref_t[i] = t;
+        bool fb = false;
+        const int bs = trace_bvh_exact<true>(hs.bnodes.data(), hs.bnode_count, hs.btri.data(), hs.btri_id.data(),
+                                             hs.nodes.data(), hs.pnodes.data(), nn, hs.slots.data(),
+                                             hs.slot_cull.data(), hs.slot_tri.data(), hs.prune_origin_max, false, o,
+                                             d, t, c, &fb);
+        bvh_tri[i] = bs >= 0 ? hs.slot_tri[bs] : -1;
+        bvh_t[i] = t;
+        fbn += fb ? 1 : 0;
+    }
+    counts[0] = rn;
+    counts[1] = rt;
+    counts[2] = c.nodes;
+    counts[3] = c.tris;
+    counts[4] = fbn;
+    return CRT_OK;
+}
+
+/* BVH box containment: every triangle's vertices lie inside the box of every
+ * BVH node above its leaf, in all 8 orders, and every order lists each
+ * triangle exactly once.  Returns the number of violations (0 expected). */
+int64_t bvh_sim_check(const crt_scene_desc *desc) {
+    HostScene hs;
+    if (prepare_scene(desc, hs) != CRT_OK) return -1;
+    if (hs.bnode_count == 0 && build_bvh(hs) != CRT_OK) return -1;
+    const int n = hs.bnode_count;
+    const int nt = (int)hs.btri.size();
+    int64_t bad = 0;
+    for (int oct = 0; oct < 8; ++oct) {
+        const BNode *p = bnode_order(hs.bnodes.data(), n, oct);
+        std::vector<int> seen(nt, 0);
+        int path[128];
+        int top = 0;
+        for (int i = 0; i < n; ++i) {
+            while (top > 0 && p[path[top - 1]].skip <= i) --top;
+            const int cnt = p[i].leaf & 15;
+            if (cnt == 0) {
+                if (top >= 128) return -2;
+                path[top++] = i;
+                continue;
+            }
+            if (p[i].skip != i + 1) ++bad;
+            for (int k = 0; k < cnt; ++k) {
+                const int j = (p[i].leaf >> 4) + k;
+                if (j < 0 || j >= nt) { ++bad; continue; }
+                ++seen[j];
+                const DTriGeo &g = hs.btri[j];
+                const float xs[3] = {g.v0x, g.v1x, g.v2x}, ys[3] = {g.v0y, g.v1y, g.v2y}, zs[3] = {g.v0z, g.v1z, g.v2z};
+                for (int v = 0; v < 3; ++v) {
+                    auto inside = [&](const BNode &q) {
+                        return xs[v] >= q.lo_x && xs[v] <= q.hi_x && ys[v] >= q.lo_y && ys[v] <= q.hi_y &&
+                               zs[v] >= q.lo_z && zs[v] <= q.hi_z;
+                    };
+                    bool ok = inside(p[i]);
+                    for (int u = 0; u < top; ++u) ok = ok && inside(p[path[u]]);
+                    if (!ok) ++bad;
+                }
+            }
+        }
+        for (int j = 0; j < nt; ++j) bad += seen[j] != 1;
+    }
+    return bad;
 }
 
 /* Hull containment check: every slot's triangle box lies inside the hull of
