@@ -1519,6 +1519,11 @@ CRT_REFILL_INSTANCES(CRT_REFILL_INST)
 #define CRT_REFILL_EXTERN(MAXF, T, C) extern template __global__ CRT_REFILL_SIG(MAXF, T, C)
 CRT_REFILL_INSTANCES(CRT_REFILL_EXTERN)
 #endif
+}  // namespace crt_amd
+
+#include "crt_gi_machine.h"   /* GI frames as a per-lane state machine (k_render_gi) */
+
+namespace crt_amd {
 
 
 
@@ -2038,6 +2043,8 @@ struct crt_hip_scene {
     unsigned long long *d_counters = nullptr;
     int32_t *d_next_px = nullptr;      /* pixel-refill list head (k_render_refill) */
     int gi_refill = 1;                 /* GI frames: persistent waves with pixel refill (env CRT_GI_REFILL, option "gi_refill") */
+    int gi_machine = 1;                /* ... as per-lane state machines (k_render_gi; option "gi_machine") */
+    int gi_blocks = 1024;              /* blocks of the k_render_gi grid (resident blocks per CU x CUs) */
     int refill_waves = 5120;           /* waves of the refill grid: CUs x 4 SIMDs x CRT_GI_WAVES */
     bool grid_empty = false;
     int traversal = 8;             /* 7 reference order | 8 pruned (default), see trace<> (env CRT_TRAVERSAL) */
@@ -2858,7 +2865,22 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     hipLaunchKernelGGL((k_render_refill<MAXF, T, COUNT>), dim3(rb), dim3(256), 0, stream, d_scene, ds,       \
                        plan.d_tiles, plan.ntiles, d_out, sc->d_next_px, cnt)
 #define CRT_REFILL(MAXF, COUNT) CRT_REFILL_T(MAXF, 4, COUNT)
-        if (trav == 14) {                   /* per-lane BVH walk (crt_bvh.h) */
+        if (trav == 14 && sc->gi_machine && (uint64_t)st->diffuse_reflection_ray_count < (1ull << 29) &&
+            (int64_t)sc->info.width * sc->info.height < INT32_MAX) {
+            /* per-lane state machine over the BVH walk (crt_gi_machine.h) */
+            const unsigned gb = (unsigned)std::max(1, std::min((plan.ntiles + 3) / 4, sc->gi_blocks));
+#define CRT_GIM(MAXF, COUNT)                                                                                \
+    hipLaunchKernelGGL((k_render_gi<MAXF, COUNT>), dim3(gb), dim3(256), 0, stream, d_scene, ds, plan.d_tiles, \
+                       plan.ntiles, d_out, sc->d_next_px, cnt)
+            if (frames <= 4) {
+                if (count) CRT_GIM(4, true); else CRT_GIM(4, false);
+            } else if (frames <= 16) {
+                if (count) CRT_GIM(16, true); else CRT_GIM(16, false);
+            } else {
+                if (count) CRT_GIM(64, true); else CRT_GIM(64, false);
+            }
+#undef CRT_GIM
+        } else if (trav == 14) {                   /* per-lane BVH walk (crt_bvh.h) */
             if (frames <= 4) {
                 if (count) CRT_REFILL_T(4, 14, true); else CRT_REFILL_T(4, 14, false);
             } else if (frames <= 16) {
@@ -2942,6 +2964,10 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) {
             sc->wave_slots = prop.multiProcessorCount * 4 * 6;
             sc->refill_waves = prop.multiProcessorCount * 4 * CRT_GI_WAVES;
+            int per_cu = 0;   /* resident blocks of the GI machine (registers, LDS) */
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_render_gi<4, false>, 256, 0) == hipSuccess &&
+                per_cu > 0)
+                sc->gi_blocks = prop.multiProcessorCount * per_cu;
         }
     }
     crt_host_scene_info(h, &sc->info);
@@ -3510,6 +3536,8 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         sc->window_walk = value != 0;
     } else if (k == "gi_refill") {
         sc->gi_refill = value != 0;
+    } else if (k == "gi_machine") {
+        sc->gi_machine = value != 0;
     } else if (k == "calib_k_milli") {   /* a fixed split threshold k = value / 1000 (calibrate 2) */
         if (value <= 0) return set_error(CRT_E_INVALID, "calib_k_milli must be > 0");
         sc->calib_k = (float)value / 1000.0f;
