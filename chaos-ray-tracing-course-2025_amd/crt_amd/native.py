@@ -665,7 +665,11 @@ def shard_compact_plan(width: int, height: int, bucket_size: int, shard: int, sh
         _check(int(n))
     out = np.zeros((n, 5), np.int64)
     if n:
-        lib().crt_shard_compact_plan(width, height, bucket_size, shard, shard_count, m, out.ctypes.data, n)
+        n2 = lib().crt_shard_compact_plan(width, height, bucket_size, shard, shard_count, m, out.ctypes.data, n)
+        if n2 < 0:
+            _check(int(n2))
+        if n2 != n:
+            raise RuntimeError(f"crt_shard_compact_plan: {n2} tiles on the second call, {n} on the first")
     return out
 
 

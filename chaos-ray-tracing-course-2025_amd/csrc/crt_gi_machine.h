@@ -21,9 +21,17 @@
  * whose children are traced lives at index = its ray depth.  The two deepest
  * such depths (max_ray_depth - 2, - 1: the ones every bounce touches) are in
  * LDS, one 16-float frame per lane (8 KB per wave); shallower ones go to a
- * per-lane array (scratch), touched a few times per pixel.  An activation at
- * depth max_ray_depth has only untraced (black) children and is resolved on
- * the spot (its GI draws are still taken, crt_renderer.cpp:61-78).
+ * global buffer, 64 contiguous bytes per (lane, depth) — one cache line half,
+ * L2-resident (16 MB for C4's 262 k lanes) and touched a few times per pixel.
+ * An activation at depth max_ray_depth has only untraced (black) children and
+ * is resolved on the spot (its GI draws are still taken, crt_renderer.cpp:
+ * 61-78).
+ *
+ * The walk postpones leaves (speculative while-while): a node step is
+ * branch-free, a lane reaching a live leaf parks it and waits, and the leaf
+ * triangles are tested when enough lanes hold one (or no lane can step), so
+ * the triangle code runs for many lanes at once instead of for the few lanes
+ * that happen to sit on a leaf in each round.
  */
 #pragma once
 
@@ -45,11 +53,10 @@ struct GiFrame {
     uint32_t meta;
 };
 
-template <int MAXF>
 struct GiFrames {
     GiLds *L;
+    float4 *g;                  /* this lane's frames of depths < base: 4 float4 each */
     int w, lane, base;          /* LDS holds depths base, base + 1 */
-    float spill[MAXF][16];
 
     __device__ __forceinline__ GiFrame load(int k) const {
         float v[16];
@@ -59,7 +66,10 @@ struct GiFrames {
             for (int q = 0; q < 16; ++q) v[q] = L->f[w][sl][q][lane];
         } else {
 #pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = spill[k][q];
+            for (int q = 0; q < 4; ++q) {
+                const float4 x = load_global(g, 4 * k + q);
+                v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+            }
         }
         GiFrame f;
         f.acc = vec(v[0], v[1], v[2]);
@@ -79,7 +89,7 @@ struct GiFrames {
             for (int q = 0; q < 16; ++q) L->f[w][sl][q][lane] = v[q];
         } else {
 #pragma unroll
-            for (int q = 0; q < 16; ++q) spill[k][q] = v[q];
+            for (int q = 0; q < 4; ++q) g[4 * k + q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
         }
     }
 };
@@ -104,6 +114,7 @@ struct GiWalk {
     float lim, t;
     int tri;
     bool tie;
+    int leaf;             /* parked leaf (BNode::leaf), 0 = none */
 };
 
 __device__ __forceinline__ void gi_walk_begin(const DeviceScene &s, GiWalk &w, Vec o, Vec d) {
@@ -114,21 +125,27 @@ __device__ __forceinline__ void gi_walk_begin(const DeviceScene &s, GiWalk &w, V
     w.t = 0.0f;
     w.tri = -1;
     w.tie = false;
+    w.leaf = 0;
     /* rays with a NaN component miss every cell (crt_bvh.h trace_bvh_exact) */
     if (isnan(o.x) || isnan(o.y) || isnan(o.z) || isnan(d.x) || isnan(d.y) || isnan(d.z)) w.i = s.bnode_count;
 }
 
+/* one node of the walk, branch-free: descend / move on, and park a live leaf */
 template <bool COUNT>
-__device__ __forceinline__ void gi_walk_step(const DeviceScene &s, GiWalk &w, Vec o, Vec d, LaneCounts &c) {
+__device__ __forceinline__ void gi_walk_node(GiWalk &w, LaneCounts &c) {
     const BNode nd = load_global(w.nodes, w.i);
     if (COUNT) ++c.nodes;
-    if (!bnode_alive(nd, w.pr, w.lim)) {
-        w.i = nd.skip;
-        return;
-    }
-    ++w.i;
-    const int cnt = nd.leaf & 15;
-    const int first = nd.leaf >> 4;
+    const bool alive = bnode_alive(nd, w.pr, w.lim);
+    w.i = alive ? w.i + 1 : nd.skip;      /* a leaf's skip is i + 1 */
+    w.leaf = alive ? nd.leaf : 0;
+}
+
+/* the parked leaf's triangles (crt_bvh.h walk_bvh) */
+template <bool COUNT>
+__device__ __forceinline__ void gi_walk_leaf(const DeviceScene &s, GiWalk &w, Vec o, Vec d, LaneCounts &c) {
+    const int cnt = w.leaf & 15;
+    const int first = w.leaf >> 4;
+    w.leaf = 0;
     for (int k = 0; k < cnt; ++k) {
         const DTriGeo g = load_global(s.btri, first + k);
         const int32_t id = load_global(s.btri_id, first + k);
@@ -179,20 +196,27 @@ __device__ __forceinline__ int gi_walk_finish(const DeviceScene &s, const GiWalk
 #define CRT_GIM_WAIT 32      /* a wave resolves once this many of its lanes wait */
 #endif
 
-template <int MAXF, bool COUNT>
+#ifndef CRT_GIM_LEAVES
+#define CRT_GIM_LEAVES 24    /* ... and tests parked leaves once this many lanes hold one */
+#endif
+
+/* gframes: (grid lanes) x max(0, max_ray_depth - 2) frames of 64 B */
+template <bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRT_GIM_WAVES))) void k_render_gi(
     const DeviceScene *__restrict__ scene, DSettings st, const Tile *__restrict__ tiles, int ntiles,
-    float *__restrict__ out, int32_t *__restrict__ next_px, unsigned long long *__restrict__ counters) {
+    float *__restrict__ out, int32_t *__restrict__ next_px, unsigned long long *__restrict__ counters,
+    float4 *__restrict__ gframes) {
     const int lane = (int)(threadIdx.x & 63);
     const DeviceScene &s = *scene;
     const int total = ntiles * 64;   /* pixel slots: tile k, lane j -> (j & 7, j >> 3) inside tile k */
     const unsigned long long lt = (1ull << lane) - 1ull;
     __shared__ GiLds lds;
-    GiFrames<MAXF> fs;
+    GiFrames fs;
     fs.L = &lds;
     fs.w = (int)(threadIdx.x >> 6);
     fs.lane = lane;
     fs.base = (int)st.max_ray_depth - kGiLdsFrames;
+    fs.g = gframes + (int64_t)(blockIdx.x * blockDim.x + threadIdx.x) * 4 * (fs.base > 0 ? fs.base : 0);
     LaneCounts cnt = {};
     const uint32_t maxd = st.max_ray_depth, nrays = st.diffuse_reflection_ray_count;
     const Vec bg = vec(s.background[0], s.background[1], s.background[2]);
@@ -246,9 +270,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRT_GIM_WAV
             const unsigned long long wm = __ballot(walking);
             const int waiting = __popcll(hm) - __popcll(wm);
             if (wm == 0ull || waiting >= CRT_GIM_WAIT) break;
-            if (walking) {
-                gi_walk_step<COUNT>(s, w, o, d, cnt);
-                walking = w.i < s.bnode_count;
+            const bool parked = w.leaf != 0;
+            const unsigned long long pm = __ballot(parked);
+            if (__popcll(pm) >= CRT_GIM_LEAVES || pm == wm) {   /* leaf round */
+                if (parked) {
+                    gi_walk_leaf<COUNT>(s, w, o, d, cnt);
+                    walking = w.i < s.bnode_count;
+                }
+            } else if (walking && !parked) {                     /* node round */
+                gi_walk_node<COUNT>(w, cnt);
+                walking = w.i < s.bnode_count || w.leaf != 0;
             }
         }
         if (!has || walking) continue;
@@ -409,14 +440,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRT_GIM_WAV
     }
 }
 
-#define CRT_GIM_INSTANCES(X) X(4, false) X(4, true) X(16, false) X(16, true) X(64, false) X(64, true)
-#define CRT_GIM_SIG(MAXF, C) void k_render_gi<MAXF, C>(const DeviceScene *__restrict__, DSettings, \
-    const Tile *__restrict__, int, float *__restrict__, int32_t *__restrict__, unsigned long long *__restrict__);
+#define CRT_GIM_INSTANCES(X) X(false) X(true)
+#define CRT_GIM_SIG(C) void k_render_gi<C>(const DeviceScene *__restrict__, DSettings, const Tile *__restrict__, int, \
+    float *__restrict__, int32_t *__restrict__, unsigned long long *__restrict__, float4 *__restrict__);
 #ifdef CRT_GI_TU
-#define CRT_GIM_INST(MAXF, C) template __global__ CRT_GIM_SIG(MAXF, C)
+#define CRT_GIM_INST(C) template __global__ CRT_GIM_SIG(C)
 CRT_GIM_INSTANCES(CRT_GIM_INST)
 #elif !defined(CRT_SIDE_TU)
-#define CRT_GIM_EXTERN(MAXF, C) extern template __global__ CRT_GIM_SIG(MAXF, C)
+#define CRT_GIM_EXTERN(C) extern template __global__ CRT_GIM_SIG(C)
 CRT_GIM_INSTANCES(CRT_GIM_EXTERN)
 #endif
 

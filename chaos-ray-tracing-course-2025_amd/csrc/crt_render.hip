@@ -2045,6 +2045,8 @@ struct crt_hip_scene {
     int gi_refill = 1;                 /* GI frames: persistent waves with pixel refill (env CRT_GI_REFILL, option "gi_refill") */
     int gi_machine = 1;                /* ... as per-lane state machines (k_render_gi; option "gi_machine") */
     int gi_blocks = 1024;              /* blocks of the k_render_gi grid (resident blocks per CU x CUs) */
+    void *gi_frames = nullptr;         /* k_render_gi: frames below the LDS ones (grown on demand) */
+    int64_t gi_frames_bytes = 0;
     int refill_waves = 5120;           /* waves of the refill grid: CUs x 4 SIMDs x CRT_GI_WAVES */
     bool grid_empty = false;
     int traversal = 8;             /* 7 reference order | 8 pruned (default), see trace<> (env CRT_TRAVERSAL) */
@@ -2569,6 +2571,10 @@ bool wf_overflowed(WfBuffers &w, bool wait) {
     }
     w.flag_pending = false;
     if (*w.h_flag == 0) return false;
+    /* consumed: frames still in flight were queued with the same stale sizes
+     * and are covered by this report; re-arm the device flag behind them */
+    (void)hipDeviceSynchronize();
+    (void)hipMemset(w.d_flag, 0, sizeof(int32_t));
     *w.h_flag = 0;
     w.recs.clear();
     wf_graphs_clear(w);
@@ -2723,10 +2729,8 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
     hipLaunchKernelGGL(k_wf_pixels, dim3(blocks0), dim3(256), 0, stream, w.nodes, w.cols, plan.d_tiles,
                        plan.ntiles, d_out);
     HIP_TRY(hipGetLastError());
-    if (replay) {
+    if (replay)   /* the device flag is sticky: a later frame's copy cannot hide an earlier overflow */
         HIP_TRY(hipMemcpyAsync(w.h_flag, w.d_flag, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
-        HIP_TRY(hipMemsetAsync(w.d_flag, 0, sizeof(int32_t), stream));
-    }
     return CRT_OK;
     };
     rc = enqueue();
@@ -2869,17 +2873,23 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
             (int64_t)sc->info.width * sc->info.height < INT32_MAX) {
             /* per-lane state machine over the BVH walk (crt_gi_machine.h) */
             const unsigned gb = (unsigned)std::max(1, std::min((plan.ntiles + 3) / 4, sc->gi_blocks));
-#define CRT_GIM(MAXF, COUNT)                                                                                \
-    hipLaunchKernelGGL((k_render_gi<MAXF, COUNT>), dim3(gb), dim3(256), 0, stream, d_scene, ds, plan.d_tiles, \
-                       plan.ntiles, d_out, sc->d_next_px, cnt)
-            if (frames <= 4) {
-                if (count) CRT_GIM(4, true); else CRT_GIM(4, false);
-            } else if (frames <= 16) {
-                if (count) CRT_GIM(16, true); else CRT_GIM(16, false);
-            } else {
-                if (count) CRT_GIM(64, true); else CRT_GIM(64, false);
+            /* frames of depths below the two LDS ones: 64 B per lane and depth */
+            const int64_t gneed = (int64_t)gb * 256 * std::max<int64_t>(0, (int64_t)st->max_ray_depth - 2) * 64;
+            if (gneed > sc->gi_frames_bytes) {
+                HIP_TRY(hipStreamSynchronize(stream));
+                if (sc->gi_frames) (void)hipFree(sc->gi_frames);
+                sc->gi_frames = nullptr;
+                sc->gi_frames_bytes = 0;
+                HIP_TRY(hipMalloc(&sc->gi_frames, (size_t)gneed));
+                sc->gi_frames_bytes = gneed;
             }
-#undef CRT_GIM
+            float4 *gf = static_cast<float4 *>(sc->gi_frames);
+            if (count)
+                hipLaunchKernelGGL((k_render_gi<true>), dim3(gb), dim3(256), 0, stream, d_scene, ds, plan.d_tiles,
+                                   plan.ntiles, d_out, sc->d_next_px, cnt, gf);
+            else
+                hipLaunchKernelGGL((k_render_gi<false>), dim3(gb), dim3(256), 0, stream, d_scene, ds, plan.d_tiles,
+                                   plan.ntiles, d_out, sc->d_next_px, cnt, gf);
         } else if (trav == 14) {                   /* per-lane BVH walk (crt_bvh.h) */
             if (frames <= 4) {
                 if (count) CRT_REFILL_T(4, 14, true); else CRT_REFILL_T(4, 14, false);
@@ -2965,7 +2975,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
             sc->wave_slots = prop.multiProcessorCount * 4 * 6;
             sc->refill_waves = prop.multiProcessorCount * 4 * CRT_GI_WAVES;
             int per_cu = 0;   /* resident blocks of the GI machine (registers, LDS) */
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_render_gi<4, false>, 256, 0) == hipSuccess &&
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_render_gi<false>, 256, 0) == hipSuccess &&
                 per_cu > 0)
                 sc->gi_blocks = prop.multiProcessorCount * per_cu;
         }
@@ -3146,6 +3156,7 @@ void crt_hip_scene_destroy(crt_hip_scene *sc) {
     for (void *p : sc->allocs) (void)hipFree(p);
     for (void *p : sc->plan_allocs) (void)hipFree(p);
     if (sc->d_out) (void)hipFree(sc->d_out);
+    if (sc->gi_frames) (void)hipFree(sc->gi_frames);
     wf_free(sc->wf);
     for (auto &kv : sc->unpack_plans) (void)hipFree(kv.second.first);
     for (auto &kv : sc->compact_unpack) (void)hipFree(kv.second.first);
@@ -3526,10 +3537,12 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
     if (k == "traversal") {
         if (value != 7 && value != 8) return set_error(CRT_E_INVALID, "traversal must be 7 (reference order) or 8 (pruned)");
         sc->traversal = value;
+        wf_graphs_clear(sc->wf);   /* captured wavefront frames bake in the level-0 walk */
     } else if (k == "secondary") {
         if (value != 0 && value != 4 && value != 10 && value != 14)
             return set_error(CRT_E_INVALID, "secondary must be 0, 4, 10 or 14");
         sc->secondary = value;
+        wf_graphs_clear(sc->wf);   /* ... the levels' walk */
     } else if (k == "wavefront") {
         sc->wavefront = value != 0;
     } else if (k == "window") {
@@ -3554,6 +3567,7 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
     } else if (k == "wf_rpw") {
         if (value < 1 || value > 64) return set_error(CRT_E_INVALID, "wf_rpw must be 1..64");
         sc->wf_rays_per_wave = value;
+        wf_graphs_clear(sc->wf);   /* ... and each level's rays per wave */
     } else if (k == "events") {
         sc->record_events = value != 0;
     } else if (k == "calibrate") {

@@ -38,6 +38,7 @@
 #include "core/crt_renderer.h"
 #include "core/crt_scene.h"
 #include "crt_hip.h"
+#include "crt_scene_lru.h"
 
 namespace {
 
@@ -226,8 +227,10 @@ struct Cached {
     ~Cached() { crt_hip_scene_destroy(scene); }
 };
 
+/* the two most recently rendered scenes (crt_scene_lru.h): a changed Scene
+ * replaces the older entry, whose device memory is freed */
 std::mutex g_mu;
-std::map<const crt::Scene *, std::unique_ptr<Cached>> g_cache;
+crt_shim::SceneLru<Cached> g_cache(2);
 
 [[noreturn]] void fail(const char *what) {
     throw std::runtime_error(std::string("crt_hip ") + what + ": " + crt_hip_last_error());
@@ -242,8 +245,8 @@ Image render_image(const Scene &scene, const RendererSettings &settings) {
     std::lock_guard<std::mutex> lock(g_mu);
     std::unique_ptr<Flat> now(new Flat());
     flatten(scene, *now);
-    std::unique_ptr<Cached> &c = g_cache[&scene];
-    if (!c || !same_scene(c->flat, c->vertices, c->texels, *now)) {
+    Cached *c = g_cache.find([&](const Cached &e) { return same_scene(e.flat, e.vertices, e.texels, *now); });
+    if (!c) {
         std::unique_ptr<Cached> fresh(new Cached());
         const char *dev = std::getenv("CRT_HIP_DEVICE");
         if (crt_hip_scene_from_tree(&now->desc, dev ? std::atoi(dev) : 0, &fresh->scene) != CRT_OK)
@@ -255,7 +258,7 @@ Image render_image(const Scene &scene, const RendererSettings &settings) {
                                                                          ? (size_t)t.bitmap_width * t.bitmap_height * 3
                                                                          : 0));
         fresh->flat = std::move(*now);
-        c = std::move(fresh);
+        c = g_cache.insert(std::move(fresh));
     }
     const crt_renderer_settings st{settings.max_ray_depth, settings.diffuse_reflection_ray_count, settings.shadow_bias,
                                    settings.reflection_bias, settings.diffuse_reflection_bias, settings.refraction_bias};
