@@ -193,11 +193,11 @@ __device__ __forceinline__ int gi_walk_finish(const DeviceScene &s, const GiWalk
 #define CRT_GIM_WAVES 4      /* min waves/SIMD of the GI machine */
 #endif
 #ifndef CRT_GIM_WAIT
-#define CRT_GIM_WAIT 32      /* a wave resolves once this many of its lanes wait */
+#define CRT_GIM_WAIT 48      /* a wave resolves once this many of its lanes wait (C4 1080^2: 16 / 32 / 40 / 48 / 56 / 62 -> 41.5 / 30.1 / 28.4 / 28.0 / 28.6 / 30.8 ms, profiles/r03/ab_gim) */
 #endif
 
 #ifndef CRT_GIM_LEAVES
-#define CRT_GIM_LEAVES 24    /* ... and tests parked leaves once this many lanes hold one */
+#define CRT_GIM_LEAVES 16    /* ... and tests parked leaves once this many lanes hold one (8 / 16 / 24 / 32 / 40: 32.3 / 27.6 / 28.0 / 28.2 / 31.6 ms) */
 #endif
 
 /* gframes: (grid lanes) x max(0, max_ray_depth - 2) frames of 64 B */
