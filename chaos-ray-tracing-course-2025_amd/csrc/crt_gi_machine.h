@@ -20,9 +20,9 @@
  * Pending activations (the recursion's frames): the frame of an activation
  * whose children are traced lives at index = its ray depth.  The two deepest
  * such depths (max_ray_depth - 2, - 1: the ones every bounce touches) are in
- * LDS, one 16-float frame per lane (8 KB per wave); shallower ones go to a
- * global buffer, 64 contiguous bytes per (lane, depth) — one cache line half,
- * L2-resident (16 MB for C4's 262 k lanes) and touched a few times per pixel.
+ * LDS, one 16-float frame per lane (8 KB per wave); the one above them
+ * (max_ray_depth - 3, C4's depth 0) in registers; shallower ones (deep
+ * recursion only) in a global buffer, 64 contiguous bytes per (lane, depth).
  * An activation at depth max_ray_depth has only untraced (black) children and
  * is resolved on the spot (its GI draws are still taken, crt_renderer.cpp:
  * 61-78).
@@ -55,13 +55,17 @@ struct GiFrame {
 
 struct GiFrames {
     GiLds *L;
-    float4 *g;                  /* this lane's frames of depths < base: 4 float4 each */
-    int w, lane, base;          /* LDS holds depths base, base + 1 */
+    float4 *g;                  /* this lane's frames of depths < base - 1: 4 float4 each */
+    int w, lane, base;          /* LDS holds depths base, base + 1; registers base - 1 */
+    float reg[16];
 
     __device__ __forceinline__ GiFrame load(int k) const {
         float v[16];
         const int sl = k - base;
-        if (sl >= 0 && sl < kGiLdsFrames) {
+        if (sl == -1) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = reg[q];
+        } else if (sl >= 0 && sl < kGiLdsFrames) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) v[q] = L->f[w][sl][q][lane];
         } else {
@@ -84,7 +88,10 @@ struct GiFrames {
         const float v[16] = {f.acc.x, f.acc.y, f.acc.z, f.p.x, f.p.y, f.p.z, f.n.x, f.n.y, f.n.z,
                              f.r.x,   f.r.y,   f.r.z,   f.alb.x, f.alb.y, f.alb.z, __uint_as_float(f.meta)};
         const int sl = k - base;
-        if (sl >= 0 && sl < kGiLdsFrames) {
+        if (sl == -1) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) reg[q] = v[q];
+        } else if (sl >= 0 && sl < kGiLdsFrames) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) L->f[w][sl][q][lane] = v[q];
         } else {
@@ -200,7 +207,7 @@ __device__ __forceinline__ int gi_walk_finish(const DeviceScene &s, const GiWalk
 #define CRT_GIM_LEAVES 16    /* ... and tests parked leaves once this many lanes hold one (8 / 16 / 24 / 32 / 40: 32.3 / 27.6 / 28.0 / 28.2 / 31.6 ms) */
 #endif
 
-/* gframes: (grid lanes) x max(0, max_ray_depth - 2) frames of 64 B */
+/* gframes: (grid lanes) x max(0, max_ray_depth - 3) frames of 64 B */
 template <bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRT_GIM_WAVES))) void k_render_gi(
     const DeviceScene *__restrict__ scene, DSettings st, const Tile *__restrict__ tiles, int ntiles,
@@ -216,7 +223,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRT_GIM_WAV
     fs.w = (int)(threadIdx.x >> 6);
     fs.lane = lane;
     fs.base = (int)st.max_ray_depth - kGiLdsFrames;
-    fs.g = gframes + (int64_t)(blockIdx.x * blockDim.x + threadIdx.x) * 4 * (fs.base > 0 ? fs.base : 0);
+    fs.g = gframes + (int64_t)(blockIdx.x * blockDim.x + threadIdx.x) * 4 * (fs.base > 1 ? fs.base - 1 : 0);
     LaneCounts cnt = {};
     const uint32_t maxd = st.max_ray_depth, nrays = st.diffuse_reflection_ray_count;
     const Vec bg = vec(s.background[0], s.background[1], s.background[2]);

@@ -2873,8 +2873,8 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
             (int64_t)sc->info.width * sc->info.height < INT32_MAX) {
             /* per-lane state machine over the BVH walk (crt_gi_machine.h) */
             const unsigned gb = (unsigned)std::max(1, std::min((plan.ntiles + 3) / 4, sc->gi_blocks));
-            /* frames of depths below the two LDS ones: 64 B per lane and depth */
-            const int64_t gneed = (int64_t)gb * 256 * std::max<int64_t>(0, (int64_t)st->max_ray_depth - 2) * 64;
+            /* frames below the two LDS ones and the register one: 64 B per lane and depth */
+            const int64_t gneed = (int64_t)gb * 256 * std::max<int64_t>(0, (int64_t)st->max_ray_depth - 3) * 64;
             if (gneed > sc->gi_frames_bytes) {
                 HIP_TRY(hipStreamSynchronize(stream));
                 if (sc->gi_frames) (void)hipFree(sc->gi_frames);
