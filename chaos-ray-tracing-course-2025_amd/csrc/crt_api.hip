@@ -1,0 +1,577 @@
+/*
+ * crt_api.hip — the extern "C" entry points of include/crt_hip.h: scene
+ * upload / create / destroy, render (host and device buffers), shards and
+ * their unpack, the trace hook, work counters and options.  Replaces
+ * crt::render_image (src/core/crt_renderer.cpp:157-199) for the reference's
+ * callers (src/standalone/main.cpp:38, src/python/py_crt_module.cpp:100).
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "crt_scene_impl.h"
+#include "crt_tree_build.h"
+
+extern "C" {
+
+int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **out) {
+    if (!h || !out) return set_error(CRT_E_INVALID, "null argument");
+    *out = nullptr;
+    const HostScene &hs = *reinterpret_cast<const HostScene *>(h);
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return set_error(CRT_E_INVALID, "no such HIP device");
+    HIP_TRY(hipSetDevice(device));
+    std::unique_ptr<crt_hip_scene> sc(new crt_hip_scene());
+    sc->device = device;
+#ifdef CRT_AB_OPTIONS
+    /* A/B builds only (scripts/make_variant.sh RENDER_FLAGS=-DCRT_AB_OPTIONS): environment
+     * overrides of the options (crt_hip_scene_set_option names) */
+    static const char *const kEnv[][2] = {{"CRT_TRAVERSAL", "traversal"}, {"CRT_SECONDARY", "secondary"},
+                                           {"CRT_WAVEFRONT", "wavefront"}, {"CRT_GI_REFILL", "gi_refill"},
+                                           {"CRT_WF_RPW", "wf_rpw"},       {"CRT_TRACE_WALK", "trace_walk"},
+                                           {"CRT_CALIBRATE", "calibrate"}, {"CRT_WINDOW", "window"},
+                                           {"CRT_EVENTS", "events"}};
+    for (const auto &kv : kEnv)
+        if (const char *e = std::getenv(kv[0]))
+            if (crt_hip_scene_set_option(sc.get(), kv[1], std::atoi(e)) != CRT_OK) return CRT_E_INVALID;
+    if (const char *e = std::getenv("CRT_CALIB_K")) {   /* a fixed split threshold instead of the tuned one */
+        sc->calib_k = (float)std::atof(e);
+        if (sc->calibrate) sc->calibrate = 2;
+    }
+#endif
+    if (hs.tree_on_host) sc->tile_work = tile_work_estimate(hs, (hs.width + 7) / 8, (hs.height + 7) / 8);
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) {
+            sc->wave_slots = prop.multiProcessorCount * 4 * 6;
+            sc->refill_waves = prop.multiProcessorCount * 4 * CRT_GI_WAVES;
+            int per_cu = 0;   /* resident blocks of the GI machine (registers, LDS) */
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_render_gi<false>, 256, 0) == hipSuccess &&
+                per_cu > 0)
+                sc->gi_blocks = prop.multiProcessorCount * per_cu;
+        }
+    }
+    crt_host_scene_info(h, &sc->info);
+    sc->info.device_bytes = 0;
+    for (const DMaterial &m : hs.materials) {
+        if (m.type == CRT_MATERIAL_REFLECTIVE || m.type == CRT_MATERIAL_REFRACTIVE) sc->has_secondary = true;
+        if (m.type == CRT_MATERIAL_REFRACTIVE) sc->has_refractive = true;
+        if (m.type == CRT_MATERIAL_DIFFUSE) sc->has_diffuse = true;
+    }
+    DeviceScene &ds = sc->ds;
+    int rc;
+    ds.prune_origin_max = hs.prune_origin_max;
+    if (hs.tree_on_host) {
+        if ((rc = upload(sc.get(), hs.nodes, &ds.nodes)) != CRT_OK) return rc;
+        ds.node_count = (int32_t)hs.nodes.size();
+        if ((rc = upload(sc.get(), hs.pnodes, &ds.pnodes)) != CRT_OK) return rc;
+        auto ok = [](float x) {
+            const float m = std::fabs(x);
+            return x == 0.0f || (m >= 0x1p-40f && m <= 0x1p62f);
+        };
+        ds.planes_ok = 1;
+        for (const DNode &n : hs.nodes)
+            if (!(ok(n.lo_x) && ok(n.lo_y) && ok(n.lo_z) && ok(n.hi_x) && ok(n.hi_y) && ok(n.hi_z) &&
+                  n.lo_x <= n.hi_x && n.lo_y <= n.hi_y && n.lo_z <= n.hi_z))   /* ordered: crt_device.h in_slab */
+                ds.planes_ok = 0;
+        if ((rc = upload(sc.get(), hs.slots, &ds.slots)) != CRT_OK) return rc;
+        if ((rc = upload(sc.get(), hs.slot_tri, &ds.slot_tri)) != CRT_OK) return rc;
+        if ((rc = upload(sc.get(), hs.slot_cull, &ds.slot_cull)) != CRT_OK) return rc;
+        std::vector<uint32_t> bits((hs.slot_cull.size() + 31) / 32 + 1, 0u);
+        for (size_t k = 0; k < hs.slot_cull.size(); ++k)
+            if (hs.slot_cull[k]) bits[k >> 5] |= 1u << (k & 31);
+        if ((rc = upload(sc.get(), bits, &ds.slot_cull_bits)) != CRT_OK) return rc;
+        sc->ref_bounds = hs.ref_bounds;
+        sc->ref_children = hs.ref_children;
+        sc->ref_leaf_off = hs.ref_leaf_off;
+        sc->ref_leaf_tris = hs.ref_leaf_tris;
+    } else {
+        /* exact tree build on the device (crt_tree_build.hip) */
+        DeviceTree dt;
+        rc = build_tree_device(hs, nullptr, dt);
+        for (void *p : dt.allocs) sc->allocs.push_back(p);
+        if (rc != CRT_OK) return rc;
+        ds.nodes = dt.nodes;
+        ds.node_count = dt.node_count;
+        ds.pnodes = dt.pnodes;
+        ds.planes_ok = dt.planes_ok;
+        ds.slots = dt.slots;
+        ds.slot_tri = dt.slot_tri;
+        ds.slot_cull = dt.slot_cull;
+        ds.slot_cull_bits = dt.slot_cull_bits;
+        sc->dt_ref_bounds = dt.ref_bounds;
+        sc->dt_ref_children = dt.ref_children;
+        sc->dt_ref_leaf_off = dt.ref_leaf_off;
+        sc->dt_ref_leaf_tris = dt.ref_leaf_tris;
+        sc->info.node_count = dt.node_count;
+        sc->info.leaf_count = dt.leaf_count;
+        sc->info.leaf_ref_count = dt.slot_count;
+        sc->info.max_depth = dt.max_depth;
+        sc->info.max_leaf_size = dt.max_leaf_size;
+        sc->info.tree_build_ms = dt.build_ms;
+        sc->info.tree_on_device = 1;
+        const int64_t n = dt.node_count, m = dt.slot_count;
+        sc->info.device_bytes += n * (int64_t)sizeof(DNode) + 8 * (n + 1) * (int64_t)sizeof(PNode) +
+                                 m * (int64_t)(sizeof(DTriGeo) + 4 + 1) + (m / 32 + 1) * 4;
+    }
+    if (hs.bnode_count > 0) {   /* secondary-ray BVH (crt_bvh.h) */
+        if ((rc = upload(sc.get(), hs.bnodes, &ds.bnodes)) != CRT_OK) return rc;
+        if ((rc = upload(sc.get(), hs.btri, &ds.btri)) != CRT_OK) return rc;
+        if ((rc = upload(sc.get(), hs.btri_id, &ds.btri_id)) != CRT_OK) return rc;
+        ds.bnode_count = hs.bnode_count;
+    }
+    sc->camera_fast = camera_rays_fast(hs, ds.planes_ok != 0);
+    if ((rc = upload(sc.get(), hs.tri_attr, &ds.tri_attr)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.vnormal, &ds.vnormal)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.vuv, &ds.vuv)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.materials, &ds.materials)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.textures, &ds.textures)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.texels, &ds.texels)) != CRT_OK) return rc;
+    if ((rc = upload(sc.get(), hs.lights, &ds.lights)) != CRT_OK) return rc;
+    ds.light_count = (int32_t)hs.lights.size();
+    std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
+    std::memcpy(ds.cam_rot, hs.cam_rot, sizeof ds.cam_rot);
+    ds.width = hs.width;
+    ds.height = hs.height;
+    ds.aspect = hs.aspect;
+    ds.tan_half_fov = hs.tan_half_fov;
+    std::memcpy(ds.background, hs.background, sizeof ds.background);
+    ds.gi_on = hs.gi_on;
+    ds.reflections_on = hs.reflections_on;
+    ds.refractions_on = hs.refractions_on;
+
+    HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&sc->ev_start));
+    HIP_TRY(hipEventCreate(&sc->ev_stop));
+    void *p = nullptr;
+    HIP_TRY(hipMalloc(&p, 16 * sizeof(unsigned long long)));
+    sc->allocs.push_back(p);
+    sc->d_counters = static_cast<unsigned long long *>(p);
+    p = nullptr;
+    HIP_TRY(hipMalloc(&p, 64));
+    sc->allocs.push_back(p);
+    sc->d_next_px = static_cast<int32_t *>(p);
+
+    int64_t px = 0;
+    const std::vector<DBucket> all = shard_buckets(hs.width, hs.height, hs.bucket_size, 0, 1, &px);
+    sc->grid_empty = all.empty();
+    if ((rc = make_tile_plan(sc.get(), all, true, sc->full)) != CRT_OK) return rc;
+    *out = sc.release();
+    return CRT_OK;
+}
+
+int crt_hip_scene_create_ex(const crt_scene_desc *desc, int device, int flags, crt_hip_scene **out) {
+    if (!desc || !out) return set_error(CRT_E_INVALID, "null argument");
+    int mode = flags & 3;
+    if (mode == CRT_SCENE_TREE_AUTO) {
+        if (const char *e = std::getenv("CRT_TREE_BUILD")) {
+            if (std::strcmp(e, "host") == 0) mode = CRT_SCENE_TREE_HOST;
+            if (std::strcmp(e, "device") == 0) mode = CRT_SCENE_TREE_DEVICE;
+        }
+    }
+    if (mode == CRT_SCENE_TREE_AUTO) {
+        int64_t nt = 0;
+        for (int i = 0; i < desc->mesh_count && desc->meshes; ++i) nt += desc->meshes[i].index_count / 3;
+        mode = nt >= CRT_SCENE_DEVICE_BUILD_MIN ? CRT_SCENE_TREE_DEVICE : CRT_SCENE_TREE_HOST;
+    }
+    if (mode != CRT_SCENE_TREE_HOST && mode != CRT_SCENE_TREE_DEVICE) return set_error(CRT_E_INVALID, "bad tree build flag");
+    std::unique_ptr<HostScene> hs(new HostScene());
+    int rc = prepare_scene(desc, *hs, mode == CRT_SCENE_TREE_HOST);
+    if (rc != CRT_OK) return rc;
+    return crt_hip_scene_upload(reinterpret_cast<crt_host_scene *>(hs.get()), device, out);
+}
+
+int crt_hip_scene_from_tree(const crt_tree_scene_desc *desc, int device, crt_hip_scene **out) {
+    if (!desc || !out) return set_error(CRT_E_INVALID, "null argument");
+    std::unique_ptr<HostScene> hs(new HostScene());
+    const int rc = prepare_scene_from_tree(desc, *hs);
+    if (rc != CRT_OK) return rc;
+    return crt_hip_scene_upload(reinterpret_cast<crt_host_scene *>(hs.get()), device, out);
+}
+
+int crt_hip_scene_create(const crt_scene_desc *desc, int device, crt_hip_scene **out) {
+    return crt_hip_scene_create_ex(desc, device, CRT_SCENE_TREE_AUTO, out);
+}
+
+int crt_hip_scene_tree(const crt_hip_scene *sc, float *bounds, int32_t *children, int64_t *leaf_offsets,
+                       int32_t *leaf_tris) {
+    if (!sc) return set_error(CRT_E_INVALID, "null argument");
+    const int64_t n = sc->info.node_count, m = sc->info.leaf_ref_count;
+    if (sc->info.tree_on_device) {
+        HIP_TRY(hipSetDevice(sc->device));
+        if (bounds) HIP_TRY(hipMemcpy(bounds, sc->dt_ref_bounds, (size_t)n * 6 * sizeof(float), hipMemcpyDeviceToHost));
+        if (children) HIP_TRY(hipMemcpy(children, sc->dt_ref_children, (size_t)n * 2 * sizeof(int32_t), hipMemcpyDeviceToHost));
+        if (leaf_offsets)
+            HIP_TRY(hipMemcpy(leaf_offsets, sc->dt_ref_leaf_off, (size_t)(n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+        if (leaf_tris && m > 0)
+            HIP_TRY(hipMemcpy(leaf_tris, sc->dt_ref_leaf_tris, (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost));
+        return CRT_OK;
+    }
+    if (bounds) std::memcpy(bounds, sc->ref_bounds.data(), sc->ref_bounds.size() * sizeof(float));
+    if (children) std::memcpy(children, sc->ref_children.data(), sc->ref_children.size() * sizeof(int32_t));
+    if (leaf_offsets) std::memcpy(leaf_offsets, sc->ref_leaf_off.data(), sc->ref_leaf_off.size() * sizeof(int64_t));
+    if (leaf_tris) std::memcpy(leaf_tris, sc->ref_leaf_tris.data(), sc->ref_leaf_tris.size() * sizeof(int32_t));
+    return CRT_OK;
+}
+
+int crt_hip_scene_info(const crt_hip_scene *sc, crt_scene_info *out) {
+    if (!sc || !out) return set_error(CRT_E_INVALID, "null argument");
+    *out = sc->info;
+    return CRT_OK;
+}
+
+void crt_hip_scene_destroy(crt_hip_scene *sc) {
+    if (!sc) return;
+    (void)hipSetDevice(sc->device);
+    if (sc->stream) (void)hipStreamSynchronize(sc->stream);
+    for (void *p : sc->allocs) (void)hipFree(p);
+    for (void *p : sc->plan_allocs) (void)hipFree(p);
+    if (sc->d_out) (void)hipFree(sc->d_out);
+    if (sc->gi_frames) (void)hipFree(sc->gi_frames);
+    wf_free(sc->wf);
+    for (auto &kv : sc->unpack_plans) (void)hipFree(kv.second.first);
+    for (auto &kv : sc->compact_unpack) (void)hipFree(kv.second.first);
+    if (sc->ev_start) (void)hipEventDestroy(sc->ev_start);
+    if (sc->ev_stop) (void)hipEventDestroy(sc->ev_stop);
+    if (sc->stream) (void)hipStreamDestroy(sc->stream);
+    delete sc;
+}
+
+int crt_hip_render_device(crt_hip_scene *sc, const crt_renderer_settings *st, float *d_rgb, void *stream) {
+    if (!sc || !d_rgb) return set_error(CRT_E_INVALID, "null argument");
+    int rc = check_settings(st);
+    if (rc != CRT_OK) return rc;
+    HIP_TRY(hipSetDevice(sc->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : sc->stream;
+    return render_into(sc, st, d_rgb, s, false);
+}
+
+int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rgb_out, crt_render_stats *stats) {
+    if (!sc || !rgb_out) return set_error(CRT_E_INVALID, "null argument");
+    int rc = check_settings(st);
+    if (rc != CRT_OK) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipSetDevice(sc->device));
+    const size_t nfl = (size_t)sc->info.width * sc->info.height * 3;
+    if (!sc->d_out) HIP_TRY(hipMalloc(&sc->d_out, nfl * sizeof(float)));
+    rc = render_into(sc, st, sc->d_out, sc->stream, false);
+    if (rc != CRT_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(rgb_out, sc->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
+    HIP_TRY(hipStreamSynchronize(sc->stream));
+    if (wf_overflowed(sc->wf, true)) {   /* recorded level sizes did not hold: render again with read-backs */
+        if ((rc = render_into(sc, st, sc->d_out, sc->stream, false)) != CRT_OK) return rc;
+        HIP_TRY(hipMemcpyAsync(rgb_out, sc->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
+        HIP_TRY(hipStreamSynchronize(sc->stream));
+    }
+    if (stats) {
+        std::memset(stats, 0, sizeof *stats);
+        float ms = 0.f;
+        if (!sc->grid_empty && sc->full.ntiles > 0 && sc->events_valid)
+            HIP_TRY(hipEventElapsedTime(&ms, sc->ev_start, sc->ev_stop));
+        stats->kernel_ms = ms;
+        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        stats->width = sc->info.width;
+        stats->height = sc->info.height;
+    }
+    return CRT_OK;
+}
+
+int crt_hip_plan_info(const crt_hip_scene *sc, crt_plan_info *out) {
+    if (!sc || !out) return set_error(CRT_E_INVALID, "null argument");
+    std::memset(out, 0, sizeof *out);
+    out->calib_k = (sc->calib_walk >= 0 && !sc->calib.empty()) ? (double)sc->calib_k : 0.0;
+    out->tiles = sc->full.ntiles;
+    for (const Tile &t : sc->full.tiles) out->small_tiles += t.w * t.h <= 16 ? 1 : 0;
+    return CRT_OK;
+}
+
+int crt_hip_last_kernel_ms(crt_hip_scene *sc, double *ms) {
+    if (!sc || !ms) return set_error(CRT_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(sc->device));
+    if (!sc->events_valid) return set_error(CRT_E_INVALID, "no timed render (option \"events\" is off)");
+    HIP_TRY(hipEventSynchronize(sc->ev_stop));
+    float f = 0.f;
+    HIP_TRY(hipEventElapsedTime(&f, sc->ev_start, sc->ev_stop));
+    *ms = f;
+    return CRT_OK;
+}
+
+int64_t crt_hip_shard_floats(const crt_hip_scene *sc, int shard, int shard_count) {
+    if (!sc || shard_count <= 0 || shard < 0 || shard >= shard_count) return set_error(CRT_E_INVALID, "bad shard");
+    int64_t px = 0;
+    shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size, shard, shard_count, &px);
+    return 3 * px;
+}
+
+int64_t crt_hip_shard_stride(const crt_hip_scene *sc, int shard_count) {
+    if (!sc || shard_count <= 0) return set_error(CRT_E_INVALID, "bad shard count");
+    int64_t m = 0;
+    for (int s = 0; s < shard_count; ++s) m = std::max(m, crt_hip_shard_floats(sc, s, shard_count));
+    return (m + 63) / 64 * 64;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int crt_hip_render_shard(crt_hip_scene *sc, const crt_renderer_settings *st, int shard, int shard_count,
+                         float *d_packed, void *stream) {
+    return render_shard_t(sc, st, shard, shard_count, d_packed, stream, false);
+}
+
+int crt_hip_unpack_shards(crt_hip_scene *sc, int shard_count, const float *d_gathered, float *d_rgb, void *stream) {
+    return unpack_shards_t<float>(sc, shard_count, d_gathered, d_rgb, stream, false);
+}
+
+int crt_hip_unpack_shards_rgb8(crt_hip_scene *sc, int shard_count, const uint8_t *d_gathered, uint8_t *d_rgb8,
+                               void *stream) {
+    return unpack_shards_t<uint8_t>(sc, shard_count, d_gathered, d_rgb8, stream, false);
+}
+
+int crt_hip_live_mask(crt_hip_scene *sc, uint8_t *out) {
+    if (!sc) return set_error(CRT_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(sc->device));
+    const int rc = ensure_live_mask(sc);
+    if (rc != CRT_OK) return rc;
+    if (out && !sc->live_mask.empty()) std::memcpy(out, sc->live_mask.data(), sc->live_mask.size());
+    else if (out) std::memset(out, 0, (size_t)sc->info.width * sc->info.height);
+    return CRT_OK;
+}
+
+int64_t crt_hip_compact_floats(crt_hip_scene *sc, int shard, int shard_count) {
+    if (!sc || shard_count <= 0 || shard < 0 || shard >= shard_count) return set_error(CRT_E_INVALID, "bad shard");
+    HIP_TRY(hipSetDevice(sc->device));
+    const int rc = ensure_live_mask(sc);
+    if (rc != CRT_OK) return rc;
+    int64_t px = 0;
+    compact_tiles(sc, shard, shard_count, &px);
+    return 3 * px;
+}
+
+int64_t crt_hip_compact_stride(crt_hip_scene *sc, int shard_count) {
+    if (!sc || shard_count <= 0) return set_error(CRT_E_INVALID, "bad shard count");
+    int64_t m = 0;
+    for (int s = 0; s < shard_count; ++s) {
+        const int64_t f = crt_hip_compact_floats(sc, s, shard_count);
+        if (f < 0) return f;
+        m = std::max(m, f);
+    }
+    return std::max<int64_t>(64, (m + 63) / 64 * 64);
+}
+
+int crt_hip_render_shard_compact(crt_hip_scene *sc, const crt_renderer_settings *st, int shard, int shard_count,
+                                 float *d_packed, void *stream) {
+    return render_shard_t(sc, st, shard, shard_count, d_packed, stream, true);
+}
+
+int crt_hip_unpack_compact(crt_hip_scene *sc, int shard_count, const float *d_gathered, float *d_rgb, void *stream) {
+    return unpack_shards_t<float>(sc, shard_count, d_gathered, d_rgb, stream, true);
+}
+
+int crt_hip_unpack_compact_rgb8(crt_hip_scene *sc, int shard_count, const uint8_t *d_gathered, uint8_t *d_rgb8,
+                                void *stream) {
+    return unpack_shards_t<uint8_t>(sc, shard_count, d_gathered, d_rgb8, stream, true);
+}
+
+int crt_hip_quantize_rgb8(const float *d_rgb, int64_t n, int32_t max_color_component, uint8_t *d_out, void *stream) {
+    if ((n > 0 && (!d_rgb || !d_out)) || n < 0) return set_error(CRT_E_INVALID, "bad argument");
+    if (max_color_component < 0 || max_color_component > 255)
+        return set_error(CRT_E_UNSUPPORTED, "8-bit output needs max_color_component in 0..255");
+    if (n == 0) return CRT_OK;
+    const int64_t threads = (n + 3) / 4;
+    hipLaunchKernelGGL(k_quantize, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), d_rgb, d_out, n, (float)max_color_component,
+                       max_color_component);
+    HIP_TRY(hipGetLastError());
+    return CRT_OK;
+}
+
+int crt_hip_trace_batch(crt_hip_scene *sc, const float *rays, int64_t n, crt_hit *hits_out) {
+    if (!sc || (n > 0 && (!rays || !hits_out)) || n < 0) return set_error(CRT_E_INVALID, "bad argument");
+    if (n == 0) return CRT_OK;
+    HIP_TRY(hipSetDevice(sc->device));
+    float *d_rays = nullptr;
+    crt_hit *d_hits = nullptr;
+    HIP_TRY(hipMalloc(&d_rays, (size_t)n * 6 * sizeof(float)));
+    hipError_t e = hipMalloc(&d_hits, (size_t)n * sizeof(crt_hit));
+    if (e != hipSuccess) { (void)hipFree(d_rays); return set_error(CRT_E_HIP, hipGetErrorString(e)); }
+    e = hipMemcpy(d_rays, rays, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_trace_rays, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, sc->stream, sc->ds, d_rays,
+                           n, d_hits, sc->trace_walk);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(sc->stream);
+    if (e == hipSuccess) e = hipMemcpy(hits_out, d_hits, (size_t)n * sizeof(crt_hit), hipMemcpyDeviceToHost);
+    (void)hipFree(d_rays);
+    (void)hipFree(d_hits);
+    if (e != hipSuccess) return set_error(CRT_E_HIP, hipGetErrorString(e));
+    return CRT_OK;
+}
+
+int crt_hip_profile_waves(crt_hip_scene *sc, const crt_renderer_settings *st, uint64_t *stamps, int64_t cap,
+                          int32_t *tile_xy) {
+    if (!sc || !st) return set_error(CRT_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(sc->device));
+    {
+        const int rc = ensure_plans(sc, st, sc->stream);
+        if (rc != CRT_OK) return rc;
+    }
+    const int nt = sc->full.ntiles;
+    if (!stamps || !tile_xy) return nt;      /* query the size */
+    if (cap < nt) return set_error(CRT_E_INVALID, "stamp buffer too small");
+    const size_t nfl = (size_t)sc->info.width * sc->info.height * 3;
+    if (!sc->d_out) HIP_TRY(hipMalloc(&sc->d_out, nfl * sizeof(float)));
+    unsigned long long *d = nullptr;
+    HIP_TRY(hipMalloc(&d, (size_t)nt * 2 * sizeof(unsigned long long)));
+    int rc = launch_render(sc, st, sc->full, sc->d_out, sc->stream, false, d);
+    hipError_t e = rc == CRT_OK ? hipStreamSynchronize(sc->stream) : hipSuccess;
+    if (rc == CRT_OK && e == hipSuccess)
+        e = hipMemcpy(stamps, d, (size_t)nt * 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    std::vector<Tile> tiles(nt);
+    if (rc == CRT_OK && e == hipSuccess)
+        e = hipMemcpy(tiles.data(), sc->full.d_tiles, (size_t)nt * sizeof(Tile), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (rc != CRT_OK) return rc;
+    if (e != hipSuccess) return set_error(CRT_E_HIP, hipGetErrorString(e));
+    for (int k = 0; k < nt; ++k) { tile_xy[2 * k] = tiles[k].x; tile_xy[2 * k + 1] = tiles[k].y; }
+    return nt;
+}
+
+int crt_hip_plan_tiles(crt_hip_scene *sc, const crt_renderer_settings *st, int32_t *xywh, float *cost, int64_t cap) {
+    if (!sc || !st) return set_error(CRT_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(sc->device));
+    const int rc = ensure_plans(sc, st, sc->stream);
+    if (rc != CRT_OK) return rc;
+    const ShardPlan &p = sc->full;
+    if (!xywh) return p.ntiles;
+    if (cap < p.ntiles) return set_error(CRT_E_INVALID, "tile buffer too small");
+    for (int k = 0; k < p.ntiles; ++k) {
+        xywh[4 * k] = p.tiles[k].x;
+        xywh[4 * k + 1] = p.tiles[k].y;
+        xywh[4 * k + 2] = p.tiles[k].w;
+        xywh[4 * k + 3] = p.tiles[k].h;
+        if (cost) cost[k] = p.cost.empty() ? 0.f : p.cost[k];
+    }
+    return p.ntiles;
+}
+
+int crt_hip_count_work(crt_hip_scene *sc, const crt_renderer_settings *st, crt_work_counts *out) {
+    if (!sc || !out) return set_error(CRT_E_INVALID, "null argument");
+    int rc = check_settings(st);
+    if (rc != CRT_OK) return rc;
+    HIP_TRY(hipSetDevice(sc->device));
+    std::memset(out, 0, sizeof *out);
+    if (sc->grid_empty) return CRT_OK;
+    const size_t nfl = (size_t)sc->info.width * sc->info.height * 3;
+    if (!sc->d_out) HIP_TRY(hipMalloc(&sc->d_out, nfl * sizeof(float)));
+    if ((rc = ensure_plans(sc, st, sc->stream)) != CRT_OK) return rc;
+    HIP_TRY(hipMemsetAsync(sc->d_counters, 0, 16 * sizeof(unsigned long long), sc->stream));
+    rc = launch_render(sc, st, sc->full, sc->d_out, sc->stream, true);
+    if (rc != CRT_OK) return rc;
+    unsigned long long c[16];
+    HIP_TRY(hipMemcpyAsync(c, sc->d_counters, sizeof c, hipMemcpyDeviceToHost, sc->stream));
+    HIP_TRY(hipStreamSynchronize(sc->stream));
+    out->traversals = c[0];
+    out->node_tests = c[1];
+    out->triangle_tests = c[2];
+    out->hits = c[3];
+    sc->wave_counts.node_steps = c[4];
+    sc->wave_counts.triangle_steps = c[5];
+    sc->wave_counts.edge_steps = c[6];
+    sc->wave_counts.waves = c[7];
+    sc->wave_counts.box_steps = c[8];
+    sc->wave_counts.pass_steps = c[9];
+    sc->wave_counts.window_waves = c[10];
+    sc->wave_counts.window_steps = c[11];
+    sc->wave_counts.window_slots = c[12];
+    sc->wave_counts.window_reached = c[13];
+    sc->wave_counts.window_tri_rounds = c[14];
+    return CRT_OK;
+}
+
+int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
+    if (!sc || !name) return set_error(CRT_E_INVALID, "null argument");
+    const std::string k(name);
+    if (k == "traversal") {
+        if (value != 7 && value != 8) return set_error(CRT_E_INVALID, "traversal must be 7 (reference order) or 8 (pruned)");
+        sc->traversal = value;
+        wf_graphs_clear(sc->wf);   /* captured wavefront frames bake in the level-0 walk */
+    } else if (k == "secondary") {
+        if (value != 0 && value != 4 && value != 10 && value != 14)
+            return set_error(CRT_E_INVALID, "secondary must be 0, 4, 10 or 14");
+        sc->secondary = value;
+        wf_graphs_clear(sc->wf);   /* ... the levels' walk */
+    } else if (k == "wavefront") {
+        sc->wavefront = value != 0;
+    } else if (k == "window") {
+        sc->window_walk = value != 0;
+    } else if (k == "gi_refill") {
+        sc->gi_refill = value != 0;
+    } else if (k == "gi_machine") {
+        sc->gi_machine = value != 0;
+    } else if (k == "calib_k_milli") {   /* a fixed split threshold k = value / 1000 (calibrate 2) */
+        if (value <= 0) return set_error(CRT_E_INVALID, "calib_k_milli must be > 0");
+        sc->calib_k = (float)value / 1000.0f;
+        sc->calibrate = 2;
+        sc->calib_walk = -1;
+    } else if (k == "wf_graph") {
+        sc->wf_graph = value != 0;
+        wf_graphs_clear(sc->wf);
+    } else if (k == "wf_replay") {
+        if (value < 0 || value > 2) return set_error(CRT_E_INVALID, "wf_replay must be 0, 1 or 2");
+        sc->wf_replay = value;
+        sc->wf.recs.clear();
+        wf_graphs_clear(sc->wf);
+    } else if (k == "wf_rpw") {
+        if (value < 1 || value > 64) return set_error(CRT_E_INVALID, "wf_rpw must be 1..64");
+        sc->wf_rays_per_wave = value;
+        wf_graphs_clear(sc->wf);   /* ... and each level's rays per wave */
+    } else if (k == "events") {
+        sc->record_events = value != 0;
+    } else if (k == "calibrate") {
+        if (value < 0 || value > 2) return set_error(CRT_E_INVALID, "calibrate must be 0 (estimate plan), 1 (tuned) or 2 (fixed k)");
+        if (value != sc->calibrate) sc->calib_walk = sc->calibrate ? -1 : sc->calib_walk;   /* re-plan on next use */
+        sc->calibrate = value;
+        if (!sc->calibrate && !sc->calib.empty()) {   /* back to the estimate plan */
+            HIP_TRY(hipDeviceSynchronize());
+            sc->calib.clear();
+            sc->calib_walk = -1;
+            free_plans(sc);
+            int64_t px = 0;
+            const int rc = make_tile_plan(sc, shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size, 0, 1, &px),
+                                          true, sc->full);
+            if (rc != CRT_OK) return rc;
+        }
+    } else if (k == "calib_min") {   /* smallest side the calibrated plan splits tiles down to */
+        if (value != 1 && value != 2 && value != 4 && value != 8) return set_error(CRT_E_INVALID, "calib_min must be 1, 2, 4 or 8");
+        sc->calib_min = value;
+        sc->calib_walk = -1;
+    } else if (k == "shadows") {
+        sc->shadows = value != 0;
+    } else if (k == "trace_walk") {
+        if (value < 0 || value > 2) return set_error(CRT_E_INVALID, "trace_walk must be 0, 1 or 2 (BVH)");
+        sc->trace_walk = value;
+    } else {
+        return set_error(CRT_E_INVALID, "unknown option: " + k);
+    }
+    /* tile plans depend on the walk (tile splitting): rebuild on next use */
+    return CRT_OK;
+}
+
+int crt_hip_wave_counts(crt_hip_scene *sc, crt_wave_counts *out) {
+    if (!sc || !out) return set_error(CRT_E_INVALID, "null argument");
+    *out = sc->wave_counts;
+    return CRT_OK;
+}
+
+}  // extern "C"
+

@@ -1,7 +1,6 @@
 /*
  * crt_gi_machine.h — GI frames (15-01/scene2, C4) as a per-lane state machine
- * (included by crt_render.hip after the shading helpers; instantiated in the
- * GI translation unit, crt_render_gi.hip).
+ * (compiled in crt_render_gi.hip; declared in crt_kernels.h).
  *
  * What it computes: render_region + shade_ray (crt_renderer.cpp:46-155) for
  * every pixel of a tile list, each pixel's rays in the reference's
@@ -34,6 +33,7 @@
  * that happen to sit on a leaf in each round.
  */
 #pragma once
+#include "crt_shade.h"
 
 namespace crt_amd {
 
@@ -447,15 +447,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRT_GIM_WAV
     }
 }
 
-#define CRT_GIM_INSTANCES(X) X(false) X(true)
-#define CRT_GIM_SIG(C) void k_render_gi<C>(const DeviceScene *__restrict__, DSettings, const Tile *__restrict__, int, \
-    float *__restrict__, int32_t *__restrict__, unsigned long long *__restrict__, float4 *__restrict__);
-#ifdef CRT_GI_TU
-#define CRT_GIM_INST(C) template __global__ CRT_GIM_SIG(C)
-CRT_GIM_INSTANCES(CRT_GIM_INST)
-#elif !defined(CRT_SIDE_TU)
-#define CRT_GIM_EXTERN(C) extern template __global__ CRT_GIM_SIG(C)
-CRT_GIM_INSTANCES(CRT_GIM_EXTERN)
-#endif
+
 
 }  // namespace crt_amd

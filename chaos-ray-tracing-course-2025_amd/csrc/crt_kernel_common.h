@@ -1,0 +1,88 @@
+/*
+ * crt_kernel_common.h — records and small device helpers shared by the render
+ * kernels (crt_render*.hip) and the host layer (crt_host_render.hip).
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "crt_bvh.h"
+#include "crt_device.h"
+#include "crt_host.h"
+
+namespace crt_amd {
+
+constexpr float kPi = 3.14159265358979323846f;   /* std::numbers::pi_v<float> */
+
+struct alignas(16) Tile {
+    int32_t x, y, w, h;        /* pixel rectangle, w,h <= 8 */
+    int64_t out_base;          /* output pixel index of (x, y) */
+    int32_t out_stride;        /* output pixels per row */
+    int32_t prio;              /* 1: one of the frame's heaviest waves — raised issue priority */
+};
+
+struct alignas(16) UnpackBucket {
+    int32_t x, y, w, h;
+    int64_t src;               /* float offset of the bucket inside the gathered buffer */
+    int64_t pad;
+};
+
+enum FrameKind : int32_t { kDiffuseGI = 0, kReflect = 1, kRefractA = 2, kRefractB = 3 };
+
+/* A pending shade_ray activation (crt_renderer.cpp:46-145) waiting for a child. */
+struct Frame {
+    int32_t kind, depth, i, has_refr;
+    Vec acc;    /* diffuse: GI sum | reflect: albedo | refract: reflection colour */
+    Vec p, n;   /* diffuse: hit point and shading normal                         */
+    Vec a, b;   /* diffuse: right, forward basis | refract: refraction ray o, d   */
+    Vec alb;    /* diffuse: albedo sample | refract: .x = fresnel                */
+};
+
+/* global (address space 1) load: a global_load instead of a flat one, whose
+ * completion is tracked by vmcnt alone (flat loads also count in lgkmcnt, so
+ * every wait on them drains the LDS queue too) */
+template <class T>
+__device__ __forceinline__ T load_global(const T *p, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    using GT = const __attribute__((address_space(1))) T;
+    return ((GT *)p)[i];
+#else
+    return p[i];
+#endif
+}
+
+
+struct LaneCounts {
+    uint32_t traversals, nodes, tris, hits;
+    /* wave-uniform steps of the packet walks (kept by every lane, added once per wave) */
+    uint32_t wave_nodes, wave_tris, wave_edges;
+    uint32_t wave_box, wave_pass;   /* packet walks: node steps with a box test run / with a lane passing */
+    uint32_t win_steps, win_slots, win_reached, win_rounds;   /* window walk (crt_wave_counts) */
+};
+
+__device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+/* Scene records are read-only for the whole launch: reading them through the
+ * constant address space lets a wave-uniform index become an s_load into SGPRs. */
+template <class T>
+__device__ __forceinline__ T load_scalar(const T *p, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    using CT = const __attribute__((address_space(4))) T;
+    return ((CT *)p)[i];
+#else
+    return p[i];
+#endif
+}
+
+/* Same, at a 32-bit byte offset from a wave-uniform base (SMEM base + offset
+ * addressing: no 64-bit address arithmetic per load). */
+template <class T>
+__device__ __forceinline__ T load_scalar_at(const char *base, uint32_t byte_off) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    using CT = const __attribute__((address_space(4))) T;
+    return *(CT *)((const __attribute__((address_space(4))) char *)base + byte_off);
+#else
+    return *(const T *)(base + byte_off);
+#endif
+}
+
+}  // namespace crt_amd

@@ -1,5 +1,202 @@
-/* Wavefront level kernels >= 1 (k_wf_level<SEC, false, *>) in a translation unit
- * of their own, built with their own LLVM scheduling strategy (see crt_render.hip). */
-#define CRT_SIDE_TU 1
-#define CRT_WF_TU 1
-#include "crt_render.hip"
+/*
+ * crt_render_wf.hip — the wavefront path (C3: reflection / refraction
+ * recursion without GI, crt_renderer.cpp:103-135): one kernel per recursion
+ * level, then the deepest-first composition and the pixels.  Host
+ * orchestration: crt_host_render.hip render_wavefront.  Built with its own
+ * LLVM scheduling strategy (Makefile WF_SCHED).
+ */
+#define CRT_KERNEL_TU 1
+#include "crt_kernels.h"
+#include "crt_shade.h"
+
+namespace crt_amd {
+
+template <int TRAV, bool LEVEL0, bool COUNT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CRT_WF0_WAVES : CRT_WF_WAVES))) void k_wf_level(const DeviceScene *__restrict__ scene, DSettings st,
+                                                  const Tile *__restrict__ tiles, int ntiles, WLevel lv,
+                                                  unsigned long long *__restrict__ counters) {
+    const DeviceScene &s = *scene;
+    const int gid = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int lane = (int)(threadIdx.x & 63);
+    bool has;
+    Vec o = vec(0.f, 0.f, 0.f), d = vec(0.f, 0.f, 1.f);
+    int id = gid, depth = 0;
+    if (LEVEL0) {
+        const int wave = gid >> 6;
+        if (wave >= ntiles) return;
+        const Tile tl = tiles[wave];
+        if (tl.prio) __builtin_amdgcn_s_setprio(3);
+        const int lx = lane & 7, ly = lane >> 3;
+        has = lx < tl.w && ly < tl.h;
+        if (has) camera_ray(s, tl.x + lx, tl.y + ly, o, d);
+    } else {
+        const int ray0 = (gid >> 6) * lv.rpw;
+        if (ray0 >= lv.n) return;          /* whole wave past the queue */
+        const int ray = ray0 + lane;
+        has = lane < lv.rpw && ray < lv.n;
+        if (has) {
+            const WRay r = lv.in[ray];
+            o = vec(r.ox, r.oy, r.oz);
+            d = vec(r.dx, r.dy, r.dz);
+            id = r.id;
+            depth = r.depth;
+        }
+    }
+    LaneCounts cnt = {};
+    constexpr bool kCoop = kIsCoop<TRAV>;
+    __shared__ CoopLds coop[kCoop ? 4 : 1];
+    float t;
+    const int slot = trace<TRAV, COUNT>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has, o, d, t, cnt);
+
+    WNode node = {wFinal, -1, -1, 0, 0.f, 0.f, 0.f, 0.f};
+    Vec col = vec(0.f, 0.f, 0.f);
+    int nch = 0;
+    Vec co[2], cd[2];
+    if (has) {
+        if (slot < 0) {
+            col = vec(s.background[0], s.background[1], s.background[2]);
+        } else {
+            HitRec h;
+            make_hit(s, o, d, t, slot, h);
+            const DMaterial m = s.materials[h.mat];
+            if (m.type == CRT_MATERIAL_DIFFUSE) {
+                const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+                col = diffuse_finish(s, st, vec(0.f, 0.f, 0.f), h.p, h.n, alb);
+            } else if (m.type == CRT_MATERIAL_REFLECTIVE) {                 /* :103-107 */
+                const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+                if (s.reflections_on) {
+                    node.kind = wReflect;
+                    node.a0 = alb.x; node.a1 = alb.y; node.a2 = alb.z;
+                    co[0] = vadd(h.p, vscale(h.n, st.reflection_bias));
+                    cd[0] = vsub(d, vscale(vscale(h.n, 2.0f), vdot(d, h.n)));
+                    nch = 1;
+                } else {
+                    col = alb;
+                }
+            } else if (m.type == CRT_MATERIAL_REFRACTIVE) {                 /* :109-135 */
+                if (s.refractions_on) {
+                    Vec n = h.n;
+                    float n_out = 1.0f, n_in = m.ior;
+                    if (vdot(d, n) > 0.0f) {
+                        n = vneg(n);
+                        const float tmp = n_in; n_in = n_out; n_out = tmp;
+                    }
+                    bool has_refr = false;
+                    Vec rd = d;
+                    {   /* Vector::refract (crt_vector.cpp:11-27) */
+                        const float ca = -vdot(rd, n);
+                        const float sa = sqrtf(1.0f - ca * ca);
+                        if (!(sa > n_in / n_out)) {
+                            const float sb = sa * n_out / n_in;
+                            const float cb = sqrtf(1.0f - sb * sb);
+                            rd = vadd(rd, vscale(n, ca));
+                            rd = vnormalize(rd);
+                            rd = vscale(rd, sb);
+                            rd = vadd(rd, vscale(vneg(n), cb));
+                            has_refr = true;
+                        }
+                    }
+                    node.kind = has_refr ? wRefract2 : wRefract1;
+                    node.a0 = fresnel_of(s, vdot(d, n));
+                    co[0] = vadd(h.p, vscale(n, st.reflection_bias));
+                    cd[0] = vsub(d, vscale(vscale(n, 2.0f), vdot(d, n)));
+                    co[1] = vadd(h.p, vscale(vneg(n), 1e-2f));   /* refract_at's default bias (crt_ray.h:30-50) */
+                    cd[1] = rd;
+                    nch = has_refr ? 2 : 1;
+                }
+            } else {                                                         /* Constant :137-139 */
+                col = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+            }
+        }
+    }
+    /* children deeper than max_ray_depth are black without a trace: not queued */
+    if ((uint32_t)depth + 1u > st.max_ray_depth) nch = 0;
+    const unsigned long long b1 = __ballot(nch >= 1), b2 = __ballot(nch >= 2);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const int total = __popcll(b1) + __popcll(b2);
+    if (total > 0) {
+        int base = 0;
+        if (lane == __ffsll((long long)(b1 | b2)) - 1) {
+            base = atomicAdd(lv.out_count, total);
+            if (base + total > lv.out_cap) atomicOr(lv.overflow, 1);
+        }
+        base = __shfl(base, __ffsll((long long)(b1 | b2)) - 1);
+        if (base + total > lv.out_cap) nch = 0;   /* never past the queue (the frame is then reported, not used) */
+        /* a lane's children side by side */
+        const int k0 = base + __popcll(b1 & lt) + __popcll(b2 & lt);
+        const int k1 = k0 + 1;
+        for (int c = 0; c < nch; ++c) {
+            const int k = c == 0 ? k0 : k1;
+            WRay r;
+            r.ox = co[c].x; r.oy = co[c].y; r.oz = co[c].z;
+            r.dx = cd[c].x; r.dy = cd[c].y; r.dz = cd[c].z;
+            r.id = lv.out_base + k;
+            r.depth = depth + 1;
+            lv.out[k] = r;
+            if (c == 0) node.c0 = r.id; else node.c1 = r.id;
+        }
+    }
+    if (has) {
+        lv.nodes[id] = node;
+        if (node.kind == wFinal) lv.cols[id] = DVec4{col.x, col.y, col.z, 0.f};
+    }
+    if (COUNT) {
+        atomicAdd(&counters[0], (unsigned long long)cnt.traversals);
+        atomicAdd(&counters[1], (unsigned long long)cnt.nodes);
+        atomicAdd(&counters[2], (unsigned long long)cnt.tris);
+        atomicAdd(&counters[3], (unsigned long long)cnt.hits);
+        /* levels >= 1 (coop walks): loop rounds per wave — sum, longest wave, waves */
+        if (!LEVEL0 && kCoop && lane == 0) {
+            atomicAdd(&counters[4], (unsigned long long)cnt.wave_nodes);
+            atomicMax(&counters[6], (unsigned long long)cnt.wave_nodes);
+            atomicAdd(&counters[7], 1ull);
+        }
+    }
+}
+
+__device__ __forceinline__ Vec wf_compose(const WNode &nd, const DVec4 *__restrict__ cols, Vec own) {
+    if (nd.kind == wFinal) return own;
+    const Vec black = vec(0.f, 0.f, 0.f);
+    const Vec c0 = nd.c0 >= 0 ? vec(cols[nd.c0].x, cols[nd.c0].y, cols[nd.c0].z) : black;
+    if (nd.kind == wReflect) return vmul_quirk(vec(nd.a0, nd.a1, nd.a2), c0);
+    if (nd.kind == wRefract1) return c0;   /* total internal reflection */
+    const Vec c1 = nd.c1 >= 0 ? vec(cols[nd.c1].x, cols[nd.c1].y, cols[nd.c1].z) : black;
+    const float fr = nd.a0;
+    return vadd(vscale(c0, fr), vscale(c1, 1.0f - fr));
+}
+
+/* levels >= 1, deepest first: colour of every activation of the level */
+__global__ __launch_bounds__(256) void k_wf_compose(const WNode *__restrict__ nodes, DVec4 *__restrict__ cols,
+                                                    int32_t begin, int32_t n) {
+    const int k = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (k >= n) return;
+    const int id = begin + k;
+    const WNode nd = nodes[id];
+    if (nd.kind == wFinal) return;
+    const Vec c = wf_compose(nd, cols, vec(0.f, 0.f, 0.f));
+    cols[id] = DVec4{c.x, c.y, c.z, 0.f};
+}
+
+/* level 0: compose the camera rays and write the pixels */
+__global__ __launch_bounds__(256) void k_wf_pixels(const WNode *__restrict__ nodes, const DVec4 *__restrict__ cols,
+                                                   const Tile *__restrict__ tiles, int ntiles,
+                                                   float *__restrict__ out) {
+    const int gid = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int wave = gid >> 6, lane = gid & 63;
+    if (wave >= ntiles) return;
+    const Tile tl = tiles[wave];
+    const int lx = lane & 7, ly = lane >> 3;
+    if (!(lx < tl.w && ly < tl.h)) return;
+    const WNode nd = nodes[gid];
+    const Vec own = vec(cols[gid].x, cols[gid].y, cols[gid].z);
+    const Vec c = wf_compose(nd, cols, own);
+    float *px = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
+    px[0] = c.x;
+    px[1] = c.y;
+    px[2] = c.z;
+}
+
+#define CRT_INST_WF(T, L0, C) template __global__ CRT_WF_SIG(T, L0, C)
+CRT_WF_INSTANCES(CRT_INST_WF)
+
+}  // namespace crt_amd

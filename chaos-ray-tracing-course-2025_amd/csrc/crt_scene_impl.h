@@ -1,0 +1,196 @@
+/*
+ * crt_scene_impl.h — the device scene behind the C-ABI handle (crt_hip_scene)
+ * and the host layer's internal interface, shared by crt_host_render.hip
+ * (plans, tables, launches, wavefront orchestration, shards) and crt_api.hip
+ * (the extern "C" entry points of include/crt_hip.h).
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "crt_host.h"
+#include "crt_kernels.h"
+
+#define HIP_TRY(expr)                                                                            \
+    do {                                                                                         \
+        const hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                                    \
+            return set_error(CRT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));      \
+    } while (0)
+
+namespace crt_amd {
+
+struct ShardPlan {
+    Tile *d_tiles = nullptr;
+    int ntiles = 0;
+    int64_t packed_pixels = 0;
+    std::vector<Tile> tiles;     /* host copy, dispatch order */
+    std::vector<float> cost;     /* measured cost per tile (calibrated plans), else empty */
+    bool has_small = false;      /* some tile has <= 16 pixels (walk 13 runs them with the window walk) */
+};
+
+}  // namespace crt_amd
+
+using namespace crt_amd;
+
+
+/* Device buffers of the wavefront path, grown on demand (kept across frames). */
+struct WfBuffers {
+    crt_amd::WNode *nodes = nullptr;
+    crt_amd::DVec4 *cols = nullptr;
+    int64_t cap = 0;             /* ray ids */
+    crt_amd::WRay *q[2] = {nullptr, nullptr};
+    int64_t qcap[2] = {0, 0};
+    int32_t *counts = nullptr;   /* children queued per level; counts[count_cap - 1]: overflow flag */
+    int count_cap = 0;
+    /* Level sizes of the last frame traced with host read-backs, and what they
+     * depend on (settings, tile list): a frame's level sizes are a function of
+     * its rays alone, so later frames with the same key launch every level
+     * with these sizes and no host sync (render_wavefront). */
+    struct Rec {
+        std::vector<int32_t> sizes;   /* rays of levels 1, 2, ... */
+        crt_renderer_settings st{};
+        int ntiles = 0;
+    };
+    std::map<const void *, Rec> recs;   /* by tile list (device pointer; cleared when plans are freed) */
+    /* overflow flag of recorded-size frames: device word, copied into pinned
+     * host memory behind each such frame and read once that copy is done */
+    int32_t *d_flag = nullptr;
+    int32_t *h_flag = nullptr;
+    hipEvent_t flag_ev = nullptr;
+    bool flag_pending = false;
+    /* recorded-size frames captured as HIP graphs, by everything their
+     * launches bake in (cleared whenever a buffer, tile list or record changes) */
+    struct Graph {
+        const void *tiles;
+        crt_renderer_settings st;
+        const float *out;
+        hipStream_t stream;
+        const void *scene;
+        hipGraphExec_t exec;
+    };
+    std::vector<Graph> graphs;
+};
+
+/* Deepest recursion the wavefront path accepts (levels are launched one by one). */
+constexpr int kWfMaxDepth = 4096;
+
+struct crt_hip_scene {
+    int device = 0;
+    crt_scene_info info{};
+    bool has_secondary = false;    /* any reflective / refractive material */
+    bool has_diffuse = false;
+    bool has_refractive = false;   /* Fresnel term: needs the powf table (fresnel_of) */
+    DeviceScene ds{};
+    DeviceScene ds_uploaded{};   /* what d_ds holds */
+    DeviceScene *d_ds = nullptr;
+    crt_wave_counts wave_counts{};   /* from the last crt_hip_count_work */
+    std::vector<void *> allocs;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    ShardPlan full;
+    std::map<std::pair<int, int>, ShardPlan> shard_plans;
+    std::map<int, std::pair<UnpackBucket *, int>> unpack_plans;
+    /* compact shards (crt_hip_*_compact): live-pixel mask of the frame (host),
+     * per-(shard, count) render plans, per-count unpack lists */
+    std::vector<uint8_t> live_mask;
+    std::map<std::pair<int, int>, ShardPlan> compact_plans;
+    std::map<int, std::pair<UnpackBucket *, int>> compact_unpack;
+    float *d_out = nullptr;
+    unsigned long long *d_counters = nullptr;
+    int32_t *d_next_px = nullptr;      /* pixel-refill list head (k_render_refill) */
+    int gi_refill = 1;                 /* GI frames: persistent waves with pixel refill (env CRT_GI_REFILL, option "gi_refill") */
+    int gi_machine = 1;                /* ... as per-lane state machines (k_render_gi; option "gi_machine") */
+    int gi_blocks = 1024;              /* blocks of the k_render_gi grid (resident blocks per CU x CUs) */
+    void *gi_frames = nullptr;         /* k_render_gi: frames below the LDS ones (grown on demand) */
+    int64_t gi_frames_bytes = 0;
+    int refill_waves = 5120;           /* waves of the refill grid: CUs x 4 SIMDs x CRT_GI_WAVES */
+    bool grid_empty = false;
+    int traversal = 8;             /* 7 reference order | 8 pruned (default), see trace<> (env CRT_TRAVERSAL) */
+    int shadows = 0;               /* option "shadows": trace the shadow rays (k_render_tiles<..., SHADOW>) */
+    int trace_walk = 1;            /* crt_hip_trace_batch: 0 reference-order walk, 1 pruned per-lane walk */
+    bool camera_fast = false;      /* every camera ray takes the fast box path (camera_rays_fast) */
+    /* estimate plan (no calibration): a tile is split into 4x4 (2x2) pixel
+     * waves when its work estimate exceeds split4 (split16) times the mean work
+     * per resident wave slot, i.e. when it would run for several times the
+     * ideal makespan */
+    float split4 = 4.5f, split16 = 9.0f;
+    int wave_slots = 6144;   /* CUs x 4 SIMDs x 6 resident render waves */
+    int secondary = 0;       /* walk for secondary rays: 0 = by frame, 4, 10 (env CRT_SECONDARY) */
+    std::vector<float> tile_work;  /* per 8x8 tile of the full frame */
+    /* measured-cost tile plan (calibrate_plan): per 8x8 tile of the full frame,
+     * the sub-tiles it is split into and their probed costs */
+    struct SubTile { int32_t dx, dy, w, h; float cost; };
+    std::vector<std::vector<SubTile>> calib;
+    int calib_walk = -1;           /* primary walk the calibration was measured with (-1: none) */
+    int calibrate = 1;             /* 0 estimate plan, 1 measured costs with a tuned k, 2 with calib_k (env CRT_CALIBRATE) */
+    int window_walk = 1;           /* camera walk 12 -> 13 (window walk for split tiles), env CRT_WINDOW */
+    int record_events = 1;         /* start/stop events around every render (crt_hip_last_kernel_ms), option "events" */
+    bool events_valid = false;
+    float calib_k = 4.0f;          /* split a wave whose cost exceeds k x (total cost / wave slots) (env CRT_CALIB_K) */
+    int calib_min = 2;             /* smallest sub-tile side */
+    int prio_tiles = 1024;         /* heaviest tiles run at raised issue priority */
+    float prio_min = 2.0f;         /* ... if they cost more than this x the mean per wave slot */
+    std::vector<void *> plan_allocs;   /* tile lists of the current plans */
+    /* the tree in the reference's numbering (crt_hip_scene_tree): host copies
+     * for a host-built tree, device arrays for a device-built one */
+    std::vector<float> ref_bounds;
+    std::vector<int32_t> ref_children, ref_leaf_tris;
+    std::vector<int64_t> ref_leaf_off;
+    const float *dt_ref_bounds = nullptr;
+    const int32_t *dt_ref_children = nullptr, *dt_ref_leaf_tris = nullptr;
+    const int64_t *dt_ref_leaf_off = nullptr;
+    int wavefront = 1;             /* level-by-level recursion when GI is off (env CRT_WAVEFRONT) */
+    int wf_graph = 1;              /* recorded-size wavefront frames replayed from captured HIP graphs (option "wf_graph") */
+    int wf_replay = 1;             /* wavefront frames after the first: 1 recorded level sizes, 0 read back every level,
+                                    * 2 recorded sizes minus one (tests: forces the overflow path) (option "wf_replay") */
+    int wf_rays_per_wave = 48;     /* cap on the rays per wave of wavefront levels >= 1 (each level takes
+                                    * min(cap, max(8, n / 4096)), render_wavefront), coop walks (env CRT_WF_RPW,
+                                    * option "wf_rpw"); fixed 48 / 32 / 16 / 64: 3.55 / 3.64 / 3.62 / 3.68 ms */
+    WfBuffers wf;
+};
+
+namespace crt_amd {
+
+void wf_graphs_clear(WfBuffers &w);
+void wf_free(WfBuffers &w);
+bool wf_overflowed(WfBuffers &w, bool wait);
+int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool full_frame, ShardPlan &plan);
+void free_plans(crt_hip_scene *sc);
+int sync_device_record(crt_hip_scene *sc, const DeviceScene **out);
+int check_settings(const crt_renderer_settings *st);
+int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t stream);
+int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const ShardPlan &plan, float *d_out,
+                  hipStream_t stream, bool count, unsigned long long *stamps = nullptr);
+int render_into(crt_hip_scene *sc, const crt_renderer_settings *st, float *d_rgb, hipStream_t stream, bool count);
+bool camera_rays_fast(const HostScene &hs, bool planes_ok);
+int ensure_live_mask(crt_hip_scene *sc);
+std::vector<DBucket> compact_tiles(crt_hip_scene *sc, int shard, int shard_count, int64_t *px,
+                                   std::vector<DBucket> *dead = nullptr);
+int render_shard_t(crt_hip_scene *sc, const crt_renderer_settings *st, int shard, int shard_count, float *d_packed,
+                   void *stream, bool compact);
+template <class T>
+int unpack_shards_t(crt_hip_scene *sc, int shard_count, const T *d_gathered, T *d_rgb, void *stream, bool compact);
+int scene_upload_buffers(crt_hip_scene *sc, const HostScene &hs);
+
+template <class T>
+int upload(crt_hip_scene *sc, const std::vector<T> &v, const T **dst, size_t pad = 0) {
+    /* pad: zeroed records after the data, so grouped reads past a run's end stay in bounds */
+    *dst = nullptr;
+    if (v.empty() && pad == 0) return CRT_OK;
+    void *p = nullptr;
+    const size_t bytes = (v.size() + pad) * sizeof(T);
+    HIP_TRY(hipMalloc(&p, bytes));
+    sc->allocs.push_back(p);
+    if (pad) HIP_TRY(hipMemset(static_cast<char *>(p) + v.size() * sizeof(T), 0, pad * sizeof(T)));
+    if (!v.empty()) HIP_TRY(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    sc->info.device_bytes += (int64_t)bytes;
+    *dst = static_cast<const T *>(p);
+    return CRT_OK;
+}
+
+}  // namespace crt_amd

@@ -1,0 +1,361 @@
+/*
+ * crt_shade.h — shade_ray (crt_renderer.cpp:46-145) pieces of the render
+ * kernels: the winner's record, lights, GI directions, Fresnel, and the
+ * frame-stack recursion of the tile kernels.
+ */
+#pragma once
+#include "crt_walks.h"
+
+namespace crt_amd {
+
+__device__ __forceinline__ void make_hit(const DeviceScene &s, Vec o, Vec d, float t, int slot, HitRec &h,
+                                         int32_t *tri_out = nullptr) {
+    const DTriGeo g = load_global(s.slots, slot);
+    const int32_t tri = load_global(s.slot_tri, slot);
+    const DTriAttr at = load_global(s.tri_attr, tri);
+    const DVec4 zero = {0.f, 0.f, 0.f, 0.f};
+    DVec4 n0 = zero, n1 = zero, n2 = zero;
+    if (at.mat_flags < 0) {
+        n0 = load_global(s.vnormal, at.i0);
+        n1 = load_global(s.vnormal, at.i1);
+        n2 = load_global(s.vnormal, at.i2);
+    }
+    hit_record(o, d, t, g, at, n0, n1, n2, load_global(s.vuv, at.i0), load_global(s.vuv, at.i1),
+               load_global(s.vuv, at.i2), h);
+    if (tri_out) *tri_out = tri;
+}
+
+/* Shadow ray (option "shadows", DeviceScene::shadows).  At HEAD
+ * trace_ray_with_refractions never enters its loop (crt_renderer.cpp:29-44),
+ * so every light is unoccluded.  The course's earlier renderer traced it: its
+ * committed renders 09-02/scene3 and 09-03/scene5 equal, at every pixel, the
+ * image in which a light counts only when the shadow ray's closest hit is
+ * absent or farther than the light (:90-92: distance^2 > |light - p|^2) —
+ * which is also what the loop computes when it runs, since it intersects the
+ * unchanged shadow ray every time (tests/test_shadows.py).  Per-lane pruned
+ * walk (called from divergent shading code), closest hit as the reference. */
+template <bool COUNT>
+__device__ __forceinline__ bool shadow_occluded(const DeviceScene &s, Vec o, Vec d, float r2, LaneCounts &c) {
+    float t;
+    const int best = trace_lane_pruned<COUNT>(s, true, o, d, t, c);
+    return best >= 0 && !(t * t > r2);
+}
+
+/* Diffuse direct term + normalisation (crt_renderer.cpp:81-99).  SHADOW: the
+ * shadow-ray kernels (option "shadows", k_render_tiles<..., true>); their
+ * traversals count in the work counters (c) as the oracle's do. */
+template <bool SHADOW = false, bool COUNT = false>
+__device__ __forceinline__ Vec diffuse_finish(const DeviceScene &s, const DSettings &st, Vec acc, Vec p, Vec n, Vec alb,
+                                              LaneCounts *c = nullptr) {
+    for (int l = 0; l < s.light_count; ++l) {
+        const DLight L = s.lights[l];
+        Vec ld = vsub(vec(L.px, L.py, L.pz), p);
+        const float r2 = vlen_sq(ld);
+        ld = vnormalize(ld);
+        const float dn = vdot(ld, n);
+        const float cos_law = (0.0f < dn) ? dn : 0.0f;          /* std::max(0.0f, dn) */
+        const float area = 4 * kPi * r2;
+        if (SHADOW && shadow_occluded<COUNT>(s, vadd(p, vscale(n, st.shadow_bias)), ld, r2, *c)) continue;
+        acc = vadd(acc, vscale(vdiv(vscale(alb, L.intensity), area), cos_law));
+    }
+    return vdiv(acc, (float)(st.diffuse_reflection_ray_count + 1));
+}
+
+struct alignas(8) F2 { float c, s; };
+
+/* One GI sample direction (crt_renderer.cpp:61-77).  rng.uniform() is
+ * m * 2^-23 with m = next() >> 9, so cosf/sinf of pi*u and 2pi*u are table
+ * lookups computed by the host's libm — bit-identical to the reference. */
+__device__ __forceinline__ void gi_ray(const DeviceScene &s, const DSettings &st, const Frame &f, Pcg32 &rng, Vec &o,
+                                       Vec &d) {
+    const uint32_t m1 = rng.next() >> 9;
+    const F2 cs1 = load_global(reinterpret_cast<const F2 *>(s.gi_pi), (int)m1);
+    Vec dir = vec(cs1.c, cs1.s, 0.0f);
+    const uint32_t m2 = rng.next() >> 9;
+    const F2 cs2 = load_global(reinterpret_cast<const F2 *>(s.gi_2pi), (int)m2);
+    const float c = cs2.c, sn = cs2.s;
+    const float roty[9] = {c, 0.0f, -sn, 0.0f, 1.0f, 0.0f, sn, 0.0f, c};      /* crt_matrix.cpp:14-20 */
+    dir = vec_mat(dir, roty);
+    const float basis[9] = {f.a.x, f.a.y, f.a.z, f.n.x, f.n.y, f.n.z, f.b.x, f.b.y, f.b.z};   /* from_axes */
+    dir = vec_mat(dir, basis);
+    o = vadd(f.p, vscale(f.n, st.diffuse_reflection_bias));
+    d = dir;
+}
+
+/* fresnel = 0.5f * std::pow(1.0f + dot, 5.0f) (crt_renderer.cpp:130), the
+ * host libm's powf bit for bit.  The normal is flipped so that dot <= 0
+ * (:117-121; |dot| <= 2 for any normal of length <= 2), and then
+ * x = fl(1 + dot) is a multiple of 2^-24 in [-1, 1]: for dot in (-0.5, 0]
+ * x rounds into [0.5, 1] where floats are multiples of 2^-24; for dot in
+ * [-2, -0.5] the exact sum 1 + dot is a multiple of ulp(dot) >= 2^-24 below 1
+ * in magnitude, hence representable.  So x * 2^24 is an exact integer and
+ * indexes a table of powf(x, 5) computed by the host's libm (crt_hip_scene:
+ * ensure_pow5_table).  Any other dot (NaN, or a smooth normal longer than 2)
+ * falls back to x^5 in double rounded once. */
+__device__ __forceinline__ float fresnel_of(const DeviceScene &s, float dot) {
+    const float x = 1.0f + dot;
+    if (s.pow5 != nullptr && dot >= -2.0f && dot <= 0.0f) {
+        const int k = (int)(x * 16777216.0f);
+        return 0.5f * load_global(s.pow5, k + 16777216);
+    }
+    const double xd = x;
+    double r = xd * xd;
+    r = r * r;
+    r = r * xd;
+    return 0.5f * (float)r;
+}
+
+/* shade_ray of a camera ray whose closest hit is known, for frames without
+ * recursion (FULL=false: diffuse / constant materials, GI off) — the same
+ * operations as shade_pixel<false>. */
+__device__ __forceinline__ Vec shade_primary(const DeviceScene &s, const DSettings &st, Vec o, Vec d, int slot, float t) {
+    if (slot < 0) return vec(s.background[0], s.background[1], s.background[2]);
+    HitRec h;
+    make_hit(s, o, d, t, slot, h);
+    const DMaterial m = s.materials[h.mat];
+    const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+    if (m.type == CRT_MATERIAL_DIFFUSE) return diffuse_finish(s, st, vec(0.f, 0.f, 0.f), h.p, h.n, alb);
+    return alb;
+}
+
+/* shade_ray for one camera ray (crt_renderer.cpp:46-155).
+ * FULL=false: scenes whose materials are only diffuse/constant with GI off —
+ * no recursion, no frame stack.  FULL=true: GI + reflective + refractive with
+ * a per-lane frame stack of MAXF entries (≥ max_ray_depth + 1, host-checked). */
+/* One pass of shade_pixel's loop: trace the lane's current ray (a wave-wide
+ * walk call), shade the hit, and return colours to the pending activations
+ * until one of them needs another ray.  Returns true when (o, d) holds that
+ * next ray, false when the pixel's colour is in col. */
+template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW = false>
+__device__ __forceinline__ bool shade_pass(const DeviceScene &s, const DSettings &st, LaneCounts &cnt, CoopLds *L,
+                                           bool has_px, Vec &o, Vec &d, uint32_t &depth, Pcg32 &rng, Frame *stack,
+                                           int &sp, Vec &col) {
+    /* Every pass of this loop traces exactly one ray per live lane, so all of a
+     * wave's lanes meet in the same walk call whatever their position in their
+     * own recursion (a miss shifts one lane's DFS against the others).  A call
+     * that shade_ray would answer without tracing (depth > max_ray_depth: black,
+     * crt_renderer.cpp:47-49) is resolved in the return loop below instead of
+     * costing a pass; its GI draws are still taken (gi_ray) in reference order. */
+    /* ---- shade_ray(ray) with depth <= max_ray_depth ---- */
+    bool called = false;
+    {
+        float t;
+        /* the packet walk pays for the union of its lanes' visit sets: it
+         * wins on camera rays (coherent by construction) and loses on the
+         * scattered secondary rays, which take the range-sharing walk */
+        const int slot = (SEC != TRAV && depth != 0) ? trace<SEC, COUNT>(s, L, has_px, o, d, t, cnt)
+                                                     : trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
+        if (slot < 0) {
+            col = vec(s.background[0], s.background[1], s.background[2]);
+        } else {
+            HitRec h;
+            make_hit(s, o, d, t, slot, h);
+            const DMaterial m = s.materials[h.mat];
+            if (m.type == CRT_MATERIAL_DIFFUSE) {
+                const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+                if (FULL && s.gi_on && st.diffuse_reflection_ray_count > 0) {
+                    Frame &f = stack[sp++];
+                    f.kind = kDiffuseGI;
+                    f.depth = (int32_t)depth;
+                    f.i = 0;
+                    f.acc = vec(0.f, 0.f, 0.f);
+                    f.p = h.p;
+                    f.n = h.n;
+                    f.a = vnormalize(vcross(d, h.n));       /* right   */
+                    f.b = vcross(f.a, h.n);                  /* forward */
+                    f.alb = alb;
+                    gi_ray(s, st, f, rng, o, d);
+                    depth = depth + 1;
+                    called = true;
+                } else {
+                    col = diffuse_finish<SHADOW, COUNT>(s, st, vec(0.f, 0.f, 0.f), h.p, h.n, alb, &cnt);
+                }
+            } else if (FULL && m.type == CRT_MATERIAL_REFLECTIVE) {          /* :103-107 */
+                const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+                if (s.reflections_on) {
+                    Frame &f = stack[sp++];
+                    f.kind = kReflect;
+                    f.depth = (int32_t)depth;
+                    f.acc = alb;
+                    o = vadd(h.p, vscale(h.n, st.reflection_bias));
+                    d = vsub(d, vscale(vscale(h.n, 2.0f), vdot(d, h.n)));
+                    depth = depth + 1;
+                    called = true;
+                } else {
+                    col = alb;
+                }
+            } else if (FULL && m.type == CRT_MATERIAL_REFRACTIVE) {          /* :109-135 */
+                if (!s.refractions_on) {
+                    col = vec(0.f, 0.f, 0.f);
+                } else {
+                    Vec n = h.n;
+                    float n_out = 1.0f, n_in = m.ior;
+                    if (vdot(d, n) > 0.0f) {
+                        n = vneg(n);
+                        const float tmp = n_in; n_in = n_out; n_out = tmp;
+                    }
+                    Frame &f = stack[sp++];
+                    f.kind = kRefractA;
+                    f.depth = (int32_t)depth;
+                    f.has_refr = 0;
+                    {   /* Vector::refract (crt_vector.cpp:11-27) */
+                        Vec rd = d;
+                        const float ca = -vdot(rd, n);
+                        const float sa = sqrtf(1.0f - ca * ca);
+                        if (!(sa > n_in / n_out)) {
+                            const float sb = sa * n_out / n_in;
+                            const float cb = sqrtf(1.0f - sb * sb);
+                            rd = vadd(rd, vscale(n, ca));
+                            rd = vnormalize(rd);
+                            rd = vscale(rd, sb);
+                            rd = vadd(rd, vscale(vneg(n), cb));
+                            f.has_refr = 1;
+                        }
+                        /* refracted_at → refract_at with its default 1e-2f bias (crt_ray.h:30-50) */
+                        f.a = vadd(h.p, vscale(vneg(n), 1e-2f));
+                        f.b = rd;
+                    }
+                    f.alb.x = fresnel_of(s, vdot(d, n));
+                    o = vadd(h.p, vscale(n, st.reflection_bias));
+                    d = vsub(d, vscale(vscale(n, 2.0f), vdot(d, n)));
+                    depth = depth + 1;
+                    called = true;
+                }
+            } else {                                                          /* Constant :137-139 */
+                col = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+            }
+        }
+    }
+    if (!FULL) return false;
+    if (called) {
+        if (depth <= st.max_ray_depth) return true;
+        col = vec(0.f, 0.f, 0.f);       /* the child call returns black untraced */
+        called = false;
+    }
+    /* ---- return col to the pending activations ---- */
+    while (sp > 0) {
+        Frame &f = stack[sp - 1];
+        if (f.kind == kDiffuseGI) {
+            f.acc = vadd(f.acc, col);
+            f.i += 1;
+            if ((uint32_t)f.i < st.diffuse_reflection_ray_count) {
+                gi_ray(s, st, f, rng, o, d);
+                depth = (uint32_t)f.depth + 1;
+                if (depth <= st.max_ray_depth) {
+                    called = true;
+                    break;
+                }
+                col = vec(0.f, 0.f, 0.f);
+                continue;
+            }
+            --sp;
+            col = diffuse_finish<SHADOW, COUNT>(s, st, f.acc, f.p, f.n, f.alb, &cnt);
+        } else if (f.kind == kReflect) {
+            --sp;
+            col = vmul_quirk(f.acc, col);
+        } else if (f.kind == kRefractA) {
+            if (f.has_refr) {
+                f.kind = kRefractB;
+                f.acc = col;
+                o = f.a;
+                d = f.b;
+                depth = (uint32_t)f.depth + 1;
+                if (depth <= st.max_ray_depth) {
+                    called = true;
+                    break;
+                }
+                col = vec(0.f, 0.f, 0.f);
+                continue;
+            }
+            --sp;   /* total internal reflection: the reflection colour is the result */
+        } else {
+            --sp;
+            const float fr = f.alb.x;
+            col = vadd(vscale(f.acc, fr), vscale(col, 1.0f - fr));
+        }
+    }
+    return called;
+}
+
+/* Shadow ray of shade_shadowed: true iff its closest hit is within the light
+ * (crt_renderer.cpp:92, distance^2 <= |light - p|^2).  Any hit with
+ * fl(t * t) <= r2 has t <= sqrt(r2) (1 + 2^-24) < lim0, so pruning past lim0
+ * and stopping at the first such hit give the same answer as the closest hit. */
+template <bool COUNT>
+__device__ __forceinline__ bool shadow_occluded_packet(const DeviceScene &s, bool active, Vec o, Vec d, float r2,
+                                                       LaneCounts &c) {
+    const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
+    if (COUNT && active) ++c.traversals;
+    const float lim0 = sqrtf(r2) * (1.0f + 0x1p-20f);
+    float t;
+    const int best = trace_packet_pruned_t<COUNT, false, true>(s, active, o, d, rr, t, c, lim0, r2);
+    return best >= 0 && !(t * t > r2);
+}
+
+/* Camera ray + shading with shadow rays for frames without recursion
+ * (FULL=false, option "shadows"): the same operations as diffuse_finish<true>,
+ * but each light's shadow rays are traced by the whole wave at once with the
+ * pruned packet walk — a tile's shadow rays towards one light are coherent —
+ * instead of one per-lane walk per lane. */
+template <bool COUNT>
+__device__ Vec shade_hit_shadowed(const DeviceScene &s, const DSettings &st, bool has_px, Vec o, Vec d, int slot,
+                                  float t, LaneCounts &cnt) {
+    Vec col = vec(s.background[0], s.background[1], s.background[2]);
+    bool diffuse = false;
+    HitRec h;
+    h.p = vec(0.f, 0.f, 0.f);
+    h.n = vec(0.f, 0.f, 1.f);
+    Vec alb = vec(0.f, 0.f, 0.f);
+    if (has_px && slot >= 0) {
+        make_hit(s, o, d, t, slot, h);
+        const DMaterial m = s.materials[h.mat];
+        alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
+        if (m.type == CRT_MATERIAL_DIFFUSE) diffuse = true;
+        else col = alb;                                               /* Constant :137-139 */
+    }
+    Vec acc = vec(0.f, 0.f, 0.f);
+    const int nl = s.light_count;
+    for (int l = 0; l < nl; ++l) {                                    /* :81-96 */
+        const DLight Lt = s.lights[l];
+        Vec ld = vsub(vec(Lt.px, Lt.py, Lt.pz), h.p);
+        const float r2 = vlen_sq(ld);
+        ld = vnormalize(ld);
+        const float dn = vdot(ld, h.n);
+        const float cos_law = (0.0f < dn) ? dn : 0.0f;
+        const float area = 4 * kPi * r2;
+        bool lit = true;
+        if (__ballot(diffuse) != 0ull)
+            lit = !shadow_occluded_packet<COUNT>(s, diffuse, vadd(h.p, vscale(h.n, st.shadow_bias)), ld, r2, cnt);
+        if (diffuse && lit) acc = vadd(acc, vscale(vdiv(vscale(alb, Lt.intensity), area), cos_law));
+    }
+    if (diffuse) col = vdiv(acc, (float)(st.diffuse_reflection_ray_count + 1));
+    return col;
+}
+
+template <int TRAV, bool COUNT>
+__device__ Vec shade_shadowed(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt, CoopLds *L,
+                              bool has_px) {
+    Vec o, d;
+    camera_ray(s, x, y, o, d);
+    float t;
+    const int slot = trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
+    return shade_hit_shadowed<COUNT>(s, st, has_px, o, d, slot, t, cnt);
+}
+
+template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW = false>
+__device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt, CoopLds *L,
+                           bool has_px) {
+    Vec o, d;
+    camera_ray(s, x, y, o, d);
+    uint32_t depth = 0;
+    Pcg32 rng;
+    if (FULL) rng = make_pcg((uint32_t)x, (uint32_t)y);
+    Frame stack[MAXF > 0 ? MAXF : 1];
+    int sp = 0;
+    Vec col;
+    while (shade_pass<FULL, MAXF, TRAV, SEC, COUNT, SHADOW>(s, st, cnt, L, has_px, o, d, depth, rng, stack, sp, col)) {
+    }
+    return col;
+}
+
+}  // namespace crt_amd

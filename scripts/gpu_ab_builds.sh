@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 OUT=gpurun_out/${TAG:-abbuilds}
 mkdir -p "$OUT"
 for r in 1 2; do
-  timeout -k 10 120 env CRT_PKG=abtest/${BASE:-w1} CRT_WINDOW=0 python3 scripts/render_loop.py --frames 30 > "$OUT/base_c2_$r.json" 2>&1 || exit $?
+  timeout -k 10 120 env CRT_PKG=abtest/${BASE:-w1} python3 scripts/render_loop.py --frames 30 --opt window=0 > "$OUT/base_c2_$r.json" 2>&1 || exit $?
   echo "base c2 $(tail -1 $OUT/base_c2_$r.json | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["kernel"]["default"]["median_ms"])')"
   for b in ${BUILDS:-w1 w4 w5 w6}; do
     timeout -k 10 120 env CRT_PKG=abtest/$b python3 scripts/render_loop.py --frames 30 > "$OUT/${b}_c2_$r.json" 2>&1 || exit $?

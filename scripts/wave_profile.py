@@ -17,8 +17,7 @@ scene = sys.argv[1] if len(sys.argv) > 1 else "14-01-acceleration-tree__scene1"
 variants = sys.argv[2].split(",") if len(sys.argv) > 2 else ["3"]
 out = {}
 for v in variants:
-    os.environ["CRT_TRAVERSAL"] = v
-    g = N.HipScene(load_npz(ROOT / "tests/golden/scenes" / f"{scene}.npz"))
+    g = N.HipScene(load_npz(ROOT / "tests/golden/scenes" / f"{scene}.npz"), traversal=int(v))
     g.render()
     st, xy = g.profile_waves()
     st, xy = g.profile_waves()

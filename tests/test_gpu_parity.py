@@ -197,15 +197,14 @@ def test_shard_render_and_unpack(N, name, w, h, over, shards):
     del native
 
 
-@pytest.mark.parametrize("calib_k", ["4", "1.5"])
-def test_window_walk_equals_packet_walk(N, oracle, monkeypatch, calib_k):
+@pytest.mark.parametrize("calib_k", [4000, 1500])
+def test_window_walk_equals_packet_walk(N, oracle, calib_k):
     """Walk 13 (window walk for the plan's split tiles) against
     walk 12 and the oracle on the C2 frame; a low split threshold puts many
     4x4 (16 rays x 4 nodes) and 2x2 (4 rays x 16 nodes) tiles through it."""
-    monkeypatch.setenv("CRT_CALIB_K", calib_k)
     sc = scene_npz("14-01-acceleration-tree__scene1")
     st = N.RendererSettings.default()
-    win = N.HipScene(sc)
+    win = N.HipScene(sc, calib_k_milli=calib_k)
     xywh, _ = win.plan_tiles(st)
     sizes = {(int(w), int(h)) for w, h in xywh[:, 2:4]}
     assert (2, 2) in sizes or (4, 4) in sizes
