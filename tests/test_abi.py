@@ -90,3 +90,14 @@ def test_blender_extension_package(tmp_path):
     r = subprocess.run([sys.executable, "-c", code, str(tmp_path / "x")], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert r.stdout.split() == ["3", "3", "True"]
+
+
+def test_library_resolves_every_kernel():
+    """Every kernel the host layer launches is compiled into the library: no
+    crt_amd symbol is left undefined (each kernel family is instantiated in
+    one translation unit, crt_kernels.h; the link also uses --no-undefined)."""
+    import subprocess
+    lib = ROOT / "chaos-ray-tracing-course-2025_amd" / "lib" / "libcrt_hip.so"
+    out = subprocess.run(["nm", "-DC", "--undefined-only", str(lib)], capture_output=True, text=True,
+                         check=True).stdout
+    assert "crt_amd::" not in out, [ln for ln in out.splitlines() if "crt_amd::" in ln][:5]
