@@ -62,7 +62,7 @@ CONFIGS = {
     "c2": {"scene": "14-01-acceleration-tree__scene1", "size": (1920, 1080), "settings": {}, "cpu_size": (1920, 1080),
            "label": "14-01-acceleration-tree/scene1", "note": "primary rays (HEAD traces no shadow rays)"},
     "c3": {"scene": "11-01-refractive__scene8", "size": (1920, 1080), "settings": {"max_ray_depth": 8},
-           "cpu_size": (480, 270), "label": "11-01-refractive/scene8", "note": "depth-8 reflect/refract recursion"},
+           "cpu_size": (1920, 1080), "label": "11-01-refractive/scene8", "note": "depth-8 reflect/refract recursion"},
     "c4": {"scene": "15-01-conclusion__scene2", "size": (3840, 2160), "settings": {}, "cpu_size": (240, 135),
            "label": "15-01-conclusion/scene2", "note": "GI 4 rays, depth 3 (the CLI default scene)"},
     "c5": {"synthetic": 1_000_000, "size": (3840, 2160), "settings": {}, "cpu_size": (480, 270),
@@ -111,7 +111,7 @@ def parse(argv=None):
                    help="bracket every k-th render of the timed region with HIP events (kernel time sample; "
                         "an event pair between two renders costs ~7 us of a ~165 us C2 step)")
     p.add_argument("--pmc-json", default=None,
-                   help="PMC record of the render kernel (profiles/r02/pmc_<config>.json by default); used for "
+                   help="PMC record of the render kernel (profiles/r03/pmc_<config>.json by default); used for "
                         "the issue roofline and measured HBM traffic when its build id equals the library's")
     p.add_argument("--selftest-launch", action="store_true",
                    help="launcher plumbing only: ranks join the process group and report; no GPU work")
@@ -204,27 +204,75 @@ def cpu_info() -> dict:
 
 def cpu_baseline(config: str, w: int, h: int, seconds: float, single_seconds: float, size_note: str,
                  shadows: bool = False) -> dict:
+    """Legs: hardware_concurrency() threads (the affinity mask, as
+    crt_renderer.cpp:178 would spawn), threads = the cgroup CPU quota when it
+    is smaller (what the box actually grants: `value` is the better of the
+    two, `cores` its thread count, `effective_cpus` the quota), and one
+    pinned core."""
     info = cpu_info()
-    threads = info["affinity_cpus"]          # hardware_concurrency() of this process (crt_renderer.cpp:178)
-    multi = run_cpu_worker({"config": config, "w": w, "h": h, "threads": threads, "pin": None,
-                            "seconds": seconds, "min_frames": 5, "shadows": shadows})
+    affinity = info["affinity_cpus"]
+    quota = info["cgroup_cpu_quota"]
+    effective = min(affinity, int(round(quota))) if quota else affinity
+    legs = {}
+    for n in sorted({affinity, effective}):
+        legs[n] = run_cpu_worker({"config": config, "w": w, "h": h, "threads": n, "pin": None,
+                                  "seconds": seconds, "min_frames": 5, "shadows": shadows})
     pin = sorted(os.sched_getaffinity(0))[0]
     single = run_cpu_worker({"config": config, "w": w, "h": h, "threads": 1, "pin": pin,
                              "seconds": single_seconds, "min_frames": 2, "shadows": shadows})
-    rays = multi["rays_per_frame"]
+    rays = legs[affinity]["rays_per_frame"]
+    best_n = min(legs, key=lambda n: legs[n]["median_s"])
+    multi = legs[best_n]
     return {
-        "value": round(rays / multi["median_s"] / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+        "value": round(rays / multi["median_s"] / 1e6, 3), "unit": "Mrays/s", "cores": best_n, "kind": "port",
+        "effective_cpus": effective, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
         "best": round(rays / multi["best_s"] / 1e6, 3), "frame_ms_median": round(multi["median_s"] * 1e3, 3),
         "frame_ms_best": round(multi["best_s"] * 1e3, 3),
+        "legs": {str(n): {"threads": n, "value": round(rays / l["median_s"] / 1e6, 3),
+                          "frame_ms_median": round(l["median_s"] * 1e3, 3), "frames": l["frames"]}
+                 for n, l in legs.items()},
         "single_core": {"value": round(single["rays_per_frame"] / single["median_s"] / 1e6, 3), "unit": "Mrays/s",
                         "frame_ms_median": round(single["median_s"] * 1e3, 3), "frames": single["frames"],
                         "pinned_cpu": pin},
-        "cpu_model": info["model"], "cgroup_cpu_quota": info["cgroup_cpu_quota"],
+        "cpu_model": info["model"],
         "sample": f"{multi['frames']} whole frames{size_note} of the same workload, oracle/crt_oracle.cpp "
-                  f"render_image (24-px bucket queue + {threads} threads = the affinity mask, g++ -O3, no FMA) in a "
-                  f"child process on {info['model']}; value = rays / median frame time; single_core = the same "
-                  f"on one pinned CPU ({single['frames']} frames)",
+                  f"render_image (24-px bucket queue, g++ -O3, no FMA) in a child process on {info['model']}: "
+                  f"{best_n} threads (legs: {', '.join(f'{n} threads' for n in sorted(legs))}; the affinity mask "
+                  f"is {affinity} CPUs inside a {quota} CPU cgroup quota); value = rays / median frame time; "
+                  f"single_core = the same on one pinned CPU ({single['frames']} frames)",
     }
+
+
+def cold_cli(cfg: dict, w: int, h: int, settings) -> dict | None:
+    """The reference CLI's timed region on a fresh process (main.cpp:37-43):
+    bin/crt_renderer on the config's scene written as a .crtscene of this
+    size, on one GPU.  execution_ms is the "Execution time" it prints — the
+    first crt_hip_render of a new scene: tile-plan calibration, GI / Fresnel
+    tables, the render and the D2H copy; process_ms the whole process (HIP
+    start, load, tree build, upload, render, PPM write)."""
+    if "scene" not in cfg:
+        return None
+    import tempfile
+    from crt_amd.scene_json import arrays_to_crtscene
+    sc = make_scene(cfg, w, h)
+    if any(t == 3 for t in sc.a["tex_i"]):   # bitmap textures would need their files next to the scene
+        return None
+    doc = arrays_to_crtscene(sc.a, {})
+    doc["settings"]["image_settings"].update(width=w, height=h)
+    exe = PKG / "bin" / "crt_renderer"
+    with tempfile.TemporaryDirectory() as td:
+        scene = Path(td) / "scene.crtscene"
+        scene.write_text(json.dumps(doc))
+        cmd = [str(exe), str(scene), str(Path(td) / "out.ppm"), "--gpus", "1",
+               "--max-depth", str(settings.max_ray_depth), "--gi-rays", str(settings.diffuse_reflection_ray_count)]
+        t0 = time.perf_counter()
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        wall = (time.perf_counter() - t0) * 1e3
+    if r.returncode != 0 or not r.stdout.startswith("Execution time: "):
+        return {"error": (r.stderr or r.stdout)[-300:]}
+    secs = float(r.stdout.split("Execution time: ", 1)[1].split()[0])
+    return {"execution_ms": round(secs * 1e3, 3), "process_ms": round(wall, 1),
+            "command": "bin/crt_renderer scene.crtscene out.ppm --gpus 1 (fresh process)"}
 
 
 # --------------------------------------------------------------------------
@@ -249,8 +297,10 @@ def roofline_block(kernel_ms: float, counts: dict, waves: dict, npx: int, pmc: d
     s8d = (NODE_BYTES * counts["node_tests"] + TRI_BYTES * counts["triangle_tests"] + PIXEL_BYTES * npx) * shard_frac
     uniq = (PNODE_BYTES * waves.get("node_steps", 0) + SLOT_BYTES * waves.get("triangle_steps", 0)
             + PIXEL_BYTES * npx) * shard_frac
-    cand = {"l2": {"achieved": uniq / sec / 1e9, "peak": L2_PEAK_GBS, "unit": "GB/s",
-                   "bytes_per_launch": int(uniq)}}
+    cand = {}
+    if waves.get("node_steps", 0) > 0:   # wave-unique records are counted by the packet walks only
+        cand["l2"] = {"achieved": uniq / sec / 1e9, "peak": L2_PEAK_GBS, "unit": "GB/s",
+                      "bytes_per_launch": int(uniq)}
     fresh = pmc is not None and pmc.get("build_id") == build_id
     traffic = None
     if fresh:
@@ -266,11 +316,15 @@ def roofline_block(kernel_ms: float, counts: dict, waves: dict, npx: int, pmc: d
     for c in cand.values():
         c["frac"] = round(c["achieved"] / c["peak"], 5)
         c["achieved"] = round(c["achieved"], 2)
-    bound = max(cand, key=lambda k: cand[k]["frac"])
-    b = cand[bound]
-    return {"bound": {"valu": "valu_issue", "l2": "l2", "hbm": "hbm"}[bound], "achieved": b["achieved"],
+    if not cand:   # no PMC of this build and no wave-step counts: no bound can be named
+        b, bound = {"achieved": None, "peak": None, "unit": None, "frac": None}, None
+    else:
+        bound = max(cand, key=lambda k: cand[k]["frac"])
+        b = cand[bound]
+    return {"bound": {"valu": "valu_issue", "l2": "l2", "hbm": "hbm", None: None}[bound], "achieved": b["achieved"],
             "peak": b["peak"], "unit": b["unit"], "frac": b["frac"],
             "traffic": int(traffic) if traffic else None,
+            "measured": bound is not None,
             "pmc": (f"{pmc.get('source', '?')} (build {build_id})" if fresh else
                     f"stale or absent (library build {build_id}); traffic/valu omitted"),
             "candidates": cand,
@@ -280,7 +334,7 @@ def roofline_block(kernel_ms: float, counts: dict, waves: dict, npx: int, pmc: d
 
 
 def load_pmc(path: str | None, config: str, w: int, h: int) -> dict | None:
-    p = Path(path) if path else ROOT / "profiles" / "r02" / f"pmc_{config}.json"
+    p = Path(path) if path else ROOT / "profiles" / "r03" / f"pmc_{config}.json"
     try:
         d = json.loads(p.read_text())
     except (OSError, ValueError):
@@ -355,7 +409,10 @@ def main():
     settings = N.RendererSettings.default(**cfg["settings"])
     # the library's own start/stop events (crt_hip_last_kernel_ms) would sit inside
     # this script's timing events and add ~8 us per frame: timing here uses torch's
-    gpu = N.HipScene(scene, device=local, events=0, shadows=int(a.shadows))
+    # calibrate 1: the measured tile plan with its split threshold tuned on the
+    # first frame (a long-running renderer's steady state; one-shot callers
+    # default to the fixed threshold, see cold_cli below)
+    gpu = N.HipScene(scene, device=local, events=0, shadows=int(a.shadows), calibrate=1)
     build_id = N.build_id()
     # an explicit stream: the render kernel, the gather and the timing events
     # all go on it (handle 0 would mean "the scene's own stream" to the C-ABI)
@@ -507,6 +564,9 @@ def main():
             gpu.render_host(settings, host.data_ptr())
             ts.append(time.perf_counter() - s)
         e2e = statistics.median(ts) * 1e3
+    cold = None
+    if world == 1 and rank == 0 and not a.no_e2e:
+        cold = cold_cli(cfg, W, H, settings)
 
     shard_frac = 1.0 / world if mode == "tiles" else 1.0
     pmc = load_pmc(a.pmc_json, a.config, W, H)
@@ -552,6 +612,7 @@ def main():
                        "e2e_ms": round(e2e, 4) if e2e is not None else None,
                        "e2e_note": ("crt_hip_render into a pinned host buffer: render + D2H of the fp32 image, "
                                     "the reference's render_image call (main.cpp:37-43)") if e2e is not None else None,
+                       "cold_cli": cold,
                        "check": check, "build_id": build_id,
                        "plan": gpu.plan_info()},
             "roofline": roof,

@@ -177,6 +177,13 @@ EXPORTS = [
     ("crt_host_scene_destroy", None, [_P]),
     ("crt_hip_scene_create", C.c_int, [C.POINTER(SceneDesc), C.c_int, C.POINTER(_P)]),
     ("crt_hip_scene_create_ex", C.c_int, [C.POINTER(SceneDesc), C.c_int, C.c_int, C.POINTER(_P)]),
+    ("crt_hip_device_count", C.c_int, []),
+    ("crt_hip_scene_create_on", C.c_int, [C.POINTER(SceneDesc), _P, C.c_int32, C.c_int, C.POINTER(_P)]),
+    ("crt_hip_scene_from_tree_on", C.c_int, [C.POINTER(TreeSceneDesc), _P, C.c_int32, C.POINTER(_P)]),
+    ("crt_hip_scene_create_mask", C.c_int, [C.POINTER(SceneDesc), C.c_uint64, C.c_int, C.POINTER(_P)]),
+    ("crt_hip_scene_from_tree_mask", C.c_int, [C.POINTER(TreeSceneDesc), C.c_uint64, C.POINTER(_P)]),
+    ("crt_hip_scene_devices", C.c_int, [_P, _P, C.c_int32]),
+    ("crt_hip_last_replica_ms", C.c_int, [_P, _P, C.c_int32]),
     ("crt_hip_scene_from_tree", C.c_int, [C.POINTER(TreeSceneDesc), C.c_int, C.POINTER(_P)]),
     ("crt_host_scene_from_tree", C.c_int, [C.POINTER(TreeSceneDesc), C.POINTER(_P)]),
     ("crt_hip_scene_tree", C.c_int, [_P, _P, _P, _P, _P]),
@@ -445,21 +452,45 @@ class PlanInfo(C.Structure):
 
 
 class HipScene:
-    def __init__(self, src, device: int = 0, tree_build: str = "auto", **options):
+    def __init__(self, src, device: int = 0, tree_build: str = "auto", devices=None, **options):
         """tree_build: "auto" | "host" | "device" — where the acceleration tree is
-        built (crt_hip_scene_create_ex; both builds give identical bits)."""
+        built (crt_hip_scene_create_ex; both builds give identical bits).
+        devices: a list of HIP devices (repeats allowed) — the scene replicated
+        on each, frames split over them (crt_hip_scene_create_on)."""
         h = C.c_void_p()
-        if isinstance(src, HostScene):
+        flag = {"auto": TREE_AUTO, "host": TREE_HOST, "device": TREE_DEVICE}[tree_build]
+        if devices is not None:
+            devs = np.ascontiguousarray(devices, np.int32)
+            if hasattr(src, "tree_desc_ptr"):
+                _check(lib().crt_hip_scene_from_tree_on(src.tree_desc_ptr(), devs.ctypes.data, len(devs), C.byref(h)))
+            else:
+                _check(lib().crt_hip_scene_create_on(_desc_ptr(src), devs.ctypes.data, len(devs), flag, C.byref(h)))
+            device = int(devs[0])
+        elif isinstance(src, HostScene):
             _check(lib().crt_hip_scene_upload(src.handle, device, C.byref(h)))
         elif hasattr(src, "tree_desc_ptr"):
             _check(lib().crt_hip_scene_from_tree(src.tree_desc_ptr(), device, C.byref(h)))
         else:
-            flag = {"auto": TREE_AUTO, "host": TREE_HOST, "device": TREE_DEVICE}[tree_build]
             _check(lib().crt_hip_scene_create_ex(_desc_ptr(src), device, flag, C.byref(h)))
         self._h = h
         self.device = device
         for k, v in options.items():
             self.set_option(k, v)
+
+    def devices(self) -> list:
+        """HIP devices of the scene's replicas (crt_hip_scene_devices)."""
+        n = lib().crt_hip_scene_devices(self._h, None, 0)
+        _check(min(int(n), 0))
+        out = np.zeros(n, np.int32)
+        _check(min(int(lib().crt_hip_scene_devices(self._h, out.ctypes.data, n)), 0))
+        return [int(d) for d in out]
+
+    def replica_ms(self) -> list:
+        """Kernel ms of each replica's shard in the last render (crt_hip_last_replica_ms)."""
+        n = len(self.devices())
+        out = np.zeros(n, np.float64)
+        _check(min(int(lib().crt_hip_last_replica_ms(self._h, out.ctypes.data, n)), 0))
+        return [float(x) for x in out]
 
     def set_option(self, name: str, value: int) -> "HipScene":
         """Walk selection (crt_hip_scene_set_option): traversal / secondary / wavefront / trace_walk."""

@@ -2,7 +2,7 @@
  * crt_renderer — command-line front end, drop-in for src/standalone/main.cpp.
  *
  *   crt_renderer [<scene-file>] [<output-file>]            (reference interface, main.cpp:14,28)
- *   crt_renderer [...] [--width W] [--height H] [--max-depth D] [--gi-rays N] [--device K]
+ *   crt_renderer [...] [--width W] [--height H] [--max-depth D] [--gi-rays N] [--gpus G | --device K]
  *
  * Same defaults ("../scenes/15-01-conclusion/scene2.crtscene", "output.ppm"),
  * same messages and exit codes (main.cpp:16-33), same timed region (only the
@@ -10,6 +10,11 @@
  * device-to-host copy of the image is inside it like the reference's returned
  * Image), same PPM bytes (crt_image_ppm.cpp).  The flags are additions: the
  * reference CLI always uses default RendererSettings and the file's size.
+ *
+ * Like the reference's render_image, which spans every hardware thread
+ * (crt_renderer.cpp:176-196), the render spans every visible GPU by default
+ * (crt_hip_scene_create_mask; CRT_HIP_GPUS=N limits it); --gpus G takes
+ * devices 0..G-1, --device K one device.
  */
 #include <chrono>
 #include <cstdio>
@@ -31,7 +36,7 @@ static std::string quoted(const char *p) {   /* std::filesystem::path's operator
 
 int main(int argc, char *argv[]) {
     std::vector<const char *> pos;
-    int width = -1, height = -1, device = 0;
+    int width = -1, height = -1, device = -1, gpus = 0;
     long max_depth = -1, gi_rays = -1;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
@@ -45,9 +50,10 @@ int main(int argc, char *argv[]) {
         else if (a == "--max-depth") { next(max_depth); }
         else if (a == "--gi-rays") { next(gi_rays); }
         else if (a == "--device") { next(v); device = (int)v; }
+        else if (a == "--gpus") { next(v); gpus = (int)v; }
         else if (a == "--help" || a == "-h") {
             std::printf("usage: crt_renderer [<scene-file>] [<output-file>] [--width W] [--height H] "
-                        "[--max-depth D] [--gi-rays N] [--device K]\n");
+                        "[--max-depth D] [--gi-rays N] [--gpus G | --device K]\n");
             return 0;
         } else pos.push_back(argv[i]);
     }
@@ -84,7 +90,10 @@ int main(int argc, char *argv[]) {
     if (gi_rays >= 0) settings.diffuse_reflection_ray_count = (uint32_t)gi_rays;
 
     crt_hip_scene *scene = nullptr;
-    if (crt_hip_scene_create(desc, device, &scene) != CRT_OK) {
+    const uint64_t mask = gpus > 0 ? (gpus >= 64 ? ~0ull : (1ull << gpus) - 1ull) : 0ull;
+    const int crc = device >= 0 ? crt_hip_scene_create(desc, device, &scene)
+                                : crt_hip_scene_create_mask(desc, mask, CRT_SCENE_TREE_AUTO, &scene);
+    if (crc != CRT_OK) {
         std::fprintf(stderr, "Error: %s\n", crt_hip_last_error());
         crt_scene_file_destroy(sf);
         return 1;

@@ -169,32 +169,13 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
 }
 
 int crt_hip_scene_create_ex(const crt_scene_desc *desc, int device, int flags, crt_hip_scene **out) {
-    if (!desc || !out) return set_error(CRT_E_INVALID, "null argument");
-    int mode = flags & 3;
-    if (mode == CRT_SCENE_TREE_AUTO) {
-        if (const char *e = std::getenv("CRT_TREE_BUILD")) {
-            if (std::strcmp(e, "host") == 0) mode = CRT_SCENE_TREE_HOST;
-            if (std::strcmp(e, "device") == 0) mode = CRT_SCENE_TREE_DEVICE;
-        }
-    }
-    if (mode == CRT_SCENE_TREE_AUTO) {
-        int64_t nt = 0;
-        for (int i = 0; i < desc->mesh_count && desc->meshes; ++i) nt += desc->meshes[i].index_count / 3;
-        mode = nt >= CRT_SCENE_DEVICE_BUILD_MIN ? CRT_SCENE_TREE_DEVICE : CRT_SCENE_TREE_HOST;
-    }
-    if (mode != CRT_SCENE_TREE_HOST && mode != CRT_SCENE_TREE_DEVICE) return set_error(CRT_E_INVALID, "bad tree build flag");
-    std::unique_ptr<HostScene> hs(new HostScene());
-    int rc = prepare_scene(desc, *hs, mode == CRT_SCENE_TREE_HOST);
-    if (rc != CRT_OK) return rc;
-    return crt_hip_scene_upload(reinterpret_cast<crt_host_scene *>(hs.get()), device, out);
+    const int32_t dev = device;
+    return crt_hip_scene_create_on(desc, &dev, 1, flags, out);
 }
 
 int crt_hip_scene_from_tree(const crt_tree_scene_desc *desc, int device, crt_hip_scene **out) {
-    if (!desc || !out) return set_error(CRT_E_INVALID, "null argument");
-    std::unique_ptr<HostScene> hs(new HostScene());
-    const int rc = prepare_scene_from_tree(desc, *hs);
-    if (rc != CRT_OK) return rc;
-    return crt_hip_scene_upload(reinterpret_cast<crt_host_scene *>(hs.get()), device, out);
+    const int32_t dev = device;
+    return crt_hip_scene_from_tree_on(desc, &dev, 1, out);
 }
 
 int crt_hip_scene_create(const crt_scene_desc *desc, int device, crt_hip_scene **out) {
@@ -230,6 +211,7 @@ int crt_hip_scene_info(const crt_hip_scene *sc, crt_scene_info *out) {
 
 void crt_hip_scene_destroy(crt_hip_scene *sc) {
     if (!sc) return;
+    multi_free(sc);
     (void)hipSetDevice(sc->device);
     if (sc->stream) (void)hipStreamSynchronize(sc->stream);
     for (void *p : sc->allocs) (void)hipFree(p);
@@ -251,6 +233,12 @@ int crt_hip_render_device(crt_hip_scene *sc, const crt_renderer_settings *st, fl
     if (rc != CRT_OK) return rc;
     HIP_TRY(hipSetDevice(sc->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : sc->stream;
+    if (!sc->replicas.empty()) {   /* multi-GPU scene (crt_multi.hip) */
+        if (multi_overflowed(sc))
+            return set_error(CRT_E_STATE, "a wavefront level outgrew its recorded size in the previous frame; "
+                                             "that frame is wrong (sizes are now read back again)");
+        return render_multi_into(sc, st, d_rgb, s);
+    }
     return render_into(sc, st, d_rgb, s, false);
 }
 
@@ -262,20 +250,29 @@ int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rg
     HIP_TRY(hipSetDevice(sc->device));
     const size_t nfl = (size_t)sc->info.width * sc->info.height * 3;
     if (!sc->d_out) HIP_TRY(hipMalloc(&sc->d_out, nfl * sizeof(float)));
-    rc = render_into(sc, st, sc->d_out, sc->stream, false);
+    const bool multi = !sc->replicas.empty();
+    auto frame = [&]() -> int {
+        return multi ? render_multi_into(sc, st, sc->d_out, sc->stream) : render_into(sc, st, sc->d_out, sc->stream, false);
+    };
+    rc = frame();
     if (rc != CRT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(rgb_out, sc->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
-    if (wf_overflowed(sc->wf, true)) {   /* recorded level sizes did not hold: render again with read-backs */
-        if ((rc = render_into(sc, st, sc->d_out, sc->stream, false)) != CRT_OK) return rc;
+    if (multi ? multi_overflowed(sc) : wf_overflowed(sc->wf, true)) {   /* recorded level sizes did not hold: render again with read-backs */
+        if ((rc = frame()) != CRT_OK) return rc;
         HIP_TRY(hipMemcpyAsync(rgb_out, sc->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
         HIP_TRY(hipStreamSynchronize(sc->stream));
     }
     if (stats) {
         std::memset(stats, 0, sizeof *stats);
         float ms = 0.f;
-        if (!sc->grid_empty && sc->full.ntiles > 0 && sc->events_valid)
+        if (multi) {   /* the slowest replica's shard */
+            std::vector<double> rm(1 + sc->replicas.size(), 0.0);
+            if ((rc = crt_hip_last_replica_ms(sc, rm.data(), (int32_t)rm.size())) < 0) return rc;
+            for (double r : rm) ms = std::max(ms, (float)r);
+        } else if (!sc->grid_empty && sc->full.ntiles > 0 && sc->events_valid) {
             HIP_TRY(hipEventElapsedTime(&ms, sc->ev_start, sc->ev_stop));
+        }
         stats->kernel_ms = ms;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         stats->width = sc->info.width;

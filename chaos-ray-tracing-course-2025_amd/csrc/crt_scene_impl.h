@@ -81,6 +81,15 @@ constexpr int kWfMaxDepth = 4096;
 
 struct crt_hip_scene {
     int device = 0;
+    /* Multi-GPU behind one handle (crt_multi.hip): further replicas of the
+     * scene (this one is replica 0), the gather buffer on this device and, on
+     * a replica, its packed shard and the event that its copy is done. */
+    std::vector<crt_hip_scene *> replicas;
+    float *mg_gather = nullptr;
+    int64_t mg_gather_floats = 0;
+    float *mg_packed = nullptr;
+    int64_t mg_packed_floats = 0;
+    hipEvent_t mg_done = nullptr;     /* replica: its shard is copied | replica 0: the gather is unpacked */
     crt_scene_info info{};
     bool has_secondary = false;    /* any reflective / refractive material */
     bool has_diffuse = false;
@@ -127,11 +136,14 @@ struct crt_hip_scene {
     struct SubTile { int32_t dx, dy, w, h; float cost; };
     std::vector<std::vector<SubTile>> calib;
     int calib_walk = -1;           /* primary walk the calibration was measured with (-1: none) */
-    int calibrate = 1;             /* 0 estimate plan, 1 measured costs with a tuned k, 2 with calib_k (env CRT_CALIBRATE) */
+    int calibrate = 2;             /* 0 estimate plan, 1 measured costs with a tuned k (10 candidate plans, 6 frames
+                                    * each, on the first frame: long-running hosts, bench.py), 2 (default: one-shot
+                                    * callers pay one calibration, no tuning frames) measured costs with calib_k */
     int window_walk = 1;           /* camera walk 12 -> 13 (window walk for split tiles), env CRT_WINDOW */
     int record_events = 1;         /* start/stop events around every render (crt_hip_last_kernel_ms), option "events" */
     bool events_valid = false;
-    float calib_k = 4.0f;          /* split a wave whose cost exceeds k x (total cost / wave slots) (env CRT_CALIB_K) */
+    float calib_k = 2.25f;         /* split a wave whose cost exceeds k x (total cost / wave slots); 2.25 = C2's
+                                    * tuned k (profiles/r02/gab, shard_kscan) */
     int calib_min = 2;             /* smallest sub-tile side */
     int prio_tiles = 1024;         /* heaviest tiles run at raised issue priority */
     float prio_min = 2.0f;         /* ... if they cost more than this x the mean per wave slot */
@@ -176,6 +188,12 @@ int render_shard_t(crt_hip_scene *sc, const crt_renderer_settings *st, int shard
 template <class T>
 int unpack_shards_t(crt_hip_scene *sc, int shard_count, const T *d_gathered, T *d_rgb, void *stream, bool compact);
 int scene_upload_buffers(crt_hip_scene *sc, const HostScene &hs);
+/* crt_multi.hip: the frame over every replica of a multi-GPU scene into d_rgb
+ * (on the scene's device) on `stream`; *overflow: some replica's recorded
+ * wavefront sizes did not hold (render again). */
+int render_multi_into(crt_hip_scene *sc, const crt_renderer_settings *st, float *d_rgb, hipStream_t stream);
+bool multi_overflowed(crt_hip_scene *sc);
+void multi_free(crt_hip_scene *sc);
 
 template <class T>
 int upload(crt_hip_scene *sc, const std::vector<T> &v, const T **dst, size_t pad = 0) {

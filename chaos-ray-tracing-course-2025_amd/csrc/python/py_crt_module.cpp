@@ -18,10 +18,16 @@
 #include <Python.h>
 #include <structmember.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../../include/crt_hip.h"
+
+/* the device scene of the last rendered dict (render_scene_from_dict) */
+static std::mutex g_scene_mu;
+static crt_hip_scene *g_scene = nullptr;
+static std::string g_scene_key;
 
 static PyStructSequence_Field settings_fields[] = {
     {(char *)"max_ray_depth", (char *)"Maximum recursion depth for rays"},
@@ -76,6 +82,9 @@ static PyObject *render_scene_from_dict(PyObject *, PyObject *args) {
         Py_DECREF(text);
         return nullptr;
     }
+    std::string key(root, (size_t)rn);
+    key.push_back('\0');
+    key.append(utf8, (size_t)n);
     crt_scene_file *sf = nullptr;
     const int prc = crt_scene_file_parse(utf8, (size_t)n, root, &sf);
     Py_DECREF(text);
@@ -94,11 +103,28 @@ static PyObject *render_scene_from_dict(PyObject *, PyObject *args) {
     int rc;
     std::string err;
     Py_BEGIN_ALLOW_THREADS
-    crt_hip_scene *scene = nullptr;
-    rc = crt_hip_scene_create(desc, 0, &scene);
-    if (rc == CRT_OK) rc = crt_hip_render(scene, &st, img.data(), nullptr);
-    if (rc != CRT_OK) err = crt_hip_last_error();
-    crt_hip_scene_destroy(scene);
+    {
+        /* the device scene of the last dict is kept (a Blender session
+         * re-renders the same scene with other settings): same JSON text and
+         * asset root -> no new upload, and its measured tile plan stays */
+        std::lock_guard<std::mutex> lock(g_scene_mu);
+        if (!g_scene || g_scene_key != key) {
+            crt_hip_scene_destroy(g_scene);
+            g_scene = nullptr;
+            g_scene_key.clear();
+            rc = crt_hip_scene_create_mask(desc, 0, CRT_SCENE_TREE_AUTO, &g_scene);   /* every visible GPU */
+            if (rc == CRT_OK) g_scene_key = key;
+        } else {
+            rc = CRT_OK;
+        }
+        if (rc == CRT_OK) rc = crt_hip_render(g_scene, &st, img.data(), nullptr);
+        if (rc != CRT_OK) {
+            err = crt_hip_last_error();
+            crt_hip_scene_destroy(g_scene);
+            g_scene = nullptr;
+            g_scene_key.clear();
+        }
+    }
     Py_END_ALLOW_THREADS
     crt_scene_file_destroy(sf);
     if (rc != CRT_OK) {

@@ -270,6 +270,32 @@ int  crt_hip_scene_upload(const crt_host_scene *hs, int device, crt_hip_scene **
 int  crt_hip_scene_info(const crt_hip_scene *scene, crt_scene_info *out);
 void crt_hip_scene_destroy(crt_hip_scene *scene);
 
+/* ---- several GPUs behind one scene handle ----------------------------
+ * The reference's render_image spans every hardware thread of the host
+ * (crt_renderer.cpp:176-196); a scene created on several devices spans every
+ * listed GPU.  The scene is prepared once and replicated on each device; a
+ * frame (crt_hip_render / crt_hip_render_device) deals the reference's
+ * bucket grid to the replicas (bucket k -> replica k % count, compact shards:
+ * only 8x8 tiles with a live pixel), each replica renders its shard on its
+ * own stream, the shards are copied peer to peer (xGMI) into the first
+ * device and unpacked there.  The image is bit-identical for any count.  A
+ * device may be listed more than once (several replicas on it: how a one-GPU
+ * host runs the split).  The shard / trace / count entry points act on the
+ * first replica. */
+int  crt_hip_device_count(void);          /* visible HIP devices; 0 without a GPU */
+int  crt_hip_scene_create_on(const crt_scene_desc *desc, const int32_t *devices, int32_t count, int flags,
+                             crt_hip_scene **out);
+int  crt_hip_scene_from_tree_on(const crt_tree_scene_desc *desc, const int32_t *devices, int32_t count,
+                                crt_hip_scene **out);
+/* gpu_mask: bit i = HIP device i; 0 = the first N devices for the environment
+ * variable CRT_HIP_GPUS=N, else every visible device. */
+int  crt_hip_scene_create_mask(const crt_scene_desc *desc, uint64_t gpu_mask, int flags, crt_hip_scene **out);
+int  crt_hip_scene_from_tree_mask(const crt_tree_scene_desc *desc, uint64_t gpu_mask, crt_hip_scene **out);
+/* Replica devices (devices may be NULL); returns the replica count. */
+int  crt_hip_scene_devices(const crt_hip_scene *scene, int32_t *devices, int32_t cap);
+/* Kernel ms of each replica's shard in the last render (blocks until done). */
+int  crt_hip_last_replica_ms(crt_hip_scene *scene, double *ms, int32_t cap);
+
 /* Blocking drop-in for render_image: rgb_out is caller-allocated W*H*3 fp32,
  * row-major, top row first, unclamped (crt_image.h:11-27). */
 int  crt_hip_render(crt_hip_scene *scene, const crt_renderer_settings *settings,

@@ -50,6 +50,16 @@ def test_shard_fraction_scales_per_launch_figures():
     assert half["frac"] == pytest.approx(full["frac"], rel=1e-3)
 
 
+def test_no_pmc_and_no_wave_steps_is_unmeasured():
+    """GI / wavefront walks count no wave steps: without a PMC record of the
+    benched build no bound can be named (VERDICT r02 #4)."""
+    r = bench.roofline_block(0.1, COUNTS, {}, NPX, None, "a", 1.0)
+    assert r["bound"] is None and r["frac"] is None and r["measured"] is False
+    assert r["s8d_work_rate"]["bytes_per_launch"] > 0
+    r = bench.roofline_block(0.1, COUNTS, {}, NPX, pmc_record("a"), "a", 1.0)
+    assert r["bound"] in ("valu_issue", "hbm") and r["measured"] is True
+
+
 def test_no_pmc_falls_back_to_l2():
     r = bench.roofline_block(0.1, COUNTS, WAVES, NPX, None, "a", 1.0)
     assert r["bound"] == "l2" and r["traffic"] is None
@@ -62,7 +72,7 @@ def test_committed_pmc_records_are_well_formed(config, size):
     assert d["config"] == config and tuple(d["size"]) == size
     assert len(d["build_id"]) == 16
     assert d["hbm_bytes_per_launch"] > 0 and d["valu_insts_per_launch"] > 0
-    loaded = bench.load_pmc(None, config, *size)
+    loaded = bench.load_pmc(str(path), config, *size)
     assert loaded is not None and loaded["build_id"] == d["build_id"]
     # a record for another frame size is not applied
-    assert bench.load_pmc(None, config, 64, 64) is None
+    assert bench.load_pmc(str(path), config, 64, 64) is None
