@@ -499,7 +499,8 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
     if (!sc || !name) return set_error(CRT_E_INVALID, "null argument");
     const std::string k(name);
     if (k == "traversal") {
-        if (value != 7 && value != 8) return set_error(CRT_E_INVALID, "traversal must be 7 (reference order) or 8 (pruned)");
+        if (value != 7 && value != 8 && value != 14)
+            return set_error(CRT_E_INVALID, "traversal must be 7 (reference order), 8 (pruned) or 14 (BVH)");
         sc->traversal = value;
         wf_graphs_clear(sc->wf);   /* captured wavefront frames bake in the level-0 walk */
     } else if (k == "secondary") {

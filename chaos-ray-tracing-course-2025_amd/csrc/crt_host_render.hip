@@ -205,6 +205,7 @@ int probe_tiles(crt_hip_scene *sc, const DeviceScene *d_scene, int walk, const s
         case 7: hipLaunchKernelGGL(k_probe_tiles<7>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         case 12: hipLaunchKernelGGL(k_probe_tiles<12>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         case 13: hipLaunchKernelGGL(k_probe_tiles<13>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
+        case 14: hipLaunchKernelGGL(k_probe_tiles<14>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         default: hipLaunchKernelGGL(k_probe_tiles<8>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         }
         e = hipGetLastError();
@@ -365,6 +366,7 @@ int check_settings(const crt_renderer_settings *st) {
 /* The packet walk camera rays take: walk 8 becomes its fast-only build 12
  * when the host has proven every camera ray fast. */
 int camera_walk(const crt_hip_scene *sc, int trav) {
+    if (trav == 14 && !sc->ds.bnodes) trav = 8;   /* no BVH built for this scene */
     return (trav == 8 && sc->camera_fast) ? (sc->window_walk ? 13 : 12) : trav;
 }
 
@@ -617,7 +619,9 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
 #define CRT_WF0(T, COUNT)                                                                                   \
     hipLaunchKernelGGL((k_wf_level<T, true, COUNT>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,      \
                        plan.d_tiles, plan.ntiles, lv, cnt)
-    if (primary == 12 || primary == 13) {   /* level 0 keeps 8x8 tiles' packet walk (no window build) */
+    if (primary == 14) {
+        if (count) CRT_WF0(14, true); else CRT_WF0(14, false);
+    } else if (primary == 12 || primary == 13) {   /* level 0 keeps 8x8 tiles' packet walk (no window build) */
         if (count) CRT_WF0(12, true); else CRT_WF0(12, false);
     } else if (primary == 8) {
         if (count) CRT_WF0(8, true); else CRT_WF0(8, false);
@@ -741,7 +745,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
      * ms); with GI every ray of the per-lane frame-stack kernel takes that walk
      * (the packet walk's registers would cost a wave per SIMD).
      * CRT_SECONDARY / "secondary" overrides the secondary walk. */
-    const bool pruned = sc->traversal == 8;
+    const bool pruned = sc->traversal != 7;
     int sec = sc->secondary;
     if (sec == 14 && !sc->ds.bnodes) sec = 10;   /* no BVH (device-built tree) */
     if (sec == 0) sec = !pruned ? 4 : sc->ds.bnodes ? 14 : gi ? 4 : 10;
@@ -807,6 +811,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         case 8: if (count) CRT_LAUNCH_T(false, 0, 8, true); else CRT_LAUNCH_T(false, 0, 8, false); break;
         case 12: if (count) CRT_LAUNCH_T(false, 0, 12, true); else CRT_LAUNCH_T(false, 0, 12, false); break;
         case 13: if (count) CRT_LAUNCH_T(false, 0, 13, true); else CRT_LAUNCH_T(false, 0, 13, false); break;
+        case 14: if (count) CRT_LAUNCH_T(false, 0, 14, true); else CRT_LAUNCH_T(false, 0, 14, false); break;
         default: return set_error(CRT_E_INVALID, "no such camera walk");
         }
     } else if (gi && (trav == 4 || trav == 10 || trav == 14) && sc->gi_refill && sc->d_next_px && !stamps && frames <= 64) {

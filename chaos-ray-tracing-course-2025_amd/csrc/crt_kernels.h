@@ -110,7 +110,8 @@ __global__ void k_quantize(const float *__restrict__ src, uint8_t *__restrict__ 
 #define CRT_TILES_INSTANCES(X)                                                                              \
     X(false, 0, 7, 7, false, false) X(false, 0, 7, 7, true, false) X(false, 0, 8, 8, false, false)        \
     X(false, 0, 8, 8, true, false) X(false, 0, 12, 12, false, false) X(false, 0, 12, 12, true, false)      \
-    X(false, 0, 13, 13, false, false) X(false, 0, 13, 13, true, false)                                     \
+    X(false, 0, 13, 13, false, false) X(false, 0, 13, 13, true, false) X(false, 0, 14, 14, false, false)   \
+    X(false, 0, 14, 14, true, false)                                                                       \
     X(false, 0, 8, 8, false, true) X(false, 0, 8, 8, true, true) X(false, 0, 12, 12, false, true)          \
     X(false, 0, 12, 12, true, true) X(false, 0, 13, 13, false, true) X(false, 0, 13, 13, true, true)       \
     X(true, 4, 4, 4, false, false) X(true, 4, 4, 4, true, false) X(true, 16, 4, 4, false, false)           \
@@ -129,12 +130,12 @@ __global__ void k_quantize(const float *__restrict__ src, uint8_t *__restrict__ 
 #define CRT_GIM_INSTANCES(X) X(false) X(true)
 #define CRT_GIM_SIG(C) void k_render_gi<C>(const DeviceScene *__restrict__, DSettings, const Tile *__restrict__, int, \
     float *__restrict__, int32_t *__restrict__, unsigned long long *__restrict__, float4 *__restrict__);
-#define CRT_PROBE_INSTANCES(X) X(7) X(8) X(12) X(13)
+#define CRT_PROBE_INSTANCES(X) X(7) X(8) X(12) X(13) X(14)
 #define CRT_PROBE_SIG(T) void k_probe_tiles<T>(const DeviceScene *__restrict__, const Tile *__restrict__, int, \
     uint32_t *__restrict__);
 #define CRT_WF_INSTANCES(X) X(4, false, false) X(4, false, true) X(10, false, false) X(10, false, true)        \
     X(14, false, false) X(14, false, true) X(7, true, false) X(7, true, true) X(8, true, false) X(8, true, true) \
-    X(12, true, false) X(12, true, true)
+    X(12, true, false) X(12, true, true) X(14, true, false) X(14, true, true)
 #define CRT_WF_SIG(T, L0, C) void k_wf_level<T, L0, C>(const DeviceScene *__restrict__, DSettings, \
     const Tile *__restrict__, int, WLevel, unsigned long long *__restrict__);
 

@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restri
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
     (void)trace<TRAV, true>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px, o, d, t, cnt);
-    constexpr bool kPacket = !kIsCoop<TRAV>;
+    constexpr bool kPacket = !kIsCoop<TRAV> && TRAV != 14;
     uint32_t c = kPacket ? cnt.wave_nodes + cnt.wave_tris + cnt.wave_edges : cnt.nodes + cnt.tris;
     for (int off = 32; off > 0; off >>= 1) {
         const uint32_t o2 = (uint32_t)__shfl_xor((int)c, off);

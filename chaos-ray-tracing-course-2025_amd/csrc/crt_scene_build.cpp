@@ -396,11 +396,12 @@ int flatten_tree(const std::vector<BuildNode> &bn, HostScene &hs) {
     return CRT_OK;
 }
 
-/* The secondary-ray BVH (crt_bvh.h) serves scattered rays only: built when
- * the scene makes any (GI with a diffuse material, reflective or refractive
- * materials). */
+/* The BVH (crt_bvh.h): built when the scene makes scattered rays (GI with a
+ * diffuse material, reflective or refractive materials), and for any scene
+ * small enough that the host build costs little (camera rays may take it,
+ * option "traversal" 14). */
 int maybe_build_bvh(HostScene &hs) {
-    bool need = false;
+    bool need = hs.tri_attr.size() <= ((size_t)1 << 18);
     for (const DMaterial &m : hs.materials)
         need = need || m.type == CRT_MATERIAL_REFLECTIVE || m.type == CRT_MATERIAL_REFRACTIVE ||
                (hs.gi_on && m.type == CRT_MATERIAL_DIFFUSE);
