@@ -26,4 +26,14 @@ RL="python3 scripts/render_loop.py"
 [[ $STEPS == *c3ab* ]] && run c3ab 300 $RL --scene 11-01-refractive__scene8 --depth 8 --frames 8 --counts --opt secondary=${C3AB:-10,14}
 [[ $STEPS == *c4k* ]] && run c4k 300 $RL --scene 15-01-conclusion__scene2 --width 3840 --height 2160 --frames 3
 [[ $STEPS == *bench* ]] && run bench 600 python bench.py --steps 20 --warmup 5
+if [[ $STEPS == *shards* ]]; then
+  for c in c2 c3 c4 c5; do
+    r=20; [ $c = c4 ] && r=3; [ $c = c5 ] && r=5
+    run shards_$c 300 python3 scripts/shard_times.py --config $c --reps $r --out "$OUT/shards_$c.json"
+  done
+fi
+if [[ $STEPS == *rehearse* ]]; then
+  run rehearse_c4_gloo2 600 python bench.py --config c4 --gpus 2 --backend gloo --check --steps 3 --warmup 1 --no-secondary
+  run rehearse_c2_gloo2 300 python bench.py --gpus 2 --backend gloo --check --steps 20 --warmup 3
+fi
 exit 0
