@@ -11,6 +11,13 @@ from conftest import bits, scene_npz
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(scope="module")
+def N():
+    from crt_amd import native
+    native.lib()
+    return native
+
 CASES = [
     ("14-01-acceleration-tree__scene1", 480, 270, {}),
     ("11-01-refractive__scene8", 240, 135, {"max_ray_depth": 8}),
