@@ -129,6 +129,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
         ds.bnode_count = hs.bnode_count;
     }
     sc->camera_fast = camera_rays_fast(hs, ds.planes_ok != 0);
+    if (ds.bnodes) sc->traversal = 14;   /* camera rays through the BVH too */
     if ((rc = upload(sc.get(), hs.tri_attr, &ds.tri_attr)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.vnormal, &ds.vnormal)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.vuv, &ds.vuv)) != CRT_OK) return rc;

@@ -25,9 +25,11 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("scene", nargs="?", default="14-01-acceleration-tree__scene1")
     p.add_argument("--window", type=int, default=1)
+    p.add_argument("--opt", action="append", default=[], help="NAME=V scene options (e.g. traversal=14)")
     p.add_argument("--out", default=None)
     a = p.parse_args()
-    g = N.HipScene(load_npz(ROOT / "tests/golden/scenes" / f"{a.scene}.npz"), window=a.window)
+    g = N.HipScene(load_npz(ROOT / "tests/golden/scenes" / f"{a.scene}.npz"), window=a.window,
+                   **{k: int(v) for k, v in (o.split("=") for o in a.opt)})
     st = N.RendererSettings.default()
     g.render(st)
     xywh, cost = g.plan_tiles(st)

@@ -145,12 +145,17 @@ def test_pruned_synthetic_bit_exact(N, oracle):
     sc = c5_scene(50_000, 160, 90)
     st = N.RendererSettings.default()
     want = oracle.OracleScene(sc).render(st)
-    gpu = N.HipScene(sc)
+    gpu = N.HipScene(sc, traversal=8)
     got = gpu.render(st)
     assert np.array_equal(bits(got), bits(want))
     c = gpu.count_work(st)
     r = N.HipScene(sc, traversal=7).count_work(st)
     assert c["hits"] == r["hits"] and c["node_tests"] * 2 < r["node_tests"]
+    # camera rays through the BVH (the default for scenes with one) + their proof
+    bvh = N.HipScene(sc, traversal=14)
+    assert np.array_equal(bits(bvh.render(st)), bits(want))
+    cb = bvh.count_work(st)
+    assert cb["hits"] == r["hits"] and cb["triangle_tests"] * 4 < r["triangle_tests"]
 
 
 SHARD_CASES = [
