@@ -127,6 +127,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
         if ((rc = upload(sc.get(), hs.btri, &ds.btri)) != CRT_OK) return rc;
         if ((rc = upload(sc.get(), hs.btri_id, &ds.btri_id)) != CRT_OK) return rc;
         ds.bnode_count = hs.bnode_count;
+        if ((rc = upload(sc.get(), hs.ktopo, &ds.ktopo)) != CRT_OK) return rc;
     }
     sc->camera_fast = camera_rays_fast(hs, ds.planes_ok != 0);
     if (ds.bnodes) sc->traversal = 14;   /* camera rays through the BVH too */

@@ -37,6 +37,13 @@
 #pragma once
 #include "crt_device.h"
 
+#ifndef CRT_PROOF_TOPO
+#define CRT_PROOF_TOPO 1     /* 0: the proof descends the 32-B nodes (verify_kd) even where KTopo exists */
+#endif
+#ifndef CRT_BVH_PREFETCH
+#define CRT_BVH_PREFETCH 1
+#endif
+
 namespace crt_amd {
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -68,7 +75,7 @@ CRT_HD bool bnode_alive(const BNode &n, const PruneRay &p, float lim) {
 /* Step 1: closest reference hit over all triangles.  Returns the triangle id
  * (-1: no triangle is hit), its t, and tie = another triangle hits at the
  * same t (each triangle is in the BVH once, so an equal t is another one). */
-template <bool COUNT>
+template <bool COUNT, bool PF = (CRT_BVH_PREFETCH != 0)>
 CRT_HD int walk_bvh(const BNode *nodes, int n, const DTriGeo *geo, const int32_t *tid, Vec o, Vec d,
                     const PruneRay &pr, float &best_t, bool &tie, WalkCounts &c) {
     int best = -1;
@@ -76,14 +83,30 @@ CRT_HD int walk_bvh(const BNode *nodes, int n, const DTriGeo *geo, const int32_t
     best_t = 0.0f;
     tie = false;
     int i = 0;
+    /* PF: both possible successors (i + 1, skip) are loaded before the node is
+     * tested: the walk is a chain of dependent loads, and each step's test
+     * then overlaps the next step's load (every order ends with a zero
+     * record, so i + 1 <= n and skip <= n are always in bounds).  Pays on
+     * scattered rays (C3); the coherent camera rays of C2 walk without it. */
+    BNode cur, n1, n2;
+    if constexpr (PF) cur = CRT_LDG(nodes, 0);
     while (i < n) {
-        const BNode nd = CRT_LDG(nodes, i);
+        BNode nd;
+        if constexpr (PF) {
+            nd = cur;
+            n1 = CRT_LDG(nodes, i + 1);
+            n2 = CRT_LDG(nodes, nd.skip);
+        } else {
+            nd = CRT_LDG(nodes, i);
+        }
         if (COUNT) ++c.nodes;
         if (!bnode_alive(nd, pr, lim)) {
             i = nd.skip;
+            if constexpr (PF) cur = n2;
             continue;
         }
         ++i;                                   /* interior: first child; leaf: next in preorder */
+        if constexpr (PF) cur = n1;
         const int cnt = nd.leaf & 15;
         const int first = nd.leaf >> 4;
         for (int k = 0; k < cnt; ++k) {
@@ -231,14 +254,160 @@ CRT_HD int verify_kd(const DNode *nodes, const int32_t *slot_tri, int tri, Vec o
     return slot;
 }
 
+/* The two halves of a cell on axis AX (AX = depth % 3, a template
+ * parameter so no field is selected by a run-time index; AABB::split,
+ * crt_aabb.h:24-35: the reference's child cells, the same fp32 operations,
+ * so the same bits). */
+template <int AX>
+CRT_HD void topo_halves(const DNode &c, DNode &lo, DNode &hi) {
+    lo = c;
+    hi = c;
+    if constexpr (AX == 0) {
+        const float m = (c.lo_x + c.hi_x) * 0.5f;
+        lo.hi_x = m;
+        hi.lo_x = m;
+    } else if constexpr (AX == 1) {
+        const float m = (c.lo_y + c.hi_y) * 0.5f;
+        lo.hi_y = m;
+        hi.lo_y = m;
+    } else {
+        const float m = (c.lo_z + c.hi_z) * 0.5f;
+        lo.hi_z = m;
+        hi.lo_z = m;
+    }
+}
+
+CRT_HD void topo_halves(const DNode &c, int axis, DNode &lo, DNode &hi) {   /* host build check */
+    if (axis == 0) topo_halves<0>(c, lo, hi);
+    else if (axis == 1) topo_halves<1>(c, lo, hi);
+    else topo_halves<2>(c, lo, hi);
+}
+
+/* c ? a : b field by field (a struct-valued ?: can become a select of two
+ * stack addresses) */
+CRT_HD DNode cell_sel(bool c, const DNode &a, const DNode &b) {
+    DNode r;
+    r.lo_x = c ? a.lo_x : b.lo_x;
+    r.hi_x = c ? a.hi_x : b.hi_x;
+    r.lo_y = c ? a.lo_y : b.lo_y;
+    r.hi_y = c ? a.hi_y : b.hi_y;
+    r.lo_z = c ? a.lo_z : b.lo_z;
+    r.hi_z = c ? a.hi_z : b.hi_z;
+    r.a = c ? a.a : b.a;
+    r.b = c ? a.b : b.b;
+    return r;
+}
+
+/* bit-identical cells (build-time check of the halving) */
+CRT_HD bool cell_equal(const DNode &a, const DNode &b) {
+    return __builtin_bit_cast(uint32_t, a.lo_x) == __builtin_bit_cast(uint32_t, b.lo_x) &&
+           __builtin_bit_cast(uint32_t, a.hi_x) == __builtin_bit_cast(uint32_t, b.hi_x) &&
+           __builtin_bit_cast(uint32_t, a.lo_y) == __builtin_bit_cast(uint32_t, b.lo_y) &&
+           __builtin_bit_cast(uint32_t, a.hi_y) == __builtin_bit_cast(uint32_t, b.hi_y) &&
+           __builtin_bit_cast(uint32_t, a.lo_z) == __builtin_bit_cast(uint32_t, b.lo_z) &&
+           __builtin_bit_cast(uint32_t, a.hi_z) == __builtin_bit_cast(uint32_t, b.hi_z);
+}
+
+/* One level of verify_topo's descent on axis AX: false at a leaf. */
+struct TopoWalk {
+    DNode cell;
+    KTopo tp;
+    int i, depth;
+    uint64_t upper;   /* bit k: level k went to the upper half */
+    uint64_t df;      /* byte f: depth where face f's plane was last set */
+};
+
+template <int AX>
+CRT_HD bool topo_level(const KTopo *topo, Vec p, TopoWalk &w) {
+    if (w.tp.b >= 0 || w.depth >= 62) return false;   /* verify_kd: no level below 62 */
+    DNode lo, hi;
+    topo_halves<AX>(w.cell, lo, hi);
+    const bool first_up = w.tp.b == -2;        /* the first child (i + 1) is the upper half */
+    const DNode n1 = cell_sel(first_up, hi, lo), n2 = cell_sel(first_up, lo, hi);
+    int ci = w.i + 1;
+    bool up = first_up;
+    if (w.tp.a >= 0 && !cell_holds(n1, p)) {   /* two children, p not in the first */
+        if (cell_holds(n2, p) || cell_excess(n2, p) < cell_excess(n1, p)) {
+            ci = w.tp.a;
+            up = !first_up;
+        }
+    }
+    if (up) w.upper |= 1ull << w.depth;
+    ++w.depth;
+    /* only the split plane changes: lo[AX] (face AX) going up, hi[AX] (face 3 + AX) going down */
+    const float old = up ? cell_plane(w.cell, AX) : cell_plane(w.cell, 3 + AX);
+    const float mid = up ? cell_plane(hi, AX) : cell_plane(lo, 3 + AX);
+    const int f = up ? AX : 3 + AX;
+    if (!(mid == old)) w.df = (w.df & ~(0xffull << (8 * f))) | ((uint64_t)w.depth << (8 * f));
+    w.cell = cell_sel(up, hi, lo);
+    w.i = ci;
+    w.tp = CRT_LDG(topo, ci);
+    return true;
+}
+
+/* Step 2 on the topology records (crt_layout.h KTopo): verify_kd's descent
+ * and proof with the cells computed in registers — one dependent 8-B load
+ * per level (verify_kd: one or two 32-B loads), and the full tests of the
+ * ancestors above dmin replay the path from the root cell with no load.
+ * Levels go three at a time (axes 0, 1, 2). */
+template <bool COUNT>
+CRT_HD int verify_topo(const KTopo *topo, const DNode *nodes, const int32_t *slot_tri, int tri, Vec o, Vec d,
+                       const RayRcp &rr, Vec p, WalkCounts &c) {
+    TopoWalk w;
+    w.cell = CRT_LDG(nodes, 0);                /* the root cell */
+    w.tp = CRT_LDG(topo, 0);
+    w.i = 0;
+    w.depth = 0;
+    w.upper = 0;
+    w.df = 0;
+    while (topo_level<0>(topo, p, w) && topo_level<1>(topo, p, w) && topo_level<2>(topo, p, w)) {
+    }
+    if (w.tp.b < 0) return -1;                 /* an interior node at depth 62 */
+    int slot = -1;
+    for (int k = 0; k < w.tp.a && slot < 0; ++k)
+        if (CRT_LDG(slot_tri, w.tp.b + k) == tri) slot = w.tp.b + k;
+    if (slot < 0) return -1;
+    if (COUNT) ++c.nodes;
+    const unsigned m = box_faces(o, d, rr, w.cell);
+    if (m == 0u) return -1;
+    int dmin = w.depth;
+#pragma unroll
+    for (int f = 0; f < 6; ++f)
+        if ((m >> f) & 1u) {
+            const int df = (int)((w.df >> (8 * f)) & 0xffull);
+            dmin = df < dmin ? df : dmin;
+        }
+    /* ancestors above dmin: full tests on the cells of the path, from the root */
+    DNode a = CRT_LDG(nodes, 0);
+    for (int k = 0; k < dmin; k += 3) {
+        DNode lo, hi;
+        if (COUNT) ++c.nodes;
+        if (!box_hit_r(o, d, rr, a)) return -1;
+        if (k + 1 >= dmin) break;
+        topo_halves<0>(a, lo, hi);
+        a = cell_sel(((w.upper >> k) & 1ull) != 0ull, hi, lo);
+        if (COUNT) ++c.nodes;
+        if (!box_hit_r(o, d, rr, a)) return -1;
+        if (k + 2 >= dmin) break;
+        topo_halves<1>(a, lo, hi);
+        a = cell_sel(((w.upper >> (k + 1)) & 1ull) != 0ull, hi, lo);
+        if (COUNT) ++c.nodes;
+        if (!box_hit_r(o, d, rr, a)) return -1;
+        topo_halves<2>(a, lo, hi);
+        a = cell_sel(((w.upper >> (k + 2)) & 1ull) != 0ull, hi, lo);
+    }
+    return slot;
+}
+
 /* The reference's closest hit of one ray (slot in reference visit-order
  * numbering, -1: miss) by steps 1-3.  fb (optional) is set when step 3 ran.
  * Rays with a NaN component miss every cell (each face test reads a NaN
  * coordinate), so they are answered without a walk. */
-template <bool COUNT>
+template <bool COUNT, bool PF = (CRT_BVH_PREFETCH != 0)>
 CRT_HD int trace_bvh_exact(const BNode *bnodes, int bn, const DTriGeo *btri, const int32_t *btri_id,
                            const DNode *nodes, const PNode *pnodes, int n, const DTriGeo *slots,
-                           const uint8_t *slot_cull, const int32_t *slot_tri, float prune_origin_max, bool planes_ok,
+                           const uint8_t *slot_cull, const int32_t *slot_tri, const KTopo *ktopo,
+                           float prune_origin_max, bool planes_ok,
                            Vec o, Vec d, float &best_t, WalkCounts &c, bool *fb = nullptr) {
     best_t = 0.0f;
     if (fb) *fb = false;
@@ -247,11 +416,13 @@ CRT_HD int trace_bvh_exact(const BNode *bnodes, int bn, const DTriGeo *btri, con
     const PruneRay pr = make_prune_ray(o, d, prune_origin_max);
     bool tie = false;
     float t = 0.0f;
-    const int tri = walk_bvh<COUNT>(bnode_order(bnodes, bn, oct), bn, btri, btri_id, o, d, pr, t, tie, c);
+    const int tri = walk_bvh<COUNT, PF>(bnode_order(bnodes, bn, oct), bn, btri, btri_id, o, d, pr, t, tie, c);
     if (tri < 0) return -1;
     const RayRcp rr = make_ray_rcp(o, d, planes_ok);
     if (!tie) {
-        const int slot = verify_kd<COUNT>(nodes, slot_tri, tri, o, d, rr, vadd(o, vscale(d, t)), c);
+        const Vec p = vadd(o, vscale(d, t));
+        const int slot = CRT_PROOF_TOPO && ktopo ? verify_topo<COUNT>(ktopo, nodes, slot_tri, tri, o, d, rr, p, c)
+                                                 : verify_kd<COUNT>(nodes, slot_tri, tri, o, d, rr, p, c);
         if (slot >= 0) {
             best_t = t;
             return slot;

@@ -23,6 +23,7 @@
 #include <limits>
 #include <vector>
 
+#include "crt_bvh.h"
 #include "crt_device.h"
 #include "crt_host.h"
 
@@ -242,6 +243,46 @@ int build_bvh(HostScene &hs) {
         }
     }
     hs.bnode_count = n;
+    return CRT_OK;
+}
+
+/* Topology records of the proof (crt_layout.h KTopo) over the flattened
+ * reference-order tree (interior node i: first child i + 1, second child, if
+ * any, where the first one's subtree ends, before skip(i) = a).  Each child's
+ * cell is checked to be its parent's half as verify_topo recomputes it. */
+int build_proof_tables(HostScene &hs) {
+    const std::vector<DNode> &nodes = hs.nodes;
+    const int32_t n = (int32_t)nodes.size();
+    hs.ktopo.assign((size_t)n, KTopo{0, 0});
+    for (int32_t i = 0; i < n; ++i) {
+        const DNode &nd = nodes[(size_t)i];
+        KTopo &t = hs.ktopo[(size_t)i];
+        if (nd.b >= 0) {
+            t.a = node_leaf_count(nd);
+            t.b = nd.b;
+            continue;
+        }
+        const int32_t c1 = i + 1;
+        if (c1 >= nd.a) {   /* childless interior node (the empty scene's root): a leaf without copies */
+            t.a = 0;
+            t.b = 0;
+            continue;
+        }
+        const DNode &n1 = nodes[(size_t)c1];
+        const int32_t c2 = n1.b < 0 ? n1.a : c1 + 1;
+        const int axis = node_depth(nd) % 3;
+        DNode lo_half = nd, hi_half = nd;
+        topo_halves(nd, axis, lo_half, hi_half);
+        const bool first_lo = cell_equal(n1, lo_half);
+        bool ok = first_lo || cell_equal(n1, hi_half);
+        if (c2 < nd.a) ok = ok && cell_equal(nodes[(size_t)c2], first_lo ? hi_half : lo_half);
+        if (!ok) {
+            hs.ktopo.clear();   /* not the reference's halving: the proof descends the nodes (verify_kd) */
+            return CRT_OK;
+        }
+        t.a = c2 < nd.a ? c2 : -1;
+        t.b = first_lo ? -1 : -2;
+    }
     return CRT_OK;
 }
 

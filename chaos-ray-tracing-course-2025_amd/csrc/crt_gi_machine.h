@@ -183,7 +183,9 @@ __device__ __forceinline__ int gi_walk_finish(const DeviceScene &s, const GiWalk
     WalkCounts wc = {0u, 0u};
     int slot = -1;
     if (!w.tie) {
-        slot = verify_kd<COUNT>(s.nodes, s.slot_tri, w.tri, o, d, rr, vadd(o, vscale(d, w.t)), wc);
+        const Vec p = vadd(o, vscale(d, w.t));
+        slot = CRT_PROOF_TOPO && s.ktopo ? verify_topo<COUNT>(s.ktopo, s.nodes, s.slot_tri, w.tri, o, d, rr, p, wc)
+                                         : verify_kd<COUNT>(s.nodes, s.slot_tri, w.tri, o, d, rr, p, wc);
         t = w.t;
     }
     if (slot < 0)

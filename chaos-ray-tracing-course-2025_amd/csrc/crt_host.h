@@ -85,6 +85,8 @@ struct HostScene {
     int32_t bnode_count = 0;
     std::vector<DTriGeo> btri;
     std::vector<int32_t> btri_id;   /* triangle id | back_face_culling << 31 */
+    /* the BVH proof's tree topology (crt_layout.h KTopo; build_proof_tables) */
+    std::vector<KTopo> ktopo;
 
     /* root cell (crt_acceleration_tree.cpp:89-94); tree_on_host = false when
      * prepare_scene skipped the tree (built on the device, crt_tree_build.h) */
@@ -106,6 +108,11 @@ struct HostScene {
 /* The secondary-ray BVH over hs's triangles (crt_bvh_build.cpp); needs the
  * mesh prep and prune_G. */
 int build_bvh(HostScene &hs);
+
+/* The topology records of the flattened tree hs.nodes (crt_layout.h KTopo)
+ * for crt_bvh.h verify_topo (crt_bvh_build.cpp); none (verify_kd then) if a
+ * child cell is not its parent's half. */
+int build_proof_tables(HostScene &hs);
 
 /* Mesh prep + (build_tree) the exact tree build and its flattening. */
 int prepare_scene(const crt_scene_desc *desc, HostScene &out, bool build_tree = true);

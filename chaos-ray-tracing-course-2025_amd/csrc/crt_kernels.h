@@ -20,6 +20,12 @@
 #ifndef CRT_RENDER_BOUNDS
 #define CRT_RENDER_BOUNDS __launch_bounds__(256)
 #endif
+#ifndef CRT_BVH_WINDOW
+#define CRT_BVH_WINDOW 1     /* split tiles of camera frames on the BVH: one ray per group of lanes (trace_bvh_window) */
+#endif
+#ifndef CRT_BVH_WAVES
+#define CRT_BVH_WAVES 1      /* min waves/SIMD asked of the camera BVH-walk (14) kernel (1: no bound) */
+#endif
 #ifndef CRT_PACKET_WAVES
 #define CRT_PACKET_WAVES 5   /* min waves/SIMD asked of the walk-12 kernel (as walk 13) */
 #endif

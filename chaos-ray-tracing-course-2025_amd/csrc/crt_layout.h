@@ -38,6 +38,21 @@ struct alignas(16) DNode {
 };
 static_assert(sizeof(DNode) == 32, "DNode must be 32 B");
 
+/* Topology of the reference-order tree for the BVH walk's proof (crt_bvh.h
+ * verify_topo), one 8-B record per DNode: the descent toward a hit point
+ * needs only which children exist and where the second one starts — the
+ * children's cells are the parent's halves (AABB::split, crt_aabb.h:24-35:
+ * mid = (lo + hi) * 0.5f on axis depth % 3), computed in registers.
+ *   interior: a = second child's index (-1: one child), b = -1 (first child,
+ *             i + 1, is the lower half) or -2 (it is the upper half: the
+ *             reference's LIFO walk visits child 1 first); a second child is
+ *             the other half
+ *   leaf:     a = triangle copies, b = first slot */
+struct KTopo {
+    int32_t a, b;
+};
+static_assert(sizeof(KTopo) == 8, "KTopo must be 8 B");
+
 /* Node record of the pruned walks: the reference cell (the box the
  * reference's six-face test runs on — it decides which leaf copies are
  * eligible, crt_intersection.cpp:121) plus a conservative hull of every
@@ -129,6 +144,8 @@ struct DeviceScene {
     int32_t bnode_count;
     const DTriGeo *btri;
     const int32_t *btri_id;
+    /* the proof's tree topology (KTopo); null when the tree lives on the device only */
+    const KTopo *ktopo;
     const DTriAttr *tri_attr;
     const DVec4 *vnormal;
     const DVec4 *vuv;

@@ -13,7 +13,7 @@
 namespace crt_amd {
 
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW>
-__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT_WINDOW_WAVES : TRAV == 12 ? CRT_PACKET_WAVES : (FULL && MAXF == 4 ? CRT_GI_WAVES : 1)))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
+__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT_WINDOW_WAVES : TRAV == 12 ? CRT_PACKET_WAVES : TRAV == 14 && !FULL ? CRT_BVH_WAVES : (FULL && MAXF == 4 ? CRT_GI_WAVES : 1)))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
                                                   const Tile *__restrict__ tiles,
                                                       int ntiles, float *__restrict__ out,
                                                       unsigned long long *__restrict__ counters,
@@ -79,6 +79,42 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             return;
         }
     }
+#if CRT_BVH_WINDOW
+    if constexpr (TRAV == 14 && !FULL && !SHADOW) {
+        /* tiles of <= 16 rays (the measured plan's splits of heavy tiles):
+         * each ray walked by a group of 64/R lanes (crt_walks.h trace_bvh_window) */
+        const int tw = uniform_i(tl.w), th = uniform_i(tl.h);
+        const int npx = tw * th;
+        if (npx <= 16) {
+            const int K = npx <= 4 ? 16 : 4;
+            const int r = lane / K, sl = lane % K;
+            const bool act = r < npx;
+            const int px = act ? r % tw : 0, py = act ? r / tw : 0;
+            Vec o, d;
+            camera_ray(s, tl.x + px, tl.y + py, o, d);
+            LaneCounts cw = {};
+            float t;
+            const int slot = K == 16 ? trace_bvh_window<COUNT, 16>(s, sl, act, o, d, t, cw)
+                                     : trace_bvh_window<COUNT, 4>(s, sl, act, o, d, t, cw);
+            if (act && sl == 0) {
+                const Vec c = shade_primary(s, st, o, d, slot, t);
+                float *pxo = out + 3 * (tl.out_base + (int64_t)py * tl.out_stride + px);
+                pxo[0] = c.x;
+                pxo[1] = c.y;
+                pxo[2] = c.z;
+            }
+            if (stamps && lane == 0) stamps[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
+            if (COUNT) {
+                atomicAdd(&counters[0], (unsigned long long)cw.traversals);
+                atomicAdd(&counters[1], (unsigned long long)cw.nodes);
+                atomicAdd(&counters[2], (unsigned long long)cw.tris);
+                atomicAdd(&counters[3], (unsigned long long)cw.hits);
+                if (lane == 0) atomicAdd(&counters[7], 1ull);
+            }
+            return;
+        }
+    }
+#endif
     const int lx = lane & 7, ly = lane >> 3;
     const bool has_px = lx < tl.w && ly < tl.h;
     /* the sharing walks keep pixel-less lanes as helpers (they take donated node

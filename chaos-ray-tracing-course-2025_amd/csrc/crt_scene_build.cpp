@@ -405,7 +405,10 @@ int maybe_build_bvh(HostScene &hs) {
     for (const DMaterial &m : hs.materials)
         need = need || m.type == CRT_MATERIAL_REFLECTIVE || m.type == CRT_MATERIAL_REFRACTIVE ||
                (hs.gi_on && m.type == CRT_MATERIAL_DIFFUSE);
-    return need ? build_bvh(hs) : CRT_OK;
+    if (!need) return CRT_OK;
+    const int rc = build_bvh(hs);
+    if (rc != CRT_OK || hs.nodes.empty()) return rc;   /* device-built tree: the proof descends it (verify_kd) */
+    return build_proof_tables(hs);
 }
 
 }  // namespace

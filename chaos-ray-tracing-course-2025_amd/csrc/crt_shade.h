@@ -143,8 +143,13 @@ __device__ __forceinline__ bool shade_pass(const DeviceScene &s, const DSettings
         /* the packet walk pays for the union of its lanes' visit sets: it
          * wins on camera rays (coherent by construction) and loses on the
          * scattered secondary rays, which take the range-sharing walk */
-        const int slot = (SEC != TRAV && depth != 0) ? trace<SEC, COUNT>(s, L, has_px, o, d, t, cnt)
-                                                     : trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
+        int slot;
+        if constexpr (TRAV == 14)   /* camera rays are coherent: BVH walk without successor prefetch */
+            slot = depth == 0 ? trace<TRAV, COUNT, false>(s, L, has_px, o, d, t, cnt)
+                              : trace<SEC, COUNT>(s, L, has_px, o, d, t, cnt);
+        else
+            slot = (SEC != TRAV && depth != 0) ? trace<SEC, COUNT>(s, L, has_px, o, d, t, cnt)
+                                               : trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
         if (slot < 0) {
             col = vec(s.background[0], s.background[1], s.background[2]);
         } else {

@@ -803,15 +803,15 @@ __device__ __forceinline__ int trace_lane_pruned(const DeviceScene &s, bool acti
 /* Per-lane BVH walk with its proof on the reference's tree (crt_bvh.h):
  * scattered rays (GI bounces, reflections, refractions) of the frame-stack,
  * refill and wavefront kernels when the scene has its BVH. */
-template <bool COUNT>
+template <bool COUNT, bool PF = (CRT_BVH_PREFETCH != 0)>
 __device__ __forceinline__ int trace_lane_bvh(const DeviceScene &s, bool active, Vec o, Vec d, float &best_t,
                                               LaneCounts &c) {
     best_t = 0.0f;
     if (!active) return -1;
     if (COUNT) ++c.traversals;
     WalkCounts wc = {0u, 0u};
-    const int best = trace_bvh_exact<COUNT>(s.bnodes, s.bnode_count, s.btri, s.btri_id, s.nodes, s.pnodes,
-                                            s.node_count, s.slots, s.slot_cull, s.slot_tri, s.prune_origin_max,
+    const int best = trace_bvh_exact<COUNT, PF>(s.bnodes, s.bnode_count, s.btri, s.btri_id, s.nodes, s.pnodes,
+                                            s.node_count, s.slots, s.slot_cull, s.slot_tri, s.ktopo, s.prune_origin_max,
                                             s.planes_ok != 0, o, d, best_t, wc);
     if (COUNT) {
         c.nodes += wc.nodes;
@@ -821,6 +821,168 @@ __device__ __forceinline__ int trace_lane_bvh(const DeviceScene &s, bool active,
     return best;
 }
 
+/* All-reduce over groups of K consecutive lanes (K = 16: one DPP row, row
+ * rotations 1/2/4/8; K = 4: one quad, quad permutations), every lane active. */
+template <int K>
+__device__ __forceinline__ int group_dpp(int v, int step) {
+    static_assert(K == 4 || K == 16, "group of 4 or 16 lanes");
+    if constexpr (K == 16) {
+        switch (step) {
+        case 0: return __builtin_amdgcn_update_dpp(v, v, 0x121, 0xf, 0xf, false);
+        case 1: return __builtin_amdgcn_update_dpp(v, v, 0x122, 0xf, 0xf, false);
+        case 2: return __builtin_amdgcn_update_dpp(v, v, 0x124, 0xf, 0xf, false);
+        default: return __builtin_amdgcn_update_dpp(v, v, 0x128, 0xf, 0xf, false);
+        }
+    } else {
+        return step == 0 ? __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xf, 0xf, false)    /* quad_perm [1,0,3,2] */
+                         : __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xf, 0xf, false);   /* quad_perm [2,3,0,1] */
+    }
+}
+template <int K> constexpr int kGroupSteps = K == 16 ? 4 : 2;
+template <int K> __device__ __forceinline__ unsigned group_or(unsigned v) {
+#pragma unroll
+    for (int q = 0; q < kGroupSteps<K>; ++q) v |= (unsigned)group_dpp<K>((int)v, q);
+    return v;
+}
+template <int K> __device__ __forceinline__ int group_max(int v) {
+#pragma unroll
+    for (int q = 0; q < kGroupSteps<K>; ++q) v = max(v, group_dpp<K>(v, q));
+    return v;
+}
+template <int K> __device__ __forceinline__ int group_sum(int v) {
+#pragma unroll
+    for (int q = 0; q < kGroupSteps<K>; ++q) v += group_dpp<K>(v, q);
+    return v;
+}
+template <int K> __device__ __forceinline__ float group_min(float v) {
+#pragma unroll
+    for (int q = 0; q < kGroupSteps<K>; ++q) v = fminf(v, __int_as_float(group_dpp<K>(__float_as_int(v), q)));
+    return v;
+}
+
+/* BVH window walk for the split tiles (<= 16 rays) of camera frames: the
+ * ray of lanes [K r, K r + K) is walked by all K of them (crt_bvh.h walk_bvh,
+ * same order, same boxes, same triangle test).  Each step the K lanes load
+ * the K nodes of the order from the ray's cursor on and test them at once; a
+ * dead node kills the window lanes of its subtree (its preorder range up to
+ * skip), a visited live leaf's lane tests its triangles, the group merges the
+ * candidates (min t; two at the minimum = tie) and the cursor moves past the
+ * window and every dead subtree that reaches beyond it.  The boxes are tested
+ * with the bound from before the step, a looser bound than walk_bvh's, so the
+ * triangles tested include every one walk_bvh tests at t <= its final bound:
+ * the same closest triangle, t bits and tie flag.  One step is one dependent
+ * node load for K nodes of the chain (the heavy rays' walks are ~100 nodes).
+ * Returns the group's triangle id (-1: none), row-uniform. */
+template <bool COUNT, int K>
+__device__ int walk_bvh_window(const BNode *nodes, int n, const DTriGeo *geo, const int32_t *tid, int sl, bool act,
+                               Vec o, Vec d, const PruneRay &pr, float &best_t, bool &tie, WalkCounts &c) {
+    int best = -1, i = act ? 0 : n;
+    float lim = INFINITY, bt = 0.0f;
+    bool tb = false;
+    while (__ballot(i < n) != 0ull) {
+        const int j = i + sl;
+        const bool in = i < n && j < n;
+        BNode nd = {};
+        if (in) nd = CRT_LDG(nodes, j);
+        const bool alive = in && bnode_alive(nd, pr, lim);
+        unsigned kill = 0u;
+        int jump = 0;
+        if (in && !alive) {   /* window lanes sl+1 .. e-1 lie in this dead subtree */
+            const int e = min(nd.skip - i, K);
+            kill = e > sl + 1 ? ((1u << e) - 1u) & ~((2u << sl) - 1u) : 0u;
+            jump = nd.skip;
+        }
+        kill = group_or<K>(kill);
+        jump = group_max<K>(jump);
+        const bool visit = alive && !((kill >> sl) & 1u);
+        float lt = INFINITY;
+        int lid = -1;
+        bool ltie = false;
+        if (visit && nd.leaf != 0) {
+            if (COUNT) ++c.nodes;
+            const int cnt = nd.leaf & 15, first = nd.leaf >> 4;
+            for (int k = 0; k < cnt; ++k) {
+                const DTriGeo g = CRT_LDG(geo, first + k);
+                const int32_t id = CRT_LDG(tid, first + k);
+                const uint8_t cull = (uint8_t)((uint32_t)id >> 31);
+                float t;
+                if (COUNT) ++c.tris;
+                if (tri_hit(o, d, g, &cull, t)) {
+                    if (lid < 0 || t < lt) {
+                        lt = t;
+                        lid = id & 0x7fffffff;
+                        ltie = false;
+                    } else if (t == lt) {
+                        ltie = true;
+                    }
+                }
+            }
+        } else if (COUNT && visit) {
+            ++c.nodes;
+        }
+        const float m = group_min<K>(lt);
+        const bool eq = lid >= 0 && lt == m;
+        const int neq = group_sum<K>(eq ? (ltie ? 2 : 1) : 0);
+        const int wid = group_max<K>(eq ? lid : -1);
+        if (neq > 0) {
+            if (best < 0 || m < bt) {
+                best = wid;
+                bt = m;
+                tb = neq > 1;
+                lim = m;
+            } else if (m == bt) {
+                tb = true;
+            }
+        }
+        if (i < n) i = max(i + K, jump);
+    }
+    best_t = bt;
+    tie = tb;
+    return best;
+}
+
+/* trace_bvh_exact (crt_bvh.h) with the walk done by a group of K lanes per
+ * ray (walk_bvh_window); the proof and the rare fallback run on every lane of
+ * the group with the same inputs.  act: the group has a ray. */
+template <bool COUNT, int K>
+__device__ int trace_bvh_window(const DeviceScene &s, int sl, bool act, Vec o, Vec d, float &best_t, LaneCounts &c) {
+    best_t = 0.0f;
+    const bool nan_ray = isnan(o.x) || isnan(o.y) || isnan(o.z) || isnan(d.x) || isnan(d.y) || isnan(d.z);
+    const bool walk = act && !nan_ray;
+    if (COUNT && act && sl == 0) ++c.traversals;
+    const int oct = ray_octant(d);
+    const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
+    WalkCounts wc = {0u, 0u};
+    bool tie = false;
+    float t = 0.0f;
+    const int tri = walk_bvh_window<COUNT, K>(bnode_order(s.bnodes, s.bnode_count, oct), s.bnode_count, s.btri,
+                                              s.btri_id, sl, walk, o, d, pr, t, tie, wc);
+    int slot = -1;
+    if (tri >= 0) {
+        const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
+        WalkCounts pc = {0u, 0u};
+        if (!tie) {
+            const Vec p = vadd(o, vscale(d, t));
+            slot = CRT_PROOF_TOPO && s.ktopo ? verify_topo<COUNT>(s.ktopo, s.nodes, s.slot_tri, tri, o, d, rr, p, pc)
+                                             : verify_kd<COUNT>(s.nodes, s.slot_tri, tri, o, d, rr, p, pc);
+            if (slot >= 0) best_t = t;
+        }
+        if (slot < 0)
+            slot = walk_pruned<COUNT>(pnode_order(s.pnodes, s.node_count, oct), s.node_count, s.slots, s.slot_cull, o, d,
+                                      rr, pr, best_t, pc);
+        if (COUNT && sl == 0) {
+            wc.nodes += pc.nodes;
+            wc.tris += pc.tris;
+        }
+    }
+    if (COUNT) {
+        c.nodes += wc.nodes;
+        c.tris += wc.tris;
+        if (slot >= 0 && sl == 0) ++c.hits;
+    }
+    return slot;
+}
+
 /* Walks (TRAV), all bit-identical in result:
  *   7  packet walk in the reference's node order (work counters = the reference's)
  *   8  pruned packet walk (exact t-pruning), any camera ray
@@ -828,11 +990,12 @@ __device__ __forceinline__ int trace_lane_bvh(const DeviceScene &s, bool active,
  *   13 12 + window walk for the plan's split tiles (k_render_tiles)
  *   4  cooperative walk in the reference's node order (scattered rays)
  *   10 pruned cooperative walk
- *   14 per-lane BVH walk + proof on the reference's tree (scattered rays, crt_bvh.h) */
+ *   14 per-lane BVH walk + proof on the reference's tree (scattered rays, crt_bvh.h)
+ * PF: the BVH walk loads both successors ahead (crt_bvh.h walk_bvh). */
 template <int TRAV>
 constexpr bool kIsCoop = TRAV == 4 || TRAV == 10;
 
-template <int TRAV, bool COUNT>
+template <int TRAV, bool COUNT, bool PF = (CRT_BVH_PREFETCH != 0)>
 __device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, bool active, Vec o, Vec d, float &best_t,
                                      LaneCounts &c) {
     static_assert(TRAV == 4 || TRAV == 7 || TRAV == 8 || TRAV == 10 || TRAV == 12 || TRAV == 13 || TRAV == 14,
@@ -841,7 +1004,7 @@ __device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, bool acti
     else if constexpr (TRAV == 12 || TRAV == 13) return trace_packet_pruned<COUNT, true>(s, active, o, d, best_t, c);
     else if constexpr (TRAV == 4) return trace_coop<COUNT, false>(s, *L, active, o, d, best_t, c);
     else if constexpr (TRAV == 10) return trace_coop<COUNT, true>(s, *L, active, o, d, best_t, c);
-    else if constexpr (TRAV == 14) return trace_lane_bvh<COUNT>(s, active, o, d, best_t, c);
+    else if constexpr (TRAV == 14) return trace_lane_bvh<COUNT, PF>(s, active, o, d, best_t, c);
     else return trace_packet<COUNT>(s, active, o, d, best_t, c);
 }
 

@@ -114,3 +114,22 @@ def test_bvh_far_and_nan_rays(sim):  # noqa: F811
     rs, rt, bs, bt, _ = bvh_run(sim, sc, np.concatenate([far, nan], 0))
     assert_same_tri(rs, rt, bs, bt, "far+nan")
     assert (rs[-6:] == -1).all()
+
+
+@pytest.mark.parametrize("name,w,h", SCENES)
+def test_topology_proof_equals_descent(sim, oracle, name, w, h):  # noqa: F811
+    """verify_topo (8-B topology records, child cells as the parent's halves
+    computed in registers) proves exactly what verify_kd (the 32-B node
+    descent) proves: same slot or -1 and the same node tests, ray for ray."""
+    from crt_amd.native import _desc_ptr
+    sc = scene_npz(name).set_resolution(w, h)
+    ys, xs = np.mgrid[0:h, 0:w]
+    cam = oracle.OracleScene(sc).camera_rays(np.stack([xs.ravel(), ys.ravel()], 1))
+    b1 = bounce_rays(sim, sc, cam, 1)
+    rays = np.ascontiguousarray(np.concatenate([cam, b1, stress_rays(sc, 4000, 13)], 0), np.float32)
+    sim.bvh_sim_proof_check.argtypes = [_P, _P, C.c_int64, _P]
+    sim.bvh_sim_proof_check.restype = C.c_int
+    out = np.zeros(3, np.uint64)
+    assert sim.bvh_sim_proof_check(C.cast(_desc_ptr(sc), _P), rays.ctypes.data, len(rays), out.ctypes.data) == 0
+    assert out[0] > 0 and out[1] == 0, out
+    assert out[2] > 0.95 * out[0], out

@@ -9,6 +9,7 @@
  * oracle.  Built by tests/tools/Makefile; loaded by tests/test_prune.py.
  */
 #include <cmath>
+#include <cstdio>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -97,7 +98,8 @@ int bvh_sim_trace(const crt_scene_desc *desc, const float *rays, int64_t n, int3
     HostScene hs;
     int rc = prepare_scene(desc, hs);
     if (rc != CRT_OK) return rc;
-    if (hs.bnode_count == 0 && (rc = build_bvh(hs)) != CRT_OK) return rc;   /* scenes without scattered rays */
+    if (hs.bnode_count == 0 && ((rc = build_bvh(hs)) != CRT_OK || (rc = build_proof_tables(hs)) != CRT_OK))
+        return rc;   /* scenes without scattered rays */
     const int nn = (int)hs.nodes.size();
     uint64_t rn = 0, rt = 0, fbn = 0;
     WalkCounts c = {0u, 0u};
@@ -111,7 +113,7 @@ int bvh_sim_trace(const crt_scene_desc *desc, const float *rays, int64_t n, int3
         bool fb = false;
         const int bs = trace_bvh_exact<true>(hs.bnodes.data(), hs.bnode_count, hs.btri.data(), hs.btri_id.data(),
                                              hs.nodes.data(), hs.pnodes.data(), nn, hs.slots.data(),
-                                             hs.slot_cull.data(), hs.slot_tri.data(), hs.prune_origin_max, false, o,
+                                             hs.slot_cull.data(), hs.slot_tri.data(), hs.ktopo.empty() ? nullptr : hs.ktopo.data(), hs.prune_origin_max, false, o,
                                              d, t, c, &fb);
         bvh_tri[i] = bs >= 0 ? hs.slot_tri[bs] : -1;
         bvh_t[i] = t;
@@ -122,6 +124,71 @@ int bvh_sim_trace(const crt_scene_desc *desc, const float *rays, int64_t n, int3
     counts[2] = c.nodes;
     counts[3] = c.tris;
     counts[4] = fbn;
+    return CRT_OK;
+}
+
+/* Per-ray work of trace_bvh_exact (for wave-cost analysis, scripts/bvh_wave_cost.py):
+ * out[4 i ..] = {BVH walk nodes, BVH walk triangles, proof/fallback nodes +
+ * triangles, fallback taken}. */
+int bvh_sim_ray_stats(const crt_scene_desc *desc, const float *rays, int64_t n, int32_t *out) {
+    HostScene hs;
+    int rc = prepare_scene(desc, hs);
+    if (rc != CRT_OK) return rc;
+    if (hs.bnode_count == 0 && ((rc = build_bvh(hs)) != CRT_OK || (rc = build_proof_tables(hs)) != CRT_OK)) return rc;
+    const int nn = (int)hs.nodes.size();
+    for (int64_t i = 0; i < n; ++i) {
+        const Vec o = vec(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+        const Vec d = vec(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+        WalkCounts w = {0u, 0u}, c = {0u, 0u};
+        float t = 0.f;
+        bool tie = false, fb = false;
+        const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
+        (void)walk_bvh<true>(bnode_order(hs.bnodes.data(), hs.bnode_count, ray_octant(d)), hs.bnode_count,
+                             hs.btri.data(), hs.btri_id.data(), o, d, pr, t, tie, w);
+        (void)trace_bvh_exact<true>(hs.bnodes.data(), hs.bnode_count, hs.btri.data(), hs.btri_id.data(),
+                                    hs.nodes.data(), hs.pnodes.data(), nn, hs.slots.data(), hs.slot_cull.data(),
+                                    hs.slot_tri.data(), hs.ktopo.empty() ? nullptr : hs.ktopo.data(), hs.prune_origin_max, false, o, d, t, c, &fb);
+        out[4 * i] = (int32_t)w.nodes;
+        out[4 * i + 1] = (int32_t)w.tris;
+        out[4 * i + 2] = (int32_t)(c.nodes + c.tris - w.nodes - w.tris);
+        out[4 * i + 3] = fb ? 1 : 0;
+    }
+    return CRT_OK;
+}
+
+/* The proof on the topology records against the descent of the 32-B nodes
+ * (crt_bvh.h verify_topo / verify_kd) on every ray whose BVH hit has no tie,
+ * with both division paths of the box test: the same algorithm, so the same
+ * slot (or -1) and the same node-test count for every ray.
+ * out = {proofs compared, proofs that differ, proofs that succeed}; -1: no KTopo. */
+int bvh_sim_proof_check(const crt_scene_desc *desc, const float *rays, int64_t n, uint64_t *out) {
+    HostScene hs;
+    int rc = prepare_scene(desc, hs);
+    if (rc != CRT_OK) return rc;
+    if (hs.bnode_count == 0 && ((rc = build_bvh(hs)) != CRT_OK || (rc = build_proof_tables(hs)) != CRT_OK)) return rc;
+    if (hs.ktopo.empty()) return -1;
+    for (int k = 0; k < 3; ++k) out[k] = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const Vec o = vec(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+        const Vec d = vec(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+        WalkCounts w = {0u, 0u};
+        float t = 0.f;
+        bool tie = false;
+        const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
+        const int tri = walk_bvh<true>(bnode_order(hs.bnodes.data(), hs.bnode_count, ray_octant(d)), hs.bnode_count,
+                                       hs.btri.data(), hs.btri_id.data(), o, d, pr, t, tie, w);
+        if (tri < 0 || tie) continue;
+        for (int fast = 0; fast < 2; ++fast) {
+            WalkCounts ca = {0u, 0u}, cb = {0u, 0u};
+            const RayRcp rr = make_ray_rcp(o, d, fast != 0);
+            const Vec p = vadd(o, vscale(d, t));
+            const int a = verify_topo<true>(hs.ktopo.data(), hs.nodes.data(), hs.slot_tri.data(), tri, o, d, rr, p, ca);
+            const int b = verify_kd<true>(hs.nodes.data(), hs.slot_tri.data(), tri, o, d, rr, p, cb);
+            ++out[0];
+            out[1] += (a != b || ca.nodes != cb.nodes) ? 1 : 0;
+            out[2] += a >= 0 ? 1 : 0;
+        }
+    }
     return CRT_OK;
 }
 
