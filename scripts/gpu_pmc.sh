@@ -18,7 +18,7 @@ step sq 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_IN
 step fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc/fetch" -o run --output-format csv -- python3 $CMD
 step write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc/write" -o run --output-format csv -- python3 $CMD
 step tcc 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$OUT/pmc/tcc" -o run --output-format csv -- python3 $CMD
-step record 120 python3 scripts/pmc_record.py --config $CFG --size $SIZE --kernel $KERNEL --dir "$OUT/pmc" --out "$OUT/pmc_$CFG.json" --last ${LAST:-2} --command "python3 $CMD"
+step record 120 python3 scripts/pmc_record.py --config $CFG --size $SIZE --kernel $KERNEL --dir "$OUT/pmc" --out "$OUT/pmc_$CFG.json" --last ${LAST:-2} ${FRAME_END:+--frame-end $FRAME_END} --command "python3 $CMD"
 tail -1 "$OUT/record.log" | cut -c1-900
 grep -h "$KERNEL" "$OUT"/trace/*kernel_stats.csv | head -3
 exit 0
