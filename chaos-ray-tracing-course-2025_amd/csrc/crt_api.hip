@@ -151,6 +151,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     ds.refractions_on = hs.refractions_on;
 
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
+    warm_code_objects(sc->device, sc->stream);
     HIP_TRY(hipEventCreate(&sc->ev_start));
     HIP_TRY(hipEventCreate(&sc->ev_stop));
     void *p = nullptr;
@@ -166,6 +167,17 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     const std::vector<DBucket> all = shard_buckets(hs.width, hs.height, hs.bucket_size, 0, 1, &px);
     sc->grid_empty = all.empty();
     if ((rc = make_tile_plan(sc.get(), all, true, sc->full)) != CRT_OK) return rc;
+    /* one-time costs of a first render that belong to the upload, like the
+     * runtime's own initialisation (profiles/r03/cold): the device record, the
+     * output image of crt_hip_render, and the runtime's staging for copies into
+     * pageable host memory (allocated by the first such copy) */
+    {
+        const DeviceScene *d = nullptr;
+        if ((rc = sync_device_record(sc.get(), &d)) != CRT_OK) return rc;
+        if (!sc->grid_empty) HIP_TRY(hipMalloc(&sc->d_out, (size_t)hs.width * hs.height * 3 * sizeof(float)));
+        unsigned long long probe[16];
+        HIP_TRY(hipMemcpy(probe, sc->d_counters, sizeof probe, hipMemcpyDeviceToHost));
+    }
     *out = sc.release();
     return CRT_OK;
 }
@@ -223,6 +235,7 @@ void crt_hip_scene_destroy(crt_hip_scene *sc) {
     wf_free(sc->wf);
     for (auto &kv : sc->unpack_plans) (void)hipFree(kv.second.first);
     for (auto &kv : sc->compact_unpack) (void)hipFree(kv.second.first);
+    if (sc->probe_buf) (void)hipFree(sc->probe_buf);
     if (sc->ev_start) (void)hipEventDestroy(sc->ev_start);
     if (sc->ev_stop) (void)hipEventDestroy(sc->ev_stop);
     if (sc->stream) (void)hipStreamDestroy(sc->stream);
@@ -518,8 +531,10 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         sc->gi_refill = value != 0;
     } else if (k == "gi_machine") {
         sc->gi_machine = value != 0;
+
     } else if (k == "calib_k_milli") {   /* a fixed split threshold k = value / 1000 (calibrate 2) */
         if (value <= 0) return set_error(CRT_E_INVALID, "calib_k_milli must be > 0");
+        sc->calib_defer = false;   /* an explicit plan request: calibrate on the first frame */
         sc->calib_k = (float)value / 1000.0f;
         sc->calibrate = 2;
         sc->calib_walk = -1;
@@ -539,6 +554,7 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         sc->record_events = value != 0;
     } else if (k == "calibrate") {
         if (value < 0 || value > 2) return set_error(CRT_E_INVALID, "calibrate must be 0 (estimate plan), 1 (tuned) or 2 (fixed k)");
+        sc->calib_defer = false;   /* an explicit plan request: calibrate on the first frame */
         if (value != sc->calibrate) sc->calib_walk = sc->calibrate ? -1 : sc->calib_walk;   /* re-plan on next use */
         sc->calibrate = value;
         if (!sc->calibrate && !sc->calib.empty()) {   /* back to the estimate plan */
@@ -553,6 +569,7 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         }
     } else if (k == "calib_min") {   /* smallest side the calibrated plan splits tiles down to */
         if (value != 1 && value != 2 && value != 4 && value != 8) return set_error(CRT_E_INVALID, "calib_min must be 1, 2, 4 or 8");
+        sc->calib_defer = false;   /* an explicit plan request: calibrate on the first frame */
         sc->calib_min = value;
         sc->calib_walk = -1;
     } else if (k == "shadows") {

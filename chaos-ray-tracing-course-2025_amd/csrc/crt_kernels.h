@@ -111,6 +111,10 @@ __global__ void k_unpack(const UnpackBucket *__restrict__ buckets, const T *__re
                          int width, Rgb<T> bg);
 __global__ void k_live_pixels(const DeviceScene *__restrict__ scene, uint8_t *__restrict__ live);
 __global__ void k_quantize(const float *__restrict__ src, uint8_t *__restrict__ dst, int64_t n, float maxf, int maxi);
+__global__ void k_warm_render();
+__global__ void k_warm_gi();
+__global__ void k_warm_wf();
+__global__ void k_warm_side();
 
 /* ---- instantiation lists (X(args...)) ---- */
 #define CRT_TILES_INSTANCES(X)                                                                              \

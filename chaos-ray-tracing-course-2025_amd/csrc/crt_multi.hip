@@ -141,7 +141,7 @@ int render_multi_into(crt_hip_scene *sc, const crt_renderer_settings *st, float 
         HIP_TRY(hipMemsetAsync(d_rgb, 0, (size_t)sc->info.width * sc->info.height * 3 * sizeof(float), stream));
         return CRT_OK;
     }
-    int rc = ensure_plans(sc, st, stream);
+    int rc = ensure_plans(sc, st, stream, true);
     if (rc != CRT_OK) return rc;
     if ((rc = ensure_live_mask(sc)) != CRT_OK) return rc;
     for (crt_hip_scene *r : sc->replicas)

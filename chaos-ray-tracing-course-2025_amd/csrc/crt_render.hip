@@ -191,4 +191,8 @@ __global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restri
 CRT_TILES_INSTANCES(CRT_INST_TILES)
 CRT_PROBE_INSTANCES(CRT_INST_PROBE)
 
+/* empty kernel: its launch at scene creation loads this TU's code object
+ * (warm_code_objects) */
+__global__ void k_warm_render() {}
+
 }  // namespace crt_amd

@@ -93,4 +93,8 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(MAXF == 4 ? (TRA
 CRT_REFILL_INSTANCES(CRT_INST_REFILL)
 CRT_GIM_INSTANCES(CRT_INST_GIM)
 
+/* empty kernel: its launch at scene creation loads this TU's code object
+ * (warm_code_objects) */
+__global__ void k_warm_gi() {}
+
 }  // namespace crt_amd

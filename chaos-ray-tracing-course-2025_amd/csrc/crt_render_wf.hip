@@ -199,4 +199,8 @@ __global__ __launch_bounds__(256) void k_wf_pixels(const WNode *__restrict__ nod
 #define CRT_INST_WF(T, L0, C) template __global__ CRT_WF_SIG(T, L0, C)
 CRT_WF_INSTANCES(CRT_INST_WF)
 
+/* empty kernel: its launch at scene creation loads this TU's code object
+ * (warm_code_objects) */
+__global__ void k_warm_wf() {}
+
 }  // namespace crt_amd

@@ -145,6 +145,12 @@ struct crt_hip_scene {
     float calib_k = 2.25f;         /* split a wave whose cost exceeds k x (total cost / wave slots); 2.25 = C2's
                                     * tuned k (profiles/r02/gab, shard_kscan) */
     int calib_min = 2;             /* smallest sub-tile side */
+    bool calib_defer = true;       /* calibrate 2 (one-shot default): a walk's first frame renders with the
+                                    * current plan and the calibration runs on its second frame (off once the
+                                    * caller sets calibrate / calib_k_milli / calib_min) */
+    int calib_deferred_walk = -1;  /* walk whose first frame skipped the calibration */
+    void *probe_buf = nullptr;     /* calibration probes: tile list + costs (probe_tiles) */
+    size_t probe_cap = 0;          /* bytes */
     int prio_tiles = 1024;         /* heaviest tiles run at raised issue priority */
     float prio_min = 2.0f;         /* ... if they cost more than this x the mean per wave slot */
     std::vector<void *> plan_allocs;   /* tile lists of the current plans */
@@ -175,7 +181,8 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
 void free_plans(crt_hip_scene *sc);
 int sync_device_record(crt_hip_scene *sc, const DeviceScene **out);
 int check_settings(const crt_renderer_settings *st);
-int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t stream);
+int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t stream, bool render = false);
+void warm_code_objects(int device, hipStream_t stream);
 int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const ShardPlan &plan, float *d_out,
                   hipStream_t stream, bool count, unsigned long long *stamps = nullptr);
 int render_into(crt_hip_scene *sc, const crt_renderer_settings *st, float *d_rgb, hipStream_t stream, bool count);

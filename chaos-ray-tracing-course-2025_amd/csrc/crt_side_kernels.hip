@@ -117,4 +117,8 @@ template __global__ void k_unpack<float>(const UnpackBucket *__restrict__, const
 template __global__ void k_unpack<uint8_t>(const UnpackBucket *__restrict__, const uint8_t *__restrict__,
                                            uint8_t *__restrict__, int, Rgb<uint8_t>);
 
+/* empty kernel: its launch at scene creation loads this TU's code object
+ * (warm_code_objects) */
+__global__ void k_warm_side() {}
+
 }  // namespace crt_amd

@@ -702,7 +702,7 @@ __device__ int trace_window(const DeviceScene &s, int r, int sl, bool active, Ve
             const int dd = ms[a] & 255;
             const uint32_t in_m = (uint32_t)__builtin_amdgcn_readlane((int)vreach, dd);
             const uint32_t e_m = in_m & (uint32_t)(P >> (a * R)) & (uint32_t)rmask;
-            vreach = ((ms[a] & 256) != 0) & ((int)__lane_id() == dd + 1) ? e_m : vreach;
+            vreach = (((ms[a] & 256) != 0) & ((int)__lane_id() == dd + 1)) ? e_m : vreach;
             IN |= (unsigned long long)in_m << (a * R);
         }
         const bool my_in = ((IN >> __lane_id()) & 1ull) != 0ull;

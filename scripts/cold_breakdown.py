@@ -54,6 +54,7 @@ def main():
     p.add_argument("--config", default="c2")
     p.add_argument("--runs", type=int, default=3)
     p.add_argument("--out", default=None)
+    p.add_argument("--keep", default=None, help="also write the .crtscene here (for a traced CLI run)")
     a = p.parse_args()
     import bench
     from crt_amd.scene_json import arrays_to_crtscene
@@ -67,6 +68,9 @@ def main():
         doc["settings"]["image_settings"].update(width=w, height=h)
         scene = Path(td) / "scene.crtscene"
         scene.write_text(json.dumps(doc))
+        if a.keep:
+            Path(a.keep).mkdir(parents=True, exist_ok=True)
+            (Path(a.keep) / "scene.crtscene").write_text(json.dumps(doc))
         for _ in range(a.runs):
             t0 = time.perf_counter()
             r = subprocess.run([str(PKG / "bin" / "crt_renderer"), str(scene), str(Path(td) / "o.ppm"), "--gpus", "1",

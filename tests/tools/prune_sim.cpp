@@ -8,6 +8,7 @@
  * order (crt_intersection.cpp:109-136); tests/ also checks it against the
  * oracle.  Built by tests/tools/Makefile; loaded by tests/test_prune.py.
  */
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdint>
@@ -276,3 +277,77 @@ int64_t prune_sim_check_hulls(const crt_scene_desc *desc) {
 }
 
 }  // extern "C"
+
+/* Lockstep coherence of the per-lane camera BVH walk (crt_bvh.h walk_bvh, no
+ * prefetch) over the 8x8 tiles of a frame: the wave loop runs one node step
+ * per active lane per iteration (a lane on a live leaf tests its triangles in
+ * the same iteration).  rays: [h*w, 6] camera rays, row-major.
+ * out[0] wave iterations, [1] iterations whose active lanes all stand on one
+ * node, [2] sum over iterations of distinct nodes, [3] sum of active lanes,
+ * [4] leaf rounds (max triangles of the iteration's leaf lanes),
+ * [5] max iterations of a tile, [6] tiles. */
+extern "C" int bvh_sim_tile_coherence(const crt_scene_desc *desc, const float *rays, int w, int h, uint64_t *out) {
+    HostScene hs;
+    int rc = prepare_scene(desc, hs);
+    if (rc != CRT_OK) return rc;
+    if (hs.bnode_count == 0 && ((rc = build_bvh(hs)) != CRT_OK || (rc = build_proof_tables(hs)) != CRT_OK)) return rc;
+    for (int k = 0; k < 7; ++k) out[k] = 0;
+    const int n = hs.bnode_count;
+    struct L { const BNode *nodes; PruneRay pr; Vec o, d; int i, best; float lim, bt; bool on; };
+    for (int ty = 0; ty < h; ty += 8)
+        for (int tx = 0; tx < w; tx += 8) {
+            L ln[64];
+            int nl = 0;
+            for (int y = ty; y < std::min(h, ty + 8); ++y)
+                for (int x = tx; x < std::min(w, tx + 8); ++x) {
+                    const float *r = rays + 6 * ((int64_t)y * w + x);
+                    L &l = ln[nl++];
+                    l.o = vec(r[0], r[1], r[2]);
+                    l.d = vec(r[3], r[4], r[5]);
+                    l.nodes = bnode_order(hs.bnodes.data(), n, ray_octant(l.d));
+                    l.pr = make_prune_ray(l.o, l.d, hs.prune_origin_max);
+                    l.i = 0;
+                    l.best = -1;
+                    l.lim = INFINITY;
+                    l.bt = 0.f;
+                    l.on = true;
+                }
+            uint64_t it = 0;
+            for (;;) {
+                int act = 0, leafmax = 0;
+                const BNode *addr[64];
+                for (int k = 0; k < nl; ++k) {
+                    L &l = ln[k];
+                    if (!l.on || l.i >= n) { l.on = false; continue; }
+                    addr[act++] = l.nodes + l.i;
+                    const BNode nd = l.nodes[l.i];
+                    if (!bnode_alive(nd, l.pr, l.lim)) { l.i = nd.skip; continue; }
+                    ++l.i;
+                    const int cnt = nd.leaf & 15, first = nd.leaf >> 4;
+                    leafmax = std::max(leafmax, cnt);
+                    for (int q = 0; q < cnt; ++q) {
+                        const DTriGeo g = hs.btri[first + q];
+                        const uint8_t cull = (uint8_t)((uint32_t)hs.btri_id[first + q] >> 31);
+                        float t;
+                        if (tri_hit(l.o, l.d, g, &cull, t) && (l.best < 0 || t < l.bt)) {
+                            l.bt = t;
+                            l.best = 1;
+                            l.lim = t;
+                        }
+                    }
+                }
+                if (act == 0) break;
+                ++it;
+                std::sort(addr, addr + act);
+                const int distinct = (int)(std::unique(addr, addr + act) - addr);
+                out[1] += distinct == 1;
+                out[2] += distinct;
+                out[3] += act;
+                out[4] += leafmax;
+            }
+            out[0] += it;
+            out[5] = std::max<uint64_t>(out[5], it);
+            ++out[6];
+        }
+    return CRT_OK;
+}
