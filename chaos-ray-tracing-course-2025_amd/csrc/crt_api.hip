@@ -129,6 +129,21 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
         ds.bnode_count = hs.bnode_count;
         if ((rc = upload(sc.get(), hs.ktopo, &ds.ktopo)) != CRT_OK) return rc;
     }
+    /* camera bins: frames without recursion only (no reflective / refractive
+     * material, no GI) — every camera frame of the scene is then one
+     * traversal per pixel (k_render_tiles walk 15) */
+    if (hs.bnode_count > 0 && hs.tree_on_host && !sc->has_secondary && !(hs.gi_on && sc->has_diffuse)) {
+        std::vector<CamCand> bins;
+        std::vector<int32_t> off;
+        if ((rc = build_camera_bins(hs, bins, off)) != CRT_OK) return rc;
+        if (!bins.empty()) {
+            if ((rc = upload(sc.get(), bins, &ds.bins)) != CRT_OK) return rc;
+            if ((rc = upload(sc.get(), off, &ds.bin_off)) != CRT_OK) return rc;
+            ds.bin_tx = (hs.width + 7) / 8;
+            sc->bin_count.resize(off.size() - 1);
+            for (size_t c = 0; c + 1 < off.size(); ++c) sc->bin_count[c] = off[c + 1] - off[c];
+        }
+    }
     sc->camera_fast = camera_rays_fast(hs, ds.planes_ok != 0);
     if (ds.bnodes) sc->traversal = 14;   /* camera rays through the BVH too */
     if ((rc = upload(sc.get(), hs.tri_attr, &ds.tri_attr)) != CRT_OK) return rc;
@@ -531,6 +546,17 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         sc->gi_refill = value != 0;
     } else if (k == "gi_machine") {
         sc->gi_machine = value != 0;
+    } else if (k == "bins") {   /* camera bins on / off: the full-frame plan depends on it */
+        if ((value != 0) != (sc->bins_on != 0)) {
+            HIP_TRY(hipDeviceSynchronize());
+            sc->bins_on = value != 0;
+            sc->calib_walk = -1;
+            free_plans(sc);
+            int64_t px = 0;
+            const int rc = make_tile_plan(sc, shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size, 0, 1, &px),
+                                          true, sc->full);
+            if (rc != CRT_OK) return rc;
+        }
 
     } else if (k == "calib_k_milli") {   /* a fixed split threshold k = value / 1000 (calibrate 2) */
         if (value <= 0) return set_error(CRT_E_INVALID, "calib_k_milli must be > 0");

@@ -399,6 +399,79 @@ CRT_HD int verify_topo(const KTopo *topo, const DNode *nodes, const int32_t *slo
     return slot;
 }
 
+/* Step 1 over a camera cell's candidate list (crt_layout.h CamCand) instead
+ * of the BVH: the same closest triangle, t and tie flag as walk_bvh for any
+ * camera ray of the cell.  Every triangle the ray can hit is in the list
+ * (crt_bvh_build.cpp build_camera_bins); a candidate whose hull the ray
+ * misses before lim cannot hit at t <= lim (bnode_alive, as walk_bvh's
+ * boxes); the list is sorted by dmin, a lower bound of any accepted t, so
+ * once dmin > best t no later candidate can hit at t <= best t — not even
+ * tie. */
+CRT_HD bool cand_alive(const CamCand &c, const PruneRay &p, float lim) {
+    BNode n;
+    n.lo_x = c.lo_x; n.hi_x = c.hi_x; n.lo_y = c.lo_y; n.hi_y = c.hi_y; n.lo_z = c.lo_z; n.hi_z = c.hi_z;
+    n.skip = 0;
+    n.leaf = 0;
+    return bnode_alive(n, p, lim);
+}
+
+/* one candidate into the running (best, t, tie, lim) of walk_bvh */
+CRT_HD void cand_test(const CamCand &c, Vec o, Vec d, const PruneRay &pr, int &best, float &best_t, bool &tie,
+                      float &lim) {
+    if (!cand_alive(c, pr, lim)) return;
+    const uint8_t cull = (uint8_t)((uint32_t)c.id >> 31);
+    float t;
+    if (tri_hit(o, d, c.g, &cull, t)) {
+        if (best < 0 || t < best_t) {
+            best_t = t;
+            best = c.id & 0x7fffffff;
+            tie = false;
+            lim = t;
+        } else if (t == best_t) {
+            tie = true;
+        }
+    }
+}
+
+template <bool COUNT>
+CRT_HD int walk_bins(const CamCand *cands, int beg, int end, Vec o, Vec d, const PruneRay &pr, float &best_t,
+                     bool &tie, WalkCounts &c) {
+    int best = -1;
+    float lim = INFINITY;
+    best_t = 0.0f;
+    tie = false;
+    for (int k = beg; k < end; ++k) {
+        const CamCand cc = CRT_LDG(cands, k);
+        if (best >= 0 && cc.dmin > best_t) break;
+        if (COUNT) ++c.nodes;
+        cand_test(cc, o, d, pr, best, best_t, tie, lim);
+    }
+    return best;
+}
+
+/* Steps 2-3 for the closest triangle tri at t (tie: another triangle at the
+ * same t) found by step 1: the reference's slot, or -1. */
+template <bool COUNT>
+CRT_HD int resolve_closest(const DNode *nodes, const PNode *pnodes, int n, const DTriGeo *slots,
+                           const uint8_t *slot_cull, const int32_t *slot_tri, const KTopo *ktopo, bool planes_ok,
+                           Vec o, Vec d, const PruneRay &pr, int tri, float t, bool tie, float &best_t, WalkCounts &c,
+                           bool *fb = nullptr) {
+    best_t = 0.0f;
+    if (tri < 0) return -1;
+    const RayRcp rr = make_ray_rcp(o, d, planes_ok);
+    if (!tie) {
+        const Vec p = vadd(o, vscale(d, t));
+        const int slot = CRT_PROOF_TOPO && ktopo ? verify_topo<COUNT>(ktopo, nodes, slot_tri, tri, o, d, rr, p, c)
+                                                 : verify_kd<COUNT>(nodes, slot_tri, tri, o, d, rr, p, c);
+        if (slot >= 0) {
+            best_t = t;
+            return slot;
+        }
+    }
+    if (fb) *fb = true;
+    return walk_pruned<COUNT>(pnode_order(pnodes, n, ray_octant(d)), n, slots, slot_cull, o, d, rr, pr, best_t, c);
+}
+
 /* The reference's closest hit of one ray (slot in reference visit-order
  * numbering, -1: miss) by steps 1-3.  fb (optional) is set when step 3 ran.
  * Rays with a NaN component miss every cell (each face test reads a NaN
@@ -417,19 +490,25 @@ CRT_HD int trace_bvh_exact(const BNode *bnodes, int bn, const DTriGeo *btri, con
     bool tie = false;
     float t = 0.0f;
     const int tri = walk_bvh<COUNT, PF>(bnode_order(bnodes, bn, oct), bn, btri, btri_id, o, d, pr, t, tie, c);
-    if (tri < 0) return -1;
-    const RayRcp rr = make_ray_rcp(o, d, planes_ok);
-    if (!tie) {
-        const Vec p = vadd(o, vscale(d, t));
-        const int slot = CRT_PROOF_TOPO && ktopo ? verify_topo<COUNT>(ktopo, nodes, slot_tri, tri, o, d, rr, p, c)
-                                                 : verify_kd<COUNT>(nodes, slot_tri, tri, o, d, rr, p, c);
-        if (slot >= 0) {
-            best_t = t;
-            return slot;
-        }
-    }
-    if (fb) *fb = true;
-    return walk_pruned<COUNT>(pnode_order(pnodes, n, oct), n, slots, slot_cull, o, d, rr, pr, best_t, c);
+    return resolve_closest<COUNT>(nodes, pnodes, n, slots, slot_cull, slot_tri, ktopo, planes_ok, o, d, pr, tri, t, tie,
+                                  best_t, c, fb);
+}
+
+/* The same answer for a camera ray of cell [beg, end) through the camera bins. */
+template <bool COUNT>
+CRT_HD int trace_bins_exact(const CamCand *cands, int beg, int end, const DNode *nodes, const PNode *pnodes, int n,
+                            const DTriGeo *slots, const uint8_t *slot_cull, const int32_t *slot_tri,
+                            const KTopo *ktopo, float prune_origin_max, bool planes_ok, Vec o, Vec d, float &best_t,
+                            WalkCounts &c, bool *fb = nullptr) {
+    best_t = 0.0f;
+    if (fb) *fb = false;
+    if (isnan(o.x) || isnan(o.y) || isnan(o.z) || isnan(d.x) || isnan(d.y) || isnan(d.z)) return -1;
+    const PruneRay pr = make_prune_ray(o, d, prune_origin_max);
+    bool tie = false;
+    float t = 0.0f;
+    const int tri = walk_bins<COUNT>(cands, beg, end, o, d, pr, t, tie, c);
+    return resolve_closest<COUNT>(nodes, pnodes, n, slots, slot_cull, slot_tri, ktopo, planes_ok, o, d, pr, tri, t, tie,
+                                  best_t, c, fb);
 }
 
 }  // namespace crt_amd

@@ -88,6 +88,7 @@ struct HostScene {
     /* the BVH proof's tree topology (crt_layout.h KTopo; build_proof_tables) */
     std::vector<KTopo> ktopo;
 
+
     /* root cell (crt_acceleration_tree.cpp:89-94); tree_on_host = false when
      * prepare_scene skipped the tree (built on the device, crt_tree_build.h) */
     float root_box[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -113,6 +114,14 @@ int build_bvh(HostScene &hs);
  * for crt_bvh.h verify_topo (crt_bvh_build.cpp); none (verify_kd then) if a
  * child cell is not its parent's half. */
 int build_proof_tables(HostScene &hs);
+
+/* Camera bins of hs's camera and resolution (crt_bvh_build.cpp): for each 8x8
+ * cell of the frame (row-major, (width + 7) / 8 a row), every triangle a
+ * camera ray of the cell may hit, sorted by a lower bound of its hit
+ * distance: cell c holds bins[off[c] .. off[c + 1]).  Leaves both empty (the
+ * scene then walks the BVH) when the camera is too far for the hull margins,
+ * the camera matrix is singular or the lists would be too long. */
+int build_camera_bins(const HostScene &hs, std::vector<CamCand> &bins, std::vector<int32_t> &off);
 
 /* Mesh prep + (build_tree) the exact tree build and its flattening. */
 int prepare_scene(const crt_scene_desc *desc, HostScene &out, bool build_tree = true);

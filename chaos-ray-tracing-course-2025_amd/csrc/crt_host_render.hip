@@ -127,7 +127,17 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         }
         plan.packed_pixels = total;
     }
-    if (!sc->calib.empty() && !tiles.empty()) {
+    if (bins_active(sc) && !tiles.empty()) {
+        /* camera bins: one wave per 8x8 tile on its cell's list, no split;
+         * the longest lists first */
+        const int tx = (W + 7) / 8;
+        auto cost = [&](const Tile &t) {
+            const int cx = t.x / 8, cy = t.y / 8;
+            return (t.x % 8) + t.w <= 8 && (t.y % 8) + t.h <= 8 ? sc->bin_count[(size_t)cy * tx + cx] : INT32_MAX;
+        };
+        std::stable_sort(tiles.begin(), tiles.end(), [&](const Tile &a, const Tile &b) { return cost(a) > cost(b); });
+        plan.cost.clear();
+    } else if (!sc->calib.empty() && !tiles.empty()) {
         /* measured costs: split as calibrated, heaviest first */
         const int tx = (W + 7) / 8;
         std::vector<std::pair<float, Tile>> out;
@@ -400,6 +410,7 @@ int plan_walk(const crt_hip_scene *sc, const crt_renderer_settings *st) {
     const bool full = gi || sc->has_secondary;
     if (gi) return -1;
     if (full) return sc->wavefront ? camera_walk(sc, sc->traversal == 8 ? 8 : 7) : -1;
+    if (bins_active(sc)) return -1;   /* camera bins: no plan to measure */
     return camera_walk(sc, sc->traversal);
 }
 
@@ -842,7 +853,13 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         case 8: if (count) CRT_LAUNCH_T(false, 0, 8, true); else CRT_LAUNCH_T(false, 0, 8, false); break;
         case 12: if (count) CRT_LAUNCH_T(false, 0, 12, true); else CRT_LAUNCH_T(false, 0, 12, false); break;
         case 13: if (count) CRT_LAUNCH_T(false, 0, 13, true); else CRT_LAUNCH_T(false, 0, 13, false); break;
-        case 14: if (count) CRT_LAUNCH_T(false, 0, 14, true); else CRT_LAUNCH_T(false, 0, 14, false); break;
+        case 14:
+            if (bins_active(sc)) {
+                if (count) CRT_LAUNCH_T(false, 0, 15, true); else CRT_LAUNCH_T(false, 0, 15, false);
+            } else {
+                if (count) CRT_LAUNCH_T(false, 0, 14, true); else CRT_LAUNCH_T(false, 0, 14, false);
+            }
+            break;
         default: return set_error(CRT_E_INVALID, "no such camera walk");
         }
     } else if (gi && (trav == 4 || trav == 10 || trav == 14) && sc->gi_refill && sc->d_next_px && !stamps && frames <= 64) {

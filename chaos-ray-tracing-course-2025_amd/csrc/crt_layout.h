@@ -99,6 +99,21 @@ struct alignas(16) DTriGeo {
 };
 static_assert(sizeof(DTriGeo) == 48, "DTriGeo must be 48 B");
 
+/* Camera-bin candidate (crt_bvh.h walk_bins, crt_bvh_build.cpp
+ * build_camera_bins): a triangle listed in an 8x8-pixel cell of the frame
+ * because a camera ray of that cell may hit it.  The hull box is the
+ * triangle's conservative hull (BNode's boxes are unions of the same hulls);
+ * dmin is a lower bound on the t of any hit the reference's triangle test
+ * accepts for a camera ray (the cell's list is sorted by it); g and id are
+ * the triangle as the BVH's triangle arrays hold it (id | culling << 31). */
+struct alignas(16) CamCand {
+    float lo_x, hi_x, lo_y, hi_y;
+    float lo_z, hi_z;
+    float dmin;
+    int32_t id;
+    DTriGeo g;
+};
+
 struct alignas(16) DTriAttr {
     int32_t i0, i1, i2;
     int32_t mat_flags;   /* material index | (smooth_shading << 31) */
@@ -146,6 +161,12 @@ struct DeviceScene {
     const int32_t *btri_id;
     /* the proof's tree topology (KTopo); null when the tree lives on the device only */
     const KTopo *ktopo;
+    /* camera bins (crt_bvh.h walk_bins): per 8x8 cell of the frame
+     * (bin_tx cells a row), candidates bins[bin_off[c] .. bin_off[c + 1]);
+     * null when not built */
+    const CamCand *bins;
+    const int32_t *bin_off;
+    int32_t bin_tx;
     const DTriAttr *tri_attr;
     const DVec4 *vnormal;
     const DVec4 *vuv;

@@ -13,7 +13,7 @@
 namespace crt_amd {
 
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW>
-__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT_WINDOW_WAVES : TRAV == 12 ? CRT_PACKET_WAVES : TRAV == 14 && !FULL ? CRT_BVH_WAVES : (FULL && MAXF == 4 ? CRT_GI_WAVES : 1)))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
+__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT_WINDOW_WAVES : TRAV == 12 ? CRT_PACKET_WAVES : (TRAV == 14 || TRAV == 15) && !FULL ? CRT_BVH_WAVES : (FULL && MAXF == 4 ? CRT_GI_WAVES : 1)))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
                                                   const Tile *__restrict__ tiles,
                                                       int ntiles, float *__restrict__ out,
                                                       unsigned long long *__restrict__ counters,
@@ -79,8 +79,39 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             return;
         }
     }
+    if constexpr (TRAV == 15 && !FULL && !SHADOW) {
+        /* a tile inside one 8x8 camera-bins cell: the cell's candidate list */
+        const int tx0 = uniform_i(tl.x), ty0 = uniform_i(tl.y), tw = uniform_i(tl.w), th = uniform_i(tl.h);
+        if ((tx0 & 7) + tw <= 8 && (ty0 & 7) + th <= 8) {
+            const int cell = (ty0 >> 3) * s.bin_tx + (tx0 >> 3);
+            const int beg = load_scalar(s.bin_off, cell), end = load_scalar(s.bin_off, cell + 1);
+            const int lx = lane & 7, ly = lane >> 3;
+            const bool act = lx < tw && ly < th;
+            Vec o, d;
+            camera_ray(s, tx0 + (act ? lx : 0), ty0 + (act ? ly : 0), o, d);
+            LaneCounts cw = {};
+            float t;
+            const int slot = trace_bins_wave<COUNT>(s, beg, end, act, o, d, t, cw);
+            if (act) {
+                const Vec c = shade_primary(s, st, o, d, slot, t);
+                float *pxo = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
+                pxo[0] = c.x;
+                pxo[1] = c.y;
+                pxo[2] = c.z;
+            }
+            if (stamps && lane == 0) stamps[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
+            if (COUNT) {
+                atomicAdd(&counters[0], (unsigned long long)cw.traversals);
+                atomicAdd(&counters[1], (unsigned long long)cw.nodes);
+                atomicAdd(&counters[2], (unsigned long long)cw.tris);
+                atomicAdd(&counters[3], (unsigned long long)cw.hits);
+                if (lane == 0) atomicAdd(&counters[7], 1ull);
+            }
+            return;
+        }
+    }
 #if CRT_BVH_WINDOW
-    if constexpr (TRAV == 14 && !FULL && !SHADOW) {
+    if constexpr ((TRAV == 14 || TRAV == 15) && !FULL && !SHADOW) {
         /* tiles of <= 16 rays (the measured plan's splits of heavy tiles):
          * each ray walked by a group of 64/R lanes (crt_walks.h trace_bvh_window) */
         const int tw = uniform_i(tl.w), th = uniform_i(tl.h);
@@ -129,8 +160,9 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
         c = shade_shadowed<TRAV, COUNT>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt,
                                         &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px);
     else
-        c = shade_pixel<FULL, MAXF, TRAV, SEC, COUNT, SHADOW>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0),
-                                                              cnt, &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px);
+        c = shade_pixel<FULL, MAXF, (TRAV == 15 ? 14 : TRAV), (SEC == 15 ? 14 : SEC), COUNT, SHADOW>(
+            s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt, &coop[kCoop ? (threadIdx.x >> 6) : 0],
+            has_px);
     if (has_px) {
         float *px = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
         px[0] = c.x;

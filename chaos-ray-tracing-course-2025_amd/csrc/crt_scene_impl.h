@@ -131,6 +131,7 @@ struct crt_hip_scene {
     int wave_slots = 6144;   /* CUs x 4 SIMDs x 6 resident render waves */
     int secondary = 0;       /* walk for secondary rays: 0 = by frame, 4, 10 (env CRT_SECONDARY) */
     std::vector<float> tile_work;  /* per 8x8 tile of the full frame */
+    std::vector<int32_t> bin_count;   /* camera-bins candidates per 8x8 cell (empty: no bins) */
     /* measured-cost tile plan (calibrate_plan): per 8x8 tile of the full frame,
      * the sub-tiles it is split into and their probed costs */
     struct SubTile { int32_t dx, dy, w, h; float cost; };
@@ -149,6 +150,7 @@ struct crt_hip_scene {
                                     * current plan and the calibration runs on its second frame (off once the
                                     * caller sets calibrate / calib_k_milli / calib_min) */
     int calib_deferred_walk = -1;  /* walk whose first frame skipped the calibration */
+    int bins_on = 1;               /* camera frames take the camera bins where built (walk 15; option "bins") */
     void *probe_buf = nullptr;     /* calibration probes: tile list + costs (probe_tiles) */
     size_t probe_cap = 0;          /* bytes */
     int prio_tiles = 1024;         /* heaviest tiles run at raised issue priority */
@@ -183,6 +185,9 @@ int sync_device_record(crt_hip_scene *sc, const DeviceScene **out);
 int check_settings(const crt_renderer_settings *st);
 int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t stream, bool render = false);
 void warm_code_objects(int device, hipStream_t stream);
+/* camera frames of this scene walk the camera bins (walk 15): built, enabled,
+ * and the default camera walk selected */
+inline bool bins_active(const crt_hip_scene *sc) { return sc->ds.bins && sc->bins_on && sc->traversal == 14; }
 int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const ShardPlan &plan, float *d_out,
                   hipStream_t stream, bool count, unsigned long long *stamps = nullptr);
 int render_into(crt_hip_scene *sc, const crt_renderer_settings *st, float *d_rgb, hipStream_t stream, bool count);

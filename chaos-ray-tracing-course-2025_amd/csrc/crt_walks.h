@@ -983,6 +983,46 @@ __device__ int trace_bvh_window(const DeviceScene &s, int sl, bool act, Vec o, V
     return slot;
 }
 
+/* Camera rays of one camera-bins cell (crt_bvh.h walk_bins / trace_bins_exact)
+ * with the whole wave on the cell's candidate list: the loop over candidates
+ * is wave-uniform and each record is read once by scalar loads into SGPRs
+ * (one stream of contiguous 80-B records, no dependent loads), each lane
+ * running walk_bins on its own ray and leaving the loop once the next
+ * candidate's dmin exceeds its best t; the wave leaves when every lane has.
+ * Then the proof / fallback per lane (resolve_closest).  act: the lane has a
+ * pixel.  Returns the reference's slot (-1: miss). */
+template <bool COUNT>
+__device__ int trace_bins_wave(const DeviceScene &s, int beg, int end, bool act, Vec o, Vec d, float &best_t,
+                               LaneCounts &c) {
+    best_t = 0.0f;
+    const bool nan_ray = isnan(o.x) || isnan(o.y) || isnan(o.z) || isnan(d.x) || isnan(d.y) || isnan(d.z);
+    if (COUNT && act) ++c.traversals;
+    const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
+    int best = -1;
+    float bt = 0.0f, lim = INFINITY;
+    bool tie = false, live = act && !nan_ray;
+    WalkCounts wc = {0u, 0u};
+    for (int k = beg; k < end; ++k) {
+        const CamCand cc = load_scalar(s.bins, k);
+        live = live && !(best >= 0 && cc.dmin > bt);
+        if (__ballot(live) == 0ull) break;
+        if (live) {
+            if (COUNT) ++wc.nodes;
+            cand_test(cc, o, d, pr, best, bt, tie, lim);
+        }
+    }
+    int slot = -1;
+    if (act && !nan_ray)
+        slot = resolve_closest<COUNT>(s.nodes, s.pnodes, s.node_count, s.slots, s.slot_cull, s.slot_tri, s.ktopo,
+                                      s.planes_ok != 0, o, d, pr, best, bt, tie, best_t, wc);
+    if (COUNT) {
+        c.nodes += wc.nodes;
+        c.tris += wc.tris;
+        if (slot >= 0) ++c.hits;
+    }
+    return slot;
+}
+
 /* Walks (TRAV), all bit-identical in result:
  *   7  packet walk in the reference's node order (work counters = the reference's)
  *   8  pruned packet walk (exact t-pruning), any camera ray
@@ -991,6 +1031,7 @@ __device__ int trace_bvh_window(const DeviceScene &s, int sl, bool act, Vec o, V
  *   4  cooperative walk in the reference's node order (scattered rays)
  *   10 pruned cooperative walk
  *   14 per-lane BVH walk + proof on the reference's tree (scattered rays, crt_bvh.h)
+ *   15 camera bins (trace_bins_wave; k_render_tiles only, 14 elsewhere)
  * PF: the BVH walk loads both successors ahead (crt_bvh.h walk_bvh). */
 template <int TRAV>
 constexpr bool kIsCoop = TRAV == 4 || TRAV == 10;

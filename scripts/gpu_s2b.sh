@@ -1,5 +1,5 @@
 #!/bin/bash
-# Session-2 GPU check: GPU tests, GI angle bitmap A/B on C4, cold first call.
+# Session-2 GPU steps (STEPS=tests,gi,cold,clitrace,bins,bench,shards,timeline), each under its own limit.
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out/${TAG:-s2b}; mkdir -p $OUT
@@ -18,4 +18,8 @@ run() {
 [[ ${STEPS:-tests} == *cold* ]] && run cold_c2 300 python3 scripts/cold_breakdown.py --config c2 --out $OUT/cold_c2.json --keep $OUT/scene
 [[ ${STEPS:-tests} == *clitrace* ]] && run cli_trace 200 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --stats -d $OUT/clitrace -o run --output-format csv -- chaos-ray-tracing-course-2025_amd/bin/crt_renderer $OUT/scene/scene.crtscene $OUT/scene/out.ppm --gpus 1
 [[ ${STEPS:-tests} == *cold* ]] && run cold_parts 200 python3 scripts/cold_parts.py
+[[ ${STEPS:-tests} == *bins* ]] && run c2_bins 300 python3 scripts/render_loop.py --frames 40 --opt bins=0,1 --counts
+[[ ${STEPS:-tests} == *bench* ]] && run bench_c2 600 python3 bench.py --steps 50 --warmup 5
+[[ ${STEPS:-tests} == *shards* ]] && run shards_c2 300 python3 scripts/shard_times.py --config c2 --reps 20 --out $OUT/shards_c2.json
+[[ ${STEPS:-tests} == *timeline* ]] && run timeline_c2 300 python3 scripts/wave_timeline.py --out $OUT/timeline_c2.json
 exit 0

@@ -133,3 +133,30 @@ def test_topology_proof_equals_descent(sim, oracle, name, w, h):  # noqa: F811
     assert sim.bvh_sim_proof_check(C.cast(_desc_ptr(sc), _P), rays.ctypes.data, len(rays), out.ctypes.data) == 0
     assert out[0] > 0 and out[1] == 0, out
     assert out[2] > 0.95 * out[0], out
+
+
+BINS_CASES = [("14-01-acceleration-tree__scene1", None), ("14-01-acceleration-tree__scene0", None),
+              ("12-01-textures__scene4", None), ("09-02-diffuse-smooth-shading__scene3", None),
+              ("11-01-refractive__scene0", None), ("11-01-refractive__scene8", None),
+              ("15-01-conclusion__scene2", None), ("14-01-acceleration-tree__scene1", (333, 177)),
+              ("15-01-conclusion__scene2", (1001, 643))]
+
+
+@pytest.mark.parametrize("name,size", BINS_CASES)
+def test_camera_bins_equal_bvh_walk(sim, name, size):  # noqa: F811
+    """Camera bins (crt_bvh_build.cpp build_camera_bins, crt_bvh.h walk_bins):
+    every camera ray of the frame gets the BVH walk's t bits and tie flag, and
+    its triangle where there is no tie — so the proof and the fallback, shared
+    with the BVH walk (resolve_closest), see the same inputs."""
+    from crt_amd.native import _desc_ptr
+    sc = scene_npz(name)
+    if size:
+        sc = sc.set_resolution(*size)
+    sim.bins_sim_check.argtypes = [_P, _P]
+    sim.bins_sim_check.restype = C.c_int
+    out = np.zeros(7, np.uint64)
+    assert sim.bins_sim_check(C.cast(_desc_ptr(sc), _P), out.ctypes.data) == 0
+    rays, diff, tested, _, _, cands, built = (int(x) for x in out)
+    assert built == 1
+    assert rays > 0 and diff == 0, f"{name}: {diff} of {rays} camera rays differ"
+    assert tested < 8 * rays   # the lists are short: a few candidates per ray

@@ -294,3 +294,27 @@ def test_gi_pixel_refill_bit_identical(N, oracle, w, h):
         g = N.HipScene(sc, secondary=walk)
         assert g.count_work(st) == g.count_work(st)
         assert np.array_equal(bits(g.render(st)), bits(want)), walk
+
+
+BINS_FRAMES = [("14-01-acceleration-tree__scene1", 1920, 1080), ("14-01-acceleration-tree__scene0", 480, 270),
+               ("12-01-textures__scene4", 480, 270), ("09-02-diffuse-smooth-shading__scene3", 480, 270),
+               ("13-01-optimizations__scene0", 640, 360), ("14-01-acceleration-tree__scene1", 333, 177)]
+
+
+@pytest.mark.parametrize("name,w,h", BINS_FRAMES)
+def test_camera_bins_frames_bit_exact(N, oracle, name, w, h):
+    """Camera frames through the camera bins (walk 15, the default for scenes
+    without recursion): bit-identical to the per-lane BVH walk (option bins 0)
+    and to the oracle, same traversal and hit counts; odd sizes leave partial
+    tiles at the right and bottom edges."""
+    sc = scene_npz(name).set_resolution(w, h)
+    st = N.RendererSettings.default()
+    g = N.HipScene(sc)
+    assert g.plan_info()["calib_k"] == 0.0   # no probes: one wave per 8x8 cell
+    a = g.render(st)
+    b = N.HipScene(sc, bins=0).render(st)
+    want = oracle.OracleScene(sc).render(st)
+    assert np.array_equal(bits(a), bits(want))
+    assert np.array_equal(bits(b), bits(want))
+    ca, cb = g.count_work(st), N.HipScene(sc, bins=0).count_work(st)
+    assert ca["traversals"] == cb["traversals"] == w * h and ca["hits"] == cb["hits"]

@@ -351,3 +351,99 @@ extern "C" int bvh_sim_tile_coherence(const crt_scene_desc *desc, const float *r
         }
     return CRT_OK;
 }
+
+/* Camera bins against the BVH walk (crt_bvh.h walk_bins vs walk_bvh) on every
+ * camera ray of the frame at the scene's resolution: the same t bits and tie
+ * flag, and the same closest triangle where there is no tie (with one, the
+ * triangle is not used: crt_bvh.h resolve_closest takes the exact kd walk).  out: [0] rays, [1] rays that differ,
+ * [2] candidates tested, [3] most candidates tested by one ray, [4] cells,
+ * [5] listed candidates, [6] 1 if bins were built. */
+extern "C" int bins_sim_check(const crt_scene_desc *desc, uint64_t *out) {
+    HostScene hs;
+    int rc = prepare_scene(desc, hs);
+    if (rc != CRT_OK) return rc;
+    if (hs.bnode_count == 0 && ((rc = build_bvh(hs)) != CRT_OK || (rc = build_proof_tables(hs)) != CRT_OK)) return rc;
+    std::vector<CamCand> bins;
+    std::vector<int32_t> off;
+    if ((rc = build_camera_bins(hs, bins, off)) != CRT_OK) return rc;
+    for (int k = 0; k < 7; ++k) out[k] = 0;
+    if (bins.empty()) return CRT_OK;
+    out[6] = 1;
+    out[4] = off.size() - 1;
+    out[5] = bins.size();
+    DeviceScene ds{};
+    std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
+    std::memcpy(ds.cam_rot, hs.cam_rot, sizeof ds.cam_rot);
+    ds.width = hs.width;
+    ds.height = hs.height;
+    ds.aspect = hs.aspect;
+    ds.tan_half_fov = hs.tan_half_fov;
+    const int tx = (hs.width + 7) / 8;
+    for (int y = 0; y < hs.height; ++y)
+        for (int x = 0; x < hs.width; ++x) {
+            Vec o, d;
+            camera_ray(ds, x, y, o, d);
+            const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
+            WalkCounts w = {0u, 0u}, wb = {0u, 0u};
+            float t1 = 0.f, t2 = 0.f;
+            bool tie1 = false, tie2 = false;
+            const int a = walk_bvh<true>(bnode_order(hs.bnodes.data(), hs.bnode_count, ray_octant(d)), hs.bnode_count,
+                                         hs.btri.data(), hs.btri_id.data(), o, d, pr, t1, tie1, w);
+            const int cell = (y / 8) * tx + x / 8;
+            const int b = walk_bins<true>(bins.data(), off[cell], off[cell + 1], o, d, pr, t2, tie2, wb);
+            ++out[0];
+            uint32_t u1, u2;
+            std::memcpy(&u1, &t1, 4);
+            std::memcpy(&u2, &t2, 4);
+            /* with a tie the triangle is not used (the exact kd walk decides) */
+            if ((a < 0) != (b < 0) || (a >= 0 && (u1 != u2 || tie1 != tie2 || (!tie1 && a != b)))) ++out[1];
+            out[2] += wb.nodes;
+            out[3] = std::max<uint64_t>(out[3], wb.nodes);
+        }
+    return CRT_OK;
+}
+
+/* debugging aid: the first `cap` differing rays of bins_sim_check as
+ * {x, y, bvh tri, bins tri, bvh t bits, bins t bits, tie bvh, tie bins, bvh tri listed in the cell} */
+extern "C" int bins_sim_diffs(const crt_scene_desc *desc, int64_t *rows, int cap) {
+    HostScene hs;
+    int rc = prepare_scene(desc, hs);
+    if (rc != CRT_OK) return rc;
+    if (hs.bnode_count == 0 && ((rc = build_bvh(hs)) != CRT_OK || (rc = build_proof_tables(hs)) != CRT_OK)) return rc;
+    std::vector<CamCand> bins;
+    std::vector<int32_t> off;
+    if ((rc = build_camera_bins(hs, bins, off)) != CRT_OK) return rc;
+    if (bins.empty()) return 0;
+    DeviceScene ds{};
+    std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
+    std::memcpy(ds.cam_rot, hs.cam_rot, sizeof ds.cam_rot);
+    ds.width = hs.width;
+    ds.height = hs.height;
+    ds.aspect = hs.aspect;
+    ds.tan_half_fov = hs.tan_half_fov;
+    const int tx = (hs.width + 7) / 8;
+    int n = 0;
+    for (int y = 0; y < hs.height && n < cap; ++y)
+        for (int x = 0; x < hs.width && n < cap; ++x) {
+            Vec o, d;
+            camera_ray(ds, x, y, o, d);
+            const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
+            WalkCounts w = {0u, 0u};
+            float t1 = 0.f, t2 = 0.f;
+            bool tie1 = false, tie2 = false;
+            const int a = walk_bvh<false>(bnode_order(hs.bnodes.data(), hs.bnode_count, ray_octant(d)), hs.bnode_count,
+                                          hs.btri.data(), hs.btri_id.data(), o, d, pr, t1, tie1, w);
+            const int cell = (y / 8) * tx + x / 8;
+            const int b = walk_bins<false>(bins.data(), off[cell], off[cell + 1], o, d, pr, t2, tie2, w);
+            uint32_t u1, u2;
+            std::memcpy(&u1, &t1, 4);
+            std::memcpy(&u2, &t2, 4);
+            if ((a < 0) != (b < 0) || (a >= 0 && (u1 != u2 || tie1 != tie2 || (!tie1 && a != b)))) {
+                int listed = 0;
+                for (int k = off[cell]; k < off[cell + 1]; ++k) listed |= (bins[k].id & 0x7fffffff) == a;
+                int64_t *r = rows + 9 * n++;
+                r[0] = x; r[1] = y; r[2] = a; r[3] = b; r[4] = u1; r[5] = u2; r[6] = tie1; r[7] = tie2; r[8] = listed;
+            }
+        }
+    return n;
+}
