@@ -10,6 +10,10 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -18,6 +22,116 @@
 
 #include "crt_scene_impl.h"
 #include "crt_tree_build.h"
+
+namespace {
+
+/* Persistent host threads for the host half of a staged copy (a per-call
+ * thread start would cost more than the copy chunk it serves). */
+class CopyPool {
+public:
+    explicit CopyPool(int n) {
+        for (int i = 0; i < n; ++i) th_.emplace_back([this]() { loop(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    /* f(0 .. n-1) over the pool and the calling thread; returns when all ran */
+    void run(int n, const std::function<void(int)> &f) {
+        std::unique_lock<std::mutex> l(mu_);
+        job_ = &f;
+        n_ = n;
+        next_ = 0;
+        done_ = 0;
+        cv_.notify_all();
+        while (next_ < n_) {
+            const int i = next_++;
+            l.unlock();
+            f(i);
+            l.lock();
+            ++done_;
+        }
+        done_cv_.wait(l, [&]() { return done_ == n_; });
+        job_ = nullptr;
+    }
+
+private:
+    void loop() {
+        std::unique_lock<std::mutex> l(mu_);
+        for (;;) {
+            cv_.wait(l, [&]() { return stop_ || (job_ && next_ < n_); });
+            if (stop_) return;
+            const int i = next_++;
+            const std::function<void(int)> *f = job_;
+            l.unlock();
+            (*f)(i);
+            l.lock();
+            if (++done_ == n_) done_cv_.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::vector<std::thread> th_;
+    const std::function<void(int)> *job_ = nullptr;
+    int n_ = 0, next_ = 0, done_ = 0;
+    bool stop_ = false;
+};
+
+constexpr int kStageChunks = 8;
+
+CopyPool &copy_pool() {
+    static CopyPool pool((int)std::max(1u, std::min(7u, std::thread::hardware_concurrency())));
+    return pool;
+}
+
+bool host_pinned(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+/* The scene's image d_out into host memory, queued behind the frame on the
+ * scene's stream.  Pinned (or registered) memory: one DMA.  Pageable memory:
+ * the runtime would first page-lock the caller's buffer (~10 ms for a
+ * 1920x1080 image the first time, profiles/r03/cold), so the image goes
+ * through the scene's pinned staging copy in chunks instead, each chunk
+ * copied on to the caller's buffer by a pool thread as soon as its DMA is
+ * done. */
+int image_to_host(crt_hip_scene *sc, float *dst, size_t nfl) {
+    const size_t bytes = nfl * sizeof(float);
+    if (!sc->h_stage || host_pinned(dst)) {
+        HIP_TRY(hipMemcpyAsync(dst, sc->d_out, bytes, hipMemcpyDeviceToHost, sc->stream));
+        HIP_TRY(hipStreamSynchronize(sc->stream));
+        return CRT_OK;
+    }
+    const size_t step = ((bytes + kStageChunks - 1) / kStageChunks + 4095) & ~size_t(4095);
+    int nc = 0;
+    for (size_t off = 0; off < bytes; off += step, ++nc) {
+        const size_t len = std::min(step, bytes - off);
+        HIP_TRY(hipMemcpyAsync(reinterpret_cast<char *>(sc->h_stage) + off, reinterpret_cast<const char *>(sc->d_out) + off,
+                               len, hipMemcpyDeviceToHost, sc->stream));
+        HIP_TRY(hipEventRecord(sc->stage_ev[(size_t)nc], sc->stream));
+    }
+    std::vector<hipError_t> err((size_t)nc, hipSuccess);
+    copy_pool().run(nc, [&](int i) {
+        const size_t off = (size_t)i * step, len = std::min(step, bytes - off);
+        err[(size_t)i] = hipEventSynchronize(sc->stage_ev[(size_t)i]);
+        if (err[(size_t)i] == hipSuccess)
+            std::memcpy(reinterpret_cast<char *>(dst) + off, reinterpret_cast<const char *>(sc->h_stage) + off, len);
+    });
+    for (hipError_t e : err)
+        if (e != hipSuccess) return set_error(CRT_E_HIP, std::string("image copy: ") + hipGetErrorString(e));
+    return CRT_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -189,7 +303,17 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     {
         const DeviceScene *d = nullptr;
         if ((rc = sync_device_record(sc.get(), &d)) != CRT_OK) return rc;
-        if (!sc->grid_empty) HIP_TRY(hipMalloc(&sc->d_out, (size_t)hs.width * hs.height * 3 * sizeof(float)));
+        if (!sc->grid_empty) {
+            const size_t bytes = (size_t)hs.width * hs.height * 3 * sizeof(float);
+            HIP_TRY(hipMalloc(&sc->d_out, bytes));
+            /* the staging image of copies into pageable memory (image_to_host) */
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&sc->h_stage), bytes, hipHostMallocDefault));
+            sc->stage_ev.assign(kStageChunks, nullptr);
+            for (auto &e : sc->stage_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            (void)copy_pool();
+            /* the first DMA into a fresh pinned buffer pays its one-time mapping */
+            HIP_TRY(hipMemcpy(sc->h_stage, sc->d_out, bytes, hipMemcpyDeviceToHost));
+        }
         unsigned long long probe[16];
         HIP_TRY(hipMemcpy(probe, sc->d_counters, sizeof probe, hipMemcpyDeviceToHost));
     }
@@ -251,6 +375,9 @@ void crt_hip_scene_destroy(crt_hip_scene *sc) {
     for (auto &kv : sc->unpack_plans) (void)hipFree(kv.second.first);
     for (auto &kv : sc->compact_unpack) (void)hipFree(kv.second.first);
     if (sc->probe_buf) (void)hipFree(sc->probe_buf);
+    if (sc->h_stage) (void)hipHostFree(sc->h_stage);
+    for (hipEvent_t e : sc->stage_ev)
+        if (e) (void)hipEventDestroy(e);
     if (sc->ev_start) (void)hipEventDestroy(sc->ev_start);
     if (sc->ev_stop) (void)hipEventDestroy(sc->ev_stop);
     if (sc->stream) (void)hipStreamDestroy(sc->stream);
@@ -272,6 +399,7 @@ int crt_hip_render_device(crt_hip_scene *sc, const crt_renderer_settings *st, fl
     return render_into(sc, st, d_rgb, s, false);
 }
 
+
 int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rgb_out, crt_render_stats *stats) {
     if (!sc || !rgb_out) return set_error(CRT_E_INVALID, "null argument");
     int rc = check_settings(st);
@@ -286,12 +414,10 @@ int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rg
     };
     rc = frame();
     if (rc != CRT_OK) return rc;
-    HIP_TRY(hipMemcpyAsync(rgb_out, sc->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
-    HIP_TRY(hipStreamSynchronize(sc->stream));
+    if ((rc = image_to_host(sc, rgb_out, nfl)) != CRT_OK) return rc;
     if (multi ? multi_overflowed(sc) : wf_overflowed(sc->wf, true)) {   /* recorded level sizes did not hold: render again with read-backs */
         if ((rc = frame()) != CRT_OK) return rc;
-        HIP_TRY(hipMemcpyAsync(rgb_out, sc->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
-        HIP_TRY(hipStreamSynchronize(sc->stream));
+        if ((rc = image_to_host(sc, rgb_out, nfl)) != CRT_OK) return rc;
     }
     if (stats) {
         std::memset(stats, 0, sizeof *stats);

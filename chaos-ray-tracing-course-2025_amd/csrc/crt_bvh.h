@@ -406,7 +406,9 @@ CRT_HD int verify_topo(const KTopo *topo, const DNode *nodes, const int32_t *slo
  * misses before lim cannot hit at t <= lim (bnode_alive, as walk_bvh's
  * boxes); the list is sorted by dmin, a lower bound of any accepted t, so
  * once dmin > best t no later candidate can hit at t <= best t — not even
- * tie. */
+ * tie; a candidate whose pixel mask lacks the ray's pixel (bit = 8 y + x in
+ * the cell) cannot be hit by it, and once no later one has the pixel
+ * (rest) the walk is over. */
 CRT_HD bool cand_alive(const CamCand &c, const PruneRay &p, float lim) {
     BNode n;
     n.lo_x = c.lo_x; n.hi_x = c.hi_x; n.lo_y = c.lo_y; n.hi_y = c.hi_y; n.lo_z = c.lo_z; n.hi_z = c.hi_z;
@@ -415,10 +417,11 @@ CRT_HD bool cand_alive(const CamCand &c, const PruneRay &p, float lim) {
     return bnode_alive(n, p, lim);
 }
 
-/* one candidate into the running (best, t, tie, lim) of walk_bvh */
-CRT_HD void cand_test(const CamCand &c, Vec o, Vec d, const PruneRay &pr, int &best, float &best_t, bool &tie,
+/* one candidate into the running (best, t, tie, lim) of walk_bvh; true when
+ * the triangle test ran */
+CRT_HD bool cand_test(const CamCand &c, Vec o, Vec d, const PruneRay &pr, int &best, float &best_t, bool &tie,
                       float &lim) {
-    if (!cand_alive(c, pr, lim)) return;
+    if (!cand_alive(c, pr, lim)) return false;
     const uint8_t cull = (uint8_t)((uint32_t)c.id >> 31);
     float t;
     if (tri_hit(o, d, c.g, &cull, t)) {
@@ -431,10 +434,31 @@ CRT_HD void cand_test(const CamCand &c, Vec o, Vec d, const PruneRay &pr, int &b
             tie = true;
         }
     }
+    return true;
+}
+
+/* cand_test's verdict without branches (for interleaved tests): the
+ * triangle test's conjuncts exactly as tri_hit orders them (crt_device.h,
+ * crt_intersection.cpp:47-93) and the hull against lim; t valid when true. */
+CRT_HD bool cand_hit_bf(const CamCand &c, Vec o, Vec d, const PruneRay &pr, float lim, float &t) {
+    const DTriGeo &g = c.g;
+    const Vec N = vec(g.nx, g.ny, g.nz);
+    const Vec v0 = vec(g.v0x, g.v0y, g.v0z), v1 = vec(g.v1x, g.v1y, g.v1z), v2 = vec(g.v2x, g.v2y, g.v2z);
+    const float rn = vdot(N, d);
+    const float op = vdot(N, vsub(v0, o));
+    const bool cull = ((uint32_t)c.id >> 31) != 0u;
+    t = op / rn;
+    const Vec e0 = vsub(v1, v0), e1 = vsub(v2, v1), e2 = vsub(v0, v2);
+    const Vec p = vadd(o, vscale(d, t));
+    const Vec v0p = vsub(p, v0), v1p = vsub(p, v1), v2p = vsub(p, v2);
+    return (int)cand_alive(c, pr, lim) & (int)!(fabsf(rn) < 1e-6f) & (int)((op < 0.0f) | !cull) &
+           (int)!(opposite_signs(op, rn) && fabsf(rn) < 2.0f) & (int)!(t < 0.0f) &
+           (int)(vdot(N, vcross(e0, v0p)) >= 0.0f) & (int)(vdot(N, vcross(e1, v1p)) >= 0.0f) &
+           (int)(vdot(N, vcross(e2, v2p)) >= 0.0f);
 }
 
 template <bool COUNT>
-CRT_HD int walk_bins(const CamCand *cands, int beg, int end, Vec o, Vec d, const PruneRay &pr, float &best_t,
+CRT_HD int walk_bins(const CamCand *cands, int beg, int end, int bit, Vec o, Vec d, const PruneRay &pr, float &best_t,
                      bool &tie, WalkCounts &c) {
     int best = -1;
     float lim = INFINITY;
@@ -442,9 +466,12 @@ CRT_HD int walk_bins(const CamCand *cands, int beg, int end, Vec o, Vec d, const
     tie = false;
     for (int k = beg; k < end; ++k) {
         const CamCand cc = CRT_LDG(cands, k);
+        if (((cc.rest >> bit) & 1ull) == 0ull) break;          /* no later candidate covers this pixel */
         if (best >= 0 && cc.dmin > best_t) break;
+        if (((cc.mask >> bit) & 1ull) == 0ull) continue;       /* not this pixel's */
         if (COUNT) ++c.nodes;
-        cand_test(cc, o, d, pr, best, best_t, tie, lim);
+        const bool tested = cand_test(cc, o, d, pr, best, best_t, tie, lim);
+        if (COUNT && tested) ++c.tris;
     }
     return best;
 }
@@ -496,7 +523,7 @@ CRT_HD int trace_bvh_exact(const BNode *bnodes, int bn, const DTriGeo *btri, con
 
 /* The same answer for a camera ray of cell [beg, end) through the camera bins. */
 template <bool COUNT>
-CRT_HD int trace_bins_exact(const CamCand *cands, int beg, int end, const DNode *nodes, const PNode *pnodes, int n,
+CRT_HD int trace_bins_exact(const CamCand *cands, int beg, int end, int bit, const DNode *nodes, const PNode *pnodes, int n,
                             const DTriGeo *slots, const uint8_t *slot_cull, const int32_t *slot_tri,
                             const KTopo *ktopo, float prune_origin_max, bool planes_ok, Vec o, Vec d, float &best_t,
                             WalkCounts &c, bool *fb = nullptr) {
@@ -506,7 +533,7 @@ CRT_HD int trace_bins_exact(const CamCand *cands, int beg, int end, const DNode 
     const PruneRay pr = make_prune_ray(o, d, prune_origin_max);
     bool tie = false;
     float t = 0.0f;
-    const int tri = walk_bins<COUNT>(cands, beg, end, o, d, pr, t, tie, c);
+    const int tri = walk_bins<COUNT>(cands, beg, end, bit, o, d, pr, t, tie, c);
     return resolve_closest<COUNT>(nodes, pnodes, n, slots, slot_cull, slot_tri, ktopo, planes_ok, o, d, pr, tri, t, tie,
                                   best_t, c, fb);
 }

@@ -333,7 +333,7 @@ int build_camera_bins(const HostScene &hs, std::vector<CamCand> &bins, std::vect
     constexpr int64_t kMeanCap = 32;         /* mean candidates per cell */
     constexpr int64_t kCellCap = 4096;       /* candidates of one cell */
 
-    struct Item { CamCand c; int32_t x0, x1, y0, y1; };   /* cell rectangle, x0 > x1: none */
+    struct Item { CamCand c; int32_t x0, x1, y0, y1; int32_t px0, px1, py0, py1; };   /* cells, pixels; x0 > x1: none */
     std::vector<Item> items((size_t)nt);
     int everywhere = 0;
     for (int32_t t = 0; t < nt; ++t) {
@@ -378,6 +378,7 @@ int build_camera_bins(const HostScene &hs, std::vector<CamCand> &bins, std::vect
         if (all) {
             if (++everywhere > kMaxEverywhere) return CRT_OK;
             it.x0 = 0; it.x1 = tx - 1; it.y0 = 0; it.y1 = ty - 1;
+            it.px0 = 0; it.px1 = W - 1; it.py0 = 0; it.py1 = H - 1;
             c.dmin = 0.0f;
             continue;
         }
@@ -388,10 +389,12 @@ int build_camera_bins(const HostScene &hs, std::vector<CamCand> &bins, std::vect
             it.x0 = 1; it.x1 = 0; it.y0 = 1; it.y1 = 0;
             continue;
         }
-        it.x0 = (int32_t)std::max(0.0, px0) / 8;
-        it.x1 = (int32_t)std::min((double)(W - 1), px1) / 8;
-        it.y0 = (int32_t)std::max(0.0, py0) / 8;
-        it.y1 = (int32_t)std::min((double)(H - 1), py1) / 8;
+        it.px0 = (int32_t)std::max(0.0, px0);
+        it.px1 = (int32_t)std::min((double)(W - 1), px1);
+        it.py0 = (int32_t)std::max(0.0, py0);
+        it.py1 = (int32_t)std::min((double)(H - 1), py1);
+        it.x0 = it.px0 / 8; it.x1 = it.px1 / 8;
+        it.y0 = it.py0 / 8; it.y1 = it.py1 / 8;
     }
     std::vector<int64_t> cnt((size_t)ncell + 1, 0);
     for (const Item &it : items)
@@ -409,10 +412,26 @@ int build_camera_bins(const HostScene &hs, std::vector<CamCand> &bins, std::vect
     std::vector<int32_t> fill(off.begin(), off.end() - 1);
     for (const Item &it : items)
         for (int32_t y = it.y0; y <= it.y1; ++y)
-            for (int32_t x = it.x0; x <= it.x1; ++x) bins[(size_t)fill[(size_t)y * tx + x]++] = it.c;
-    for (int64_t c = 0; c < ncell; ++c)
-        std::stable_sort(bins.begin() + off[(size_t)c], bins.begin() + off[(size_t)c + 1],
-                         [](const CamCand &a, const CamCand &b) { return a.dmin < b.dmin; });
+            for (int32_t x = it.x0; x <= it.x1; ++x) {
+                CamCand &c = bins[(size_t)fill[(size_t)y * tx + x]++];
+                c = it.c;
+                /* the cell's pixels inside the candidate's pixel rectangle */
+                uint64_t m = 0;
+                for (int32_t py = std::max(8 * y, it.py0); py <= std::min(8 * y + 7, it.py1); ++py)
+                    for (int32_t px = std::max(8 * x, it.px0); px <= std::min(8 * x + 7, it.px1); ++px)
+                        m |= 1ull << (8 * (py - 8 * y) + (px - 8 * x));
+                c.mask = m;
+            }
+    for (int64_t c = 0; c < ncell; ++c) {
+        const auto b = bins.begin() + off[(size_t)c], e = bins.begin() + off[(size_t)c + 1];
+        std::stable_sort(b, e, [](const CamCand &u, const CamCand &v) { return u.dmin < v.dmin; });
+        uint64_t r = 0;
+        for (auto q = e; q != b;) {
+            --q;
+            r |= q->mask;
+            q->rest = r;
+        }
+    }
     return CRT_OK;
 }
 

@@ -105,14 +105,19 @@ static_assert(sizeof(DTriGeo) == 48, "DTriGeo must be 48 B");
  * triangle's conservative hull (BNode's boxes are unions of the same hulls);
  * dmin is a lower bound on the t of any hit the reference's triangle test
  * accepts for a camera ray (the cell's list is sorted by it); g and id are
- * the triangle as the BVH's triangle arrays hold it (id | culling << 31). */
+ * the triangle as the BVH's triangle arrays hold it (id | culling << 31);
+ * mask / rest let a pixel skip candidates it cannot hit and stop once none
+ * is left. */
 struct alignas(16) CamCand {
     float lo_x, hi_x, lo_y, hi_y;
     float lo_z, hi_z;
     float dmin;
     int32_t id;
     DTriGeo g;
+    uint64_t mask;   /* pixels of the cell (bit 8 y + x) whose camera ray may hit it */
+    uint64_t rest;   /* OR of mask over this and every later candidate of the cell */
 };
+static_assert(sizeof(CamCand) == 96, "CamCand must be 96 B");
 
 struct alignas(16) DTriAttr {
     int32_t i0, i1, i2;

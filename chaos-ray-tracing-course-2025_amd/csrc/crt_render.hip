@@ -91,7 +91,10 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             camera_ray(s, tx0 + (act ? lx : 0), ty0 + (act ? ly : 0), o, d);
             LaneCounts cw = {};
             float t;
-            const int slot = trace_bins_wave<COUNT>(s, beg, end, act, o, d, t, cw);
+            __shared__ CamCand stage[4 * kBinChunk];
+            const int bit = 8 * ((ty0 & 7) + ly) + (tx0 & 7) + lx;
+            const int slot = trace_bins_wave<COUNT>(s, stage + (threadIdx.x >> 6) * kBinChunk, beg, end, bit, act, o,
+                                                    d, t, cw, stamps ? &stamps[2 * wave] : nullptr);
             if (act) {
                 const Vec c = shade_primary(s, st, o, d, slot, t);
                 float *pxo = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);

@@ -101,6 +101,10 @@ struct crt_hip_scene {
     std::vector<void *> allocs;
     hipStream_t stream = nullptr;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    /* crt_hip_render into pageable host memory (stage_to_host): a pinned
+     * staging image and one event per chunk of the copy */
+    float *h_stage = nullptr;
+    std::vector<hipEvent_t> stage_ev;
     ShardPlan full;
     std::map<std::pair<int, int>, ShardPlan> shard_plans;
     std::map<int, std::pair<UnpackBucket *, int>> unpack_plans;

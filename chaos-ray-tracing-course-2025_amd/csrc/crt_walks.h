@@ -984,33 +984,82 @@ __device__ int trace_bvh_window(const DeviceScene &s, int sl, bool act, Vec o, V
 }
 
 /* Camera rays of one camera-bins cell (crt_bvh.h walk_bins / trace_bins_exact)
- * with the whole wave on the cell's candidate list: the loop over candidates
- * is wave-uniform and each record is read once by scalar loads into SGPRs
- * (one stream of contiguous 80-B records, no dependent loads), each lane
- * running walk_bins on its own ray and leaving the loop once the next
- * candidate's dmin exceeds its best t; the wave leaves when every lane has.
- * Then the proof / fallback per lane (resolve_closest).  act: the lane has a
- * pixel.  Returns the reference's slot (-1: miss). */
+ * with the whole wave on the cell's candidate list.  The list is staged
+ * through LDS kBinChunk records at a time (one coalesced global load per lane,
+ * so one memory latency per chunk instead of one per record); every lane then
+ * reads each record at the same LDS address (a broadcast) and runs walk_bins
+ * on its own ray: it skips records whose pixel mask lacks its pixel and
+ * leaves once no later record has it (rest) or the next dmin exceeds its best
+ * t; the wave leaves when every lane has.  Then the proof / fallback per lane
+ * (resolve_closest).  stage: this wave's kBinChunk LDS records; bit: the
+ * lane's pixel in the cell (8 y + x); act: the lane has a pixel.  Returns the
+ * reference's slot (-1: miss). */
+constexpr int kBinChunk = 32;
+#ifndef CRT_BINS_ILP
+#define CRT_BINS_ILP 2       /* candidates tested side by side per loop round (interleaved dependency chains) */
+#endif
+
 template <bool COUNT>
-__device__ int trace_bins_wave(const DeviceScene &s, int beg, int end, bool act, Vec o, Vec d, float &best_t,
-                               LaneCounts &c) {
+__device__ int trace_bins_wave(const DeviceScene &s, CamCand *stage, int beg, int end, int bit, bool act, Vec o,
+                               Vec d, float &best_t, LaneCounts &c, unsigned long long *phase = nullptr) {
+    constexpr int U = CRT_BINS_ILP;
+    static_assert(kBinChunk % U == 0, "chunk of whole rounds");
     best_t = 0.0f;
     const bool nan_ray = isnan(o.x) || isnan(o.y) || isnan(o.z) || isnan(d.x) || isnan(d.y) || isnan(d.z);
     if (COUNT && act) ++c.traversals;
     const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
+    const int lane = (int)__lane_id();
     int best = -1;
     float bt = 0.0f, lim = INFINITY;
     bool tie = false, live = act && !nan_ray;
     WalkCounts wc = {0u, 0u};
-    for (int k = beg; k < end; ++k) {
-        const CamCand cc = load_scalar(s.bins, k);
-        live = live && !(best >= 0 && cc.dmin > bt);
+    for (int k0 = beg; k0 < end; k0 += kBinChunk) {
         if (__ballot(live) == 0ull) break;
-        if (live) {
-            if (COUNT) ++wc.nodes;
-            cand_test(cc, o, d, pr, best, bt, tie, lim);
+        const int n = min(kBinChunk, end - k0);
+        if (lane < n) stage[lane] = load_global(s.bins, k0 + lane);
+        __builtin_amdgcn_wave_barrier();
+        for (int j = 0; j < n; j += U) {
+            /* U candidates tested against the round's lim side by side, then
+             * merged in list order with walk_bins's exits.  Exact: a
+             * candidate whose hull is dead for the current lim but alive for
+             * the round's (larger) one can only hit at t > lim >= best t —
+             * neither a better hit nor a tie. */
+            CamCand cc[U];
+            bool hit[U];
+            float th[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                cc[u] = stage[min(j + u, n - 1)];
+                hit[u] = cand_hit_bf(cc[u], o, d, pr, lim, th[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (j + u < n) {
+                    live = live && ((cc[u].rest >> bit) & 1ull) != 0ull && !(best >= 0 && cc[u].dmin > bt);
+                    if (live && ((cc[u].mask >> bit) & 1ull) != 0ull) {
+                        if (COUNT) ++wc.nodes;
+                        if (hit[u]) {
+                            if (best < 0 || th[u] < bt) {
+                                bt = th[u];
+                                best = cc[u].id & 0x7fffffff;
+                                tie = false;
+                                lim = th[u];
+                            } else if (th[u] == bt) {
+                                tie = true;
+                            }
+                        }
+                    }
+                }
+            }
+            if (__ballot(live) == 0ull) break;
         }
+        __builtin_amdgcn_wave_barrier();
     }
+#ifdef CRT_BINS_PHASE
+    if (phase && lane == 0) *phase = __builtin_amdgcn_s_memrealtime();   /* diagnostic builds: loop end */
+#else
+    (void)phase;
+#endif
     int slot = -1;
     if (act && !nan_ray)
         slot = resolve_closest<COUNT>(s.nodes, s.pnodes, s.node_count, s.slots, s.slot_cull, s.slot_tri, s.ktopo,

@@ -393,29 +393,43 @@ typedef struct crt_wave_counts {
 int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
 
 /* Options (results are identical for every setting; work and speed differ):
- *   "traversal"  7 = packet walk in the reference's node order (work counters
- *                equal the reference's) | 8 = exact t-pruned walks (default)
- *   "secondary"  walk of secondary rays: 0 = by frame (default), 4 =
- *                cooperative walk in the reference's order, 10 = pruned cooperative
+ *   "traversal"  camera walk: 7 = packet walk in the reference's node order
+ *                (work counters equal the reference's) | 8 = exact t-pruned
+ *                packet walks | 14 = BVH walk + proof on the reference's tree
+ *                (default where the scene has a BVH: host-built trees up to
+ *                2^18 triangles), camera frames without recursion then take
+ *                the camera bins ("bins")
+ *   "bins"       0/1 (default 1): camera frames of scenes without reflective /
+ *                refractive materials or GI walk per-8x8-cell candidate lists
+ *                 where they were built
+ *   "secondary"  walk of secondary rays: 0 = by frame (default: 14 where the
+ *                scene has a BVH), 4 = cooperative walk in the reference's
+ *                order, 10 = pruned cooperative, 14 = BVH + proof
  *   "wavefront"  0/1 (default 1): level-by-level recursion when GI is off
  *   "window"     0/1 (default 1): the plan's split tiles of <= 16 camera rays
  *                take the window walk
  *   "calibrate"  0 = estimate plan | 1 = measured-cost tile plan, split
- *                threshold tuned by timing candidate plans (default) | 2 = the
- *                threshold of env CRT_CALIB_K (default 4)
+ *                threshold tuned by timing candidate plans (long-running
+ *                hosts, bench.py) | 2 = measured-cost plan with a fixed
+ *                threshold (default; a one-shot caller's first frame of a walk
+ *                renders with the estimate plan and the second calibrates)
+ *   "calib_k_milli" k x 1000: a fixed split threshold (sets "calibrate" 2)
+ *   "calib_min"  1/2/4/8: smallest side a calibrated plan splits tiles to
  *   "gi_refill"  0/1 (default 1): GI frames run persistent waves that refill
  *                finished lanes with the next pixel of the tile list
+ *   "gi_machine" 0/1 (default 1): ... as per-lane state machines (k_render_gi)
  *   "wf_rpw"     1..64 (default 48): cap on the rays per wave of wavefront
- *                levels >= 1; a level of n rays takes min(cap, max(8, n / 4096))
- *                and the other lanes start idle and take donated pieces
+ *                levels >= 1 with a cooperative walk; a level of n rays takes
+ *                min(cap, max(8, n / 4096)) and the other lanes start idle and
+ *                take donated pieces
  *   "wf_replay"  1 (default): a wavefront frame whose settings and tile list
  *                were rendered before launches every level with the recorded
  *                level sizes, no host read-back | 0: read every level's size
  *                back | 2: tests only, recorded sizes minus one (overflow path)
  *   "wf_graph"   0/1 (default 1): such frames run as a HIP graph captured on
  *                their first replay (per tile list, settings, output, stream)
- *   "calib_k_milli" k x 1000: a fixed split threshold (sets "calibrate" 2)
- *   "trace_walk" 0 = reference order, 1 = pruned per-ray walk (crt_hip_trace_batch)
+ *   "trace_walk" 0 = reference order, 1 = pruned per-ray walk, 2 = BVH + proof
+ *                (crt_hip_trace_batch)
  *   "events"     0/1 (default 1): start/stop events around every render
  *   "shadows"    0/1 (default 0): trace the shadow rays — NOT HEAD's image.
  *                At HEAD trace_ray_with_refractions never runs its loop
@@ -427,9 +441,8 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  *                (bench.py --shadows), never the HEAD-parity headline; the
  *                frame runs the frame-stack kernel with per-lane shadow walks,
  *                and crt_hip_count_work counts the shadow rays as traversals.
- * Environment variables CRT_TRAVERSAL, CRT_SECONDARY, CRT_WAVEFRONT, CRT_WINDOW,
- * CRT_CALIBRATE, CRT_GI_REFILL, CRT_WF_RPW, CRT_TRACE_WALK and CRT_EVENTS set
- * the initial values (an invalid value makes scene creation fail). */
+ * Environment overrides of these (CRT_TRAVERSAL, ...) exist in A/B builds only
+ * (-DCRT_AB_OPTIONS). */
 int  crt_hip_scene_set_option(crt_hip_scene *scene, const char *name, int value);
 
 /* Diagnostics: the full-frame tile plan in dispatch order (x, y, w, h per

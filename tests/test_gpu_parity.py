@@ -209,16 +209,16 @@ def test_window_walk_equals_packet_walk(N, oracle, calib_k):
     4x4 (16 rays x 4 nodes) and 2x2 (4 rays x 16 nodes) tiles through it."""
     sc = scene_npz("14-01-acceleration-tree__scene1")
     st = N.RendererSettings.default()
-    win = N.HipScene(sc, calib_k_milli=calib_k)
+    win = N.HipScene(sc, traversal=8, calib_k_milli=calib_k)
     xywh, _ = win.plan_tiles(st)
     sizes = {(int(w), int(h)) for w, h in xywh[:, 2:4]}
     assert (2, 2) in sizes or (4, 4) in sizes
     a = win.render(st)
-    b = N.HipScene(sc, window=0).render(st)
+    b = N.HipScene(sc, traversal=8, window=0).render(st)
     want = oracle.OracleScene(sc).render(st)
     assert np.array_equal(bits(a), bits(want))
     assert np.array_equal(bits(b), bits(want))
-    ca, cb = win.count_work(st), N.HipScene(sc, window=0).count_work(st)
+    ca, cb = win.count_work(st), N.HipScene(sc, traversal=8, window=0).count_work(st)
     assert ca["traversals"] == cb["traversals"] == 1920 * 1080 and ca["hits"] == cb["hits"]
 
 

@@ -390,7 +390,7 @@ extern "C" int bins_sim_check(const crt_scene_desc *desc, uint64_t *out) {
             const int a = walk_bvh<true>(bnode_order(hs.bnodes.data(), hs.bnode_count, ray_octant(d)), hs.bnode_count,
                                          hs.btri.data(), hs.btri_id.data(), o, d, pr, t1, tie1, w);
             const int cell = (y / 8) * tx + x / 8;
-            const int b = walk_bins<true>(bins.data(), off[cell], off[cell + 1], o, d, pr, t2, tie2, wb);
+            const int b = walk_bins<true>(bins.data(), off[cell], off[cell + 1], 8 * (y % 8) + x % 8, o, d, pr, t2, tie2, wb);
             ++out[0];
             uint32_t u1, u2;
             std::memcpy(&u1, &t1, 4);
@@ -434,7 +434,7 @@ extern "C" int bins_sim_diffs(const crt_scene_desc *desc, int64_t *rows, int cap
             const int a = walk_bvh<false>(bnode_order(hs.bnodes.data(), hs.bnode_count, ray_octant(d)), hs.bnode_count,
                                           hs.btri.data(), hs.btri_id.data(), o, d, pr, t1, tie1, w);
             const int cell = (y / 8) * tx + x / 8;
-            const int b = walk_bins<false>(bins.data(), off[cell], off[cell + 1], o, d, pr, t2, tie2, w);
+            const int b = walk_bins<false>(bins.data(), off[cell], off[cell + 1], 8 * (y % 8) + x % 8, o, d, pr, t2, tie2, w);
             uint32_t u1, u2;
             std::memcpy(&u1, &t1, 4);
             std::memcpy(&u2, &t2, 4);
@@ -446,4 +446,69 @@ extern "C" int bins_sim_diffs(const crt_scene_desc *desc, int64_t *rows, int cap
             }
         }
     return n;
+}
+
+/* Per 8x8 cell of the camera bins: [0] list length, [1] the wave's loop
+ * iterations (the largest index a lane of the cell leaves walk_bins at, as
+ * the device loop runs), [2] candidates the cell's lanes test in total,
+ * [3] most candidates one lane tests, [4] longest proof / fallback (node +
+ * triangle steps), [5] lanes with a tie, [6] lanes that fell back.  out: 8
+ * per cell. */
+extern "C" int bins_sim_cells(const crt_scene_desc *desc, int64_t *out) {
+    HostScene hs;
+    int rc = prepare_scene(desc, hs);
+    if (rc != CRT_OK) return rc;
+    if (hs.bnode_count == 0 && ((rc = build_bvh(hs)) != CRT_OK || (rc = build_proof_tables(hs)) != CRT_OK)) return rc;
+    std::vector<CamCand> bins;
+    std::vector<int32_t> off;
+    if ((rc = build_camera_bins(hs, bins, off)) != CRT_OK) return rc;
+    if (bins.empty()) return -1;
+    DeviceScene ds{};
+    std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
+    std::memcpy(ds.cam_rot, hs.cam_rot, sizeof ds.cam_rot);
+    ds.width = hs.width;
+    ds.height = hs.height;
+    ds.aspect = hs.aspect;
+    ds.tan_half_fov = hs.tan_half_fov;
+    const int tx = (hs.width + 7) / 8, ty = (hs.height + 7) / 8;
+    for (int cy = 0; cy < ty; ++cy)
+        for (int cx = 0; cx < tx; ++cx) {
+            const int cell = cy * tx + cx;
+            int64_t *r = out + 8 * (int64_t)cell;
+            r[0] = off[cell + 1] - off[cell];
+            r[1] = r[2] = r[3] = r[4] = r[5] = r[6] = r[7] = 0;
+            for (int y = 8 * cy; y < std::min(hs.height, 8 * cy + 8); ++y)
+                for (int x = 8 * cx; x < std::min(hs.width, 8 * cx + 8); ++x) {
+                    Vec o, d;
+                    camera_ray(ds, x, y, o, d);
+                    const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
+                    const int bit = 8 * (y - 8 * cy) + (x - 8 * cx);
+                    int best = -1;
+                    float bt = 0.f, lim = INFINITY;
+                    bool tie = false;
+                    int k = off[cell], tested = 0;
+                    for (; k < off[cell + 1]; ++k) {
+                        const CamCand &cc = bins[k];
+                        if (((cc.rest >> bit) & 1ull) == 0ull) break;
+                        if (best >= 0 && cc.dmin > bt) break;
+                        if (((cc.mask >> bit) & 1ull) == 0ull) continue;
+                        ++tested;
+                        cand_test(cc, o, d, pr, best, bt, tie, lim);
+                    }
+                    r[1] = std::max<int64_t>(r[1], k - off[cell]);
+                    r[2] += tested;
+                    r[3] = std::max<int64_t>(r[3], tested);
+                    WalkCounts pc = {0u, 0u};
+                    bool fb = false;
+                    float tt = 0.f;
+                    (void)resolve_closest<true>(hs.nodes.data(), hs.pnodes.data(), (int)hs.nodes.size(), hs.slots.data(),
+                                                hs.slot_cull.data(), hs.slot_tri.data(),
+                                                hs.ktopo.empty() ? nullptr : hs.ktopo.data(), false, o, d, pr, best, bt,
+                                                tie, tt, pc, &fb);
+                    r[4] = std::max<int64_t>(r[4], pc.nodes + pc.tris);
+                    r[5] += tie ? 1 : 0;
+                    r[6] += fb ? 1 : 0;
+                }
+        }
+    return CRT_OK;
 }
