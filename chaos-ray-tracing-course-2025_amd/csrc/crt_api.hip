@@ -311,8 +311,10 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
             sc->stage_ev.assign(kStageChunks, nullptr);
             for (auto &e : sc->stage_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             (void)copy_pool();
-            /* the first DMA into a fresh pinned buffer pays its one-time mapping */
-            HIP_TRY(hipMemcpy(sc->h_stage, sc->d_out, bytes, hipMemcpyDeviceToHost));
+            /* the first DMA into a fresh pinned buffer, and the stream's first
+             * asynchronous copy, pay one-time setup (~7 ms: profiles/r03/cold) */
+            HIP_TRY(hipMemcpyAsync(sc->h_stage, sc->d_out, bytes, hipMemcpyDeviceToHost, sc->stream));
+            HIP_TRY(hipStreamSynchronize(sc->stream));
         }
         unsigned long long probe[16];
         HIP_TRY(hipMemcpy(probe, sc->d_counters, sizeof probe, hipMemcpyDeviceToHost));
@@ -672,10 +674,12 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         sc->gi_refill = value != 0;
     } else if (k == "gi_machine") {
         sc->gi_machine = value != 0;
-    } else if (k == "bins") {   /* camera bins on / off: the full-frame plan depends on it */
-        if ((value != 0) != (sc->bins_on != 0)) {
+    } else if (k == "bins" || k == "bins_split") {   /* camera bins: the full-frame plan depends on them */
+        if (k == "bins_split" && value < 1) return set_error(CRT_E_INVALID, "bins_split must be >= 1");
+        if (k == "bins_split" ? value != sc->bins_split : (value != 0) != (sc->bins_on != 0)) {
             HIP_TRY(hipDeviceSynchronize());
-            sc->bins_on = value != 0;
+            if (k == "bins") sc->bins_on = value != 0;
+            else sc->bins_split = value;
             sc->calib_walk = -1;
             free_plans(sc);
             int64_t px = 0;

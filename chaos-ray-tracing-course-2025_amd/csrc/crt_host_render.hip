@@ -128,13 +128,30 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         plan.packed_pixels = total;
     }
     if (bins_active(sc) && !tiles.empty()) {
-        /* camera bins: one wave per 8x8 tile on its cell's list, no split;
-         * the longest lists first */
+        /* camera bins: one wave per 8x8 tile on its cell's list; a cell
+         * whose list is long is split into four 4x4 waves (each leaves the
+         * list once its 16 pixels are done: the list's tail latency is
+         * spread over four waves); the longest lists first, the split ones
+         * at raised issue priority */
         const int tx = (W + 7) / 8;
         auto cost = [&](const Tile &t) {
             const int cx = t.x / 8, cy = t.y / 8;
             return (t.x % 8) + t.w <= 8 && (t.y % 8) + t.h <= 8 ? sc->bin_count[(size_t)cy * tx + cx] : INT32_MAX;
         };
+        std::vector<Tile> split;
+        split.reserve(tiles.size());
+        for (const Tile &t : tiles) {
+            const int c = cost(t);
+            if (c >= sc->bins_split && c != INT32_MAX) {
+                for (int yy = 0; yy < t.h; yy += 4)
+                    for (int xx = 0; xx < t.w; xx += 4)
+                        split.push_back(Tile{t.x + xx, t.y + yy, std::min(4, t.w - xx), std::min(4, t.h - yy),
+                                             t.out_base + (int64_t)yy * t.out_stride + xx, t.out_stride, 1});
+            } else {
+                split.push_back(t);
+            }
+        }
+        tiles.swap(split);
         std::stable_sort(tiles.begin(), tiles.end(), [&](const Tile &a, const Tile &b) { return cost(a) > cost(b); });
         plan.cost.clear();
     } else if (!sc->calib.empty() && !tiles.empty()) {

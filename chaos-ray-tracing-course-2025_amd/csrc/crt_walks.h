@@ -985,25 +985,23 @@ __device__ int trace_bvh_window(const DeviceScene &s, int sl, bool act, Vec o, V
 
 /* Camera rays of one camera-bins cell (crt_bvh.h walk_bins / trace_bins_exact)
  * with the whole wave on the cell's candidate list.  The list is staged
- * through LDS kBinChunk records at a time (one coalesced global load per lane,
- * so one memory latency per chunk instead of one per record); every lane then
- * reads each record at the same LDS address (a broadcast) and runs walk_bins
- * on its own ray: it skips records whose pixel mask lacks its pixel and
- * leaves once no later record has it (rest) or the next dmin exceeds its best
- * t; the wave leaves when every lane has.  Then the proof / fallback per lane
- * (resolve_closest).  stage: this wave's kBinChunk LDS records; bit: the
- * lane's pixel in the cell (8 y + x); act: the lane has a pixel.  Returns the
- * reference's slot (-1: miss). */
+ * through LDS kBinChunk records at a time (one coalesced global load per
+ * lane: one memory latency per chunk).  Each lane first gathers, from the
+ * chunk's pixel masks (read by broadcast), the bits of the records that
+ * cover its pixel, then walks only those, in list order, at its own pace —
+ * so a chunk costs the wave as many rounds as its busiest lane has records,
+ * not as many as the chunk holds.  Per lane this is walk_bins exactly: the
+ * covered records in order, the same dmin exit (the list is sorted by dmin,
+ * so an uncovered record past best t only means a covered one later is past
+ * it too) and the same end when no later record covers the pixel.  Then the
+ * proof / fallback per lane (resolve_closest).  stage: this wave's kBinChunk
+ * LDS records; bit: the lane's pixel in the cell (8 y + x); act: the lane
+ * has a pixel.  Returns the reference's slot (-1: miss). */
 constexpr int kBinChunk = 32;
-#ifndef CRT_BINS_ILP
-#define CRT_BINS_ILP 2       /* candidates tested side by side per loop round (interleaved dependency chains) */
-#endif
 
 template <bool COUNT>
 __device__ int trace_bins_wave(const DeviceScene &s, CamCand *stage, int beg, int end, int bit, bool act, Vec o,
                                Vec d, float &best_t, LaneCounts &c, unsigned long long *phase = nullptr) {
-    constexpr int U = CRT_BINS_ILP;
-    static_assert(kBinChunk % U == 0, "chunk of whole rounds");
     best_t = 0.0f;
     const bool nan_ray = isnan(o.x) || isnan(o.y) || isnan(o.z) || isnan(d.x) || isnan(d.y) || isnan(d.z);
     if (COUNT && act) ++c.traversals;
@@ -1018,40 +1016,26 @@ __device__ int trace_bins_wave(const DeviceScene &s, CamCand *stage, int beg, in
         const int n = min(kBinChunk, end - k0);
         if (lane < n) stage[lane] = load_global(s.bins, k0 + lane);
         __builtin_amdgcn_wave_barrier();
-        for (int j = 0; j < n; j += U) {
-            /* U candidates tested against the round's lim side by side, then
-             * merged in list order with walk_bins's exits.  Exact: a
-             * candidate whose hull is dead for the current lim but alive for
-             * the round's (larger) one can only hit at t > lim >= best t —
-             * neither a better hit nor a tie. */
-            CamCand cc[U];
-            bool hit[U];
-            float th[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                cc[u] = stage[min(j + u, n - 1)];
-                hit[u] = cand_hit_bf(cc[u], o, d, pr, lim, th[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (j + u < n) {
-                    live = live && ((cc[u].rest >> bit) & 1ull) != 0ull && !(best >= 0 && cc[u].dmin > bt);
-                    if (live && ((cc[u].mask >> bit) & 1ull) != 0ull) {
-                        if (COUNT) ++wc.nodes;
-                        if (hit[u]) {
-                            if (best < 0 || th[u] < bt) {
-                                bt = th[u];
-                                best = cc[u].id & 0x7fffffff;
-                                tie = false;
-                                lim = th[u];
-                            } else if (th[u] == bt) {
-                                tie = true;
-                            }
-                        }
-                    }
+        live = live && ((stage[0].rest >> bit) & 1ull) != 0ull;   /* a later record covers the pixel */
+        uint32_t w = 0u;
+        if (__ballot(live) != 0ull) {
+            for (int j = 0; j < n; ++j) w |= (uint32_t)((stage[j].mask >> bit) & 1ull) << j;
+        }
+        if (!live) w = 0u;
+        while (__ballot(w != 0u) != 0ull) {
+            if (w != 0u) {
+                const int j = __builtin_ctz(w);
+                w &= w - 1u;
+                const CamCand cc = stage[j];
+                if (best >= 0 && cc.dmin > bt) {   /* sorted by dmin: nothing later can hit at t <= best t */
+                    live = false;
+                    w = 0u;
+                } else {
+                    if (COUNT) ++wc.nodes;
+                    const bool tested = cand_test(cc, o, d, pr, best, bt, tie, lim);
+                    if (COUNT && tested) ++wc.tris;
                 }
             }
-            if (__ballot(live) == 0ull) break;
         }
         __builtin_amdgcn_wave_barrier();
     }
