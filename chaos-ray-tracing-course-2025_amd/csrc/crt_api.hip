@@ -242,11 +242,16 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
         if ((rc = upload(sc.get(), hs.btri_id, &ds.btri_id)) != CRT_OK) return rc;
         ds.bnode_count = hs.bnode_count;
         if ((rc = upload(sc.get(), hs.ktopo, &ds.ktopo)) != CRT_OK) return rc;
+        if (!hs.ktopo.empty() && !hs.pleaf_off.empty()) {
+            if ((rc = upload(sc.get(), hs.pleaf, &ds.pleaf)) != CRT_OK) return rc;
+            if ((rc = upload(sc.get(), hs.pleaf_off, &ds.pleaf_off)) != CRT_OK) return rc;
+        }
     }
-    /* camera bins: frames without recursion only (no reflective / refractive
-     * material, no GI) — every camera frame of the scene is then one
-     * traversal per pixel (k_render_tiles walk 15) */
-    if (hs.bnode_count > 0 && hs.tree_on_host && !sc->has_secondary && !(hs.gi_on && sc->has_diffuse)) {
+    /* camera bins: scenes whose camera rays are traced by the tile kernels —
+     * frames without recursion (k_render_tiles walk 15) and level 0 of the
+     * wavefront recursion (k_wf_level<15, true>); GI frames trace theirs in
+     * the GI machine */
+    if (hs.bnode_count > 0 && hs.tree_on_host && !(hs.gi_on && sc->has_diffuse)) {
         std::vector<CamCand> bins;
         std::vector<int32_t> off;
         if ((rc = build_camera_bins(hs, bins, off)) != CRT_OK) return rc;

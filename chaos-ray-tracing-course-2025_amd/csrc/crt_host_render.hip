@@ -426,8 +426,8 @@ int plan_walk(const crt_hip_scene *sc, const crt_renderer_settings *st) {
     const bool gi = sc->info.gi_on && sc->has_diffuse && st->diffuse_reflection_ray_count > 0;
     const bool full = gi || sc->has_secondary;
     if (gi) return -1;
-    if (full) return sc->wavefront ? camera_walk(sc, sc->traversal == 8 ? 8 : 7) : -1;
     if (bins_active(sc)) return -1;   /* camera bins: no plan to measure */
+    if (full) return sc->wavefront ? camera_walk(sc, sc->traversal == 8 ? 8 : 7) : -1;
     return camera_walk(sc, sc->traversal);
 }
 
@@ -678,7 +678,9 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
 #define CRT_WF0(T, COUNT)                                                                                   \
     hipLaunchKernelGGL((k_wf_level<T, true, COUNT>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,      \
                        plan.d_tiles, plan.ntiles, lv, cnt)
-    if (primary == 14) {
+    if (primary == 14 && bins_active(sc)) {   /* camera bins for the camera rays */
+        if (count) CRT_WF0(15, true); else CRT_WF0(15, false);
+    } else if (primary == 14) {
         if (count) CRT_WF0(14, true); else CRT_WF0(14, false);
     } else if (primary == 12 || primary == 13) {   /* level 0 keeps 8x8 tiles' packet walk (no window build) */
         if (count) CRT_WF0(12, true); else CRT_WF0(12, false);

@@ -21,10 +21,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
     bool has;
     Vec o = vec(0.f, 0.f, 0.f), d = vec(0.f, 0.f, 1.f);
     int id = gid, depth = 0;
+    Tile tl = {};
     if (LEVEL0) {
         const int wave = gid >> 6;
         if (wave >= ntiles) return;
-        const Tile tl = tiles[wave];
+        tl = tiles[wave];
         if (tl.prio) __builtin_amdgcn_s_setprio(3);
         const int lx = lane & 7, ly = lane >> 3;
         has = lx < tl.w && ly < tl.h;
@@ -46,7 +47,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
     constexpr bool kCoop = kIsCoop<TRAV>;
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
-    const int slot = trace<TRAV, COUNT>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has, o, d, t, cnt);
+    int slot;
+    if constexpr (LEVEL0 && TRAV == 15) {
+        /* camera bins (crt_walks.h trace_bins_wave) for a tile inside one 8x8 cell */
+        __shared__ CamCand stage[4 * kBinChunk];
+        const int tx0 = uniform_i(tl.x), ty0 = uniform_i(tl.y), tw = uniform_i(tl.w), th = uniform_i(tl.h);
+        if ((tx0 & 7) + tw <= 8 && (ty0 & 7) + th <= 8) {
+            const int cell = (ty0 >> 3) * s.bin_tx + (tx0 >> 3);
+            const int beg = load_scalar(s.bin_off, cell), end = load_scalar(s.bin_off, cell + 1);
+            const int bit = 8 * ((ty0 & 7) + (lane >> 3)) + (tx0 & 7) + (lane & 7);
+            slot = trace_bins_wave<COUNT>(s, stage + (threadIdx.x >> 6) * kBinChunk, beg, end, bit, has, o, d, t, cnt);
+        } else {
+            slot = trace<14, COUNT>(s, &coop[0], has, o, d, t, cnt);
+        }
+    } else {
+        slot = trace<TRAV, COUNT>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has, o, d, t, cnt);
+    }
 
     WNode node = {wFinal, -1, -1, 0, 0.f, 0.f, 0.f, 0.f};
     Vec col = vec(0.f, 0.f, 0.f);

@@ -811,7 +811,8 @@ __device__ __forceinline__ int trace_lane_bvh(const DeviceScene &s, bool active,
     if (COUNT) ++c.traversals;
     WalkCounts wc = {0u, 0u};
     const int best = trace_bvh_exact<COUNT, PF>(s.bnodes, s.bnode_count, s.btri, s.btri_id, s.nodes, s.pnodes,
-                                            s.node_count, s.slots, s.slot_cull, s.slot_tri, s.ktopo, s.prune_origin_max,
+                                            s.node_count, s.slots, s.slot_cull, s.slot_tri,
+                                            ProofTables(s.ktopo, s.pleaf, s.pleaf_off), s.prune_origin_max,
                                             s.planes_ok != 0, o, d, best_t, wc);
     if (COUNT) {
         c.nodes += wc.nodes;
@@ -963,8 +964,7 @@ __device__ int trace_bvh_window(const DeviceScene &s, int sl, bool act, Vec o, V
         WalkCounts pc = {0u, 0u};
         if (!tie) {
             const Vec p = vadd(o, vscale(d, t));
-            slot = CRT_PROOF_TOPO && s.ktopo ? verify_topo<COUNT>(s.ktopo, s.nodes, s.slot_tri, tri, o, d, rr, p, pc)
-                                             : verify_kd<COUNT>(s.nodes, s.slot_tri, tri, o, d, rr, p, pc);
+            slot = prove<COUNT>(ProofTables(s.ktopo, s.pleaf, s.pleaf_off), s.nodes, s.slot_tri, tri, o, d, rr, p, pc);
             if (slot >= 0) best_t = t;
         }
         if (slot < 0)
@@ -998,6 +998,9 @@ __device__ int trace_bvh_window(const DeviceScene &s, int sl, bool act, Vec o, V
  * LDS records; bit: the lane's pixel in the cell (8 y + x); act: the lane
  * has a pixel.  Returns the reference's slot (-1: miss). */
 constexpr int kBinChunk = 32;
+#ifndef CRT_BINS_LANE_ILP
+#define CRT_BINS_LANE_ILP 1   /* records a lane tests side by side per round (A/B builds: 2) */
+#endif
 
 template <bool COUNT>
 __device__ int trace_bins_wave(const DeviceScene &s, CamCand *stage, int beg, int end, int bit, bool act, Vec o,
@@ -1022,6 +1025,58 @@ __device__ int trace_bins_wave(const DeviceScene &s, CamCand *stage, int beg, in
             for (int j = 0; j < n; ++j) w |= (uint32_t)((stage[j].mask >> bit) & 1ull) << j;
         }
         if (!live) w = 0u;
+#if CRT_BINS_LANE_ILP > 1
+        /* two of the lane's records per round, both tested against the
+         * round's lim and merged in order (a record dead for the updated lim
+         * can only hit past best t: no change) */
+        while (__ballot(w != 0u) != 0ull) {
+            if (w != 0u) {
+                const int j1 = __builtin_ctz(w);
+                w &= w - 1u;
+                const bool two = w != 0u;
+                const int j2 = two ? __builtin_ctz(w) : j1;
+                if (two) w &= w - 1u;
+                const CamCand c1 = stage[j1], c2 = stage[j2];
+                if (best >= 0 && c1.dmin > bt) {
+                    live = false;
+                    w = 0u;
+                } else {
+                    float t1, t2;
+                    const bool h1 = cand_hit_bf(c1, o, d, pr, lim, t1);
+                    const bool h2 = two && cand_hit_bf(c2, o, d, pr, lim, t2);
+                    if (COUNT) ++wc.nodes;
+                    if (h1) {
+                        if (best < 0 || t1 < bt) {
+                            bt = t1;
+                            best = c1.id & 0x7fffffff;
+                            tie = false;
+                            lim = t1;
+                        } else if (t1 == bt) {
+                            tie = true;
+                        }
+                    }
+                    if (two) {
+                        if (best >= 0 && c2.dmin > bt) {
+                            live = false;
+                            w = 0u;
+                        } else {
+                            if (COUNT) ++wc.nodes;
+                            if (h2) {
+                                if (best < 0 || t2 < bt) {
+                                    bt = t2;
+                                    best = c2.id & 0x7fffffff;
+                                    tie = false;
+                                    lim = t2;
+                                } else if (t2 == bt) {
+                                    tie = true;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+        }
+#else
         while (__ballot(w != 0u) != 0ull) {
             if (w != 0u) {
                 const int j = __builtin_ctz(w);
@@ -1037,6 +1092,7 @@ __device__ int trace_bins_wave(const DeviceScene &s, CamCand *stage, int beg, in
                 }
             }
         }
+#endif
         __builtin_amdgcn_wave_barrier();
     }
 #ifdef CRT_BINS_PHASE
@@ -1046,8 +1102,9 @@ __device__ int trace_bins_wave(const DeviceScene &s, CamCand *stage, int beg, in
 #endif
     int slot = -1;
     if (act && !nan_ray)
-        slot = resolve_closest<COUNT>(s.nodes, s.pnodes, s.node_count, s.slots, s.slot_cull, s.slot_tri, s.ktopo,
-                                      s.planes_ok != 0, o, d, pr, best, bt, tie, best_t, wc);
+        slot = resolve_closest<COUNT>(s.nodes, s.pnodes, s.node_count, s.slots, s.slot_cull, s.slot_tri,
+                                      ProofTables(s.ktopo, s.pleaf, s.pleaf_off), s.planes_ok != 0, o, d, pr, best, bt,
+                                      tie, best_t, wc);
     if (COUNT) {
         c.nodes += wc.nodes;
         c.tris += wc.tris;
