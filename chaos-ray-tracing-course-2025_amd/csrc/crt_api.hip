@@ -242,10 +242,6 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
         if ((rc = upload(sc.get(), hs.btri_id, &ds.btri_id)) != CRT_OK) return rc;
         ds.bnode_count = hs.bnode_count;
         if ((rc = upload(sc.get(), hs.ktopo, &ds.ktopo)) != CRT_OK) return rc;
-        if (!hs.ktopo.empty() && !hs.pleaf_off.empty()) {
-            if ((rc = upload(sc.get(), hs.pleaf, &ds.pleaf)) != CRT_OK) return rc;
-            if ((rc = upload(sc.get(), hs.pleaf_off, &ds.pleaf_off)) != CRT_OK) return rc;
-        }
     }
     /* camera bins: scenes whose camera rays are traced by the tile kernels —
      * frames without recursion (k_render_tiles walk 15) and level 0 of the

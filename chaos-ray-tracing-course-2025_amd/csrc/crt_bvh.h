@@ -399,88 +399,6 @@ CRT_HD int verify_topo(const KTopo *topo, const DNode *nodes, const int32_t *slo
     return slot;
 }
 
-/* The proof's tables (null members: not built) */
-struct ProofTables {
-    const KTopo *topo;
-    const ProofLeaf *leaf;
-    const int32_t *leaf_off;
-    CRT_HD ProofTables(const KTopo *t = nullptr, const ProofLeaf *l = nullptr, const int32_t *o = nullptr)
-        : topo(t), leaf(l), leaf_off(o) {}
-};
-
-constexpr int kProofLeafScan = 16;   /* triangles with more copies take the descent */
-
-/* verify_topo's last steps on one recorded leaf copy: its six-face test, then
- * the full tests of the ancestors above the deepest level where a passing
- * face's plane was set (root cell halved along the recorded path). */
-template <bool COUNT>
-CRT_HD bool prove_leaf(const ProofLeaf &L, const DNode *nodes, Vec o, Vec d, const RayRcp &rr, WalkCounts &c) {
-    DNode cell;
-    cell.lo_x = L.lo_x; cell.hi_x = L.hi_x; cell.lo_y = L.lo_y; cell.hi_y = L.hi_y; cell.lo_z = L.lo_z;
-    cell.hi_z = L.hi_z;
-    cell.a = 0;
-    cell.b = 0;
-    if (COUNT) ++c.nodes;
-    const unsigned m = box_faces(o, d, rr, cell);
-    if (m == 0u) return false;
-    int dmin = (int)(L.depth_df & 0xffu);
-    const uint64_t df = ((uint64_t)L.depth_df >> 8) | ((uint64_t)L.df345 << 24);
-#pragma unroll
-    for (int f = 0; f < 6; ++f)
-        if ((m >> f) & 1u) {
-            const int v = (int)((df >> (8 * f)) & 0xffull);
-            dmin = v < dmin ? v : dmin;
-        }
-    DNode a = CRT_LDG(nodes, 0);
-    for (int k = 0; k < dmin; k += 3) {
-        DNode lo, hi;
-        if (COUNT) ++c.nodes;
-        if (!box_hit_r(o, d, rr, a)) return false;
-        if (k + 1 >= dmin) break;
-        topo_halves<0>(a, lo, hi);
-        a = cell_sel(((L.upper >> k) & 1ull) != 0ull, hi, lo);
-        if (COUNT) ++c.nodes;
-        if (!box_hit_r(o, d, rr, a)) return false;
-        if (k + 2 >= dmin) break;
-        topo_halves<1>(a, lo, hi);
-        a = cell_sel(((L.upper >> (k + 1)) & 1ull) != 0ull, hi, lo);
-        if (COUNT) ++c.nodes;
-        if (!box_hit_r(o, d, rr, a)) return false;
-        topo_halves<2>(a, lo, hi);
-        a = cell_sel(((L.upper >> (k + 2)) & 1ull) != 0ull, hi, lo);
-    }
-    return true;
-}
-
-/* Step 2: a copy of triangle tri the reference reaches, or -1.  First the
- * triangle's recorded leaf copies whose cell holds p (no descent: two
- * dependent loads), then — when none holds p, or the triangle has many
- * copies — the descent towards p (verify_topo, verify_kd).  Any copy whose
- * path passes every six-face test proves the reference's answer (step 2
- * above; copies of a triangle give the same record), whichever copy it is.
- * A -1 only sends the ray to the exact kd walk (step 3). */
-template <bool COUNT>
-CRT_HD int prove(const ProofTables &pt, const DNode *nodes, const int32_t *slot_tri, int tri, Vec o, Vec d,
-                 const RayRcp &rr, Vec p, WalkCounts &c) {
-    if (pt.leaf) {
-        const int beg = CRT_LDG(pt.leaf_off, tri), end = CRT_LDG(pt.leaf_off, tri + 1);
-        if (end - beg <= kProofLeafScan) {
-            bool held = false;
-            for (int k = beg; k < end; ++k) {
-                const ProofLeaf L = CRT_LDG(pt.leaf, k);
-                if (!(p.x >= L.lo_x && p.x <= L.hi_x && p.y >= L.lo_y && p.y <= L.hi_y && p.z >= L.lo_z &&
-                      p.z <= L.hi_z))
-                    continue;
-                held = true;
-                if (prove_leaf<COUNT>(L, nodes, o, d, rr, c)) return L.slot;
-            }
-            if (held) return -1;   /* the descent would end in one of these (or fail): step 3 */
-        }
-    }
-    return CRT_PROOF_TOPO && pt.topo ? verify_topo<COUNT>(pt.topo, nodes, slot_tri, tri, o, d, rr, p, c)
-                                     : verify_kd<COUNT>(nodes, slot_tri, tri, o, d, rr, p, c);
-}
-
 /* Step 1 over a camera cell's candidate list (crt_layout.h CamCand) instead
  * of the BVH: the same closest triangle, t and tie flag as walk_bvh for any
  * camera ray of the cell.  Every triangle the ray can hit is in the list
@@ -562,7 +480,7 @@ CRT_HD int walk_bins(const CamCand *cands, int beg, int end, int bit, Vec o, Vec
  * same t) found by step 1: the reference's slot, or -1. */
 template <bool COUNT>
 CRT_HD int resolve_closest(const DNode *nodes, const PNode *pnodes, int n, const DTriGeo *slots,
-                           const uint8_t *slot_cull, const int32_t *slot_tri, const ProofTables &pt, bool planes_ok,
+                           const uint8_t *slot_cull, const int32_t *slot_tri, const KTopo *ktopo, bool planes_ok,
                            Vec o, Vec d, const PruneRay &pr, int tri, float t, bool tie, float &best_t, WalkCounts &c,
                            bool *fb = nullptr) {
     best_t = 0.0f;
@@ -570,7 +488,8 @@ CRT_HD int resolve_closest(const DNode *nodes, const PNode *pnodes, int n, const
     const RayRcp rr = make_ray_rcp(o, d, planes_ok);
     if (!tie) {
         const Vec p = vadd(o, vscale(d, t));
-        const int slot = prove<COUNT>(pt, nodes, slot_tri, tri, o, d, rr, p, c);
+        const int slot = CRT_PROOF_TOPO && ktopo ? verify_topo<COUNT>(ktopo, nodes, slot_tri, tri, o, d, rr, p, c)
+                                                 : verify_kd<COUNT>(nodes, slot_tri, tri, o, d, rr, p, c);
         if (slot >= 0) {
             best_t = t;
             return slot;
@@ -587,7 +506,7 @@ CRT_HD int resolve_closest(const DNode *nodes, const PNode *pnodes, int n, const
 template <bool COUNT, bool PF = (CRT_BVH_PREFETCH != 0)>
 CRT_HD int trace_bvh_exact(const BNode *bnodes, int bn, const DTriGeo *btri, const int32_t *btri_id,
                            const DNode *nodes, const PNode *pnodes, int n, const DTriGeo *slots,
-                           const uint8_t *slot_cull, const int32_t *slot_tri, const ProofTables &pt,
+                           const uint8_t *slot_cull, const int32_t *slot_tri, const KTopo *ktopo,
                            float prune_origin_max, bool planes_ok,
                            Vec o, Vec d, float &best_t, WalkCounts &c, bool *fb = nullptr) {
     best_t = 0.0f;
@@ -598,7 +517,7 @@ CRT_HD int trace_bvh_exact(const BNode *bnodes, int bn, const DTriGeo *btri, con
     bool tie = false;
     float t = 0.0f;
     const int tri = walk_bvh<COUNT, PF>(bnode_order(bnodes, bn, oct), bn, btri, btri_id, o, d, pr, t, tie, c);
-    return resolve_closest<COUNT>(nodes, pnodes, n, slots, slot_cull, slot_tri, pt, planes_ok, o, d, pr, tri, t, tie,
+    return resolve_closest<COUNT>(nodes, pnodes, n, slots, slot_cull, slot_tri, ktopo, planes_ok, o, d, pr, tri, t, tie,
                                   best_t, c, fb);
 }
 
@@ -606,7 +525,7 @@ CRT_HD int trace_bvh_exact(const BNode *bnodes, int bn, const DTriGeo *btri, con
 template <bool COUNT>
 CRT_HD int trace_bins_exact(const CamCand *cands, int beg, int end, int bit, const DNode *nodes, const PNode *pnodes, int n,
                             const DTriGeo *slots, const uint8_t *slot_cull, const int32_t *slot_tri,
-                            const ProofTables &pt, float prune_origin_max, bool planes_ok, Vec o, Vec d, float &best_t,
+                            const KTopo *ktopo, float prune_origin_max, bool planes_ok, Vec o, Vec d, float &best_t,
                             WalkCounts &c, bool *fb = nullptr) {
     best_t = 0.0f;
     if (fb) *fb = false;
@@ -615,7 +534,7 @@ CRT_HD int trace_bins_exact(const CamCand *cands, int beg, int end, int bit, con
     bool tie = false;
     float t = 0.0f;
     const int tri = walk_bins<COUNT>(cands, beg, end, bit, o, d, pr, t, tie, c);
-    return resolve_closest<COUNT>(nodes, pnodes, n, slots, slot_cull, slot_tri, pt, planes_ok, o, d, pr, tri, t, tie,
+    return resolve_closest<COUNT>(nodes, pnodes, n, slots, slot_cull, slot_tri, ktopo, planes_ok, o, d, pr, tri, t, tie,
                                   best_t, c, fb);
 }
 

@@ -283,64 +283,6 @@ int build_proof_tables(HostScene &hs) {
         t.a = c2 < nd.a ? c2 : -1;
         t.b = first_lo ? -1 : -2;
     }
-    /* per triangle its leaf copies with the path prove_leaf replays: depth,
-     * the depth where each face's plane was last set, the half taken per level */
-    hs.pleaf.clear();
-    hs.pleaf_off.assign(hs.tri_attr.size() + 1, 0);
-    struct Path { int32_t i, depth; uint64_t upper; uint8_t df[6]; };
-    std::vector<Path> st{Path{0, 0, 0ull, {0, 0, 0, 0, 0, 0}}};
-    std::vector<std::pair<int32_t, ProofLeaf>> recs;
-    bool deep = false;
-    while (!st.empty()) {
-        const Path w = st.back();
-        st.pop_back();
-        const DNode &nd = nodes[(size_t)w.i];
-        if (nd.b >= 0) {
-            ProofLeaf L{};
-            L.lo_x = nd.lo_x; L.hi_x = nd.hi_x; L.lo_y = nd.lo_y; L.hi_y = nd.hi_y; L.lo_z = nd.lo_z; L.hi_z = nd.hi_z;
-            L.depth_df = (uint32_t)w.depth | (uint32_t)w.df[0] << 8 | (uint32_t)w.df[1] << 16 | (uint32_t)w.df[2] << 24;
-            L.df345 = (uint32_t)w.df[3] | (uint32_t)w.df[4] << 8 | (uint32_t)w.df[5] << 16;
-            L.upper = w.upper;
-            for (int k = 0; k < node_leaf_count(nd); ++k) {
-                L.slot = nd.b + k;
-                recs.push_back({hs.slot_tri[(size_t)(nd.b + k)], L});
-            }
-            continue;
-        }
-        const KTopo &t = hs.ktopo[(size_t)w.i];
-        if (w.i + 1 >= nd.a) continue;                  /* childless interior node */
-        if (w.depth >= 62) { deep = true; continue; }   /* verify_topo's depth limit */
-        const int32_t kids[2] = {w.i + 1, t.a};
-        for (int q = 1; q >= 0; --q) {                  /* first child on top of the stack */
-            const int32_t ci = kids[q];
-            if (ci < 0) continue;
-            const DNode &ch = nodes[(size_t)ci];
-            Path c = w;
-            c.i = ci;
-            c.depth = w.depth + 1;
-            const bool up = (q == 0) == (t.b == -2);    /* first child upper iff t.b == -2 */
-            if (up) c.upper |= 1ull << w.depth;
-            const float pp[6] = {nd.lo_x, nd.lo_y, nd.lo_z, nd.hi_x, nd.hi_y, nd.hi_z};
-            const float cp[6] = {ch.lo_x, ch.lo_y, ch.lo_z, ch.hi_x, ch.hi_y, ch.hi_z};
-            for (int f = 0; f < 6; ++f)
-                if (!(cp[f] == pp[f])) c.df[f] = (uint8_t)c.depth;
-            st.push_back(c);
-        }
-    }
-    if (deep) {   /* the descent stops at 62 levels: no lists (the descent decides) */
-        hs.pleaf_off.clear();
-        return CRT_OK;
-    }
-    std::stable_sort(recs.begin(), recs.end(),
-                     [](const std::pair<int32_t, ProofLeaf> &a, const std::pair<int32_t, ProofLeaf> &b) {
-                         return a.first < b.first;
-                     });
-    hs.pleaf.reserve(recs.size());
-    for (const auto &r : recs) {
-        ++hs.pleaf_off[(size_t)r.first + 1];
-        hs.pleaf.push_back(r.second);
-    }
-    for (size_t k = 1; k < hs.pleaf_off.size(); ++k) hs.pleaf_off[k] += hs.pleaf_off[k - 1];
     return CRT_OK;
 }
 

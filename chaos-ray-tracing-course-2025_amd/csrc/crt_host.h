@@ -87,8 +87,6 @@ struct HostScene {
     std::vector<int32_t> btri_id;   /* triangle id | back_face_culling << 31 */
     /* the BVH proof's tree topology (crt_layout.h KTopo; build_proof_tables) */
     std::vector<KTopo> ktopo;
-    std::vector<ProofLeaf> pleaf;       /* per triangle its leaf copies (crt_layout.h ProofLeaf) */
-    std::vector<int32_t> pleaf_off;     /* triangles + 1 */
 
 
     /* root cell (crt_acceleration_tree.cpp:89-94); tree_on_host = false when

@@ -99,21 +99,6 @@ struct alignas(16) DTriGeo {
 };
 static_assert(sizeof(DTriGeo) == 48, "DTriGeo must be 48 B");
 
-/* A leaf copy of a triangle with the path the proof replays (crt_bvh.h
- * prove, crt_bvh_build.cpp build_proof_tables): the leaf's reference cell,
- * its slot, its depth, per face the depth where that face's plane was last
- * set on the way down (df), and which half each level took (upper, bit k). */
-struct alignas(16) ProofLeaf {
-    float lo_x, hi_x, lo_y, hi_y;
-    float lo_z, hi_z;
-    int32_t slot;
-    uint32_t depth_df;   /* depth | df[0] << 8 | df[1] << 16 | df[2] << 24 */
-    uint32_t df345;      /* df[3] | df[4] << 8 | df[5] << 16 */
-    uint32_t pad;
-    uint64_t upper;
-};
-static_assert(sizeof(ProofLeaf) == 48, "ProofLeaf must be 48 B");
-
 /* Camera-bin candidate (crt_bvh.h walk_bins, crt_bvh_build.cpp
  * build_camera_bins): a triangle listed in an 8x8-pixel cell of the frame
  * because a camera ray of that cell may hit it.  The hull box is the
@@ -181,10 +166,6 @@ struct DeviceScene {
     const int32_t *btri_id;
     /* the proof's tree topology (KTopo); null when the tree lives on the device only */
     const KTopo *ktopo;
-    /* per triangle its leaf copies with their paths: pleaf[pleaf_off[t] ..
-     * pleaf_off[t + 1]); null with ktopo */
-    const ProofLeaf *pleaf;
-    const int32_t *pleaf_off;
     /* camera bins (crt_bvh.h walk_bins): per 8x8 cell of the frame
      * (bin_tx cells a row), candidates bins[bin_off[c] .. bin_off[c + 1]);
      * null when not built */

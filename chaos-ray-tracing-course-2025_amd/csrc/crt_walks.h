@@ -811,8 +811,7 @@ __device__ __forceinline__ int trace_lane_bvh(const DeviceScene &s, bool active,
     if (COUNT) ++c.traversals;
     WalkCounts wc = {0u, 0u};
     const int best = trace_bvh_exact<COUNT, PF>(s.bnodes, s.bnode_count, s.btri, s.btri_id, s.nodes, s.pnodes,
-                                            s.node_count, s.slots, s.slot_cull, s.slot_tri,
-                                            ProofTables(s.ktopo, s.pleaf, s.pleaf_off), s.prune_origin_max,
+                                            s.node_count, s.slots, s.slot_cull, s.slot_tri, s.ktopo, s.prune_origin_max,
                                             s.planes_ok != 0, o, d, best_t, wc);
     if (COUNT) {
         c.nodes += wc.nodes;
@@ -964,7 +963,8 @@ __device__ int trace_bvh_window(const DeviceScene &s, int sl, bool act, Vec o, V
         WalkCounts pc = {0u, 0u};
         if (!tie) {
             const Vec p = vadd(o, vscale(d, t));
-            slot = prove<COUNT>(ProofTables(s.ktopo, s.pleaf, s.pleaf_off), s.nodes, s.slot_tri, tri, o, d, rr, p, pc);
+            slot = CRT_PROOF_TOPO && s.ktopo ? verify_topo<COUNT>(s.ktopo, s.nodes, s.slot_tri, tri, o, d, rr, p, pc)
+                                             : verify_kd<COUNT>(s.nodes, s.slot_tri, tri, o, d, rr, p, pc);
             if (slot >= 0) best_t = t;
         }
         if (slot < 0)
@@ -1102,9 +1102,8 @@ __device__ int trace_bins_wave(const DeviceScene &s, CamCand *stage, int beg, in
 #endif
     int slot = -1;
     if (act && !nan_ray)
-        slot = resolve_closest<COUNT>(s.nodes, s.pnodes, s.node_count, s.slots, s.slot_cull, s.slot_tri,
-                                      ProofTables(s.ktopo, s.pleaf, s.pleaf_off), s.planes_ok != 0, o, d, pr, best, bt,
-                                      tie, best_t, wc);
+        slot = resolve_closest<COUNT>(s.nodes, s.pnodes, s.node_count, s.slots, s.slot_cull, s.slot_tri, s.ktopo,
+                                      s.planes_ok != 0, o, d, pr, best, bt, tie, best_t, wc);
     if (COUNT) {
         c.nodes += wc.nodes;
         c.tris += wc.tris;

@@ -23,13 +23,6 @@ using namespace crt_amd;
 
 namespace {
 
-/* the proof's tables as the device gets them (crt_api.hip) */
-ProofTables proof_tables(const HostScene &hs) {
-    if (hs.ktopo.empty()) return ProofTables();
-    return ProofTables(hs.ktopo.data(), hs.pleaf_off.empty() ? nullptr : hs.pleaf.data(),
-                       hs.pleaf_off.empty() ? nullptr : hs.pleaf_off.data());
-}
-
 int walk_reference(const HostScene &hs, Vec o, Vec d, float &best_t, uint64_t &nodes, uint64_t &tris) {
     int best = -1;
     best_t = 0.0f;
@@ -121,7 +114,7 @@ int bvh_sim_trace(const crt_scene_desc *desc, const float *rays, int64_t n, int3
         bool fb = false;
         const int bs = trace_bvh_exact<true>(hs.bnodes.data(), hs.bnode_count, hs.btri.data(), hs.btri_id.data(),
                                              hs.nodes.data(), hs.pnodes.data(), nn, hs.slots.data(),
-                                             hs.slot_cull.data(), hs.slot_tri.data(), proof_tables(hs), hs.prune_origin_max, false, o,
+                                             hs.slot_cull.data(), hs.slot_tri.data(), hs.ktopo.empty() ? nullptr : hs.ktopo.data(), hs.prune_origin_max, false, o,
                                              d, t, c, &fb);
         bvh_tri[i] = bs >= 0 ? hs.slot_tri[bs] : -1;
         bvh_t[i] = t;
@@ -155,7 +148,7 @@ int bvh_sim_ray_stats(const crt_scene_desc *desc, const float *rays, int64_t n, 
                              hs.btri.data(), hs.btri_id.data(), o, d, pr, t, tie, w);
         (void)trace_bvh_exact<true>(hs.bnodes.data(), hs.bnode_count, hs.btri.data(), hs.btri_id.data(),
                                     hs.nodes.data(), hs.pnodes.data(), nn, hs.slots.data(), hs.slot_cull.data(),
-                                    hs.slot_tri.data(), proof_tables(hs), hs.prune_origin_max, false, o, d, t, c, &fb);
+                                    hs.slot_tri.data(), hs.ktopo.empty() ? nullptr : hs.ktopo.data(), hs.prune_origin_max, false, o, d, t, c, &fb);
         out[4 * i] = (int32_t)w.nodes;
         out[4 * i + 1] = (int32_t)w.tris;
         out[4 * i + 2] = (int32_t)(c.nodes + c.tris - w.nodes - w.tris);
@@ -510,7 +503,7 @@ extern "C" int bins_sim_cells(const crt_scene_desc *desc, int64_t *out) {
                     float tt = 0.f;
                     (void)resolve_closest<true>(hs.nodes.data(), hs.pnodes.data(), (int)hs.nodes.size(), hs.slots.data(),
                                                 hs.slot_cull.data(), hs.slot_tri.data(),
-                                                proof_tables(hs), false, o, d, pr, best, bt,
+                                                hs.ktopo.empty() ? nullptr : hs.ktopo.data(), false, o, d, pr, best, bt,
                                                 tie, tt, pc, &fb);
                     r[4] = std::max<int64_t>(r[4], pc.nodes + pc.tris);
                     r[5] += tie ? 1 : 0;
