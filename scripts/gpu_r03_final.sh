@@ -7,7 +7,8 @@
 #      read them (bench.py load_pmc checks the build id)
 #   3. bench.py lines: C2 (default), C3, C4, C5; rocprofv3 kernel trace of the C2 bench
 #   4. shard times of every config
-#   TAG=final STEPS=tests,pmc,bench,trace,shards bash scripts/gpu_r03_final.sh
+#   5. one-GPU gloo rehearsals of the N=2 tiles path with --check
+#   TAG=final STEPS=tests,pmc,bench,trace,shards,rehearse bash scripts/gpu_r03_final.sh
 set -u
 cd "$(dirname "$0")/.."
 TAG=${TAG:-final}
@@ -42,5 +43,9 @@ if [[ $STEPS == *shards* ]]; then
     r=20; [ $c = c4 ] && r=3; [ $c = c5 ] && r=5
     run shards_$c 400 python3 scripts/shard_times.py --config $c --reps $r --out "$OUT/shards_$c.json"
   done
+fi
+if [[ $STEPS == *rehearse* ]]; then
+  run rehearse_c2_gloo2 400 python bench.py --gpus 2 --backend gloo --check --steps 20 --warmup 3
+  run rehearse_c4_gloo2 600 python bench.py --config c4 --gpus 2 --backend gloo --check --steps 3 --warmup 1 --no-secondary
 fi
 exit 0
