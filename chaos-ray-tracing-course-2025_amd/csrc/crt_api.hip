@@ -675,12 +675,13 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
         sc->gi_refill = value != 0;
     } else if (k == "gi_machine") {
         sc->gi_machine = value != 0;
-    } else if (k == "bins" || k == "bins_split") {   /* camera bins: the full-frame plan depends on them */
+    } else if (k == "bins" || k == "bins_split" || k == "bins_quad") {   /* camera bins: the full-frame plan depends on them */
         if (k == "bins_split" && value < 1) return set_error(CRT_E_INVALID, "bins_split must be >= 1");
-        if (k == "bins_split" ? value != sc->bins_split : (value != 0) != (sc->bins_on != 0)) {
+        int &field = k == "bins" ? sc->bins_on : k == "bins_quad" ? sc->bins_quad : sc->bins_split;
+        const int v = k == "bins" || k == "bins_quad" ? (value != 0) : (int)value;
+        if (v != field) {
             HIP_TRY(hipDeviceSynchronize());
-            if (k == "bins") sc->bins_on = value != 0;
-            else sc->bins_split = value;
+            field = v;
             sc->calib_walk = -1;
             free_plans(sc);
             int64_t px = 0;

@@ -131,8 +131,8 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         /* camera bins: one wave per 8x8 tile on its cell's list; a cell
          * whose list is long is split into four 4x4 waves (each leaves the
          * list once its 16 pixels are done: the list's tail latency is
-         * spread over four waves); the longest lists first, the split ones
-         * at raised issue priority */
+         * spread over four waves) walking with four lanes per pixel; the
+         * longest lists first, the split ones at raised issue priority */
         const int tx = (W + 7) / 8;
         auto cost = [&](const Tile &t) {
             const int cx = t.x / 8, cy = t.y / 8;
@@ -146,7 +146,8 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
                 for (int yy = 0; yy < t.h; yy += 4)
                     for (int xx = 0; xx < t.w; xx += 4)
                         split.push_back(Tile{t.x + xx, t.y + yy, std::min(4, t.w - xx), std::min(4, t.h - yy),
-                                             t.out_base + (int64_t)yy * t.out_stride + xx, t.out_stride, 1});
+                                             t.out_base + (int64_t)yy * t.out_stride + xx, t.out_stride,
+                                             sc->bins_quad ? 3 : 1});
             } else {
                 split.push_back(t);
             }

@@ -17,7 +17,8 @@ struct alignas(16) Tile {
     int32_t x, y, w, h;        /* pixel rectangle, w,h <= 8 */
     int64_t out_base;          /* output pixel index of (x, y) */
     int32_t out_stride;        /* output pixels per row */
-    int32_t prio;              /* 1: one of the frame's heaviest waves — raised issue priority */
+    int32_t prio;              /* bit 0: one of the frame's heaviest waves — raised issue priority;
+                                * bit 1: camera-bins split tile, four lanes per pixel */
 };
 
 struct alignas(16) UnpackBucket {

@@ -31,7 +31,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
     /* the heaviest tiles set the frame length (their walks are long chains of
      * dependent loads): they get issue priority over the light waves that
      * share their SIMD (s_setprio; scheduling only, results unchanged) */
-    if (tl.prio) __builtin_amdgcn_s_setprio(3);
+    if (tl.prio & 1) __builtin_amdgcn_s_setprio(3);
     if constexpr (TRAV == 13 && !FULL) {
         /* tiles of <= 16 rays (the measured plan's splits of heavy tiles): window walk */
         const int tw = uniform_i(tl.w), th = uniform_i(tl.h);
@@ -85,13 +85,41 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
         if ((tx0 & 7) + tw <= 8 && (ty0 & 7) + th <= 8) {
             const int cell = (ty0 >> 3) * s.bin_tx + (tx0 >> 3);
             const int beg = load_scalar(s.bin_off, cell), end = load_scalar(s.bin_off, cell + 1);
+            __shared__ CamCand stage[4 * kBinChunk];
+            if ((tl.prio & 2) && tw <= 4 && th <= 4) {
+                /* a split tile of a long list: four lanes per pixel (trace_bins_lanes) */
+                const int p = lane >> 2, sl = lane & 3, lx = p & 3, ly = p >> 2;
+                const bool act = lx < tw && ly < th;
+                Vec o, d;
+                camera_ray(s, tx0 + (act ? lx : 0), ty0 + (act ? ly : 0), o, d);
+                LaneCounts cw = {};
+                float t;
+                const int bit = 8 * ((ty0 & 7) + ly) + (tx0 & 7) + lx;
+                CamCand *stw = stage + (threadIdx.x >> 6) * kBinChunk;
+                const int slot = trace_bins_lanes<COUNT, 4>(s, stw, beg, end, bit, sl, act, o, d, t, cw);
+                if (act && sl == 0) {
+                    const Vec c = shade_primary(s, st, o, d, slot, t);
+                    float *pxo = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
+                    pxo[0] = c.x;
+                    pxo[1] = c.y;
+                    pxo[2] = c.z;
+                }
+                if (stamps && lane == 0) stamps[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
+                if (COUNT) {
+                    atomicAdd(&counters[0], (unsigned long long)cw.traversals);
+                    atomicAdd(&counters[1], (unsigned long long)cw.nodes);
+                    atomicAdd(&counters[2], (unsigned long long)cw.tris);
+                    atomicAdd(&counters[3], (unsigned long long)cw.hits);
+                    if (lane == 0) atomicAdd(&counters[7], 1ull);
+                }
+                return;
+            }
             const int lx = lane & 7, ly = lane >> 3;
             const bool act = lx < tw && ly < th;
             Vec o, d;
             camera_ray(s, tx0 + (act ? lx : 0), ty0 + (act ? ly : 0), o, d);
             LaneCounts cw = {};
             float t;
-            __shared__ CamCand stage[4 * kBinChunk];
             const int bit = 8 * ((ty0 & 7) + ly) + (tx0 & 7) + lx;
             const int slot = trace_bins_wave<COUNT>(s, stage + (threadIdx.x >> 6) * kBinChunk, beg, end, bit, act, o,
                                                     d, t, cw, stamps ? &stamps[2 * wave] : nullptr);

@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         const int wave = gid >> 6;
         if (wave >= ntiles) return;
         tl = tiles[wave];
-        if (tl.prio) __builtin_amdgcn_s_setprio(3);
+        if (tl.prio & 1) __builtin_amdgcn_s_setprio(3);
         const int lx = lane & 7, ly = lane >> 3;
         has = lx < tl.w && ly < tl.h;
         if (has) camera_ray(s, tl.x + lx, tl.y + ly, o, d);

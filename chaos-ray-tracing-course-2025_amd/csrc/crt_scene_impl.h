@@ -156,6 +156,7 @@ struct crt_hip_scene {
     int calib_deferred_walk = -1;  /* walk whose first frame skipped the calibration */
     int bins_on = 1;               /* camera frames take the camera bins where built (walk 15; option "bins") */
     int bins_split = 48;           /* cells with this many candidates run as four 4x4 waves (option "bins_split") */
+    int bins_quad = 1;             /* those waves walk with four lanes per pixel (option "bins_quad") */
     void *probe_buf = nullptr;     /* calibration probes: tile list + costs (probe_tiles) */
     size_t probe_cap = 0;          /* bytes */
     int prio_tiles = 1024;         /* heaviest tiles run at raised issue priority */

@@ -1112,6 +1112,94 @@ __device__ int trace_bins_wave(const DeviceScene &s, CamCand *stage, int beg, in
     return slot;
 }
 
+/* trace_bins_wave with K lanes per pixel (lane = K p + sl; K = 4: a tile of
+ * at most 4x4 pixels, K = 2: at most 8x4): lane sl walks the pixel's covering
+ * records at chunk positions j = sl (mod K), and the K share their lim (the
+ * smallest best t among them) after every round.  Merged at the end: the
+ * smallest t, the record of the lowest lane holding it, tie when two lanes
+ * hold it or one of them saw two hits there.  That is walk_bins' (best, t,
+ * tie): every record hitting at the final t is tested by its lane (its dmin
+ * and hull pass any lim >= that t), and a lane's own best may lag the shared
+ * lim but never lowers the minimum wrongly.  Lane sl = 0 resolves
+ * (resolve_closest).  act: the lane's pixel exists (same on its K lanes). */
+template <bool COUNT, int K>
+__device__ int trace_bins_lanes(const DeviceScene &s, CamCand *stage, int beg, int end, int bit, int sl, bool act, Vec o,
+                                Vec d, float &best_t, LaneCounts &c) {
+    static_assert(K == 2 || K == 4, "two or four lanes per pixel");
+    best_t = 0.0f;
+    const bool nan_ray = isnan(o.x) || isnan(o.y) || isnan(o.z) || isnan(d.x) || isnan(d.y) || isnan(d.z);
+    if (COUNT && act && sl == 0) ++c.traversals;
+    const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
+    const int lane = (int)__lane_id();
+    int best = -1;
+    float bt = 0.0f, lim = INFINITY;
+    bool tie = false, live = act && !nan_ray;
+    WalkCounts wc = {0u, 0u};
+    for (int k0 = beg; k0 < end; k0 += kBinChunk) {
+        if (__ballot(live) == 0ull) break;
+        const int n = min(kBinChunk, end - k0);
+        if (lane < n) stage[lane] = load_global(s.bins, k0 + lane);
+        __builtin_amdgcn_wave_barrier();
+        live = live && ((stage[0].rest >> bit) & 1ull) != 0ull;   /* a later record covers the pixel */
+        uint32_t w = 0u;
+        if (live) {
+            for (int j = sl; j < n; j += K) w |= (uint32_t)((stage[j].mask >> bit) & 1ull) << j;
+        }
+        while (__ballot(w != 0u) != 0ull) {
+            if (w != 0u) {
+                const int j = __builtin_ctz(w);
+                w &= w - 1u;
+                const CamCand cc = stage[j];
+                if (cc.dmin > lim) {   /* sorted by dmin: nothing later hits at t <= the pixel's best t */
+                    live = false;
+                    w = 0u;
+                } else {
+                    if (COUNT) ++wc.nodes;
+                    if (cand_alive(cc, pr, lim)) {
+                        if (COUNT) ++wc.tris;
+                        const uint8_t cull = (uint8_t)((uint32_t)cc.id >> 31);
+                        float t;
+                        if (tri_hit(o, d, cc.g, &cull, t)) {
+                            if (best < 0 || t < bt) {
+                                bt = t;
+                                best = cc.id & 0x7fffffff;
+                                tie = false;
+                                lim = fminf(lim, t);
+                            } else if (t == bt) {
+                                tie = true;
+                            }
+                        }
+                    }
+                }
+            }
+            lim = fminf(lim, __shfl_xor(lim, 1));
+            if (K == 4) lim = fminf(lim, __shfl_xor(lim, 2));
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    /* merge the pixel's K lanes */
+    const float mine = best >= 0 ? bt : INFINITY;
+    float g = fminf(mine, __shfl_xor(mine, 1));
+    if (K == 4) g = fminf(g, __shfl_xor(g, 2));
+    const bool at = best >= 0 && bt == g;
+    const int q = lane & ~(K - 1);
+    const uint32_t holders = (uint32_t)(__ballot(at) >> q) & ((1u << K) - 1u);
+    const uint32_t ties = (uint32_t)(__ballot(at && tie) >> q) & ((1u << K) - 1u);
+    const int src = q + (holders ? __builtin_ctz(holders) : 0);
+    const int gbest = __shfl(best, src);
+    int slot = -1;
+    if (act && !nan_ray && sl == 0 && holders != 0u)
+        slot = resolve_closest<COUNT>(s.nodes, s.pnodes, s.node_count, s.slots, s.slot_cull, s.slot_tri, s.ktopo,
+                                      s.planes_ok != 0, o, d, pr, gbest, g, __builtin_popcount(holders) > 1 || ties != 0u,
+                                      best_t, wc);
+    if (COUNT) {
+        c.nodes += wc.nodes;
+        c.tris += wc.tris;
+        if (slot >= 0) ++c.hits;
+    }
+    return slot;
+}
+
 /* Walks (TRAV), all bit-identical in result:
  *   7  packet walk in the reference's node order (work counters = the reference's)
  *   8  pruned packet walk (exact t-pruning), any camera ray

@@ -402,6 +402,10 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  *   "bins"       0/1 (default 1): camera frames of scenes without reflective /
  *                refractive materials or GI walk per-8x8-cell candidate lists
  *                 where they were built
+ *   "bins_split" >= 1 (default 48): cells with this many candidates run as
+ *                four 4x4-pixel waves
+ *   "bins_quad"  0/1 (default 1): those waves walk the list with four lanes
+ *                per pixel
  *   "secondary"  walk of secondary rays: 0 = by frame (default: 14 where the
  *                scene has a BVH), 4 = cooperative walk in the reference's
  *                order, 10 = pruned cooperative, 14 = BVH + proof

@@ -313,10 +313,15 @@ def test_camera_bins_frames_bit_exact(N, oracle, name, w, h):
     assert g.plan_info()["calib_k"] == 0.0   # no probes: one wave per 8x8 cell
     a = g.render(st)
     b = N.HipScene(sc, bins=0).render(st)
-    q = N.HipScene(sc, bins_split=1).render(st)   # every cell with a candidate as four 4x4 waves
+    gq = N.HipScene(sc, bins_split=1)   # every cell with a candidate as four 4x4 waves, four lanes per pixel
+    q = gq.render(st)
+    q1 = N.HipScene(sc, bins_split=1, bins_quad=0).render(st)   # ... one lane per pixel
     want = oracle.OracleScene(sc).render(st)
     assert np.array_equal(bits(a), bits(want))
     assert np.array_equal(bits(b), bits(want))
     assert np.array_equal(bits(q), bits(want))
+    assert np.array_equal(bits(q1), bits(want))
     ca, cb = g.count_work(st), N.HipScene(sc, bins=0).count_work(st)
     assert ca["traversals"] == cb["traversals"] == w * h and ca["hits"] == cb["hits"]
+    cq = gq.count_work(st)
+    assert cq["traversals"] == w * h and cq["hits"] == ca["hits"]
