@@ -160,3 +160,24 @@ def test_camera_bins_equal_bvh_walk(sim, name, size):  # noqa: F811
     assert built == 1
     assert rays > 0 and diff == 0, f"{name}: {diff} of {rays} camera rays differ"
     assert tested < 8 * rays   # the lists are short: a few candidates per ray
+
+
+@pytest.mark.parametrize("name,size", BINS_CASES)
+def test_camera_bins_lanes_equal_serial_walk(sim, name, size):  # noqa: F811
+    """K lanes per pixel on one cell's list (crt_walks.h trace_bins_lanes, the
+    split 4x4 waves of camera-bins frames), restated on the host with the
+    device's schedule (positions j = lane mod K, one record per lane per
+    round, the bound shared after every round, then the merge): the same hit,
+    t bits and tie flag as the serial walk_bins on every camera ray, and the
+    same triangle where there is no tie."""
+    from crt_amd.native import _desc_ptr
+    sc = scene_npz(name)
+    if size:
+        sc = sc.set_resolution(*size)
+    sim.bins_sim_lanes_check.argtypes = [_P, C.c_int, _P]
+    sim.bins_sim_lanes_check.restype = C.c_int
+    for k in (4, 2):
+        out = np.zeros(3, np.uint64)
+        assert sim.bins_sim_lanes_check(C.cast(_desc_ptr(sc), _P), k, out.ctypes.data) == 0
+        rays, diff, _shared = (int(x) for x in out)
+        assert rays > 0 and diff == 0, f"{name} K={k}: {diff} of {rays} camera rays differ"

@@ -403,6 +403,112 @@ extern "C" int bins_sim_check(const crt_scene_desc *desc, uint64_t *out) {
     return CRT_OK;
 }
 
+/* Host restatement of crt_walks.h trace_bins_lanes' schedule (K lanes per
+ * pixel: lane sl takes the covering records at chunk positions j = sl mod K,
+ * one per round, the K share lim after every round; merged: smallest t, the
+ * lowest lane holding it, tie when two lanes hold it or one saw two hits
+ * there) against walk_bins on every camera ray of the frame.  out[0] rays,
+ * out[1] rays whose (hit, t bits, tie, triangle when no tie) differ, out[2]
+ * rays where some lane stopped on the shared bound (the sharing mattered). */
+extern "C" int bins_sim_lanes_check(const crt_scene_desc *desc, int K, uint64_t *out) {
+    if (K != 2 && K != 4) return -1;
+    HostScene hs;
+    int rc = prepare_scene(desc, hs);
+    if (rc != CRT_OK) return rc;
+    if (hs.bnode_count == 0 && ((rc = build_bvh(hs)) != CRT_OK || (rc = build_proof_tables(hs)) != CRT_OK)) return rc;
+    std::vector<CamCand> bins;
+    std::vector<int32_t> off;
+    if ((rc = build_camera_bins(hs, bins, off)) != CRT_OK) return rc;
+    out[0] = out[1] = out[2] = 0;
+    if (bins.empty()) return CRT_OK;
+    DeviceScene ds{};
+    std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
+    std::memcpy(ds.cam_rot, hs.cam_rot, sizeof ds.cam_rot);
+    ds.width = hs.width;
+    ds.height = hs.height;
+    ds.aspect = hs.aspect;
+    ds.tan_half_fov = hs.tan_half_fov;
+    const int tx = (hs.width + 7) / 8;
+    constexpr int kChunk = 32;   /* crt_walks.h kBinChunk */
+    for (int y = 0; y < hs.height; ++y)
+        for (int x = 0; x < hs.width; ++x) {
+            Vec o, d;
+            camera_ray(ds, x, y, o, d);
+            const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
+            const int cell = (y / 8) * tx + x / 8, bit = 8 * (y % 8) + x % 8;
+            WalkCounts wc = {0u, 0u};
+            float ts = 0.f;
+            bool ties = false;
+            const int a = walk_bins<false>(bins.data(), off[cell], off[cell + 1], bit, o, d, pr, ts, ties, wc);
+            int best[4] = {-1, -1, -1, -1};
+            float bt[4] = {0.f, 0.f, 0.f, 0.f}, lim = INFINITY;
+            bool tie[4] = {false, false, false, false}, live[4], shared_stop = false;
+            for (int l = 0; l < K; ++l) live[l] = true;
+            for (int k0 = off[cell]; k0 < off[cell + 1]; k0 += kChunk) {
+                bool any = false;
+                for (int l = 0; l < K; ++l) any = any || live[l];
+                if (!any) break;
+                const int n = std::min(kChunk, off[cell + 1] - k0);
+                const bool rest = ((bins[k0].rest >> bit) & 1ull) != 0ull;
+                uint32_t w[4] = {0u, 0u, 0u, 0u};
+                for (int l = 0; l < K; ++l) {
+                    live[l] = live[l] && rest;
+                    if (live[l])
+                        for (int j = l; j < n; j += K) w[l] |= (uint32_t)((bins[k0 + j].mask >> bit) & 1ull) << j;
+                }
+                for (;;) {
+                    bool busy = false;
+                    for (int l = 0; l < K; ++l) busy = busy || w[l] != 0u;
+                    if (!busy) break;
+                    for (int l = 0; l < K; ++l) {
+                        if (w[l] == 0u) continue;
+                        const int j = __builtin_ctz(w[l]);
+                        w[l] &= w[l] - 1u;
+                        const CamCand &cc = bins[k0 + j];
+                        if (cc.dmin > lim) {
+                            if (best[l] < 0 || cc.dmin <= bt[l]) shared_stop = true;   /* alone it would go on */
+                            live[l] = false;
+                            w[l] = 0u;
+                        } else if (cand_alive(cc, pr, lim)) {
+                            const uint8_t cull = (uint8_t)((uint32_t)cc.id >> 31);
+                            float t;
+                            if (tri_hit(o, d, cc.g, &cull, t)) {
+                                if (best[l] < 0 || t < bt[l]) {
+                                    bt[l] = t;
+                                    best[l] = cc.id & 0x7fffffff;
+                                    tie[l] = false;
+                                } else if (t == bt[l]) {
+                                    tie[l] = true;
+                                }
+                            }
+                        }
+                    }
+                    for (int l = 0; l < K; ++l)
+                        if (best[l] >= 0) lim = std::min(lim, bt[l]);
+                }
+            }
+            float g = INFINITY;
+            for (int l = 0; l < K; ++l)
+                if (best[l] >= 0) g = std::min(g, bt[l]);
+            int holders = 0, b = -1;
+            bool tg = false;
+            for (int l = 0; l < K; ++l)
+                if (best[l] >= 0 && bt[l] == g) {
+                    if (b < 0) b = best[l];
+                    ++holders;
+                    tg = tg || tie[l];
+                }
+            tg = tg || holders > 1;
+            ++out[0];
+            out[2] += shared_stop;
+            uint32_t u1, u2;
+            std::memcpy(&u1, &ts, 4);
+            std::memcpy(&u2, &g, 4);
+            if ((a < 0) != (b < 0) || (a >= 0 && (u1 != u2 || ties != tg || (!ties && a != b)))) ++out[1];
+        }
+    return CRT_OK;
+}
+
 /* debugging aid: the first `cap` differing rays of bins_sim_check as
  * {x, y, bvh tri, bins tri, bvh t bits, bins t bits, tie bvh, tie bins, bvh tri listed in the cell} */
 extern "C" int bins_sim_diffs(const crt_scene_desc *desc, int64_t *rows, int cap) {
