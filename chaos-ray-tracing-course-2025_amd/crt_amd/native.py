@@ -128,7 +128,8 @@ class SceneInfo(C.Structure):
                 ("max_leaf_size", C.c_int32), ("device_bytes", C.c_int64), ("width", C.c_int32),
                 ("height", C.c_int32), ("bucket_size", C.c_int32), ("gi_on", C.c_int32),
                 ("reflections_on", C.c_int32), ("refractions_on", C.c_int32), ("tree_on_device", C.c_int32),
-                ("tree_build_ms", C.c_double)]
+                ("tree_build_ms", C.c_double), ("prep_ms", C.c_double), ("bvh_ms", C.c_double),
+                ("bins_ms", C.c_double), ("upload_ms", C.c_double), ("create_ms", C.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -207,6 +208,8 @@ EXPORTS = [
     ("crt_shard_compact_plan", C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int, C.c_int, _P, _P, C.c_int64]),
     ("crt_shard_plan", C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int, C.c_int, _P, C.c_int64]),
     ("crt_hip_trace_batch", C.c_int, [_P, _P, C.c_int64, _P]),
+    ("crt_hip_camera_bins", C.c_int64, [_P, _P, _P, C.c_int64]),
+    ("crt_host_camera_bins", C.c_int64, [_P, _P, _P, C.c_int64]),
     ("crt_hip_count_work", C.c_int, [_P, C.POINTER(RendererSettings), C.POINTER(WorkCounts)]),
     ("crt_hip_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_double)]),
     ("crt_hip_plan_info", C.c_int, [_P, _P]),
@@ -389,6 +392,29 @@ def _desc_ptr(src):
     return src
 
 
+# crt_layout.h CamCand (96 B): one camera-bins candidate
+CAMCAND_DTYPE = np.dtype([("lo_x", "<f4"), ("hi_x", "<f4"), ("lo_y", "<f4"), ("hi_y", "<f4"), ("lo_z", "<f4"),
+                          ("hi_z", "<f4"), ("dmin", "<f4"), ("id", "<i4"), ("g", "<f4", (12,)), ("mask", "<u8"),
+                          ("rest", "<u8")])
+assert CAMCAND_DTYPE.itemsize == 96
+
+
+def _camera_bins(fn, handle, width: int, height: int):
+    """(len[cells], records) of a camera-bins hook (crt_hip_camera_bins /
+    crt_host_camera_bins): per 8x8 cell its list length (-1: over the cell cap)
+    and the lists back to back in cell order."""
+    ncell = ((width + 7) // 8) * ((height + 7) // 8)
+    ln = np.zeros(ncell, np.int32)
+    n = fn(handle, ln.ctypes.data, None, 0)
+    if n < 0:
+        _check(int(n))
+    recs = np.zeros(max(int(n), 1), CAMCAND_DTYPE)
+    m = fn(handle, ln.ctypes.data, recs.ctypes.data, max(int(n), 1))
+    if m < 0:
+        _check(int(m))
+    return ln, recs[:int(m)]
+
+
 # --------------------------------------------------------------------------
 #  host scene (mesh prep + tree build, no GPU)
 # --------------------------------------------------------------------------
@@ -422,6 +448,11 @@ class HostScene:
         out = np.zeros((self.info()["vertex_count"], 3), np.float32)
         _check(lib().crt_host_scene_vertex_normals(self._h, out.ctypes.data))
         return out
+
+    def camera_bins(self):
+        """The host checker's camera bins (build_camera_bins): (len[cells], records)."""
+        i = self.info()
+        return _camera_bins(lib().crt_host_camera_bins, self._h, i["width"], i["height"])
 
     def face_normals(self) -> np.ndarray:
         out = np.zeros((self.info()["triangle_count"], 3), np.float32)
@@ -607,6 +638,11 @@ class HipScene:
         v = C.c_double()
         _check(lib().crt_hip_last_kernel_ms(self._h, C.byref(v)))
         return v.value
+
+    def camera_bins(self):
+        """One frame's device camera bins (crt_bins.hip): (len[cells], records)."""
+        i = self.info()
+        return _camera_bins(lib().crt_hip_camera_bins, self._h, i["width"], i["height"])
 
     def trace(self, rays: np.ndarray) -> np.ndarray:
         rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)

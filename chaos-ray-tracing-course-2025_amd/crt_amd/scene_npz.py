@@ -120,6 +120,16 @@ class ArrayScene:
         self._desc.camera.height = height
         return self
 
+    def set_camera(self, location=None, rotation=None, fov_degrees=None) -> "ArrayScene":
+        """Move the camera (crt_camera.h: location, row-major rotation, fov)."""
+        if location is not None:
+            self._desc.camera.location = Vec3(*(float(x) for x in location))
+        if rotation is not None:
+            self._desc.camera.rotation = (C.c_float * 9)(*(float(x) for x in np.ravel(rotation)))
+        if fov_degrees is not None:
+            self._desc.camera.fov_degrees = float(fov_degrees)
+        return self
+
     def set_settings(self, *, gi_on=None, reflections_on=None, refractions_on=None, bucket_size=None):
         if gi_on is not None:
             self._desc.gi_on = int(gi_on)

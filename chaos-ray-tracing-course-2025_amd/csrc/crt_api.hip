@@ -40,8 +40,12 @@ public:
         cv_.notify_all();
         for (auto &t : th_) t.join();
     }
-    /* f(0 .. n-1) over the pool and the calling thread; returns when all ran */
+    /* f(0 .. n-1) over the pool and the calling thread; returns when all ran.
+     * One job at a time: concurrent callers (renders of different scenes on
+     * different host threads) queue on run_mu_, so a job's counters are never
+     * reset while its workers still run it. */
     void run(int n, const std::function<void(int)> &f) {
+        std::lock_guard<std::mutex> one(run_mu_);
         std::unique_lock<std::mutex> l(mu_);
         job_ = &f;
         n_ = n;
@@ -73,6 +77,7 @@ private:
             if (++done_ == n_) done_cv_.notify_all();
         }
     }
+    std::mutex run_mu_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
     std::vector<std::thread> th_;
@@ -133,12 +138,14 @@ int image_to_host(crt_hip_scene *sc, float *dst, size_t nfl) {
 
 }  // namespace
 
-extern "C" {
+namespace crt_amd {
 
-int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **out) {
-    if (!h || !out) return set_error(CRT_E_INVALID, "null argument");
+/* A prepared host scene into HBM of `device`.  primary = false: a further
+ * replica of a multi-GPU handle (crt_multi.hip), which renders into the
+ * gather buffers only — no output image, no pinned staging image. */
+int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **out) {
     *out = nullptr;
-    const HostScene &hs = *reinterpret_cast<const HostScene *>(h);
+    const auto t_up = std::chrono::steady_clock::now();
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return set_error(CRT_E_INVALID, "no such HIP device");
@@ -173,7 +180,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
                 sc->gi_blocks = prop.multiProcessorCount * per_cu;
         }
     }
-    crt_host_scene_info(h, &sc->info);
+    crt_host_scene_info(reinterpret_cast<const crt_host_scene *>(&hs), &sc->info);
     sc->info.device_bytes = 0;
     for (const DMaterial &m : hs.materials) {
         if (m.type == CRT_MATERIAL_REFLECTIVE || m.type == CRT_MATERIAL_REFRACTIVE) sc->has_secondary = true;
@@ -243,22 +250,6 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
         ds.bnode_count = hs.bnode_count;
         if ((rc = upload(sc.get(), hs.ktopo, &ds.ktopo)) != CRT_OK) return rc;
     }
-    /* camera bins: scenes whose camera rays are traced by the tile kernels —
-     * frames without recursion (k_render_tiles walk 15) and level 0 of the
-     * wavefront recursion (k_wf_level<15, true>); GI frames trace theirs in
-     * the GI machine */
-    if (hs.bnode_count > 0 && hs.tree_on_host && !(hs.gi_on && sc->has_diffuse)) {
-        std::vector<CamCand> bins;
-        std::vector<int32_t> off;
-        if ((rc = build_camera_bins(hs, bins, off)) != CRT_OK) return rc;
-        if (!bins.empty()) {
-            if ((rc = upload(sc.get(), bins, &ds.bins)) != CRT_OK) return rc;
-            if ((rc = upload(sc.get(), off, &ds.bin_off)) != CRT_OK) return rc;
-            ds.bin_tx = (hs.width + 7) / 8;
-            sc->bin_count.resize(off.size() - 1);
-            for (size_t c = 0; c + 1 < off.size(); ++c) sc->bin_count[c] = off[c + 1] - off[c];
-        }
-    }
     sc->camera_fast = camera_rays_fast(hs, ds.planes_ok != 0);
     if (ds.bnodes) sc->traversal = 14;   /* camera rays through the BVH too */
     if ((rc = upload(sc.get(), hs.tri_attr, &ds.tri_attr)) != CRT_OK) return rc;
@@ -282,6 +273,11 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
 
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
     warm_code_objects(sc->device, sc->stream);
+    /* camera bins (crt_bins.hip), rebuilt on the device by every camera frame
+     * of scenes whose camera rays the tile kernels trace without recursion
+     * (no reflective / refractive material, no GI with a diffuse one) */
+    if (hs.bnode_count > 0 && hs.tree_on_host && !sc->has_secondary && !(hs.gi_on && sc->has_diffuse))
+        if ((rc = bins_setup(sc.get(), hs)) != CRT_OK) return rc;
     HIP_TRY(hipEventCreate(&sc->ev_start));
     HIP_TRY(hipEventCreate(&sc->ev_stop));
     void *p = nullptr;
@@ -304,7 +300,7 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
     {
         const DeviceScene *d = nullptr;
         if ((rc = sync_device_record(sc.get(), &d)) != CRT_OK) return rc;
-        if (!sc->grid_empty) {
+        if (!sc->grid_empty && primary) {
             const size_t bytes = (size_t)hs.width * hs.height * 3 * sizeof(float);
             HIP_TRY(hipMalloc(&sc->d_out, bytes));
             /* the staging image of copies into pageable memory (image_to_host) */
@@ -320,8 +316,19 @@ int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **ou
         unsigned long long probe[16];
         HIP_TRY(hipMemcpy(probe, sc->d_counters, sizeof probe, hipMemcpyDeviceToHost));
     }
+    sc->info.bins_ms = sc->bins.setup_ms;
+    sc->info.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_up).count();
     *out = sc.release();
     return CRT_OK;
+}
+
+}  // namespace crt_amd
+
+extern "C" {
+
+int crt_hip_scene_upload(const crt_host_scene *h, int device, crt_hip_scene **out) {
+    if (!h || !out) return set_error(CRT_E_INVALID, "null argument");
+    return scene_upload(*reinterpret_cast<const HostScene *>(h), device, true, out);
 }
 
 int crt_hip_scene_create_ex(const crt_scene_desc *desc, int device, int flags, crt_hip_scene **out) {
@@ -372,6 +379,7 @@ void crt_hip_scene_destroy(crt_hip_scene *sc) {
     if (sc->stream) (void)hipStreamSynchronize(sc->stream);
     for (void *p : sc->allocs) (void)hipFree(p);
     for (void *p : sc->plan_allocs) (void)hipFree(p);
+    bins_free(sc);
     if (sc->d_out) (void)hipFree(sc->d_out);
     if (sc->gi_frames) (void)hipFree(sc->gi_frames);
     wf_free(sc->wf);
@@ -581,24 +589,61 @@ int crt_hip_profile_waves(crt_hip_scene *sc, const crt_renderer_settings *st, ui
         const int rc = ensure_plans(sc, st, sc->stream);
         if (rc != CRT_OK) return rc;
     }
-    const int nt = sc->full.ntiles;
+    const int nt = sc->full.waves;
     if (!stamps || !tile_xy) return nt;      /* query the size */
     if (cap < nt) return set_error(CRT_E_INVALID, "stamp buffer too small");
     const size_t nfl = (size_t)sc->info.width * sc->info.height * 3;
     if (!sc->d_out) HIP_TRY(hipMalloc(&sc->d_out, nfl * sizeof(float)));
     unsigned long long *d = nullptr;
     HIP_TRY(hipMalloc(&d, (size_t)nt * 2 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(d, 0, (size_t)nt * 2 * sizeof(unsigned long long)));
     int rc = launch_render(sc, st, sc->full, sc->d_out, sc->stream, false, d);
     hipError_t e = rc == CRT_OK ? hipStreamSynchronize(sc->stream) : hipSuccess;
     if (rc == CRT_OK && e == hipSuccess)
         e = hipMemcpy(stamps, d, (size_t)nt * 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
-    std::vector<Tile> tiles(nt);
-    if (rc == CRT_OK && e == hipSuccess)
-        e = hipMemcpy(tiles.data(), sc->full.d_tiles, (size_t)nt * sizeof(Tile), hipMemcpyDeviceToHost);
+    /* each wave's tile: the plan's tiles in order, or (camera bins) the frame's
+     * priority lists ahead of the untaken tiles */
+    const ShardPlan &p = sc->full;
+    const BinsPlan &bp = p.bp;
+    std::vector<int32_t> prio, taken, phdr(2, 0);
+    if (rc == CRT_OK && e == hipSuccess && bp.cell_tile) {
+        prio.resize((size_t)(bp.e_h + bp.e_m));
+        taken.resize((size_t)bp.nbase);
+        e = hipMemcpy(prio.data(), bp.prio, prio.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(taken.data(), bp.taken, taken.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(phdr.data(), bp.phdr, 2 * sizeof(int32_t), hipMemcpyDeviceToHost);
+    }
     (void)hipFree(d);
     if (rc != CRT_OK) return rc;
     if (e != hipSuccess) return set_error(CRT_E_HIP, hipGetErrorString(e));
-    for (int k = 0; k < nt; ++k) { tile_xy[2 * k] = tiles[k].x; tile_xy[2 * k + 1] = tiles[k].y; }
+    for (int k = 0; k < nt; ++k) {
+        int x = -1, y = -1;
+        if (!bp.cell_tile) {
+            x = p.tiles[(size_t)k].x;
+            y = p.tiles[(size_t)k].y;
+        } else if (k < 4 * bp.e_h) {
+            if (k / 4 < std::min(phdr[0], bp.e_h)) {
+                const Tile &t = p.tiles[(size_t)prio[(size_t)(k / 4)]];
+                x = t.x + (k & 1) * 4;
+                y = t.y + ((k >> 1) & 1) * 4;
+            }
+        } else if (k < 4 * bp.e_h + bp.e_m) {
+            const int s2 = k - 4 * bp.e_h;
+            if (s2 < std::min(phdr[1], bp.e_m)) {
+                const Tile &t = p.tiles[(size_t)prio[(size_t)(bp.e_h + s2)]];
+                x = t.x;
+                y = t.y;
+            }
+        } else {
+            const int b = k - 4 * bp.e_h - bp.e_m;
+            if (!taken[(size_t)b]) {
+                x = p.tiles[(size_t)b].x;
+                y = p.tiles[(size_t)b].y;
+            }
+        }
+        tile_xy[2 * k] = x;
+        tile_xy[2 * k + 1] = y;
+    }
     return nt;
 }
 
@@ -654,8 +699,8 @@ int crt_hip_count_work(crt_hip_scene *sc, const crt_renderer_settings *st, crt_w
     return CRT_OK;
 }
 
-int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
-    if (!sc || !name) return set_error(CRT_E_INVALID, "null argument");
+/* One replica's option (on its device). */
+static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
     const std::string k(name);
     if (k == "traversal") {
         if (value != 7 && value != 8 && value != 14)
@@ -740,6 +785,21 @@ int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
     }
     /* tile plans depend on the walk (tile splitting): rebuild on next use */
     return CRT_OK;
+}
+
+/* Every replica of a multi-GPU handle takes the option (each renders its own
+ * shard with its own settings: an option set on the first alone would mix two
+ * renderers in one image). */
+int crt_hip_scene_set_option(crt_hip_scene *sc, const char *name, int value) {
+    if (!sc || !name) return set_error(CRT_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(sc->device));
+    int rc = set_option_one(sc, name, value);
+    for (size_t i = 0; rc == CRT_OK && i < sc->replicas.size(); ++i) {
+        HIP_TRY(hipSetDevice(sc->replicas[i]->device));
+        rc = set_option_one(sc->replicas[i], name, value);
+    }
+    HIP_TRY(hipSetDevice(sc->device));
+    return rc;
 }
 
 int crt_hip_wave_counts(crt_hip_scene *sc, crt_wave_counts *out) {

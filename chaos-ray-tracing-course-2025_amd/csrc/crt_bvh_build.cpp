@@ -23,6 +23,7 @@
 #include <limits>
 #include <vector>
 
+#include "crt_bins.h"
 #include "crt_bvh.h"
 #include "crt_device.h"
 #include "crt_host.h"
@@ -286,62 +287,48 @@ int build_proof_tables(HostScene &hs) {
     return CRT_OK;
 }
 
-/* Camera bins (crt_layout.h CamCand, crt_bvh.h walk_bins).
- *
- * Why a cell's list holds every triangle its camera rays can hit.  The
- * reference accepts a hit at t only when the exact point q = o + d t lies in
- * the triangle's hull (the hull margins, crt_scene_build.cpp "pruned-walk
- * structures"; they hold for |o|_inf <= prune_origin_max, checked here).  A hull entirely in front of the camera projects into the rectangle
- * of its eight projected corners, and q projects to the point of the image
- * plane its camera ray passes: pixel x's ray passes X = x + 1/2 exactly up to
- * the fp32 rounding of Camera::generate_ray (crt_camera.cpp:7-35: a few ulps
- * of the direction, ~1e-3 px at 1920 wide), far inside the 2-pixel margin
- * added on every side.  Hulls not strictly in front of the camera (or
- * unbounded) are listed in every cell.
- *
- * Why dmin bounds t from below.  t = |q - o| / |d| >= dist(o, hull) / |d|,
- * and |d| of the normalised fp32 direction is 1 within a few ulps: dist is
- * computed in double from the fp32 box and scaled by 1 - 2^-20 before it is
- * rounded down. */
-int build_camera_bins(const HostScene &hs, std::vector<CamCand> &bins, std::vector<int32_t> &off) {
-    bins.clear();
-    off.clear();
+/* Camera bins (crt_bins.h): the host restatement of the device binning
+ * (crt_bins.hip), used as its checker and by the CPU walk checks. */
+bool bin_camera(const HostScene &hs, BinCamera &cam) {
     const int W = hs.width, H = hs.height;
-    const int32_t nt = (int32_t)hs.tri_attr.size();
-    if (W <= 0 || H <= 0 || nt == 0) return CRT_OK;
-    const double o[3] = {hs.cam_loc[0], hs.cam_loc[1], hs.cam_loc[2]};
-    for (int k = 0; k < 3; ++k)
-        if (!(std::fabs(o[k]) <= (double)hs.prune_origin_max)) return CRT_OK;
-    double M[3][3], Mi[3][3];
+    if (W <= 0 || H <= 0 || hs.tri_attr.empty()) return false;
+    for (int k = 0; k < 3; ++k) {
+        cam.o[k] = hs.cam_loc[k];
+        if (!(std::fabs(cam.o[k]) <= (double)hs.prune_origin_max)) return false;
+    }
+    double M[3][3];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) M[i][j] = hs.cam_rot[3 * i + j];
     const double det = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) -
                        M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) +
                        M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]);
-    if (!std::isfinite(det) || !(std::fabs(det) > 1e-12)) return CRT_OK;
+    if (!std::isfinite(det) || !(std::fabs(det) > 1e-12)) return false;
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) {
             const int i1 = (j + 1) % 3, i2 = (j + 2) % 3, j1 = (i + 1) % 3, j2 = (i + 2) % 3;
-            Mi[i][j] = (M[i1][j1] * M[i2][j2] - M[i1][j2] * M[i2][j1]) / det;
+            cam.Mi[i][j] = (M[i1][j1] * M[i2][j2] - M[i1][j2] * M[i2][j1]) / det;
         }
-    const double sx = (double)hs.aspect * (double)hs.tan_half_fov, sy = hs.tan_half_fov;
-    if (!(sx > 0.0) || !(sy > 0.0) || !std::isfinite(sx) || !std::isfinite(sy)) return CRT_OK;
-    const int tx = (W + 7) / 8, ty = (H + 7) / 8;
-    const int64_t ncell = (int64_t)tx * ty;
-    constexpr double kMargin = 2.0;          /* pixels */
-    constexpr int kMaxEverywhere = 64;       /* hulls listed in every cell */
-    constexpr int64_t kMeanCap = 32;         /* mean candidates per cell */
-    constexpr int64_t kCellCap = 4096;       /* candidates of one cell */
+    cam.sx = (double)hs.aspect * (double)hs.tan_half_fov;
+    cam.sy = hs.tan_half_fov;
+    if (!(cam.sx > 0.0) || !(cam.sy > 0.0) || !std::isfinite(cam.sx) || !std::isfinite(cam.sy)) return false;
+    cam.W = W;
+    cam.H = H;
+    cam.tx = (W + 7) / 8;
+    cam.ty = (H + 7) / 8;
+    return true;
+}
 
-    struct Item { CamCand c; int32_t x0, x1, y0, y1; int32_t px0, px1, py0, py1; };   /* cells, pixels; x0 > x1: none */
-    std::vector<Item> items((size_t)nt);
-    int everywhere = 0;
+/* Per triangle: its hull box (crt_device.h triangle_hull, rounded outwards),
+ * id | culling << 31 and geometry as the BVH's triangle arrays hold them; the
+ * per-frame fields (dmin, mask, rest) zero. */
+void bin_templates(const HostScene &hs, std::vector<CamCand> &tpl) {
+    const int32_t nt = (int32_t)hs.tri_attr.size();
+    tpl.assign((size_t)nt, CamCand{});
     for (int32_t t = 0; t < nt; ++t) {
         const DTriAttr &at = hs.tri_attr[t];
         const float *v[3] = {&hs.vpos[3 * (size_t)at.i0], &hs.vpos[3 * (size_t)at.i1], &hs.vpos[3 * (size_t)at.i2]};
         const HullD hd = triangle_hull(v[0], v[1], v[2], &hs.face_normal[3 * (size_t)t], hs.prune_G);
-        Item &it = items[(size_t)t];
-        CamCand &c = it.c;
+        CamCand &c = tpl[(size_t)t];
         c.lo_x = round_down(hd.lo[0]); c.lo_y = round_down(hd.lo[1]); c.lo_z = round_down(hd.lo[2]);
         c.hi_x = round_up(hd.hi[0]); c.hi_y = round_up(hd.hi[1]); c.hi_z = round_up(hd.hi[2]);
         c.id = t | (hs.tri_cull[t] ? (int32_t)0x80000000 : 0);
@@ -350,78 +337,59 @@ int build_camera_bins(const HostScene &hs, std::vector<CamCand> &bins, std::vect
         c.g.v2x = v[2][0]; c.g.v2y = v[2][1]; c.g.v2z = v[2][2];
         c.g.nx = hs.face_normal[3 * (size_t)t]; c.g.ny = hs.face_normal[3 * (size_t)t + 1];
         c.g.nz = hs.face_normal[3 * (size_t)t + 2];
-        const double lo[3] = {c.lo_x, c.lo_y, c.lo_z}, hi[3] = {c.hi_x, c.hi_y, c.hi_z};
-        double d2 = 0.0;
-        for (int k = 0; k < 3; ++k) {
-            const double e = std::max(std::max(lo[k] - o[k], o[k] - hi[k]), 0.0);
-            d2 += e * e;
-        }
-        const double dist = std::sqrt(d2) * (1.0 - 0x1p-20);
-        c.dmin = std::isfinite(dist) ? round_down(dist) : 0.0f;
-        bool all = false;
-        double X0 = INFINITY, X1 = -INFINITY, Y0 = INFINITY, Y1 = -INFINITY;
-        for (int q = 0; q < 8 && !all; ++q) {
-            const double p[3] = {(q & 1) ? hi[0] : lo[0], (q & 2) ? hi[1] : lo[1], (q & 4) ? hi[2] : lo[2]};
-            const double w[3] = {p[0] - o[0], p[1] - o[1], p[2] - o[2]};
-            double cv[3];
-            for (int j = 0; j < 3; ++j) cv[j] = w[0] * Mi[0][j] + w[1] * Mi[1][j] + w[2] * Mi[2][j];
-            const double wn = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-            if (!std::isfinite(wn) || !std::isfinite(cv[0]) || !std::isfinite(cv[1]) || !std::isfinite(cv[2]) ||
-                !(cv[2] < -1e-9 * wn)) {
-                all = true;
-                break;
-            }
-            const double X = (cv[0] / -cv[2] / sx + 1.0) * 0.5 * W, Y = (1.0 - cv[1] / -cv[2] / sy) * 0.5 * H;
-            X0 = std::min(X0, X); X1 = std::max(X1, X);
-            Y0 = std::min(Y0, Y); Y1 = std::max(Y1, Y);
-        }
-        if (all) {
-            if (++everywhere > kMaxEverywhere) return CRT_OK;
-            it.x0 = 0; it.x1 = tx - 1; it.y0 = 0; it.y1 = ty - 1;
-            it.px0 = 0; it.px1 = W - 1; it.py0 = 0; it.py1 = H - 1;
-            c.dmin = 0.0f;
-            continue;
-        }
-        /* pixels whose centre X = x + 1/2 lies within the margin of [X0, X1] */
-        const double px0 = std::ceil(X0 - 0.5 - kMargin), px1 = std::floor(X1 - 0.5 + kMargin);
-        const double py0 = std::ceil(Y0 - 0.5 - kMargin), py1 = std::floor(Y1 - 0.5 + kMargin);
-        if (px1 < 0.0 || py1 < 0.0 || px0 > W - 1 || py0 > H - 1 || px0 > px1 || py0 > py1) {
-            it.x0 = 1; it.x1 = 0; it.y0 = 1; it.y1 = 0;
-            continue;
-        }
-        it.px0 = (int32_t)std::max(0.0, px0);
-        it.px1 = (int32_t)std::min((double)(W - 1), px1);
-        it.py0 = (int32_t)std::max(0.0, py0);
-        it.py1 = (int32_t)std::min((double)(H - 1), py1);
-        it.x0 = it.px0 / 8; it.x1 = it.px1 / 8;
-        it.y0 = it.py0 / 8; it.y1 = it.py1 / 8;
     }
-    std::vector<int64_t> cnt((size_t)ncell + 1, 0);
-    for (const Item &it : items)
-        for (int32_t y = it.y0; y <= it.y1; ++y)
-            for (int32_t x = it.x0; x <= it.x1; ++x) ++cnt[(size_t)y * tx + x];
+}
+
+int build_camera_bins(const HostScene &hs, std::vector<CamCand> &bins, std::vector<int32_t> &off,
+                      std::vector<uint8_t> *over) {
+    bins.clear();
+    off.clear();
+    if (over) over->clear();
+    BinCamera cam;
+    if (!bin_camera(hs, cam)) return CRT_OK;
+    const int32_t nt = (int32_t)hs.tri_attr.size();
+    const int tx = cam.tx, ty = cam.ty;
+    const int64_t ncell = (int64_t)tx * ty;
+    std::vector<CamCand> tpl;
+    bin_templates(hs, tpl);
+    std::vector<BinItem> items((size_t)nt);
+    int everywhere = 0;
+    for (int32_t t = 0; t < nt; ++t) {
+        const CamCand &c = tpl[(size_t)t];
+        const float lo[3] = {c.lo_x, c.lo_y, c.lo_z}, hi[3] = {c.hi_x, c.hi_y, c.hi_z};
+        items[(size_t)t] = bin_project(lo, hi, cam);
+        if (items[(size_t)t].every && ++everywhere > kBinMaxEverywhere) return CRT_OK;
+    }
+    /* cell lists in triangle order, then a stable sort by dmin: ordered by (dmin, id) */
+    std::vector<int64_t> cnt((size_t)ncell, 0);
+    for (const BinItem &it : items)
+        if (it.px0 <= it.px1)
+            for (int32_t y = it.py0 / 8; y <= it.py1 / 8; ++y)
+                for (int32_t x = it.px0 / 8; x <= it.px1 / 8; ++x) ++cnt[(size_t)y * tx + x];
+    std::vector<uint8_t> ov((size_t)ncell, 0);
     int64_t total = 0;
     for (int64_t c = 0; c < ncell; ++c) {
-        if (cnt[(size_t)c] > kCellCap) return CRT_OK;
-        total += cnt[(size_t)c];
+        if (cnt[(size_t)c] > kBinCellCap) ov[(size_t)c] = 1;   /* this cell's pixels walk the BVH */
+        else total += cnt[(size_t)c];
     }
-    if (total > kMeanCap * ncell || total >= (int64_t)std::numeric_limits<int32_t>::max()) return CRT_OK;
+    if (total > kBinMeanCap * ncell || total >= (int64_t)std::numeric_limits<int32_t>::max()) return CRT_OK;
     off.assign((size_t)ncell + 1, 0);
-    for (int64_t c = 0; c < ncell; ++c) off[(size_t)c + 1] = off[(size_t)c] + (int32_t)cnt[(size_t)c];
+    for (int64_t c = 0; c < ncell; ++c) off[(size_t)c + 1] = off[(size_t)c] + (ov[(size_t)c] ? 0 : (int32_t)cnt[(size_t)c]);
     bins.resize((size_t)total);
     std::vector<int32_t> fill(off.begin(), off.end() - 1);
-    for (const Item &it : items)
-        for (int32_t y = it.y0; y <= it.y1; ++y)
-            for (int32_t x = it.x0; x <= it.x1; ++x) {
-                CamCand &c = bins[(size_t)fill[(size_t)y * tx + x]++];
-                c = it.c;
-                /* the cell's pixels inside the candidate's pixel rectangle */
-                uint64_t m = 0;
-                for (int32_t py = std::max(8 * y, it.py0); py <= std::min(8 * y + 7, it.py1); ++py)
-                    for (int32_t px = std::max(8 * x, it.px0); px <= std::min(8 * x + 7, it.px1); ++px)
-                        m |= 1ull << (8 * (py - 8 * y) + (px - 8 * x));
-                c.mask = m;
+    for (int32_t t = 0; t < nt; ++t) {
+        const BinItem &it = items[(size_t)t];
+        if (it.px0 > it.px1) continue;
+        for (int32_t y = it.py0 / 8; y <= it.py1 / 8; ++y)
+            for (int32_t x = it.px0 / 8; x <= it.px1 / 8; ++x) {
+                const size_t cell = (size_t)y * tx + x;
+                if (ov[cell]) continue;
+                CamCand &c = bins[(size_t)fill[cell]++];
+                c = tpl[(size_t)t];
+                c.dmin = it.dmin;
+                c.mask = bin_mask(it, x, y);
             }
+    }
     for (int64_t c = 0; c < ncell; ++c) {
         const auto b = bins.begin() + off[(size_t)c], e = bins.begin() + off[(size_t)c + 1];
         std::stable_sort(b, e, [](const CamCand &u, const CamCand &v) { return u.dmin < v.dmin; });
@@ -432,6 +400,7 @@ int build_camera_bins(const HostScene &hs, std::vector<CamCand> &bins, std::vect
             q->rest = r;
         }
     }
+    if (over) over->swap(ov);
     return CRT_OK;
 }
 

@@ -101,6 +101,7 @@ struct HostScene {
     std::vector<DLight> lights;
 
     /* stats */
+    double tree_build_ms = 0.0, bvh_ms = 0.0, prep_ms = 0.0;   /* wall time of the host builds */
     int64_t leaf_count = 0;
     int32_t max_depth = 0;
     int32_t max_leaf_size = 0;
@@ -115,13 +116,21 @@ int build_bvh(HostScene &hs);
  * child cell is not its parent's half. */
 int build_proof_tables(HostScene &hs);
 
-/* Camera bins of hs's camera and resolution (crt_bvh_build.cpp): for each 8x8
- * cell of the frame (row-major, (width + 7) / 8 a row), every triangle a
- * camera ray of the cell may hit, sorted by a lower bound of its hit
- * distance: cell c holds bins[off[c] .. off[c + 1]).  Leaves both empty (the
- * scene then walks the BVH) when the camera is too far for the hull margins,
- * the camera matrix is singular or the lists would be too long. */
-int build_camera_bins(const HostScene &hs, std::vector<CamCand> &bins, std::vector<int32_t> &off);
+/* Camera bins of hs's camera and resolution (crt_bins.h; the host checker of
+ * the device binning, crt_bins.hip): for each 8x8 cell of the frame
+ * (row-major, (width + 7) / 8 a row), every triangle a camera ray of the cell
+ * may hit, sorted by (dmin, id): cell c holds bins[off[c] .. off[c + 1]); a
+ * cell with more than kBinCellCap candidates holds none and is marked in
+ * *over (its pixels walk the BVH).  Leaves everything empty (the scene then
+ * walks the BVH) when bin_camera fails or the lists would be too long. */
+struct BinCamera;
+int build_camera_bins(const HostScene &hs, std::vector<CamCand> &bins, std::vector<int32_t> &off,
+                      std::vector<uint8_t> *over = nullptr);
+/* The projection constants of hs's camera (false: no bins — the camera is too
+ * far for the hull margins, its matrix singular or the field of view bad). */
+bool bin_camera(const HostScene &hs, BinCamera &cam);
+/* Per-triangle static part of the candidate records (hull box, id, geometry). */
+void bin_templates(const HostScene &hs, std::vector<CamCand> &tpl);
 
 /* Mesh prep + (build_tree) the exact tree build and its flattening. */
 int prepare_scene(const crt_scene_desc *desc, HostScene &out, bool build_tree = true);

@@ -70,6 +70,7 @@ void warm_code_objects(int device, hipStream_t stream) {
     hipLaunchKernelGGL(k_warm_gi, dim3(1), dim3(64), 0, stream);
     hipLaunchKernelGGL(k_warm_wf, dim3(1), dim3(64), 0, stream);
     hipLaunchKernelGGL(k_warm_side, dim3(1), dim3(64), 0, stream);
+    hipLaunchKernelGGL(k_warm_bins, dim3(1), dim3(64), 0, stream);
     (void)hipGetLastError();
 }
 
@@ -128,32 +129,9 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         plan.packed_pixels = total;
     }
     if (bins_active(sc) && !tiles.empty()) {
-        /* camera bins: one wave per 8x8 tile on its cell's list; a cell
-         * whose list is long is split into four 4x4 waves (each leaves the
-         * list once its 16 pixels are done: the list's tail latency is
-         * spread over four waves) walking with four lanes per pixel; the
-         * longest lists first, the split ones at raised issue priority */
-        const int tx = (W + 7) / 8;
-        auto cost = [&](const Tile &t) {
-            const int cx = t.x / 8, cy = t.y / 8;
-            return (t.x % 8) + t.w <= 8 && (t.y % 8) + t.h <= 8 ? sc->bin_count[(size_t)cy * tx + cx] : INT32_MAX;
-        };
-        std::vector<Tile> split;
-        split.reserve(tiles.size());
-        for (const Tile &t : tiles) {
-            const int c = cost(t);
-            if (c >= sc->bins_split && c != INT32_MAX) {
-                for (int yy = 0; yy < t.h; yy += 4)
-                    for (int xx = 0; xx < t.w; xx += 4)
-                        split.push_back(Tile{t.x + xx, t.y + yy, std::min(4, t.w - xx), std::min(4, t.h - yy),
-                                             t.out_base + (int64_t)yy * t.out_stride + xx, t.out_stride,
-                                             sc->bins_quad ? 3 : 1});
-            } else {
-                split.push_back(t);
-            }
-        }
-        tiles.swap(split);
-        std::stable_sort(tiles.begin(), tiles.end(), [&](const Tile &a, const Tile &b) { return cost(a) > cost(b); });
+        /* camera bins: the tiles stay in plan order; each frame's binning
+         * queues its heavy and medium cells for the waves dispatched first
+         * (crt_bins.hip bins_plan) */
         plan.cost.clear();
     } else if (!sc->calib.empty() && !tiles.empty()) {
         /* measured costs: split as calibrated, heaviest first */
@@ -219,6 +197,8 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         tiles.swap(sorted);
     }
     plan.ntiles = (int)tiles.size();
+    plan.waves = plan.ntiles;
+    plan.bp = BinsPlan{};
     plan.has_small = false;
     for (const Tile &t : tiles) plan.has_small = plan.has_small || t.w * t.h <= 16;
     plan.tiles = tiles;
@@ -228,6 +208,7 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         HIP_TRY(hipMemcpy(p, tiles.data(), tiles.size() * sizeof(Tile), hipMemcpyHostToDevice));
         sc->plan_allocs.push_back(p);
         plan.d_tiles = static_cast<Tile *>(p);
+        if (bins_active(sc)) return bins_plan(sc, plan);
     }
     return CRT_OK;
 }
@@ -679,9 +660,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
 #define CRT_WF0(T, COUNT)                                                                                   \
     hipLaunchKernelGGL((k_wf_level<T, true, COUNT>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,      \
                        plan.d_tiles, plan.ntiles, lv, cnt)
-    if (primary == 14 && bins_active(sc)) {   /* camera bins for the camera rays */
-        if (count) CRT_WF0(15, true); else CRT_WF0(15, false);
-    } else if (primary == 14) {
+    if (primary == 14) {   /* level 0 on the BVH (camera bins there measured neutral, profiles/r03/ab_level0_bins) */
         if (count) CRT_WF0(14, true); else CRT_WF0(14, false);
     } else if (primary == 12 || primary == 13) {   /* level 0 keeps 8x8 tiles' packet walk (no window build) */
         if (count) CRT_WF0(12, true); else CRT_WF0(12, false);
@@ -823,7 +802,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
             if (tr == 13 && !plan.has_small) tr = 12;
 #define CRT_LAUNCH_SH(TR, COUNT)                                                                            \
     hipLaunchKernelGGL((k_render_tiles<false, 0, TR, TR, COUNT, true>), dim3(nb), dim3(256), 0, stream, d_scene, ds, \
-                       plan.d_tiles, plan.ntiles, d_out, cn, nullptr)
+                       plan.d_tiles, plan.ntiles, d_out, cn, nullptr, BinsPlan{})
             if (tr == 13) {
                 if (count) CRT_LAUNCH_SH(13, true); else CRT_LAUNCH_SH(13, false);
             } else if (tr == 12) {
@@ -837,7 +816,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         }
 #define CRT_LAUNCH_S(MAXF, COUNT)                                                                           \
     hipLaunchKernelGGL((k_render_tiles<true, MAXF, 10, 10, COUNT, true>), dim3(nb), dim3(256), 0, stream,      \
-                       d_scene, ds, plan.d_tiles, plan.ntiles, d_out, cn, nullptr)
+                       d_scene, ds, plan.d_tiles, plan.ntiles, d_out, cn, nullptr, BinsPlan{})
         if (nf <= 4) {
             if (count) CRT_LAUNCH_S(4, true); else CRT_LAUNCH_S(4, false);
         } else if (nf <= 16) {
@@ -861,7 +840,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     unsigned long long *cnt = sc->d_counters;
 #define CRT_LAUNCH_T(FULL, MAXF, TRAV, COUNT)                                                               \
     hipLaunchKernelGGL((k_render_tiles<FULL, MAXF, TRAV, TRAV, COUNT>), dim3(blocks), dim3(256), 0, stream,      \
-                       d_scene, ds, plan.d_tiles, plan.ntiles, d_out, cnt, stamps)
+                       d_scene, ds, plan.d_tiles, plan.ntiles, d_out, cnt, stamps, BinsPlan{})
 #define CRT_LAUNCH(MAXF, COUNT)                                                                             \
     do {                                                                                                   \
         if (trav == 10 || trav == 14) CRT_LAUNCH_T(true, MAXF, 10, COUNT);                                  \
@@ -874,8 +853,16 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         case 12: if (count) CRT_LAUNCH_T(false, 0, 12, true); else CRT_LAUNCH_T(false, 0, 12, false); break;
         case 13: if (count) CRT_LAUNCH_T(false, 0, 13, true); else CRT_LAUNCH_T(false, 0, 13, false); break;
         case 14:
-            if (bins_active(sc)) {
-                if (count) CRT_LAUNCH_T(false, 0, 15, true); else CRT_LAUNCH_T(false, 0, 15, false);
+            if (bins_active(sc) && plan.bp.cell_tile) {
+                /* this frame's camera bins, then the render over the bins plan's grid */
+                const int rc = bins_enqueue(sc, plan, stream);
+                if (rc != CRT_OK) return rc;
+                const unsigned bb = (unsigned)((plan.waves + 3) / 4);
+#define CRT_LAUNCH_B(COUNT)                                                                                 \
+    hipLaunchKernelGGL((k_render_tiles<false, 0, 15, 15, COUNT>), dim3(bb), dim3(256), 0, stream, d_scene, ds, \
+                       plan.d_tiles, plan.waves, d_out, cnt, stamps, plan.bp)
+                if (count) CRT_LAUNCH_B(true); else CRT_LAUNCH_B(false);
+#undef CRT_LAUNCH_B
             } else {
                 if (count) CRT_LAUNCH_T(false, 0, 14, true); else CRT_LAUNCH_T(false, 0, 14, false);
             }

@@ -21,6 +21,25 @@ struct alignas(16) Tile {
                                 * bit 1: camera-bins split tile, four lanes per pixel */
 };
 
+/* Camera-bins dispatch of a tile plan (crt_bins.hip): the render grid's first
+ * 4 e_h waves take the cells k_bins_sort queued as heavy (four 4x4 waves
+ * each), the next e_m the medium ones (one 8x8 wave each), the rest the
+ * plan's base tiles in plan order, skipping the ones a priority wave took. */
+struct BinsPlan {
+    int32_t *cell_tile;   /* per cell: the plan's one tile inside it; -1 none (the cell is not rendered), -2 several */
+    int32_t *taken;       /* per base tile: rendered by a priority wave this frame */
+    int32_t *prio;        /* e_h heavy, then e_m medium base-tile indices */
+    int32_t *phdr;        /* [0] heavy, [1] medium cells queued this frame */
+    int32_t e_h, e_m, nbase;
+    int32_t split, medium, quad;
+};
+
+/* Per-frame counters of the device binning (crt_bins.hip). */
+struct BinsHdr {
+    int32_t n_every, n_nonempty, total, done;
+    int32_t last_every, last_nonempty, last_total, pad;
+};
+
 struct alignas(16) UnpackBucket {
     int32_t x, y, w, h;
     int64_t src;               /* float offset of the bucket inside the gathered buffer */

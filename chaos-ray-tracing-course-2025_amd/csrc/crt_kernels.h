@@ -86,7 +86,7 @@ struct Rgb { T c[3]; };
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW = false>
 __global__ void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st, const Tile *__restrict__ tiles,
                                int ntiles, float *__restrict__ out, unsigned long long *__restrict__ counters,
-                               unsigned long long *__restrict__ stamps);
+                               unsigned long long *__restrict__ stamps, BinsPlan bp);
 template <int MAXF, int TRAV, bool COUNT>
 __global__ void k_render_refill(const DeviceScene *__restrict__ scene, DSettings st, const Tile *__restrict__ tiles,
                                 int ntiles, float *__restrict__ out, int32_t *__restrict__ next_px,
@@ -115,6 +115,7 @@ __global__ void k_warm_render();
 __global__ void k_warm_gi();
 __global__ void k_warm_wf();
 __global__ void k_warm_side();
+__global__ void k_warm_bins();
 
 /* ---- instantiation lists (X(args...)) ---- */
 #define CRT_TILES_INSTANCES(X)                                                                              \
@@ -132,7 +133,7 @@ __global__ void k_warm_side();
     X(true, 16, 10, 10, true, true) X(true, 64, 10, 10, false, true) X(true, 64, 10, 10, true, true)
 #define CRT_TILES_SIG(F, M, T, S, C, SH) void k_render_tiles<F, M, T, S, C, SH>(const DeviceScene *__restrict__, \
     DSettings, const Tile *__restrict__, int, float *__restrict__, unsigned long long *__restrict__,          \
-    unsigned long long *__restrict__);
+    unsigned long long *__restrict__, BinsPlan);
 #define CRT_REFILL_INSTANCES(X) X(4, 4, false) X(4, 4, true) X(4, 10, false) X(4, 10, true) \
     X(16, 4, false) X(16, 4, true) X(64, 4, false) X(64, 4, true)
 #define CRT_REFILL_SIG(MAXF, T, C) void k_render_refill<MAXF, T, C>(const DeviceScene *__restrict__, DSettings, \
@@ -145,7 +146,7 @@ __global__ void k_warm_side();
     uint32_t *__restrict__);
 #define CRT_WF_INSTANCES(X) X(4, false, false) X(4, false, true) X(10, false, false) X(10, false, true)        \
     X(14, false, false) X(14, false, true) X(7, true, false) X(7, true, true) X(8, true, false) X(8, true, true) \
-    X(12, true, false) X(12, true, true) X(14, true, false) X(14, true, true) X(15, true, false) X(15, true, true)
+    X(12, true, false) X(12, true, true) X(14, true, false) X(14, true, true)
 #define CRT_WF_SIG(T, L0, C) void k_wf_level<T, L0, C>(const DeviceScene *__restrict__, DSettings, \
     const Tile *__restrict__, int, WLevel, unsigned long long *__restrict__);
 

@@ -166,11 +166,13 @@ struct DeviceScene {
     const int32_t *btri_id;
     /* the proof's tree topology (KTopo); null when the tree lives on the device only */
     const KTopo *ktopo;
-    /* camera bins (crt_bvh.h walk_bins): per 8x8 cell of the frame
-     * (bin_tx cells a row), candidates bins[bin_off[c] .. bin_off[c + 1]);
-     * null when not built */
+    /* camera bins (crt_bvh.h walk_bins), rebuilt on the device by every camera
+     * frame (crt_bins.hip): per 8x8 cell of the frame (bin_tx cells a row),
+     * candidates bins[bin_off[c] .. bin_off[c] + bin_len[c]), bin_len -1: the
+     * cell's pixels walk the BVH; null when the scene takes no bins */
     const CamCand *bins;
     const int32_t *bin_off;
+    const int32_t *bin_len;
     int32_t bin_tx;
     const DTriAttr *tri_attr;
     const DVec4 *vnormal;

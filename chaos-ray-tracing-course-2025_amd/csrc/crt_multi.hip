@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -51,15 +52,15 @@ void enable_peers(int a, int b) {
 /* One prepared host scene uploaded to every listed device. */
 int upload_on(const HostScene &hs, const int32_t *devices, int32_t count, crt_hip_scene **out) {
     *out = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     if (!devices || count < 1) return set_error(CRT_E_INVALID, "no devices");
     crt_hip_scene *first = nullptr;
-    int rc = crt_hip_scene_upload(reinterpret_cast<const crt_host_scene *>(&hs), devices[0], &first);
+    int rc = scene_upload(hs, devices[0], true, &first);
     if (rc != CRT_OK) return rc;
     std::unique_ptr<crt_hip_scene, void (*)(crt_hip_scene *)> sc(first, crt_hip_scene_destroy);
     for (int32_t i = 1; i < count; ++i) {
         crt_hip_scene *r = nullptr;
-        if ((rc = crt_hip_scene_upload(reinterpret_cast<const crt_host_scene *>(&hs), devices[i], &r)) != CRT_OK)
-            return rc;
+        if ((rc = scene_upload(hs, devices[i], false, &r)) != CRT_OK) return rc;
         sc->replicas.push_back(r);
         enable_peers(devices[0], devices[i]);
         HIP_TRY(hipSetDevice(devices[i]));
@@ -69,6 +70,7 @@ int upload_on(const HostScene &hs, const int32_t *devices, int32_t count, crt_hi
         HIP_TRY(hipSetDevice(devices[0]));
         HIP_TRY(hipEventCreateWithFlags(&sc->mg_done, hipEventDisableTiming));   /* "gather unpacked" */
     }
+    sc->info.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     *out = sc.release();
     return CRT_OK;
 }
@@ -237,10 +239,13 @@ int crt_hip_scene_create_on(const crt_scene_desc *desc, const int32_t *devices, 
     *out = nullptr;
     const int mode = tree_mode(desc, flags);
     if (mode != CRT_SCENE_TREE_HOST && mode != CRT_SCENE_TREE_DEVICE) return set_error(CRT_E_INVALID, "bad tree build flag");
+    const auto t0 = std::chrono::steady_clock::now();
     std::unique_ptr<HostScene> hs(new HostScene());
-    const int rc = prepare_scene(desc, *hs, mode == CRT_SCENE_TREE_HOST);
+    int rc = prepare_scene(desc, *hs, mode == CRT_SCENE_TREE_HOST);
     if (rc != CRT_OK) return rc;
-    return upload_on(*hs, devices, count, out);
+    if ((rc = upload_on(*hs, devices, count, out)) != CRT_OK) return rc;
+    (*out)->info.create_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return CRT_OK;
 }
 
 int crt_hip_scene_create_mask(const crt_scene_desc *desc, uint64_t gpu_mask, int flags, crt_hip_scene **out) {
@@ -254,10 +259,15 @@ int crt_hip_scene_from_tree_on(const crt_tree_scene_desc *desc, const int32_t *d
                                crt_hip_scene **out) {
     if (!desc || !out) return set_error(CRT_E_INVALID, "null argument");
     *out = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     std::unique_ptr<HostScene> hs(new HostScene());
-    const int rc = prepare_scene_from_tree(desc, *hs);
+    int rc = prepare_scene_from_tree(desc, *hs);
     if (rc != CRT_OK) return rc;
-    return upload_on(*hs, devices, count, out);
+    const double prep = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if ((rc = upload_on(*hs, devices, count, out)) != CRT_OK) return rc;
+    (*out)->info.prep_ms = prep;
+    (*out)->info.create_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return CRT_OK;
 }
 
 int crt_hip_scene_from_tree_mask(const crt_tree_scene_desc *desc, uint64_t gpu_mask, crt_hip_scene **out) {

@@ -12,12 +12,45 @@
 
 namespace crt_amd {
 
+/* The tile a wave of a camera-bins grid renders (crt_kernel_common.h
+ * BinsPlan): a quarter of a heavy cell, a medium cell, or the next base tile
+ * no priority wave took.  false: nothing to do (an unused priority slot). */
+__device__ __forceinline__ bool bins_tile(const BinsPlan &bp, const Tile *__restrict__ tiles, int wave, Tile &tl) {
+    const int ph = 4 * bp.e_h, pm = ph + bp.e_m;
+    int k, q = -1;
+    if (wave < ph) {
+        const int s = wave >> 2;
+        if (s >= min(load_scalar(bp.phdr, 0), bp.e_h)) return false;
+        k = load_scalar(bp.prio, s);
+        q = wave & 3;
+    } else if (wave < pm) {
+        const int s = wave - ph;
+        if (s >= min(load_scalar(bp.phdr, 1), bp.e_m)) return false;
+        k = load_scalar(bp.prio, bp.e_h + s);
+    } else {
+        k = wave - pm;
+        if (k >= bp.nbase || load_scalar(bp.taken, k) != 0) return false;
+    }
+    tl = tiles[k];
+    if (q >= 0) {
+        const int xx = (q & 1) * 4, yy = (q >> 1) * 4;
+        if (xx >= tl.w || yy >= tl.h) return false;
+        tl.x += xx;
+        tl.y += yy;
+        tl.w = min(4, tl.w - xx);
+        tl.h = min(4, tl.h - yy);
+        tl.out_base += (int64_t)yy * tl.out_stride + xx;
+        tl.prio = bp.quad ? 3 : 1;
+    }
+    return true;
+}
+
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW>
 __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT_WINDOW_WAVES : TRAV == 12 ? CRT_PACKET_WAVES : (TRAV == 14 || TRAV == 15) && !FULL ? CRT_BVH_WAVES : (FULL && MAXF == 4 ? CRT_GI_WAVES : 1)))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
                                                   const Tile *__restrict__ tiles,
                                                       int ntiles, float *__restrict__ out,
                                                       unsigned long long *__restrict__ counters,
-                                                      unsigned long long *__restrict__ stamps) {
+                                                      unsigned long long *__restrict__ stamps, BinsPlan bp) {
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int lane = (int)(threadIdx.x & 63);
     if (wave >= ntiles) return;
@@ -27,7 +60,13 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
     const DeviceScene &s = *scene;
     /* diagnostic build only (stamps != nullptr): wave start / end in s_memrealtime ticks (100 MHz) */
     if (stamps && lane == 0) stamps[2 * wave] = __builtin_amdgcn_s_memrealtime();
-    const Tile tl = tiles[wave];
+    Tile tl;
+    if constexpr (TRAV == 15 && !FULL && !SHADOW) {
+        if (!bins_tile(bp, tiles, wave, tl)) return;
+    } else {
+        (void)bp;
+        tl = tiles[wave];
+    }
     /* the heaviest tiles set the frame length (their walks are long chains of
      * dependent loads): they get issue priority over the light waves that
      * share their SIMD (s_setprio; scheduling only, results unchanged) */
@@ -82,9 +121,10 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
     if constexpr (TRAV == 15 && !FULL && !SHADOW) {
         /* a tile inside one 8x8 camera-bins cell: the cell's candidate list */
         const int tx0 = uniform_i(tl.x), ty0 = uniform_i(tl.y), tw = uniform_i(tl.w), th = uniform_i(tl.h);
-        if ((tx0 & 7) + tw <= 8 && (ty0 & 7) + th <= 8) {
-            const int cell = (ty0 >> 3) * s.bin_tx + (tx0 >> 3);
-            const int beg = load_scalar(s.bin_off, cell), end = load_scalar(s.bin_off, cell + 1);
+        const int cell = (ty0 >> 3) * s.bin_tx + (tx0 >> 3);
+        const int len = (tx0 & 7) + tw <= 8 && (ty0 & 7) + th <= 8 ? load_scalar(s.bin_len, cell) : -1;
+        if (len >= 0) {   /* -1: not inside one cell, or the cell's list is over the cap: the BVH walk below */
+            const int beg = load_scalar(s.bin_off, cell), end = beg + len;
             __shared__ CamCand stage[4 * kBinChunk];
             if ((tl.prio & 2) && tw <= 4 && th <= 4) {
                 /* a split tile of a long list: four lanes per pixel (trace_bins_lanes) */

@@ -57,21 +57,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
     int slot;
-    if constexpr (LEVEL0 && TRAV == 15) {
-        /* camera bins (crt_walks.h trace_bins_wave) for a tile inside one 8x8 cell */
-        __shared__ CamCand stage[4 * kBinChunk];
-        const int tx0 = uniform_i(tl.x), ty0 = uniform_i(tl.y), tw = uniform_i(tl.w), th = uniform_i(tl.h);
-        if ((tx0 & 7) + tw <= 8 && (ty0 & 7) + th <= 8) {
-            const int cell = (ty0 >> 3) * s.bin_tx + (tx0 >> 3);
-            const int beg = load_scalar(s.bin_off, cell), end = load_scalar(s.bin_off, cell + 1);
-            const int bit = 8 * ((ty0 & 7) + (lane >> 3)) + (tx0 & 7) + (lane & 7);
-            slot = trace_bins_wave<COUNT>(s, stage + (threadIdx.x >> 6) * kBinChunk, beg, end, bit, has, o, d, t, cnt);
-        } else {
-            slot = trace<14, COUNT>(s, &coop[0], has, o, d, t, cnt);
-        }
-    } else {
-        slot = trace<TRAV, COUNT>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has, o, d, t, cnt);
-    }
+    slot = trace<TRAV, COUNT>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has, o, d, t, cnt);
 
     WNode node = {wFinal, -1, -1, 0, 0.f, 0.f, 0.f, 0.f};
     Vec col = vec(0.f, 0.f, 0.f);

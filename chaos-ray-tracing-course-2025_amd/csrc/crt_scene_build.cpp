@@ -15,6 +15,7 @@
  * before its child1 is created.
  */
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -400,7 +401,17 @@ int flatten_tree(const std::vector<BuildNode> &bn, HostScene &hs) {
  * diffuse material, reflective or refractive materials), and for any scene
  * small enough that the host build costs little (camera rays may take it,
  * option "traversal" 14). */
+int maybe_build_bvh_(HostScene &hs);
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
 int maybe_build_bvh(HostScene &hs) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = maybe_build_bvh_(hs);
+    hs.bvh_ms = ms_since(t0);
+    return rc;
+}
+int maybe_build_bvh_(HostScene &hs) {
     bool need = hs.tri_attr.size() <= ((size_t)1 << 18);
     for (const DMaterial &m : hs.materials)
         need = need || m.type == CRT_MATERIAL_REFLECTIVE || m.type == CRT_MATERIAL_REFRACTIVE ||
@@ -413,7 +424,15 @@ int maybe_build_bvh(HostScene &hs) {
 
 }  // namespace
 
+int prepare_scene_(const crt_scene_desc *d, HostScene &hs, bool build_tree_on_host);
 int prepare_scene(const crt_scene_desc *d, HostScene &hs, bool build_tree_on_host) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = prepare_scene_(d, hs, build_tree_on_host);
+    hs.prep_ms = ms_since(t0);
+    return rc;
+}
+
+int prepare_scene_(const crt_scene_desc *d, HostScene &hs, bool build_tree_on_host) {
     if (!d) return set_error(CRT_E_INVALID, "null scene description");
     if (d->camera.width <= 0 || d->camera.height <= 0)
         return set_error(CRT_E_INVALID, "image width/height must be positive");
@@ -524,6 +543,7 @@ int prepare_scene(const crt_scene_desc *d, HostScene &hs, bool build_tree_on_hos
         hs.tree_on_host = false;
         return maybe_build_bvh(hs);
     }
+    const auto tb0 = std::chrono::steady_clock::now();
     std::vector<Box6> tri_boxes((size_t)nt);
     for (int64_t t = 0; t < nt; ++t) {
         Box6 b{{inf, inf, inf}, {-inf, -inf, -inf}};
@@ -546,6 +566,7 @@ int prepare_scene(const crt_scene_desc *d, HostScene &hs, bool build_tree_on_hos
     std::vector<BuildNode> bn;
     build_tree(tri_boxes, root, bn);
     if ((rc = flatten_tree(bn, hs)) != CRT_OK) return rc;
+    hs.tree_build_ms = ms_since(tb0);
     return maybe_build_bvh(hs);
 }
 
@@ -799,6 +820,9 @@ int crt_host_scene_info(const crt_host_scene *h, crt_scene_info *out) {
     out->gi_on = hs.gi_on;
     out->reflections_on = hs.reflections_on;
     out->refractions_on = hs.refractions_on;
+    out->tree_build_ms = hs.tree_build_ms;
+    out->prep_ms = hs.prep_ms;
+    out->bvh_ms = hs.bvh_ms;
     return CRT_OK;
 }
 

@@ -12,6 +12,7 @@
 #include <utility>
 #include <vector>
 
+#include "crt_bins.h"
 #include "crt_host.h"
 #include "crt_kernels.h"
 
@@ -27,6 +28,8 @@ namespace crt_amd {
 struct ShardPlan {
     Tile *d_tiles = nullptr;
     int ntiles = 0;
+    int waves = 0;               /* waves of the render grid (camera bins: priority waves + ntiles) */
+    BinsPlan bp{};               /* camera-bins dispatch (crt_bins.hip bins_plan); cell_tile null otherwise */
     int64_t packed_pixels = 0;
     std::vector<Tile> tiles;     /* host copy, dispatch order */
     std::vector<float> cost;     /* measured cost per tile (calibrated plans), else empty */
@@ -36,6 +39,27 @@ struct ShardPlan {
 }  // namespace crt_amd
 
 using namespace crt_amd;
+
+/* Device buffers of the camera bins (crt_bins.hip), per scene. */
+struct BinsDev {
+    crt_amd::BinCamera cam{};
+    int nt = 0, tx = 0, ncell = 0;
+    crt_amd::CamCand *tpl = nullptr;      /* per triangle: the records' static part */
+    crt_amd::BinItem *items = nullptr;    /* per triangle: this frame's projection */
+    int32_t *cnt = nullptr;               /* per cell: candidates (zero between frames) */
+    int32_t *keys = nullptr;              /* per cell: kBinCellCap triangle ids */
+    int32_t *every = nullptr;             /* everywhere triangles */
+    int32_t *nonempty = nullptr;          /* cells with a candidate, in arrival order */
+    crt_amd::BinsHdr *hdr = nullptr;
+    crt_amd::CamCand *recs = nullptr;     /* the lists */
+    int32_t rec_cap = 0;
+    int32_t *off = nullptr, *len = nullptr;   /* per cell */
+    std::vector<int32_t> count;           /* per cell: list length of the sizing pass (-1 over the cap) */
+    int sort_blocks = 0;
+    int64_t records = 0;                  /* records of the sizing pass */
+    double setup_ms = 0.0;
+    std::vector<void *> allocs;
+};
 
 
 /* Device buffers of the wavefront path, grown on demand (kept across frames). */
@@ -135,7 +159,7 @@ struct crt_hip_scene {
     int wave_slots = 6144;   /* CUs x 4 SIMDs x 6 resident render waves */
     int secondary = 0;       /* walk for secondary rays: 0 = by frame, 4, 10 (env CRT_SECONDARY) */
     std::vector<float> tile_work;  /* per 8x8 tile of the full frame */
-    std::vector<int32_t> bin_count;   /* camera-bins candidates per 8x8 cell (empty: no bins) */
+    BinsDev bins;                  /* camera bins (crt_bins.hip) */
     /* measured-cost tile plan (calibrate_plan): per 8x8 tile of the full frame,
      * the sub-tiles it is split into and their probed costs */
     struct SubTile { int32_t dx, dy, w, h; float cost; };
@@ -206,6 +230,12 @@ int render_shard_t(crt_hip_scene *sc, const crt_renderer_settings *st, int shard
 template <class T>
 int unpack_shards_t(crt_hip_scene *sc, int shard_count, const T *d_gathered, T *d_rgb, void *stream, bool compact);
 int scene_upload_buffers(crt_hip_scene *sc, const HostScene &hs);
+int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **out);
+/* crt_bins.hip: camera bins built on the device by every camera frame */
+int bins_setup(crt_hip_scene *sc, const HostScene &hs);
+int bins_plan(crt_hip_scene *sc, ShardPlan &plan);
+int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s);
+void bins_free(crt_hip_scene *sc);
 /* crt_multi.hip: the frame over every replica of a multi-GPU scene into d_rgb
  * (on the scene's device) on `stream`; *overflow: some replica's recorded
  * wavefront sizes did not hold (render again). */

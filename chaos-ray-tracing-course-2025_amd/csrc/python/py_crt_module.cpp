@@ -99,6 +99,20 @@ static PyObject *render_scene_from_dict(PyObject *, PyObject *args) {
     }
     const crt_scene_desc *desc = crt_scene_file_desc(sf);
     const int W = desc->camera.width, H = desc->camera.height;
+    /* bitmap textures are read from disk by every parse (as the reference
+     * reloads them every call): their decoded texels are part of the key, so an
+     * edited texture file never reuses the kept device scene */
+    for (int32_t i = 0; i < desc->texture_count; ++i) {
+        const crt_texture_desc &t = desc->textures[i];
+        if (t.type != CRT_TEXTURE_BITMAP || !t.bitmap_rgb) continue;
+        uint64_t hsh = 1469598103934665603ull;   /* FNV-1a over the texel bytes */
+        const unsigned char *b = reinterpret_cast<const unsigned char *>(t.bitmap_rgb);
+        const size_t nb = (size_t)t.bitmap_width * t.bitmap_height * 3 * sizeof(float);
+        for (size_t k = 0; k < nb; ++k) hsh = (hsh ^ b[k]) * 1099511628211ull;
+        key.push_back('\0');
+        key.append(std::to_string(i) + ":" + std::to_string(t.bitmap_width) + "x" + std::to_string(t.bitmap_height) +
+                   ":" + std::to_string(hsh));
+    }
     std::vector<float> img((size_t)W * H * 3);
     int rc;
     std::string err;

@@ -135,7 +135,13 @@ typedef struct crt_scene_info {
     int32_t bucket_size;
     int32_t gi_on, reflections_on, refractions_on;
     int32_t tree_on_device;    /* 1: tree built by crt_tree_build.hip on the GPU   */
-    double  tree_build_ms;     /* wall time of the device build (0 for host builds) */
+    double  tree_build_ms;     /* wall time of the tree build (host: build + flatten into the device layout) */
+    /* scene-create cost (wall ms; host scenes: the host parts only) */
+    double  prep_ms;           /* host preparation in all: mesh prep, host tree build, BVH */
+    double  bvh_ms;            /* the secondary-ray BVH and proof tables (host) */
+    double  bins_ms;           /* camera-bins setup: templates, buffers, the sizing pass (device) */
+    double  upload_ms;         /* upload to every device (incl. device tree build and bins setup) */
+    double  create_ms;         /* the whole crt_hip_scene_create* call */
 } crt_scene_info;
 
 typedef struct crt_render_stats {
@@ -369,6 +375,19 @@ int  crt_hip_quantize_rgb8(const float *d_rgb, int64_t n, int32_t max_color_comp
  * (rays = n * 6 floats: origin xyz, direction xyz), host buffers. */
 int  crt_hip_trace_batch(crt_hip_scene *scene, const float *rays, int64_t n, crt_hit *hits_out);
 
+/* Test hooks of the camera bins (per 8x8 cell of the frame, the triangles a
+ * camera ray of the cell may hit, sorted by a lower bound of the hit
+ * distance).  crt_hip_camera_bins runs one frame's device
+ * binning (crt_bins.hip) and returns its lists; crt_host_camera_bins the host
+ * checker's (build_camera_bins, no GPU).  len_out (cells = ceil(W/8) x
+ * ceil(H/8), row-major) gets each cell's list length (-1: more than the cell
+ * cap — that cell's pixels walk the BVH); recs_out (96-B records,
+ * csrc/crt_layout.h CamCand) the lists back to back in cell order, at most cap
+ * records.  Either may be NULL.  Returns the record count (0 and every length 0
+ * when the scene takes no camera bins). */
+int64_t crt_hip_camera_bins(crt_hip_scene *scene, int32_t *len_out, void *recs_out, int64_t cap);
+int64_t crt_host_camera_bins(const crt_host_scene *hs, int32_t *len_out, void *recs_out, int64_t cap);
+
 /* Work counters of one frame (instrumented variant of the render kernel). */
 int  crt_hip_count_work(crt_hip_scene *scene, const crt_renderer_settings *settings,
                         crt_work_counts *out);
@@ -467,8 +486,10 @@ typedef struct crt_plan_info {
 int  crt_hip_plan_info(const crt_hip_scene *scene, crt_plan_info *out);
 
 /* Diagnostics: render one full frame with per-wave s_memrealtime stamps
- * (100 MHz ticks; stamps = 2 per 8x8 tile: start, end; tile_xy = tile origin,
- * in dispatch order).  With NULL buffers returns the tile count. */
+ * (100 MHz ticks; stamps = 2 per wave of the render grid: start, end;
+ * tile_xy = the origin of the wave's tile, in dispatch order, -1 for a wave
+ * with nothing to do — an unused camera-bins priority slot, stamps 0).  With
+ * NULL buffers returns the wave count. */
 
 int  crt_hip_profile_waves(crt_hip_scene *scene, const crt_renderer_settings *settings, uint64_t *stamps,
                            int64_t cap, int32_t *tile_xy);

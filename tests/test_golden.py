@@ -37,6 +37,8 @@ def test_product_tree_signature(name):
     assert (info["node_count"], info["leaf_count"], info["leaf_ref_count"]) == \
         (want["nodes"], want["leaves"], want["leaf_refs"])
     assert sha(*hs.tree()) == want["sha256"]
+    # scene-create cost is reported for host builds too (crt_scene_info)
+    assert info["tree_build_ms"] > 0.0 and info["prep_ms"] >= info["tree_build_ms"]
 
 
 @pytest.mark.parametrize("name", sorted(p.stem[4:] for p in GOLDEN.glob("kat_*.npz")))

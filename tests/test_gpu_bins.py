@@ -1,0 +1,102 @@
+"""Camera bins built on the device inside every camera frame (crt_bins.hip):
+the lists equal the host checker's (crt_bvh_build.cpp build_camera_bins, the
+restatement the CPU walk checks in test_bvh.py run on) record for record —
+per 8x8 cell the same length (-1: over the cell cap, the BVH walk), and the
+same records in the same order: hull box, dmin bits, id, geometry, pixel mask
+and `rest` — and frames rendered through them stay bit-identical to the BVH
+walk and to the oracle, frame after frame (the per-frame counters reset)."""
+import numpy as np
+import pytest
+
+from conftest import bits, scene_npz
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def N():
+    from crt_amd import native
+    native.lib()
+    return native
+
+
+def floor_scene(N, w, h, n=600, seed=5, cam=(0.0, 0.3, 0.0), rot=None, fov=70.0):
+    """A random triangle cloud in front of the camera above a large floor that
+    reaches behind it: the floor's two hulls are not in front of the camera,
+    so every cell lists them (the everywhere path)."""
+    rng = np.random.default_rng(seed)
+    c = rng.uniform([-2.0, -0.5, -6.0], [2.0, 1.5, -2.0], (n, 3)).astype(np.float32)
+    v = (c[:, None, :] + rng.uniform(-0.15, 0.15, (n, 3, 3))).astype(np.float32).reshape(-1, 3)
+    floor = np.array([[-40, -1, 40], [40, -1, 40], [40, -1, -40], [-40, -1, -40]], np.float32)
+    pos = np.concatenate([v, floor], 0)
+    b = len(v)
+    idx = np.concatenate([np.arange(len(v), dtype=np.int32), np.array([b, b + 1, b + 2, b, b + 2, b + 3], np.int32)])
+    return N.SyntheticScene(pos, idx, width=w, height=h, camera_location=cam, camera_rotation=rot, fov_degrees=fov)
+
+
+CASES = [("14-01-acceleration-tree__scene1", None), ("14-01-acceleration-tree__scene1", (333, 177)),
+         ("14-01-acceleration-tree__scene1", (3840, 2160)), ("14-01-acceleration-tree__scene0", None),
+         ("12-01-textures__scene4", None), ("12-01-textures__scene3", (517, 301)),
+         ("09-02-diffuse-smooth-shading__scene3", None), ("09-01-barycentric-coordinates__scene1", (1001, 643)),
+         ("13-01-optimizations__scene0", (640, 360))]
+
+
+def _compare(N, sc):
+    hl, hr = N.HostScene(sc).camera_bins()
+    g = N.HipScene(sc)
+    dl, dr = g.camera_bins()
+    assert len(hr) > 0, "the host built no bins"
+    assert len(dr) > 0, "the device built no bins"
+    assert np.array_equal(hl, dl), f"list lengths differ in {int((hl != dl).sum())} cells"
+    assert hr.tobytes() == dr.tobytes(), "records differ"
+    dl2, dr2 = g.camera_bins()   # a second frame: counters were reset
+    assert np.array_equal(dl2, dl) and dr2.tobytes() == dr.tobytes()
+    return hl
+
+
+@pytest.mark.parametrize("name,size", CASES)
+def test_device_bins_equal_host(N, name, size):
+    sc = scene_npz(name)
+    if size:
+        sc = sc.set_resolution(*size)
+    _compare(N, sc)
+
+
+def test_device_bins_everywhere_and_overflow(N):
+    sc = floor_scene(N, 400, 240)
+    ln = _compare(N, sc)
+    assert (ln >= 2).all() or (ln < 0).any()   # the floor is in every cell's list
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_device_bins_random_cameras(N, oracle, seed):
+    rng = np.random.default_rng(seed)
+    a, b = rng.uniform(-0.4, 0.4, 2)
+    ca, sa, cb, sb = np.cos(a), np.sin(a), np.cos(b), np.sin(b)
+    rot = (np.array([[cb, 0, -sb], [0, 1, 0], [sb, 0, cb]]) @ np.array([[1, 0, 0], [0, ca, sa], [0, -sa, ca]]))
+    w, h = [(257, 129), (96, 311), (400, 225)][seed - 1]
+    sc = floor_scene(N, w, h, seed=seed, rot=tuple(float(x) for x in rot.ravel()), fov=float(rng.uniform(20, 150)))
+    _compare(N, sc)
+    st = N.RendererSettings.default()
+    g = N.HipScene(sc)
+    ref = oracle.OracleScene(sc).render(st)
+    for _ in range(2):
+        assert np.array_equal(bits(g.render(st)), bits(ref))
+
+
+def test_bins_frames_repeat_bit_exact(N, oracle, devbuf):
+    """C2's scene through the camera bins, several frames back to back into
+    device memory (the binning, the priority lists and the counters of every
+    frame) and through the host entry point: every frame equals the oracle."""
+    sc = scene_npz("14-01-acceleration-tree__scene1").set_resolution(640, 360)
+    st = N.RendererSettings.default()
+    want = bits(oracle.OracleScene(sc).render(st))
+    g = N.HipScene(sc)
+    d = devbuf.alloc(640 * 360 * 3 * 4)
+    for _ in range(3):
+        g.render_device(st, d)
+    for _ in range(3):
+        g.render_device(st, d)
+        assert np.array_equal(bits(devbuf.download(d, (360, 640, 3), np.float32)), want)
+    assert np.array_equal(bits(g.render(st)), want)
+    assert np.array_equal(bits(N.HipScene(sc, bins_split=1000).render(st)), want)   # no heavy cells split

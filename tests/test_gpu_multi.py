@@ -69,3 +69,47 @@ def test_replicas_from_tree(N):
     want = N.HipScene(sc).render(st)
     got = N.HipScene(ts, devices=[0, 0]).render(st)
     assert np.array_equal(bits(got), bits(want))
+
+
+@pytest.mark.parametrize("opts,over", [({"shadows": 1}, {}), ({"traversal": 8}, {}), ({"bins": 0}, {}),
+                                       ({"bins_split": 1, "bins_quad": 0}, {}),
+                                       ({"secondary": 10}, {"max_ray_depth": 5})])
+def test_options_reach_every_replica(N, opts, over):
+    """An option set on a multi-GPU handle applies to every replica: the image
+    equals the single-device render with the same option (shadows change it)."""
+    name = "09-03-reflective__scene5" if "secondary" in opts else "14-01-acceleration-tree__scene1"
+    sc = scene_npz(name).set_resolution(200, 112)
+    st = N.RendererSettings.default(**over)
+    want = N.HipScene(sc, **opts).render(st)
+    multi = N.HipScene(sc, devices=[0, 0, 0])
+    for k, v in opts.items():
+        multi.set_option(k, v)
+    assert np.array_equal(bits(multi.render(st)), bits(want))
+
+
+def test_concurrent_renders_into_pageable_memory(N):
+    """Two host threads rendering two scenes into pageable buffers at once: the
+    staged copies (one host copy pool) keep each image whole."""
+    import threading
+    a = scene_npz("14-01-acceleration-tree__scene1").set_resolution(640, 360)
+    b = scene_npz("12-01-textures__scene4").set_resolution(512, 288)
+    st = N.RendererSettings.default()
+    ga, gb = N.HipScene(a), N.HipScene(b)
+    wa, wb = ga.render(st), gb.render(st)
+    errs = []
+
+    def run(g, want):
+        try:
+            for _ in range(20):
+                if not np.array_equal(bits(g.render(st)), bits(want)):
+                    errs.append("differs")
+        except Exception as e:   # noqa: BLE001
+            errs.append(repr(e))
+
+    ts = [threading.Thread(target=run, args=(ga, wa)), threading.Thread(target=run, args=(gb, wb))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert not any(t.is_alive() for t in ts), "a render did not return"
+    assert errs == []

@@ -85,3 +85,33 @@ def test_crt_module_matches_oracle(oracle, name, w, h, over):
         _crt.render_scene_from_dict(doc, str(GOLDEN), (1, 2, 3, 4, 5, 6))
     with pytest.raises(ValueError):
         _crt.render_scene_from_dict({"settings": {}}, str(PKG), settings)
+
+
+def test_crt_module_reloads_an_edited_bitmap(tmp_path):
+    """_crt keeps the last dict's device scene, but a bitmap texture file edited
+    between two calls with the same dict is read again (as the reference
+    reloads every call): the second image is the edited texture's, equal to a
+    fresh parse + render of the same files."""
+    if str(PKG) not in sys.path:
+        sys.path.insert(0, str(PKG))
+    import _crt
+    from crt_amd import native
+    _, doc = _doc("12-01-textures__scene4", 96, 54)
+    shutil.copytree(GOLDEN / "textures", tmp_path / "textures")
+    st = native.RendererSettings.default()
+    settings = _crt.RendererSettings((st.max_ray_depth, st.diffuse_reflection_ray_count, st.shadow_bias,
+                                      st.reflection_bias, st.diffuse_reflection_bias, st.refraction_bias))
+
+    def image(px):
+        return np.array([p[:3] for p in px], np.float32).reshape(54, 96, 3)[::-1]
+
+    a = image(_crt.render_scene_from_dict(doc, str(tmp_path), settings))
+    jpg = tmp_path / "textures" / "dragon.jpg"
+    b = bytearray(jpg.read_bytes())
+    q = b.index(b"\xff\xdb") + 5          # first quantisation value (DC) of the first table
+    b[q] = b[q] * 3 % 250 + 2             # still a valid JPEG, other pixel values
+    jpg.write_bytes(bytes(b))
+    c = image(_crt.render_scene_from_dict(doc, str(tmp_path), settings))
+    fresh = native.HipScene(native.SceneFile(text=json.dumps(doc), asset_root=str(tmp_path))).render(st)
+    assert not np.array_equal(bits(np.ascontiguousarray(a)), bits(np.ascontiguousarray(c)))
+    assert np.array_equal(bits(np.ascontiguousarray(c)), bits(fresh))

@@ -9,6 +9,8 @@
  * oracle.  Built by tests/tools/Makefile; loaded by tests/test_prune.py.
  */
 #include <algorithm>
+#include <array>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdint>
@@ -18,6 +20,7 @@
 #include "../../chaos-ray-tracing-course-2025_amd/csrc/crt_host.h"
 #include "../../chaos-ray-tracing-course-2025_amd/csrc/crt_device.h"
 #include "../../chaos-ray-tracing-course-2025_amd/csrc/crt_bvh.h"
+#include "../../chaos-ray-tracing-course-2025_amd/csrc/crt_bins.h"
 
 using namespace crt_amd;
 
@@ -365,7 +368,8 @@ extern "C" int bins_sim_check(const crt_scene_desc *desc, uint64_t *out) {
     if (hs.bnode_count == 0 && ((rc = build_bvh(hs)) != CRT_OK || (rc = build_proof_tables(hs)) != CRT_OK)) return rc;
     std::vector<CamCand> bins;
     std::vector<int32_t> off;
-    if ((rc = build_camera_bins(hs, bins, off)) != CRT_OK) return rc;
+    std::vector<uint8_t> over;   /* cells over the cap walk the BVH (crt_bins.h): no list to check */
+    if ((rc = build_camera_bins(hs, bins, off, &over)) != CRT_OK) return rc;
     for (int k = 0; k < 7; ++k) out[k] = 0;
     if (bins.empty()) return CRT_OK;
     out[6] = 1;
@@ -390,6 +394,7 @@ extern "C" int bins_sim_check(const crt_scene_desc *desc, uint64_t *out) {
             const int a = walk_bvh<true>(bnode_order(hs.bnodes.data(), hs.bnode_count, ray_octant(d)), hs.bnode_count,
                                          hs.btri.data(), hs.btri_id.data(), o, d, pr, t1, tie1, w);
             const int cell = (y / 8) * tx + x / 8;
+            if (over[(size_t)cell]) continue;
             const int b = walk_bins<true>(bins.data(), off[cell], off[cell + 1], 8 * (y % 8) + x % 8, o, d, pr, t2, tie2, wb);
             ++out[0];
             uint32_t u1, u2;
@@ -418,7 +423,8 @@ extern "C" int bins_sim_lanes_check(const crt_scene_desc *desc, int K, uint64_t 
     if (hs.bnode_count == 0 && ((rc = build_bvh(hs)) != CRT_OK || (rc = build_proof_tables(hs)) != CRT_OK)) return rc;
     std::vector<CamCand> bins;
     std::vector<int32_t> off;
-    if ((rc = build_camera_bins(hs, bins, off)) != CRT_OK) return rc;
+    std::vector<uint8_t> over;   /* cells over the cap walk the BVH (crt_bins.h): no list to check */
+    if ((rc = build_camera_bins(hs, bins, off, &over)) != CRT_OK) return rc;
     out[0] = out[1] = out[2] = 0;
     if (bins.empty()) return CRT_OK;
     DeviceScene ds{};
@@ -436,6 +442,7 @@ extern "C" int bins_sim_lanes_check(const crt_scene_desc *desc, int K, uint64_t 
             camera_ray(ds, x, y, o, d);
             const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
             const int cell = (y / 8) * tx + x / 8, bit = 8 * (y % 8) + x % 8;
+            if (over[(size_t)cell]) continue;
             WalkCounts wc = {0u, 0u};
             float ts = 0.f;
             bool ties = false;
@@ -518,7 +525,8 @@ extern "C" int bins_sim_diffs(const crt_scene_desc *desc, int64_t *rows, int cap
     if (hs.bnode_count == 0 && ((rc = build_bvh(hs)) != CRT_OK || (rc = build_proof_tables(hs)) != CRT_OK)) return rc;
     std::vector<CamCand> bins;
     std::vector<int32_t> off;
-    if ((rc = build_camera_bins(hs, bins, off)) != CRT_OK) return rc;
+    std::vector<uint8_t> over;   /* cells over the cap walk the BVH (crt_bins.h): no list to check */
+    if ((rc = build_camera_bins(hs, bins, off, &over)) != CRT_OK) return rc;
     if (bins.empty()) return 0;
     DeviceScene ds{};
     std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
@@ -540,6 +548,7 @@ extern "C" int bins_sim_diffs(const crt_scene_desc *desc, int64_t *rows, int cap
             const int a = walk_bvh<false>(bnode_order(hs.bnodes.data(), hs.bnode_count, ray_octant(d)), hs.bnode_count,
                                           hs.btri.data(), hs.btri_id.data(), o, d, pr, t1, tie1, w);
             const int cell = (y / 8) * tx + x / 8;
+            if (over[(size_t)cell]) continue;
             const int b = walk_bins<false>(bins.data(), off[cell], off[cell + 1], 8 * (y % 8) + x % 8, o, d, pr, t2, tie2, w);
             uint32_t u1, u2;
             std::memcpy(&u1, &t1, 4);
@@ -567,7 +576,8 @@ extern "C" int bins_sim_cells(const crt_scene_desc *desc, int64_t *out) {
     if (hs.bnode_count == 0 && ((rc = build_bvh(hs)) != CRT_OK || (rc = build_proof_tables(hs)) != CRT_OK)) return rc;
     std::vector<CamCand> bins;
     std::vector<int32_t> off;
-    if ((rc = build_camera_bins(hs, bins, off)) != CRT_OK) return rc;
+    std::vector<uint8_t> over;   /* cells over the cap walk the BVH (crt_bins.h): no list to check */
+    if ((rc = build_camera_bins(hs, bins, off, &over)) != CRT_OK) return rc;
     if (bins.empty()) return -1;
     DeviceScene ds{};
     std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
@@ -616,5 +626,142 @@ extern "C" int bins_sim_cells(const crt_scene_desc *desc, int64_t *out) {
                     r[6] += fb ? 1 : 0;
                 }
         }
+    return CRT_OK;
+}
+
+/* Camera fuzz (tests/test_bins_fuzz.py).  Every camera ray of the scene's
+ * camera: (a) the camera-bins walk against the BVH walk — the same t bits and
+ * tie flag, and the same triangle without a tie — and (b) the whole product
+ * answer (bins where the cell has a list, else the BVH walk; then the proof
+ * or the exact kd fallback, resolve_closest) against the reference-order walk
+ * (walk_reference: the reference's node order and first-found rule) — the
+ * same triangle and t bits (the leaf copies of a triangle are one record).  Rows are spread over `nthreads` threads.
+ * out: [0] rays, [1] bins != BVH, [2] product != reference, [3] 1 if bins
+ * were built, [4] rays in cells over the cap (BVH walk), [5] rays with a tie,
+ * [6] rays that took the kd fallback, [7] everywhere hulls, [8] hits,
+ * [9] bin records, [10] 1 if the camera is beyond prune_origin_max.
+ * sample: n_sample pixel indices whose product answer (slot's triangle or -1,
+ * t bits) goes to sample_out (2 per pixel), for the oracle comparison. */
+extern "C" int bins_fuzz(const crt_scene_desc *desc, int nthreads, uint64_t *out, const int64_t *sample,
+                         int64_t n_sample, int64_t *sample_out) {
+    HostScene hs;
+    int rc = prepare_scene(desc, hs);
+    if (rc != CRT_OK) return rc;
+    if (hs.bnode_count == 0 && ((rc = build_bvh(hs)) != CRT_OK || (rc = build_proof_tables(hs)) != CRT_OK)) return rc;
+    std::vector<CamCand> bins;
+    std::vector<int32_t> off;
+    std::vector<uint8_t> over;
+    if ((rc = build_camera_bins(hs, bins, off, &over)) != CRT_OK) return rc;
+    for (int k = 0; k < 11; ++k) out[k] = 0;
+    const bool built = !off.empty();
+    out[3] = built;
+    out[9] = bins.size();
+    {
+        BinCamera cam;
+        if (bin_camera(hs, cam)) {
+            std::vector<CamCand> tpl;
+            bin_templates(hs, tpl);
+            for (const CamCand &c : tpl) {
+                const float lo[3] = {c.lo_x, c.lo_y, c.lo_z}, hi[3] = {c.hi_x, c.hi_y, c.hi_z};
+                out[7] += bin_project(lo, hi, cam).every;
+            }
+        }
+        for (int k = 0; k < 3; ++k) out[10] |= !(std::fabs(hs.cam_loc[k]) <= hs.prune_origin_max);
+    }
+    auto ok = [](float x) {
+        const float m = std::fabs(x);
+        return x == 0.0f || (m >= 0x1p-40f && m <= 0x1p62f);
+    };
+    bool planes_ok = true;   /* as crt_api.hip scene_upload */
+    for (const DNode &n : hs.nodes)
+        planes_ok = planes_ok && ok(n.lo_x) && ok(n.lo_y) && ok(n.lo_z) && ok(n.hi_x) && ok(n.hi_y) && ok(n.hi_z) &&
+                    n.lo_x <= n.hi_x && n.lo_y <= n.hi_y && n.lo_z <= n.hi_z;
+    DeviceScene ds{};
+    std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
+    std::memcpy(ds.cam_rot, hs.cam_rot, sizeof ds.cam_rot);
+    ds.width = hs.width;
+    ds.height = hs.height;
+    ds.aspect = hs.aspect;
+    ds.tan_half_fov = hs.tan_half_fov;
+    const int W = hs.width, H = hs.height, tx = (W + 7) / 8;
+    std::vector<int32_t> res_slot((size_t)W * H);
+    std::vector<float> res_t((size_t)W * H);
+    const int nth = std::max(1, std::min(64, nthreads));
+    std::vector<std::array<uint64_t, 7>> part((size_t)nth);
+    auto work = [&](int th) {
+        std::array<uint64_t, 7> c{};
+        for (int y = th; y < H; y += nth)
+            for (int x = 0; x < W; ++x) {
+                Vec o, d;
+                camera_ray(ds, x, y, o, d);
+                const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
+                WalkCounts w = {0u, 0u};
+                float t1 = 0.f, t2 = 0.f;
+                bool tie1 = false, tie2 = false;
+                const int a = walk_bvh<false>(bnode_order(hs.bnodes.data(), hs.bnode_count, ray_octant(d)),
+                                              hs.bnode_count, hs.btri.data(), hs.btri_id.data(), o, d, pr, t1, tie1, w);
+                const int cell = (y / 8) * tx + x / 8;
+                int tri = a;
+                float tt = t1;
+                bool tie = tie1;
+                if (built && !over[(size_t)cell]) {
+                    const int b = walk_bins<false>(bins.data(), off[cell], off[cell + 1], 8 * (y % 8) + x % 8, o, d, pr,
+                                                   t2, tie2, w);
+                    uint32_t u1, u2;
+                    std::memcpy(&u1, &t1, 4);
+                    std::memcpy(&u2, &t2, 4);
+                    if ((a < 0) != (b < 0) || (a >= 0 && (u1 != u2 || tie1 != tie2 || (!tie1 && a != b)))) ++c[1];
+                    tri = b;
+                    tt = t2;
+                    tie = tie2;
+                } else if (built) {
+                    ++c[4];
+                }
+                c[5] += tri >= 0 && tie;
+                bool fb = false;
+                float bt = 0.f;
+                const int slot = resolve_closest<false>(hs.nodes.data(), hs.pnodes.data(), (int)hs.nodes.size(),
+                                                        hs.slots.data(), hs.slot_cull.data(), hs.slot_tri.data(),
+                                                        hs.ktopo.empty() ? nullptr : hs.ktopo.data(), planes_ok, o, d,
+                                                        pr, tri, tt, tie, bt, w, &fb);
+                c[6] += fb;
+                float rt = 0.f;
+                uint64_t rn = 0, rtr = 0;
+                const int rs = walk_reference(hs, o, d, rt, rn, rtr);
+                uint32_t v1, v2;
+                std::memcpy(&v1, &bt, 4);
+                std::memcpy(&v2, &rt, 4);
+                /* copies of one triangle in several leaves are the same record (crt_acceleration_tree.cpp:44-58):
+                 * the answer is the triangle and t */
+                const int ta = slot >= 0 ? hs.slot_tri[(size_t)slot] : -1, tb = rs >= 0 ? hs.slot_tri[(size_t)rs] : -1;
+                if (ta != tb || (slot >= 0 && v1 != v2)) ++c[2];
+                c[3] += slot >= 0;
+                ++c[0];
+                res_slot[(size_t)y * W + x] = slot;
+                res_t[(size_t)y * W + x] = bt;
+            }
+        part[(size_t)th] = c;
+    };
+    std::vector<std::thread> pool;
+    for (int th = 0; th < nth; ++th) pool.emplace_back(work, th);
+    for (auto &t : pool) t.join();
+    for (const auto &c : part) {
+        out[0] += c[0];
+        out[1] += c[1];
+        out[2] += c[2];
+        out[4] += c[4];
+        out[5] += c[5];
+        out[6] += c[6];
+        out[8] += c[3];
+    }
+    for (int64_t i = 0; i < n_sample; ++i) {
+        const int64_t p = sample[i];
+        if (p < 0 || p >= (int64_t)W * H) return -1;
+        const int s = res_slot[(size_t)p];
+        uint32_t u;
+        std::memcpy(&u, &res_t[(size_t)p], 4);
+        sample_out[2 * i] = s >= 0 ? hs.slot_tri[(size_t)s] : -1;
+        sample_out[2 * i + 1] = s >= 0 ? (int64_t)u : 0;
+    }
     return CRT_OK;
 }
