@@ -412,7 +412,9 @@ def main():
     # calibrate 1: the measured tile plan with its split threshold tuned on the
     # first frame (a long-running renderer's steady state; one-shot callers
     # default to the fixed threshold, see cold_cli below)
+    t_create = time.perf_counter()
     gpu = N.HipScene(scene, device=local, events=0, shadows=int(a.shadows), calibrate=1)
+    create_wall_ms = (time.perf_counter() - t_create) * 1e3
     build_id = N.build_id()
     # an explicit stream: the render kernel, the gather and the timing events
     # all go on it (handle 0 would mean "the scene's own stream" to the C-ABI)
@@ -522,6 +524,29 @@ def main():
 
     elapsed, kern_ms = measure(mode, a.steps)
 
+    # camera bins (crt_bins.hip): every frame above rebuilds them on the device
+    # before its render kernel; their device time alone, and the same frame
+    # with the bins off (every camera ray through the BVH walk, no binning)
+    bins = None
+    if mode == "single" and not a.shadows:
+        b_ms = gpu.bins_ms(50)
+        if b_ms > 0.0:
+            gpu.set_option("bins", 0)
+            for _ in range(a.warmup):
+                step(mode)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                step(mode)
+            torch.cuda.synchronize()
+            off_ms = (time.perf_counter() - t0) / a.steps * 1e3
+            gpu.set_option("bins", 1)
+            bins = {"rebuilt_every_frame": True, "bins_ms": round(b_ms, 5),
+                    "frame_ms_bins_off": round(off_ms, 5),
+                    "value_bins_off": round(rays_per_frame / (off_ms * 1e-3) / 1e6, 3),
+                    "note": "frame = device binning (k_bins_project + k_bins_sort) + render; bins_ms = the binning "
+                            "alone (HIP events, 50 frames); bins off = the BVH walk for every camera ray"}
+
     check = None
     if a.check and rank == 0:
         want = gpu.render(settings)
@@ -614,6 +639,11 @@ def main():
                                     "the reference's render_image call (main.cpp:37-43)") if e2e is not None else None,
                        "cold_cli": cold,
                        "check": check, "build_id": build_id,
+                       "camera_bins": bins,
+                       "scene_create_ms": {"wall": round(create_wall_ms, 3),
+                                           **{k: round(v, 3) for k, v in gpu.info().items()
+                                              if k in ("prep_ms", "tree_build_ms", "bvh_ms", "bins_ms", "upload_ms",
+                                                       "create_ms")}},
                        "plan": gpu.plan_info()},
             "roofline": roof,
             "secondary": secondary,

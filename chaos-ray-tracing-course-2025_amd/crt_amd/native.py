@@ -184,6 +184,11 @@ EXPORTS = [
     ("crt_hip_scene_create_mask", C.c_int, [C.POINTER(SceneDesc), C.c_uint64, C.c_int, C.POINTER(_P)]),
     ("crt_hip_scene_from_tree_mask", C.c_int, [C.POINTER(TreeSceneDesc), C.c_uint64, C.POINTER(_P)]),
     ("crt_hip_scene_devices", C.c_int, [_P, _P, C.c_int32]),
+    ("crt_auto_gpus", C.c_int, [C.POINTER(SceneDesc), C.POINTER(RendererSettings), C.c_int]),
+    ("crt_auto_gpus_tree", C.c_int, [C.POINTER(TreeSceneDesc), C.POINTER(RendererSettings), C.c_int]),
+    ("crt_hip_scene_create_auto", C.c_int, [C.POINTER(SceneDesc), C.POINTER(RendererSettings), C.c_int, C.POINTER(_P)]),
+    ("crt_hip_scene_from_tree_auto", C.c_int, [C.POINTER(TreeSceneDesc), C.POINTER(RendererSettings),
+                                               C.POINTER(_P)]),
     ("crt_hip_last_replica_ms", C.c_int, [_P, _P, C.c_int32]),
     ("crt_hip_scene_from_tree", C.c_int, [C.POINTER(TreeSceneDesc), C.c_int, C.POINTER(_P)]),
     ("crt_host_scene_from_tree", C.c_int, [C.POINTER(TreeSceneDesc), C.POINTER(_P)]),
@@ -210,6 +215,7 @@ EXPORTS = [
     ("crt_hip_trace_batch", C.c_int, [_P, _P, C.c_int64, _P]),
     ("crt_hip_camera_bins", C.c_int64, [_P, _P, _P, C.c_int64]),
     ("crt_host_camera_bins", C.c_int64, [_P, _P, _P, C.c_int64]),
+    ("crt_hip_bins_time", C.c_int, [_P, C.c_int32, C.POINTER(C.c_double)]),
     ("crt_hip_count_work", C.c_int, [_P, C.POINTER(RendererSettings), C.POINTER(WorkCounts)]),
     ("crt_hip_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_double)]),
     ("crt_hip_plan_info", C.c_int, [_P, _P]),
@@ -637,6 +643,12 @@ class HipScene:
     def last_kernel_ms(self) -> float:
         v = C.c_double()
         _check(lib().crt_hip_last_kernel_ms(self._h, C.byref(v)))
+        return v.value
+
+    def bins_ms(self, frames: int = 50) -> float:
+        """Device ms of one frame's camera binning alone (0 without camera bins)."""
+        v = C.c_double()
+        _check(lib().crt_hip_bins_time(self._h, frames, C.byref(v)))
         return v.value
 
     def camera_bins(self):

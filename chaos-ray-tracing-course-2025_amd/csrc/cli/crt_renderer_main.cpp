@@ -12,10 +12,12 @@
  * reference CLI always uses default RendererSettings and the file's size.
  *
  * Like the reference's render_image, which spans every hardware thread
- * (crt_renderer.cpp:176-196), the render spans every visible GPU by default
- * (crt_hip_scene_create_mask; CRT_HIP_GPUS=N limits it); --gpus G takes
- * devices 0..G-1, --device K one device.
+ * (crt_renderer.cpp:176-196), the render may span several GPUs: by default as
+ * many as the frame's size pays for (crt_hip_scene_create_auto: one GPU for a
+ * short frame, all of them for a GI or very large one; CRT_HIP_GPUS=N sets
+ * the count); --gpus G takes devices 0..G-1, --device K one device.
  */
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -90,9 +92,10 @@ int main(int argc, char *argv[]) {
     if (gi_rays >= 0) settings.diffuse_reflection_ray_count = (uint32_t)gi_rays;
 
     crt_hip_scene *scene = nullptr;
-    const uint64_t mask = gpus > 0 ? (gpus >= 64 ? ~0ull : (1ull << gpus) - 1ull) : 0ull;
+    const uint64_t mask = gpus >= 64 ? ~0ull : (1ull << std::max(gpus, 0)) - 1ull;
     const int crc = device >= 0 ? crt_hip_scene_create(desc, device, &scene)
-                                : crt_hip_scene_create_mask(desc, mask, CRT_SCENE_TREE_AUTO, &scene);
+                    : gpus > 0  ? crt_hip_scene_create_mask(desc, mask, CRT_SCENE_TREE_AUTO, &scene)
+                                : crt_hip_scene_create_auto(desc, &settings, CRT_SCENE_TREE_AUTO, &scene);
     if (crc != CRT_OK) {
         std::fprintf(stderr, "Error: %s\n", crt_hip_last_error());
         crt_scene_file_destroy(sf);

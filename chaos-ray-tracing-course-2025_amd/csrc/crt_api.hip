@@ -605,37 +605,44 @@ int crt_hip_profile_waves(crt_hip_scene *sc, const crt_renderer_settings *st, ui
      * priority lists ahead of the untaken tiles */
     const ShardPlan &p = sc->full;
     const BinsPlan &bp = p.bp;
-    std::vector<int32_t> prio, taken, phdr(2, 0);
+    std::vector<int32_t> prio, taken, phdr(2 * kBinShards, 0), ph_all;
     if (rc == CRT_OK && e == hipSuccess && bp.cell_tile) {
-        prio.resize((size_t)(bp.e_h + bp.e_m));
+        const int par = (int)((sc->bins.frame - 1) & 1);   /* the parity the frame just used */
+        prio.resize((size_t)(kBinShards * (bp.ch + bp.cm)));
         taken.resize((size_t)bp.nbase);
         e = hipMemcpy(prio.data(), bp.prio, prio.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
         if (e == hipSuccess) e = hipMemcpy(taken.data(), bp.taken, taken.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
-        if (e == hipSuccess) e = hipMemcpy(phdr.data(), bp.phdr, 2 * sizeof(int32_t), hipMemcpyDeviceToHost);
+        ph_all.resize((size_t)kBinsPhdrInts);
+        if (e == hipSuccess) e = hipMemcpy(ph_all.data(), bp.phdr, ph_all.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
+        for (int kind = 0; kind < 2; ++kind)
+            for (int sh = 0; sh < kBinShards; ++sh)
+                phdr[(size_t)(kind * kBinShards + sh)] = ph_all[(size_t)bins_phdr_at(par, kind, sh)];
     }
     (void)hipFree(d);
     if (rc != CRT_OK) return rc;
     if (e != hipSuccess) return set_error(CRT_E_HIP, hipGetErrorString(e));
+    const int nh = 4 * kBinShards * bp.ch, nm = kBinShards * bp.cm;
     for (int k = 0; k < nt; ++k) {
         int x = -1, y = -1;
         if (!bp.cell_tile) {
             x = p.tiles[(size_t)k].x;
             y = p.tiles[(size_t)k].y;
-        } else if (k < 4 * bp.e_h) {
-            if (k / 4 < std::min(phdr[0], bp.e_h)) {
-                const Tile &t = p.tiles[(size_t)prio[(size_t)(k / 4)]];
+        } else if (k < nh) {
+            const int slot = k / 4, sh = slot % kBinShards, i2 = slot / kBinShards;
+            if (i2 < std::min(phdr[(size_t)sh], bp.ch)) {
+                const Tile &t = p.tiles[(size_t)prio[(size_t)(sh * bp.ch + i2)]];
                 x = t.x + (k & 1) * 4;
                 y = t.y + ((k >> 1) & 1) * 4;
             }
-        } else if (k < 4 * bp.e_h + bp.e_m) {
-            const int s2 = k - 4 * bp.e_h;
-            if (s2 < std::min(phdr[1], bp.e_m)) {
-                const Tile &t = p.tiles[(size_t)prio[(size_t)(bp.e_h + s2)]];
+        } else if (k < nh + nm) {
+            const int slot = k - nh, sh = slot % kBinShards, i2 = slot / kBinShards;
+            if (i2 < std::min(phdr[(size_t)(kBinShards + sh)], bp.cm)) {
+                const Tile &t = p.tiles[(size_t)prio[(size_t)(kBinShards * bp.ch + sh * bp.cm + i2)]];
                 x = t.x;
                 y = t.y;
             }
         } else {
-            const int b = k - 4 * bp.e_h - bp.e_m;
+            const int b = k - nh - nm;
             if (!taken[(size_t)b]) {
                 x = p.tiles[(size_t)b].x;
                 y = p.tiles[(size_t)b].y;
@@ -720,6 +727,9 @@ static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
         sc->gi_refill = value != 0;
     } else if (k == "gi_machine") {
         sc->gi_machine = value != 0;
+    } else if (k == "rec_machine") {
+        sc->rec_machine = value != 0;
+        sc->calib_walk = -1;
     } else if (k == "bins" || k == "bins_split" || k == "bins_quad") {   /* camera bins: the full-frame plan depends on them */
         if (k == "bins_split" && value < 1) return set_error(CRT_E_INVALID, "bins_split must be >= 1");
         int &field = k == "bins" ? sc->bins_on : k == "bins_quad" ? sc->bins_quad : sc->bins_split;

@@ -62,38 +62,41 @@ struct alignas(16) BinItem {
     int32_t pad0, pad1;
 };
 
-CRT_HD BinItem bin_project(const float blo[3], const float bhi[3], const BinCamera &cam) {
-    BinItem it;
-    it.every = 0;
-    it.pad0 = it.pad1 = 0;
-    const double lo[3] = {blo[0], blo[1], blo[2]}, hi[3] = {bhi[0], bhi[1], bhi[2]};
+/* One corner q (0..7) of a hull box projected: false if it is not strictly
+ * in front of the camera (or not finite), else its image-plane X, Y. */
+CRT_HD bool bin_corner(const double lo[3], const double hi[3], int q, const BinCamera &cam, double &X, double &Y) {
+    const double p[3] = {(q & 1) ? hi[0] : lo[0], (q & 2) ? hi[1] : lo[1], (q & 4) ? hi[2] : lo[2]};
+    const double w[3] = {p[0] - cam.o[0], p[1] - cam.o[1], p[2] - cam.o[2]};
+    double cv[3];
+    for (int j = 0; j < 3; ++j) cv[j] = w[0] * cam.Mi[0][j] + w[1] * cam.Mi[1][j] + w[2] * cam.Mi[2][j];
+    const double wn = sqrt_rn(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    if (!isfinite(wn) || !isfinite(cv[0]) || !isfinite(cv[1]) || !isfinite(cv[2]) || !(cv[2] < -1e-9 * wn))
+        return false;
+    X = (div_rn(div_rn(cv[0], -cv[2]), cam.sx) + 1.0) * 0.5 * cam.W;
+    Y = (1.0 - div_rn(div_rn(cv[1], -cv[2]), cam.sy)) * 0.5 * cam.H;
+    return true;
+}
+
+/* dmin of a hull box: its distance from the camera, scaled by 1 - 2^-20,
+ * rounded down (0 if not finite). */
+CRT_HD float bin_dmin(const double lo[3], const double hi[3], const BinCamera &cam) {
     double d2 = 0.0;
     for (int k = 0; k < 3; ++k) {
         const double e = fmax(fmax(lo[k] - cam.o[k], cam.o[k] - hi[k]), 0.0);
         d2 += e * e;
     }
     const double dist = sqrt_rn(d2) * (1.0 - 0x1p-20);
-    it.dmin = isfinite(dist) ? round_down(dist) : 0.0f;
-    bool all = false;
-    double X0 = INFINITY, X1 = -INFINITY, Y0 = INFINITY, Y1 = -INFINITY;
-    for (int q = 0; q < 8 && !all; ++q) {
-        const double p[3] = {(q & 1) ? hi[0] : lo[0], (q & 2) ? hi[1] : lo[1], (q & 4) ? hi[2] : lo[2]};
-        const double w[3] = {p[0] - cam.o[0], p[1] - cam.o[1], p[2] - cam.o[2]};
-        double cv[3];
-        for (int j = 0; j < 3; ++j) cv[j] = w[0] * cam.Mi[0][j] + w[1] * cam.Mi[1][j] + w[2] * cam.Mi[2][j];
-        const double wn = sqrt_rn(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-        if (!isfinite(wn) || !isfinite(cv[0]) || !isfinite(cv[1]) || !isfinite(cv[2]) || !(cv[2] < -1e-9 * wn)) {
-            all = true;
-            break;
-        }
-        const double X = (div_rn(div_rn(cv[0], -cv[2]), cam.sx) + 1.0) * 0.5 * cam.W;
-        const double Y = (1.0 - div_rn(div_rn(cv[1], -cv[2]), cam.sy)) * 0.5 * cam.H;
-        X0 = fmin(X0, X);
-        X1 = fmax(X1, X);
-        Y0 = fmin(Y0, Y);
-        Y1 = fmax(Y1, Y);
-    }
-    if (all) {
+    return isfinite(dist) ? round_down(dist) : 0.0f;
+}
+
+/* The item from the corners' bounds (every: some corner not in front).  The
+ * bounds are exact minima / maxima, so any order of the corners gives them. */
+CRT_HD BinItem bin_finish(bool every, double X0, double X1, double Y0, double Y1, float dmin, const BinCamera &cam) {
+    BinItem it;
+    it.every = 0;
+    it.pad0 = it.pad1 = 0;
+    it.dmin = dmin;
+    if (every) {
         it.every = 1;
         it.px0 = 0;
         it.px1 = cam.W - 1;
@@ -117,6 +120,24 @@ CRT_HD BinItem bin_project(const float blo[3], const float bhi[3], const BinCame
     it.py0 = (int32_t)fmax(0.0, py0);
     it.py1 = (int32_t)fmin((double)(cam.H - 1), py1);
     return it;
+}
+
+CRT_HD BinItem bin_project(const float blo[3], const float bhi[3], const BinCamera &cam) {
+    const double lo[3] = {blo[0], blo[1], blo[2]}, hi[3] = {bhi[0], bhi[1], bhi[2]};
+    bool every = false;
+    double X0 = INFINITY, X1 = -INFINITY, Y0 = INFINITY, Y1 = -INFINITY;
+    for (int q = 0; q < 8 && !every; ++q) {
+        double X, Y;
+        if (!bin_corner(lo, hi, q, cam, X, Y)) {
+            every = true;
+            break;
+        }
+        X0 = fmin(X0, X);
+        X1 = fmax(X1, X);
+        Y0 = fmin(Y0, Y);
+        Y1 = fmax(Y1, Y);
+    }
+    return bin_finish(every, X0, X1, Y0, Y1, bin_dmin(lo, hi, cam), cam);
 }
 
 /* The pixels of cell (cx, cy) inside the item's rectangle (bit 8 y + x). */

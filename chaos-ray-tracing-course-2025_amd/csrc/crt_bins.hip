@@ -40,7 +40,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "crt_bins.h"
@@ -48,9 +51,54 @@
 
 namespace crt_amd {
 
+#ifdef CRT_BINS_CHECK
+/* diagnostic builds only: every index of the binning kernels checked against
+ * its buffer's size; the first violation is recorded (and the index clamped
+ * to 0, so the kernels stay on their control flow) */
+struct BinsDbg {
+    int32_t code, idx, bound, pad;
+    int32_t nt, ncell, ne_cap, rec_cap, ntaken, prio_cap;
+};
+__device__ BinsDbg g_bins_dbg;
+__device__ int bins_ck(int64_t i, int64_t n, int code) {
+    if (i < 0 || i >= n) {
+        if (atomicCAS(&g_bins_dbg.code, 0, code) == 0) {
+            g_bins_dbg.idx = (int32_t)i;
+            g_bins_dbg.bound = (int32_t)n;
+        }
+        return 0;
+    }
+    return (int)i;
+}
+#define BCK(i, n, code) bins_ck((int64_t)(i), (int64_t)(n), (code))
+#define BDBG(f) g_bins_dbg.f
+#else
+#define BCK(i, n, code) (i)
+#endif
+
+#ifdef CRT_BINS_STAMPS
+/* diagnostic builds only: per block of k_bins_project, s_memrealtime (100 MHz)
+ * at its start, after the projection, after the pair-count scan and at its end */
+__device__ unsigned long long g_bins_stamps[8192 * 4];
+#define BSTAMP(k) \
+    if (threadIdx.x == 0) g_bins_stamps[4 * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime()
+/* ... and per block of k_bins_sort: start, counters read, cell read, list written, end; the list length */
+__device__ unsigned long long g_bins_stamps4[16384 * 6];
+#define BSTAMP4(k) \
+    if (threadIdx.x == 0 && blockIdx.x < 16384) g_bins_stamps4[6 * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime()
+/* (k_bins_sort: wave 0 of each block) */
+#else
+#define BSTAMP(k)
+#define BSTAMP4(k)
+#endif
+
 namespace {
 
-constexpr int kProjTris = 64;     /* triangles per k_bins_project block (256 threads) */
+#ifndef CRT_BINS_CNT_STRIDE
+#define CRT_BINS_CNT_STRIDE 16   /* int32 between two cells' counters (atomics on one line serialise) */
+#endif
+constexpr int kCntStride = CRT_BINS_CNT_STRIDE;
+constexpr int kProjTris = 32;     /* triangles per k_bins_project block: 8 lanes each (one hull corner per lane) */
 
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
     const int lo = __shfl_xor((int)(uint32_t)v, m), hi = __shfl_xor((int)(uint32_t)(v >> 32), m);
@@ -59,6 +107,11 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
 __device__ __forceinline__ uint64_t shfl_down_u64(uint64_t v, int d) {
     const int lo = __shfl_down((int)(uint32_t)v, d), hi = __shfl_down((int)(uint32_t)(v >> 32), d);
     return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+__device__ __forceinline__ double shfl_xor_f64(double v, int m) {
+    const uint64_t u = shfl_xor_u64((uint64_t)__double_as_longlong(v), m);
+    return __longlong_as_double((long long)u);
 }
 
 /* ascending bitonic sort of one key per lane over the wave */
@@ -83,218 +136,396 @@ __device__ __forceinline__ uint64_t wave_suffix_or(uint64_t v, int lane) {
 
 }  // namespace
 
+/* Projection: 8 lanes per triangle (lane q projects hull corner q; the
+ * bounds are reduced over the 8), the item, the triangle's (triangle, cell)
+ * pair count np and its exclusive prefix inside the block's group of
+ * kProjTris triangles, the group's sum; the everywhere list.  Also the
+ * frame's resets: the other parity's counters, this frame's per-cell lengths
+ * and the plan's taken flags. */
 __global__ __launch_bounds__(256) void k_bins_project(const CamCand *__restrict__ tpl, int nt, BinCamera cam,
-                                                      BinItem *__restrict__ items, int32_t *__restrict__ cnt,
-                                                      int32_t *__restrict__ keys, int32_t *__restrict__ every,
-                                                      int32_t *__restrict__ nonempty, BinsHdr *__restrict__ hdr,
+                                                      BinItem *__restrict__ items, int32_t *__restrict__ tpref,
+                                                      int32_t *__restrict__ gsum, int32_t *__restrict__ every,
+                                                      BinsHdr *__restrict__ hdr2, int par,
                                                       int32_t *__restrict__ bin_len, int ncell,
                                                       int32_t *__restrict__ taken, int ntaken,
-                                                      int32_t *__restrict__ phdr) {
-    __shared__ int32_t pref[kProjTris + 1];
-    __shared__ int32_t cw[kProjTris], cx0[kProjTris], cy0[kProjTris];
+                                                      int32_t *__restrict__ phdr2) {
+    __shared__ int32_t npl[kProjTris];
     const int tid = (int)threadIdx.x;
+    BSTAMP(0);
+    BinsHdr *hdr = hdr2 + par;
+    /* the other parity's counters start the next frame at zero (this frame
+     * does not touch them; the previous one is done with them) */
+    if (blockIdx.x == 0) {
+        BinsHdr *o = hdr2 + (par ^ 1);
+        if (tid == 0) o->n_every.v = 0;
+        if (tid < kBinShards) {
+            o->ne[tid].v = 0;
+            o->rec[tid].v = 0;
+        }
+        if (phdr2 && tid < 2 * kBinShards)
+            phdr2[BCK(bins_phdr_at(par ^ 1, tid / kBinShards, tid % kBinShards), kBinsPhdrInts, 1)] = 0;
+    }
     /* this frame's per-cell lengths and plan state start empty (k_bins_sort fills them) */
     const int g = (int)(blockIdx.x * blockDim.x) + tid, gn = (int)(gridDim.x * blockDim.x);
-    for (int i = g; i < ncell; i += gn) bin_len[i] = 0;
-    for (int i = g; i < ntaken; i += gn) taken[i] = 0;
-    if (g == 0 && phdr) {
-        phdr[0] = 0;
-        phdr[1] = 0;
+    for (int i = g; i < ncell; i += gn) bin_len[BCK(i, BDBG(ncell), 2)] = 0;
+    for (int i = g; i < ntaken; i += gn) taken[BCK(i, BDBG(ntaken), 3)] = 0;
+    const int tl = tid >> 3, q = tid & 7;
+    const int t = (int)blockIdx.x * kProjTris + tl;
+    double lo[3] = {0.0, 0.0, 0.0}, hi[3] = {0.0, 0.0, 0.0};
+    double X0 = INFINITY, X1 = -INFINITY, Y0 = INFINITY, Y1 = -INFINITY;
+    int behind = 0;
+    if (t < nt) {
+        const float *b = reinterpret_cast<const float *>(tpl + BCK(t, BDBG(nt), 4));   /* lo_x, hi_x, lo_y, ... */
+        lo[0] = b[0]; hi[0] = b[1]; lo[1] = b[2]; hi[1] = b[3]; lo[2] = b[4]; hi[2] = b[5];
+        double X, Y;
+        if (bin_corner(lo, hi, q, cam, X, Y)) {
+            X0 = X1 = X;
+            Y0 = Y1 = Y;
+        } else {
+            behind = 1;
+        }
     }
-    if (tid < kProjTris) {   /* wave 0: one triangle per lane */
-        const int t = (int)blockIdx.x * kProjTris + tid;
+    for (int d = 1; d < 8; d <<= 1) {
+        X0 = fmin(X0, shfl_xor_f64(X0, d));
+        X1 = fmax(X1, shfl_xor_f64(X1, d));
+        Y0 = fmin(Y0, shfl_xor_f64(Y0, d));
+        Y1 = fmax(Y1, shfl_xor_f64(Y1, d));
+        behind |= __shfl_xor(behind, d);
+    }
+    if (q == 0) {
         int np = 0;
         if (t < nt) {
-            const float *b = reinterpret_cast<const float *>(tpl + t);   /* lo_x, hi_x, lo_y, hi_y, lo_z, hi_z */
-            const float lo[3] = {b[0], b[2], b[4]}, hi[3] = {b[1], b[3], b[5]};
-            const BinItem it = bin_project(lo, hi, cam);
-            items[t] = it;
+            const BinItem it = bin_finish(behind != 0, X0, X1, Y0, Y1, bin_dmin(lo, hi, cam), cam);
+            items[BCK(t, BDBG(nt), 5)] = it;
             if (it.every) {
-                const int k = atomicAdd(&hdr->n_every, 1);
-                if (k < kBinMaxEverywhere) every[k] = t;
+                const int k = atomicAdd(&hdr->n_every.v, 1);
+                if (k < kBinMaxEverywhere) every[BCK(k, kBinMaxEverywhere, 6)] = t;
             } else if (it.px0 <= it.px1) {
-                const int x0 = it.px0 >> 3, x1 = it.px1 >> 3, y0 = it.py0 >> 3, y1 = it.py1 >> 3;
-                np = (x1 - x0 + 1) * (y1 - y0 + 1);
-                cw[tid] = x1 - x0 + 1;
-                cx0[tid] = x0;
-                cy0[tid] = y0;
+                np = ((it.px1 >> 3) - (it.px0 >> 3) + 1) * ((it.py1 >> 3) - (it.py0 >> 3) + 1);
             }
         }
+        npl[tl] = np;
+    }
+    BSTAMP(1);
+    __syncthreads();
+    if (tid < 64) {   /* wave 0: the group's exclusive prefix and sum */
+        const int np = tid < kProjTris ? npl[tid] : 0;
         int incl = np;
         for (int d = 1; d < 64; d <<= 1) {
             const int v = __shfl_up(incl, d);
             if (tid >= d) incl += v;
         }
-        pref[tid] = incl - np;
-        if (tid == 63) pref[kProjTris] = incl;
+        const int tt = (int)blockIdx.x * kProjTris + tid;
+        if (tid < kProjTris && tt < nt) tpref[BCK(tt, BDBG(nt), 33)] = incl - np;
+        if (tid == kProjTris - 1) gsum[blockIdx.x] = incl;
     }
-    __syncthreads();
-    const int total = pref[kProjTris];
-    for (int p = tid; p < total; p += (int)blockDim.x) {
-        int lo = 0, hi = kProjTris - 1;   /* the last triangle whose pairs start at or before p */
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (pref[mid] <= p) lo = mid;
-            else hi = mid - 1;
-        }
-        const int j = p - pref[lo], w = cw[lo];
-        const int cell = (cy0[lo] + j / w) * cam.tx + cx0[lo] + j % w;
-        const int slot = atomicAdd(&cnt[cell], 1);
-        if (slot == 0) nonempty[atomicAdd(&hdr->n_nonempty, 1)] = cell;
-        if (slot < kBinCellCap) keys[(size_t)cell * kBinCellCap + slot] = (int)blockIdx.x * kProjTris + lo;
-    }
+    BSTAMP(2);
 }
 
-/* One cell's list: n candidates (m own ids in keys, then the everywhere ids),
- * sorted, written from `start`.  n <= 64: one candidate per lane in registers. */
-__device__ void bins_emit_small(const CamCand *__restrict__ tpl, const BinItem *__restrict__ items,
-                                const int32_t *__restrict__ ids, int m, const int32_t *__restrict__ every, int n,
-                                int cx, int cy, CamCand *__restrict__ out, int lane) {
-    uint64_t key = ~0ull;
-    if (lane < n) {
-        const int t = lane < m ? ids[lane] : every[lane - m];
-        key = bin_key(items[t].dmin, t);
-    }
-    key = wave_sort(key, lane);
-    uint64_t mask = 0ull;
-    int t = 0;
-    BinItem it{};
-    if (lane < n) {
-        t = (int)(uint32_t)key;
-        it = items[t];
-        mask = bin_mask(it, cx, cy);
-    }
-    const uint64_t rest = wave_suffix_or(mask, lane);
-    if (lane < n) {
-        CamCand c = tpl[t];
-        c.dmin = it.dmin;
-        c.mask = mask;
-        c.rest = rest;
-        out[lane] = c;
-    }
-}
+/* Scatter: every (triangle, cell) pair of the frame, spread evenly over the
+ * grid (a triangle covering thousands of cells shares its pairs among many
+ * blocks), takes a slot of its cell (atomic count; kBinCellCap slots per
+ * cell) and writes the triangle id there; the first pair of a cell lists the
+ * cell in its shard's non-empty list.  Each block scans the groups' sums in
+ * LDS and finds each of its pairs' group, then its triangle (the group's
+ * prefix), then its cell. */
+constexpr int kPairsPerThread = 2;
+constexpr int kMaxGroups = 8192;   /* 2^18 triangles (bins are built up to the BVH's limit) */
 
-/* n in (64, kBinCellCap]: bitonic sort in LDS (sk, padded to a power of two),
- * then the records written chunk by chunk from the list's end (rest carried). */
-__device__ void bins_emit_large(const CamCand *__restrict__ tpl, const BinItem *__restrict__ items,
-                                const int32_t *__restrict__ ids, int m, const int32_t *__restrict__ every, int n,
-                                int cx, int cy, CamCand *__restrict__ out, uint64_t *sk, int lane) {
-    int P = 128;
-    while (P < n) P <<= 1;
-    for (int j = lane; j < P; j += 64) {
-        uint64_t key = ~0ull;
-        if (j < n) {
-            const int t = j < m ? ids[j] : every[j - m];
-            key = bin_key(items[t].dmin, t);
+__global__ __launch_bounds__(256) void k_bins_pairs(const BinItem *__restrict__ items,
+                                                    const int32_t *__restrict__ tpref,
+                                                    const int32_t *__restrict__ gsum, int ngroups, int nt, int tx,
+                                                    int32_t *__restrict__ cnt, uint64_t *__restrict__ keys,
+                                                    int32_t *__restrict__ nonempty, int cap_shard,
+                                                    BinsHdr *__restrict__ hdr2, int par) {
+    __shared__ int32_t gp[kMaxGroups + 1];
+    __shared__ int32_t part[256];
+    const int tid = (int)threadIdx.x;
+    BinsHdr *hdr = hdr2 + par;
+    /* exclusive prefix of the groups' sums: each thread sums a run, then the runs are scanned */
+    const int per = (ngroups + 255) / 256, g0 = tid * per, g1 = min(ngroups, g0 + per);
+    int run = 0;
+    for (int k = g0; k < g1; ++k) run += gsum[k];
+    part[tid] = run;
+    __syncthreads();
+    if (tid < 64) {
+        int a = 0;
+        for (int k = 0; k < 4; ++k) a += part[4 * tid + k];
+        int incl = a;
+        for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(incl, d);
+            if (tid >= d) incl += v;
         }
-        sk[j] = key;
+        int base = incl - a;
+        for (int k = 0; k < 4; ++k) {
+            const int v = part[4 * tid + k];
+            part[4 * tid + k] = base;
+            base += v;
+        }
+        if (tid == 63) gp[kMaxGroups] = incl;
     }
     __syncthreads();
-    for (int size = 2; size <= P; size <<= 1)
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = lane; i < (P >> 1); i += 64) {
-                const int a = 2 * stride * (i / stride) + (i % stride), b = a + stride;
-                const bool up = (a & size) == 0;
-                const uint64_t ka = sk[a], kb = sk[b];
-                if ((ka > kb) == up) {
-                    sk[a] = kb;
-                    sk[b] = ka;
-                }
+    {
+        int acc = part[tid];
+        for (int k = g0; k < g1; ++k) {
+            gp[k] = acc;
+            acc += gsum[k];
+        }
+    }
+    __syncthreads();
+    const int total = gp[kMaxGroups];
+    const int64_t G = gridDim.x;
+    const int p0 = (int)((int64_t)total * blockIdx.x / G), p1 = (int)((int64_t)total * (blockIdx.x + 1) / G);
+    for (int pb = p0 + tid; pb < p1; pb += 256 * kPairsPerThread) {
+        int cell[kPairsPerThread];
+        uint64_t key[kPairsPerThread];
+#pragma unroll
+        for (int u = 0; u < kPairsPerThread; ++u) {
+            const int p = pb + u * 256;
+            cell[u] = -1;
+            if (p >= p1) continue;
+            int lo = 0, hi = ngroups - 1;   /* the last group whose pairs start at or before p */
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (gp[mid] <= p) lo = mid;
+                else hi = mid - 1;
             }
-            __syncthreads();
+            const int r = p - gp[lo];
+            /* ... and the triangle inside the group: the group's prefixes in one
+             * round of loads (kProjTris contiguous ints), the last one <= r */
+            const int a0 = lo * kProjTris, na = min(nt - a0, kProjTris);
+            const int4 *tp4 = reinterpret_cast<const int4 *>(tpref + BCK(a0, BDBG(nt), 34));
+            int4 v[kProjTris / 4];
+#pragma unroll
+            for (int q = 0; q < kProjTris / 4; ++q) v[q] = load_global(tp4, q);
+            int a = a0, pr = 0;
+#pragma unroll
+            for (int q = 0; q < kProjTris / 4; ++q) {
+                const int e[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+                for (int z = 0; z < 4; ++z)
+                    if (4 * q + z < na && e[z] <= r) {
+                        a = a0 + 4 * q + z;
+                        pr = e[z];
+                    }
+            }
+            const BinItem it = items[BCK(a, BDBG(nt), 35)];
+            const int j = r - pr, x0 = it.px0 >> 3, w = (it.px1 >> 3) - x0 + 1;
+            cell[u] = ((it.py0 >> 3) + j / w) * tx + x0 + j % w;
+            key[u] = bin_key(it.dmin, a);   /* the cell's sort key: (dmin, id) */
         }
+        int slot[kPairsPerThread];
+#pragma unroll
+        for (int u = 0; u < kPairsPerThread; ++u)   /* the atomics in flight together */
+            slot[u] = cell[u] >= 0 ? atomicAdd(&cnt[(size_t)BCK(cell[u], BDBG(ncell), 7) * kCntStride], 1) : kBinCellCap;
+#pragma unroll
+        for (int u = 0; u < kPairsPerThread; ++u) {
+            if (cell[u] < 0) continue;
+            if (slot[u] < kBinCellCap)
+                keys[BCK((size_t)cell[u] * kBinCellCap + slot[u], (int64_t)BDBG(ncell) * kBinCellCap, 8)] = key[u];
+            if (slot[u] == 0) {   /* the cell's first candidate: list the cell in its shard */
+                const int sh = cell[u] % kBinShards;
+                nonempty[BCK(sh * cap_shard + atomicAdd(&hdr->ne[BCK(sh, kBinShards, 9)].v, 1), BDBG(ne_cap), 10)] =
+                    cell[u];
+            }
+        }
+    }
+}
+
+/* k_bins_sort: one wave per listed cell (every cell when some hull is
+ * everywhere), four independent waves a block.  The cell's keys (its own
+ * from the scatter, then the everywhere ids at dmin 0) are ranked in LDS —
+ * each key's rank is the number of smaller keys (keys are distinct: they hold
+ * the id) — and put in order; then the records are written chunk by chunk from
+ * the list's end, so `rest` (the OR of the masks from here to the end) is
+ * carried: the static part from the triangle's template, dmin from the key,
+ * the cell's pixels inside the triangle's rectangle. */
+constexpr int kSortWaves = 4;
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int kPer>   /* keys per lane: n <= 64 kPer */
+__device__ void bins_emit(const CamCand *__restrict__ tpl, const BinItem *__restrict__ items,
+                          const uint64_t *__restrict__ own, int m, const int32_t *__restrict__ every, int n, int cx,
+                          int cy, CamCand *__restrict__ out, uint64_t *sk, int lane) {
+    uint64_t mine[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+        const int j = lane + 64 * r;
+        mine[r] = ~0ull;
+        if (j < n) mine[r] = j < m ? own[BCK(j, kBinCellCap, 11)] : bin_key(0.0f, every[BCK(j - m, kBinMaxEverywhere, 12)]);
+        if (j < n) sk[j] = mine[r];
+    }
+    wave_lds_sync();
+    int rank[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) rank[r] = 0;
+    for (int i = 0; i < n; ++i) {   /* broadcast reads: every lane compares its keys with key i */
+        const uint64_t k = sk[i];
+#pragma unroll
+        for (int r = 0; r < kPer; ++r) rank[r] += k < mine[r] ? 1 : 0;
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < kPer; ++r)
+        if (lane + 64 * r < n) sk[rank[r]] = mine[r];
+    wave_lds_sync();
     uint64_t carry = 0ull;
+    static_assert(sizeof(CamCand) == 6 * sizeof(float4), "CamCand is six float4");
     for (int base = ((n - 1) >> 6) << 6; base >= 0; base -= 64) {
         const int j = base + lane;
         uint64_t mask = 0ull;
-        int t = 0;
-        BinItem it{};
+        float4 q[6];   /* the record in registers (loaded with the item: one round trip) */
+        float dmin = 0.0f;
         if (j < n) {
-            t = (int)(uint32_t)sk[j];
-            it = items[t];
+            const int t = (int)(uint32_t)sk[j];
+            const BinItem it = items[BCK(t, BDBG(nt), 19)];
+            const float4 *src = reinterpret_cast<const float4 *>(tpl + BCK(t, BDBG(nt), 20));
+#pragma unroll
+            for (int r = 0; r < 6; ++r) q[r] = load_global(src, r);
             mask = bin_mask(it, cx, cy);
+            dmin = it.dmin;
         }
         const uint64_t rest = wave_suffix_or(mask, lane) | carry;
-        carry = (uint64_t)__shfl((long long)rest, 0);
-        if (j < n) {
-            CamCand c = tpl[t];
-            c.dmin = it.dmin;
-            c.mask = mask;
-            c.rest = rest;
-            out[j] = c;
+        {
+            const int lo = __shfl((int)(uint32_t)rest, 0), hi = __shfl((int)(uint32_t)(rest >> 32), 0);
+            carry = ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+        }
+        if (j < n) {   /* dmin: float 6; mask: floats 20-21; rest: 22-23 */
+            q[1].z = dmin;
+            q[5].x = __uint_as_float((uint32_t)mask);
+            q[5].y = __uint_as_float((uint32_t)(mask >> 32));
+            q[5].z = __uint_as_float((uint32_t)rest);
+            q[5].w = __uint_as_float((uint32_t)(rest >> 32));
+            float4 *dst = reinterpret_cast<float4 *>(out + j);
+#pragma unroll
+            for (int r = 0; r < 6; ++r) dst[r] = q[r];
         }
     }
-    __syncthreads();   /* sk is reused by the next cell */
+    wave_lds_sync();   /* sk is reused by the wave's next cell */
 }
 
-__global__ __launch_bounds__(64) void k_bins_sort(const CamCand *__restrict__ tpl, const BinItem *__restrict__ items,
-                                                  int32_t *__restrict__ cnt, const int32_t *__restrict__ keys,
-                                                  const int32_t *__restrict__ every,
-                                                  const int32_t *__restrict__ nonempty, BinsHdr *__restrict__ hdr,
-                                                  CamCand *__restrict__ recs, int32_t rec_cap,
-                                                  int32_t *__restrict__ bin_off, int32_t *__restrict__ bin_len,
-                                                  int tx, int ncell, BinsPlan bp) {
-    __shared__ uint64_t sk[kBinCellCap];
-    const int lane = (int)threadIdx.x;
-    const int n_every = hdr->n_every;
+/* n <= 64 (nearly every cell): one candidate per lane; its template and item
+ * are loaded in list order while the keys are ranked, the record is written
+ * straight to its ranked position, and only the masks and `rest` go through
+ * LDS (sk[0..63] keys, [64..127] masks by rank, [128..191] rest by rank). */
+__device__ void bins_emit64(const CamCand *__restrict__ tpl, const BinItem *__restrict__ items,
+                            const uint64_t *__restrict__ own, int m, const int32_t *__restrict__ every, int n, int cx,
+                            int cy, CamCand *__restrict__ out, uint64_t *sk, int lane) {
+    const bool on = lane < n;
+    uint64_t key = ~0ull;
+    if (on) key = lane < m ? own[BCK(lane, kBinCellCap, 11)] : bin_key(0.0f, every[BCK(lane - m, kBinMaxEverywhere, 12)]);
+    const int t = (int)(uint32_t)key;
+    BinItem it{};
+    float4 q[6];
+    if (on) {   /* in flight during the ranking */
+        it = items[BCK(t, BDBG(nt), 19)];
+        const float4 *src = reinterpret_cast<const float4 *>(tpl + BCK(t, BDBG(nt), 20));
+#pragma unroll
+        for (int r = 0; r < 6; ++r) q[r] = load_global(src, r);
+    }
+    if (on) sk[lane] = key;
+    wave_lds_sync();
+    int rank = 0;
+    for (int i = 0; i < n; ++i) rank += sk[i] < key ? 1 : 0;
+    const uint64_t mask = on ? bin_mask(it, cx, cy) : 0ull;
+    if (on) sk[64 + rank] = mask;
+    wave_lds_sync();
+    const uint64_t rest = wave_suffix_or(on ? sk[64 + lane] : 0ull, lane);   /* lane i: the rank-i record's rest */
+    if (on) sk[128 + lane] = rest;
+    wave_lds_sync();
+    if (on) {   /* dmin: float 6; mask: floats 20-21; rest: 22-23 */
+        const uint64_t rr = sk[128 + rank];
+        q[1].z = it.dmin;
+        q[5].x = __uint_as_float((uint32_t)mask);
+        q[5].y = __uint_as_float((uint32_t)(mask >> 32));
+        q[5].z = __uint_as_float((uint32_t)rr);
+        q[5].w = __uint_as_float((uint32_t)(rr >> 32));
+        float4 *dst = reinterpret_cast<float4 *>(out + rank);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) dst[r] = q[r];
+    }
+    wave_lds_sync();   /* sk is reused by the wave's next cell */
+}
+
+__global__ __launch_bounds__(64 * kSortWaves) void k_bins_sort(
+    const CamCand *__restrict__ tpl, const BinItem *__restrict__ items, int32_t *__restrict__ cnt,
+    const uint64_t *__restrict__ keys, const int32_t *__restrict__ every, const int32_t *__restrict__ nonempty,
+    int cap_shard, BinsHdr *__restrict__ hdr2, int par, CamCand *__restrict__ recs, BinsCaps caps,
+    int32_t *__restrict__ bin_off, int32_t *__restrict__ bin_len, int tx, int ncell, BinsPlan bp) {
+    __shared__ uint64_t sks[kSortWaves][kBinCellCap];
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    uint64_t *sk = sks[wv];
+    const int wave = (int)blockIdx.x * kSortWaves + wv, nwaves = (int)gridDim.x * kSortWaves;
+    BSTAMP4(0);
+    BinsHdr *hdr = hdr2 + par;
+    int32_t *ph = bp.phdr;
+    const int n_every = hdr->n_every.v;
     const bool all = n_every > 0;   /* everywhere hulls: every cell has a list */
-    const int nlist = all ? ncell : hdr->n_nonempty;
-    for (int i = (int)blockIdx.x; i < nlist; i += (int)gridDim.x) {
-        const int c = all ? i : nonempty[i];
-        const int m = cnt[c];
-        const int k = bp.cell_tile ? bp.cell_tile[c] : -2;   /* -1: no tile of this plan reads the cell */
+    int mx = lane < kBinShards ? hdr->ne[lane].v : 0;   /* the longest shard list, over the whole wave */
+    for (int d = 1; d < 64; d <<= 1) mx = max(mx, __shfl_xor(mx, d));
+    const int nslots = __builtin_amdgcn_readfirstlane(all ? ncell : kBinShards * mx);   /* wave-uniform: the
+                                                       loop body holds the wave's shuffles and LDS hand-offs */
+    BSTAMP4(1);
+    for (int i = wave; i < nslots; i += nwaves) {
+        int c = i;
+        if (!all) {   /* slot i: shard i % kBinShards, entry i / kBinShards */
+            const int sh = i % kBinShards, e = i / kBinShards;
+            if (e >= hdr->ne[sh].v) continue;
+            c = nonempty[BCK(sh * cap_shard + e, BDBG(ne_cap), 21)];
+        }
+        c = __builtin_amdgcn_readfirstlane(c);
+        const int sh = c % kBinShards;
+        const int m = cnt[(size_t)BCK(c, BDBG(ncell), 22) * kCntStride];
+        const int k = bp.cell_tile ? bp.cell_tile[BCK(c, BDBG(ncell), 23)] : -2;   /* -1: no tile of this plan reads the cell */
         const int n = n_every > kBinMaxEverywhere ? kBinCellCap + 1 : m + n_every;
+        BSTAMP4(2);
+#ifdef CRT_BINS_STAMPS
+        if (lane == 0 && blockIdx.x < 16384) g_bins_stamps4[6 * blockIdx.x + 5] = (unsigned long long)n;
+#endif
         int start = -1;
         if (k != -1 && n <= kBinCellCap) {
-            if (lane == 0) start = atomicAdd(&hdr->total, n);
+            if (lane == 0) start = atomicAdd(&hdr->rec[sh].v, n);
             start = __shfl(start, 0);
-            if (start > rec_cap - n) start = -1;   /* does not fit: the cell walks the BVH */
+            if (start > caps.cap[sh] - n) start = -1;   /* does not fit: the cell walks the BVH */
         }
         if (start >= 0) {
-            const int cx = c % tx, cy = c / tx;
-            const int32_t *ids = keys + (size_t)c * kBinCellCap;
-            if (n <= 64) bins_emit_small(tpl, items, ids, m, every, n, cx, cy, recs + start, lane);
-            else bins_emit_large(tpl, items, ids, m, every, n, cx, cy, recs + start, sk, lane);
+            const uint64_t *own = keys + (size_t)c * kBinCellCap;
+            CamCand *out = recs + caps.base[BCK(sh, kBinShards, 24)] + start;
+            if (n <= 64) bins_emit64(tpl, items, own, m, every, n, c % tx, c / tx, out, sk, lane);
+            else if (n <= 128) bins_emit<2>(tpl, items, own, m, every, n, c % tx, c / tx, out, sk, lane);
+            else if (n <= 256) bins_emit<4>(tpl, items, own, m, every, n, c % tx, c / tx, out, sk, lane);
+            else bins_emit<kBinCellCap / 64>(tpl, items, own, m, every, n, c % tx, c / tx, out, sk, lane);
         }
+        BSTAMP4(3);
         if (lane == 0) {
             if (k != -1) {
-                bin_off[c] = start >= 0 ? start : 0;
-                bin_len[c] = start >= 0 ? n : -1;
+                bin_off[BCK(c, BDBG(ncell), 26)] = start >= 0 ? caps.base[sh] + start : 0;
+                bin_len[BCK(c, BDBG(ncell), 27)] = start >= 0 ? n : -1;
             }
-            if (k >= 0 && start >= 0) {   /* the plan's priority lists */
+            if (k >= 0 && start >= 0 && ph) {   /* the plan's priority lists */
                 if (n >= bp.split) {
-                    const int s = atomicAdd(&bp.phdr[0], 1);
-                    if (s < bp.e_h) {
-                        bp.prio[s] = k;
-                        bp.taken[k] = 1;
+                    const int s2 = atomicAdd(&ph[bins_phdr_at(par, 0, sh)], 1);
+                    if (s2 < bp.ch) {
+                        bp.prio[BCK(sh * bp.ch + s2, BDBG(prio_cap), 28)] = k;
+                        bp.taken[BCK(k, BDBG(ntaken), 29)] = 1;
                     }
                 } else if (n >= bp.medium) {
-                    const int s = atomicAdd(&bp.phdr[1], 1);
-                    if (s < bp.e_m) {
-                        bp.prio[bp.e_h + s] = k;
-                        bp.taken[k] = 1;
+                    const int s2 = atomicAdd(&ph[bins_phdr_at(par, 1, sh)], 1);
+                    if (s2 < bp.cm) {
+                        bp.prio[BCK(kBinShards * bp.ch + sh * bp.cm + s2, BDBG(prio_cap), 30)] = k;
+                        bp.taken[BCK(k, BDBG(ntaken), 31)] = 1;
                     }
                 }
             }
-            if (m) cnt[c] = 0;   /* next frame's counts start at zero */
+            if (m) cnt[(size_t)BCK(c, BDBG(ncell), 32) * kCntStride] = 0;   /* next frame's counts start at zero */
         }
     }
-    /* the last block resets the frame's counters for the next frame (every block
-     * has read them by the time it arrives here) */
-    if (lane == 0) {
-        __threadfence();
-        if (atomicAdd(&hdr->done, 1) == (int)gridDim.x - 1) {
-            __threadfence();
-            hdr->last_every = hdr->n_every;
-            hdr->last_nonempty = hdr->n_nonempty;
-            hdr->last_total = hdr->total;
-            hdr->n_every = 0;
-            hdr->n_nonempty = 0;
-            hdr->total = 0;
-            hdr->done = 0;
-            __threadfence();
-        }
-    }
+    BSTAMP4(4);
 }
 
 /* empty kernel: its launch at scene creation loads this TU's code object */
@@ -324,16 +555,44 @@ int bins_alloc(crt_hip_scene *sc, T **p, size_t n, bool zero = false) {
     return CRT_OK;
 }
 
-int launch_project(crt_hip_scene *sc, hipStream_t s, int32_t *taken, int ntaken, int32_t *phdr) {
+int launch_project(crt_hip_scene *sc, hipStream_t s, int par, int32_t *taken, int ntaken, int32_t *phdr) {
     BinsDev &b = sc->bins;
-    const unsigned blocks = (unsigned)((b.nt + kProjTris - 1) / kProjTris);
-    hipLaunchKernelGGL(k_bins_project, dim3(blocks), dim3(256), 0, s, b.tpl, b.nt, b.cam, b.items, b.cnt, b.keys,
-                       b.every, b.nonempty, b.hdr, b.len, b.ncell, taken, ntaken, phdr);
+    const int groups = (b.nt + kProjTris - 1) / kProjTris;
+    hipLaunchKernelGGL(k_bins_project, dim3((unsigned)groups), dim3(256), 0, s, b.tpl, b.nt, b.cam, b.items, b.tpref,
+                       b.gsum, b.every, b.hdr, par, b.len, b.ncell, taken, ntaken, phdr);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_bins_pairs, dim3((unsigned)b.pair_blocks), dim3(256), 0, s, b.items, b.tpref, b.gsum, groups,
+                       b.nt, b.tx, b.cnt, b.keys, b.nonempty, b.cap_shard, b.hdr, par);
     HIP_TRY(hipGetLastError());
     return CRT_OK;
 }
 
 }  // namespace
+
+/* diagnostic builds (CRT_BINS_CHECK): report a violation of the last frame
+ * and arm the checks with this frame's buffer sizes */
+int bins_dbg_arm(crt_hip_scene *sc, const ShardPlan &plan) {
+#ifdef CRT_BINS_CHECK
+    BinsDev &b = sc->bins;
+    BinsDbg d{};
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(&d, HIP_SYMBOL(g_bins_dbg), sizeof d));
+    if (d.code)
+        return set_error(CRT_E_STATE, "bins check: code " + std::to_string(d.code) + " index " + std::to_string(d.idx) +
+                                          " bound " + std::to_string(d.bound));
+    d.nt = b.nt;
+    d.ncell = b.ncell;
+    d.ne_cap = kBinShards * b.cap_shard;
+    d.rec_cap = b.rec_cap;
+    d.ntaken = plan.bp.taken ? plan.bp.nbase : 0;
+    d.prio_cap = kBinShards * (plan.bp.ch + plan.bp.cm);
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_bins_dbg), &d, sizeof d));
+#else
+    (void)sc;
+    (void)plan;
+#endif
+    return CRT_OK;
+}
 
 /* Scene create: the per-triangle templates and the buffers, sized by one
  * projection pass of this camera (its counts are read back; the lists are
@@ -348,48 +607,73 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
     b.nt = (int)hs.tri_attr.size();
     b.tx = cam.tx;
     b.ncell = cam.tx * cam.ty;
+    b.cap_shard = (b.ncell + kBinShards - 1) / kBinShards;
     std::vector<CamCand> tpl;
     bin_templates(hs, tpl);
     int rc;
     if ((rc = bins_alloc(sc, &b.tpl, tpl.size())) != CRT_OK) return rc;
     HIP_TRY(hipMemcpy(b.tpl, tpl.data(), tpl.size() * sizeof(CamCand), hipMemcpyHostToDevice));
     if ((rc = bins_alloc(sc, &b.items, (size_t)b.nt)) != CRT_OK) return rc;
-    if ((rc = bins_alloc(sc, &b.cnt, (size_t)b.ncell, true)) != CRT_OK) return rc;
-    if ((rc = bins_alloc(sc, &b.keys, (size_t)b.ncell * kBinCellCap)) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.tpref, (size_t)((b.nt + kProjTris - 1) / kProjTris) * kProjTris)) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.gsum, (size_t)((b.nt + kProjTris - 1) / kProjTris))) != CRT_OK) return rc;
+    if ((b.nt + kProjTris - 1) / kProjTris > kMaxGroups) {   /* beyond the BVH's triangle limit: no bins */
+        bins_free(sc);
+        return CRT_OK;
+    }
+    b.pair_blocks = 256;   /* the sizing pass's grid; resized from its pair count below */
+    if ((rc = bins_alloc(sc, &b.cnt, (size_t)b.ncell * kCntStride, true)) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.keys, (size_t)b.ncell * kBinCellCap)) != CRT_OK) return rc;   /* 64-bit keys */
     if ((rc = bins_alloc(sc, &b.every, (size_t)kBinMaxEverywhere)) != CRT_OK) return rc;
-    if ((rc = bins_alloc(sc, &b.nonempty, (size_t)b.ncell)) != CRT_OK) return rc;
-    if ((rc = bins_alloc(sc, &b.hdr, 1, true)) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.nonempty, (size_t)kBinShards * b.cap_shard)) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.hdr, 2, true)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.off, (size_t)b.ncell, true)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.len, (size_t)b.ncell, true)) != CRT_OK) return rc;
     /* sizing pass: counts per cell of this camera */
-    if ((rc = launch_project(sc, sc->stream, nullptr, 0, nullptr)) != CRT_OK) return rc;
-    std::vector<int32_t> cnt((size_t)b.ncell);
+    if ((rc = bins_dbg_arm(sc, ShardPlan{})) != CRT_OK) return rc;
+    if ((rc = launch_project(sc, sc->stream, 0, nullptr, 0, nullptr)) != CRT_OK) return rc;
+    std::vector<int32_t> cnt((size_t)b.ncell * kCntStride);
     BinsHdr h;
     HIP_TRY(hipMemcpyAsync(cnt.data(), b.cnt, cnt.size() * sizeof(int32_t), hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipMemcpyAsync(&h, b.hdr, sizeof h, hipMemcpyDeviceToHost, sc->stream));
+    const int n_every = h.n_every.v;
     HIP_TRY(hipStreamSynchronize(sc->stream));
     HIP_TRY(hipMemsetAsync(b.cnt, 0, cnt.size() * sizeof(int32_t), sc->stream));
-    HIP_TRY(hipMemsetAsync(b.hdr, 0, sizeof(BinsHdr), sc->stream));
+    HIP_TRY(hipMemsetAsync(b.hdr, 0, 2 * sizeof(BinsHdr), sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
+    b.frame = 0;
     b.count.assign((size_t)b.ncell, 0);
-    int64_t total = 0, listed = 0;
+    int64_t pairs = 0;
+    for (int c = 0; c < b.ncell; ++c) pairs += cnt[(size_t)c * kCntStride];
+    b.pair_blocks = (int)std::max<int64_t>(32, std::min<int64_t>(2048, (pairs + 511) / 512));   /* ~2 pairs a thread */
+    int64_t total = 0, shard_rec[kBinShards] = {0}, shard_listed[kBinShards] = {0};
     for (int c = 0; c < b.ncell; ++c) {
-        const int64_t n = (int64_t)cnt[(size_t)c] + h.n_every;
-        if (n > kBinCellCap || h.n_every > kBinMaxEverywhere) {
+        const int64_t n = (int64_t)cnt[(size_t)c * kCntStride] + n_every;
+        if (n > kBinCellCap || n_every > kBinMaxEverywhere) {
             b.count[(size_t)c] = -1;
         } else {
             b.count[(size_t)c] = (int32_t)n;
             total += n;
+            shard_rec[c % kBinShards] += n;
         }
-        listed += n > 0;
+        shard_listed[c % kBinShards] += n > 0;
     }
-    if (h.n_every > kBinMaxEverywhere || total > kBinMeanCap * b.ncell || total >= INT32_MAX / 2) {
+    if (n_every > kBinMaxEverywhere || total > kBinMeanCap * b.ncell || total >= INT32_MAX / 4) {
         bins_free(sc);   /* the scene walks the BVH */
         return CRT_OK;
     }
-    b.rec_cap = (int32_t)std::min<int64_t>(INT32_MAX / 2, total + total / 8 + 1024);
+    /* each shard's records in a region of its own, sized from the pass with slack */
+    int64_t base = 0, most = 0;
+    for (int s2 = 0; s2 < kBinShards; ++s2) {
+        const int64_t cap = shard_rec[s2] + shard_rec[s2] / 8 + 256;
+        b.caps.base[s2] = (int32_t)base;
+        b.caps.cap[s2] = (int32_t)cap;
+        base += cap;
+        most = std::max(most, shard_listed[s2]);
+    }
+    b.rec_cap = (int32_t)base;
     if ((rc = bins_alloc(sc, &b.recs, (size_t)b.rec_cap)) != CRT_OK) return rc;
-    b.sort_blocks = (int)std::max<int64_t>(64, std::min<int64_t>(16384, h.n_every > 0 ? b.ncell : listed));
+    /* one wave per listed cell (every cell when some hull is everywhere) */
+    b.sort_blocks = (int)std::max<int64_t>(64, std::min<int64_t>(16384, n_every > 0 ? b.ncell : kBinShards * most));
     b.records = total;
     b.setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     sc->ds.bins = b.recs;
@@ -400,8 +684,8 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
 }
 
 /* A plan's camera-bins dispatch (BinsPlan): the base tiles stay in plan order;
- * the render grid puts 4 x e_h heavy-split waves and e_m medium waves before
- * them.  Capacities from the sizing pass's counts, with slack. */
+ * the render grid puts the heavy-split and the medium waves before them, per
+ * shard ch / cm slots.  Capacities from the sizing pass's counts, with slack. */
 int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
     BinsDev &b = sc->bins;
     const int nb = plan.ntiles;
@@ -412,22 +696,25 @@ int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
         int32_t &e = cell_tile[(size_t)(t.y >> 3) * b.tx + (t.x >> 3)];
         e = e == -1 ? k : -2;   /* several tiles in one cell: none of them split */
     }
-    int heavy = 0, medium = 0;
+    int heavy[kBinShards] = {0}, medium[kBinShards] = {0};
     for (int c = 0; c < b.ncell; ++c) {
         if (cell_tile[(size_t)c] < 0) continue;
         const int n = b.count[(size_t)c];
-        if (n >= sc->bins_split) ++heavy;
-        else if (n >= kBinsMedium) ++medium;
+        if (n >= sc->bins_split) ++heavy[c % kBinShards];
+        else if (n >= kBinsMedium) ++medium[c % kBinShards];
     }
     BinsPlan &bp = plan.bp;
-    bp.e_h = heavy + heavy / 4 + 8;
-    bp.e_m = medium + medium / 4 + 16;
+    const int mh = *std::max_element(heavy, heavy + kBinShards), mm = *std::max_element(medium, medium + kBinShards);
+    bp.ch = mh + mh / 4 + (mh > 0 ? 1 : 0);
+    bp.cm = mm + mm / 4 + (mm > 0 ? 1 : 0);
     bp.split = sc->bins_split;
     bp.medium = kBinsMedium;
     bp.quad = sc->bins_quad;
     bp.nbase = nb;
+    bp.par = 0;
     std::vector<void *> ps(4, nullptr);
-    const size_t sizes[4] = {(size_t)b.ncell, (size_t)std::max(1, nb), (size_t)(bp.e_h + bp.e_m), 2};
+    const size_t sizes[4] = {(size_t)b.ncell, (size_t)std::max(1, nb),
+                             (size_t)std::max(1, kBinShards * (bp.ch + bp.cm)), (size_t)kBinsPhdrInts};
     for (int i = 0; i < 4; ++i) {
         HIP_TRY(hipMalloc(&ps[(size_t)i], sizes[i] * sizeof(int32_t)));
         sc->plan_allocs.push_back(ps[(size_t)i]);
@@ -438,18 +725,52 @@ int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
     bp.taken = static_cast<int32_t *>(ps[1]);
     bp.prio = static_cast<int32_t *>(ps[2]);
     bp.phdr = static_cast<int32_t *>(ps[3]);
-    plan.waves = 4 * bp.e_h + bp.e_m + nb;
+    plan.waves = 4 * kBinShards * bp.ch + kBinShards * bp.cm + nb;
     return CRT_OK;
 }
 
-/* The frame's lists, on `s`, before its render kernel. */
-int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s) {
+/* The frame's lists, on `s`, before its render kernel; returns the frame's
+ * parity (the render reads that set of the plan's counters). */
+int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *par_out) {
     BinsDev &b = sc->bins;
-    int rc = launch_project(sc, s, plan.bp.taken, plan.bp.taken ? plan.bp.nbase : 0, plan.bp.phdr);
+    const int par = (int)(b.frame++ & 1);
+    {
+        const int rc0 = bins_dbg_arm(sc, plan);
+        if (rc0 != CRT_OK) return rc0;
+    }
+    int rc = launch_project(sc, s, par, plan.bp.taken, plan.bp.taken ? plan.bp.nbase : 0, plan.bp.phdr);
     if (rc != CRT_OK) return rc;
-    hipLaunchKernelGGL(k_bins_sort, dim3((unsigned)b.sort_blocks), dim3(64), 0, s, b.tpl, b.items, b.cnt, b.keys,
-                       b.every, b.nonempty, b.hdr, b.recs, b.rec_cap, b.off, b.len, b.tx, b.ncell, plan.bp);
+    BinsPlan bp = plan.bp;
+    bp.par = par;
+    hipLaunchKernelGGL(k_bins_sort, dim3((unsigned)((b.sort_blocks + kSortWaves - 1) / kSortWaves)), dim3(64 * kSortWaves), 0, s, b.tpl, b.items, b.cnt, b.keys,
+                       b.every, b.nonempty, b.cap_shard, b.hdr, par, b.recs, b.caps, b.off, b.len, b.tx, b.ncell, bp);
     HIP_TRY(hipGetLastError());
+    if (par_out) *par_out = par;
+#ifdef CRT_BINS_STAMPS
+    if (const char *fn = std::getenv("CRT_BINS_STAMPS_FILE")) {
+        static int dumped = 0;
+        if (++dumped == 20) {   /* one warm frame */
+            HIP_TRY(hipStreamSynchronize(s));
+            const int nb = (b.nt + kProjTris - 1) / kProjTris;
+            std::vector<unsigned long long> st((size_t)nb * 4);
+            HIP_TRY(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_bins_stamps), st.size() * sizeof(unsigned long long)));
+            if (FILE *f = std::fopen(fn, "w")) {
+                for (int i = 0; i < nb; ++i)
+                    std::fprintf(f, "%llu %llu %llu %llu\n", st[4 * i], st[4 * i + 1], st[4 * i + 2], st[4 * i + 3]);
+                std::fclose(f);
+            }
+            const int ns = std::min((b.sort_blocks + kSortWaves - 1) / kSortWaves, 16384);
+            std::vector<unsigned long long> s4((size_t)ns * 6);
+            HIP_TRY(hipMemcpyFromSymbol(s4.data(), HIP_SYMBOL(g_bins_stamps4), s4.size() * sizeof(unsigned long long)));
+            if (FILE *f = std::fopen((std::string(fn) + ".sort").c_str(), "w")) {
+                for (int i = 0; i < ns; ++i)
+                    std::fprintf(f, "%llu %llu %llu %llu %llu %llu\n", s4[6 * i], s4[6 * i + 1], s4[6 * i + 2],
+                                 s4[6 * i + 3], s4[6 * i + 4], s4[6 * i + 5]);
+                std::fclose(f);
+            }
+        }
+    }
+#endif
     return CRT_OK;
 }
 
@@ -468,10 +789,11 @@ int64_t crt_hip_camera_bins(crt_hip_scene *sc, int32_t *len_out, void *recs_out,
     }
     HIP_TRY(hipStreamSynchronize(sc->stream));
     ShardPlan none;   /* no tile plan: every cell's list */
-    int rc = bins_enqueue(sc, none, sc->stream);
+    int rc = bins_enqueue(sc, none, sc->stream, nullptr);
     if (rc != CRT_OK) return rc;
+    if ((rc = bins_dbg_arm(sc, none)) != CRT_OK) return rc;   /* diagnostic builds: this frame's violations */
     std::vector<int32_t> off((size_t)b.ncell), len((size_t)b.ncell);
-    std::vector<CamCand> recs((size_t)b.rec_cap);
+    std::vector<CamCand> recs((size_t)b.rec_cap);   /* every shard's region */
     HIP_TRY(hipMemcpyAsync(off.data(), b.off, off.size() * sizeof(int32_t), hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipMemcpyAsync(len.data(), b.len, len.size() * sizeof(int32_t), hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipMemcpyAsync(recs.data(), b.recs, recs.size() * sizeof(CamCand), hipMemcpyDeviceToHost, sc->stream));
@@ -485,6 +807,30 @@ int64_t crt_hip_camera_bins(crt_hip_scene *sc, int32_t *len_out, void *recs_out,
     for (int c = 0; c < b.ncell; ++c)
         for (int j = 0; j < len[(size_t)c]; ++j) *o++ = recs[(size_t)off[(size_t)c] + j];
     return total;
+}
+
+int crt_hip_bins_time(crt_hip_scene *sc, int32_t frames, double *ms) {
+    if (!sc || !ms || frames < 1) return set_error(CRT_E_INVALID, "bad argument");
+    HIP_TRY(hipSetDevice(sc->device));
+    *ms = 0.0;
+    if (!sc->ds.bins || !sc->full.bp.cell_tile) return CRT_OK;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    int rc = CRT_OK;
+    for (int w = 0; w < 3 && rc == CRT_OK; ++w) rc = bins_enqueue(sc, sc->full, sc->stream, nullptr);   /* warm */
+    hipError_t e = rc == CRT_OK ? hipEventRecord(e0, sc->stream) : hipSuccess;
+    for (int f = 0; f < frames && rc == CRT_OK && e == hipSuccess; ++f) rc = bins_enqueue(sc, sc->full, sc->stream, nullptr);
+    if (rc == CRT_OK && e == hipSuccess) e = hipEventRecord(e1, sc->stream);
+    if (rc == CRT_OK && e == hipSuccess) e = hipEventSynchronize(e1);
+    float f = 0.f;
+    if (rc == CRT_OK && e == hipSuccess) e = hipEventElapsedTime(&f, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc != CRT_OK) return rc;
+    if (e != hipSuccess) return set_error(CRT_E_HIP, hipGetErrorString(e));
+    *ms = (double)f / frames;
+    return CRT_OK;
 }
 
 int64_t crt_host_camera_bins(const crt_host_scene *h, int32_t *len_out, void *recs_out, int64_t cap) {

@@ -395,6 +395,14 @@ int check_settings(const crt_renderer_settings *st) {
     return CRT_OK;
 }
 
+/* Frames with reflective / refractive recursion and no GI taken by the GI
+ * kernel's per-lane state machine (k_render_gi; option "rec_machine"): needs
+ * the BVH and the pixel-refill head, at most 63 levels. */
+bool rec_machine_on(const crt_hip_scene *sc, const crt_renderer_settings *st) {
+    return sc->rec_machine && sc->ds.bnodes && sc->d_next_px && sc->secondary != 4 && sc->secondary != 10 &&
+           st->max_ray_depth <= 63 && (int64_t)sc->info.width * sc->info.height < INT32_MAX;
+}
+
 /* The packet walk camera rays take: walk 8 becomes its fast-only build 12
  * when the host has proven every camera ray fast. */
 int camera_walk(const crt_hip_scene *sc, int trav) {
@@ -409,6 +417,7 @@ int plan_walk(const crt_hip_scene *sc, const crt_renderer_settings *st) {
     const bool full = gi || sc->has_secondary;
     if (gi) return -1;
     if (bins_active(sc)) return -1;   /* camera bins: no plan to measure */
+    if (full && rec_machine_on(sc, st)) return -1;   /* per-lane state machine: pixels pulled in order */
     if (full) return sc->wavefront ? camera_walk(sc, sc->traversal == 8 ? 8 : 7) : -1;
     return camera_walk(sc, sc->traversal);
 }
@@ -830,7 +839,9 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         HIP_TRY(hipGetLastError());
         return CRT_OK;
     }
-    if (full && !gi && sc->wavefront && !stamps)
+    /* recursion without GI (C3): the per-lane state machine (rec_machine), or level by level (wavefront) */
+    const bool rec_machine = full && !gi && rec_machine_on(sc, st) && !stamps;
+    if (full && !gi && sc->wavefront && !stamps && !rec_machine)
         return render_wavefront(sc, ds, st, plan, d_out, stream, count, d_scene, sec, camera_walk(sc, sc->traversal));
     /* frame-stack kernel: one walk for every ray */
     int trav = full ? sec : camera_walk(sc, sc->traversal);
@@ -855,12 +866,15 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         case 14:
             if (bins_active(sc) && plan.bp.cell_tile) {
                 /* this frame's camera bins, then the render over the bins plan's grid */
-                const int rc = bins_enqueue(sc, plan, stream);
+                int par = 0;
+                const int rc = bins_enqueue(sc, plan, stream, &par);
                 if (rc != CRT_OK) return rc;
+                BinsPlan bp = plan.bp;
+                bp.par = par;
                 const unsigned bb = (unsigned)((plan.waves + 3) / 4);
 #define CRT_LAUNCH_B(COUNT)                                                                                 \
     hipLaunchKernelGGL((k_render_tiles<false, 0, 15, 15, COUNT>), dim3(bb), dim3(256), 0, stream, d_scene, ds, \
-                       plan.d_tiles, plan.waves, d_out, cnt, stamps, plan.bp)
+                       plan.d_tiles, plan.waves, d_out, cnt, stamps, bp)
                 if (count) CRT_LAUNCH_B(true); else CRT_LAUNCH_B(false);
 #undef CRT_LAUNCH_B
             } else {
@@ -869,7 +883,8 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
             break;
         default: return set_error(CRT_E_INVALID, "no such camera walk");
         }
-    } else if (gi && (trav == 4 || trav == 10 || trav == 14) && sc->gi_refill && sc->d_next_px && !stamps && frames <= 64) {
+    } else if (rec_machine || (gi && (trav == 4 || trav == 10 || trav == 14) && sc->gi_refill && sc->d_next_px && !stamps &&
+                               frames <= 64)) {
         /* GI: persistent waves with pixel refill (k_render_refill) */
         HIP_TRY(hipMemsetAsync(sc->d_next_px, 0, sizeof(int32_t), stream));
         const int nw = std::max(1, std::min(plan.ntiles, sc->refill_waves));
@@ -878,8 +893,8 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     hipLaunchKernelGGL((k_render_refill<MAXF, T, COUNT>), dim3(rb), dim3(256), 0, stream, d_scene, ds,       \
                        plan.d_tiles, plan.ntiles, d_out, sc->d_next_px, cnt)
 #define CRT_REFILL(MAXF, COUNT) CRT_REFILL_T(MAXF, 4, COUNT)
-        if (trav == 14 && sc->gi_machine && (uint64_t)st->diffuse_reflection_ray_count < (1ull << 29) &&
-            (int64_t)sc->info.width * sc->info.height < INT32_MAX) {
+        if (rec_machine || (trav == 14 && sc->gi_machine && (uint64_t)st->diffuse_reflection_ray_count < (1ull << 29) &&
+                            (int64_t)sc->info.width * sc->info.height < INT32_MAX)) {
             /* per-lane state machine over the BVH walk (crt_gi_machine.h) */
             const unsigned gb = (unsigned)std::max(1, std::min((plan.ntiles + 3) / 4, sc->gi_blocks));
             /* frames below the two LDS ones and the register one: 64 B per lane and depth */

@@ -21,23 +21,49 @@ struct alignas(16) Tile {
                                 * bit 1: camera-bins split tile, four lanes per pixel */
 };
 
+/* Counters of the device binning are sharded by cell (cell % kBinShards): a
+ * device-scope atomic on one word serialises at ~88 per microsecond. */
+constexpr int kBinShards = 16;
+
 /* Camera-bins dispatch of a tile plan (crt_bins.hip): the render grid's first
- * 4 e_h waves take the cells k_bins_sort queued as heavy (four 4x4 waves
- * each), the next e_m the medium ones (one 8x8 wave each), the rest the
- * plan's base tiles in plan order, skipping the ones a priority wave took. */
+ * 4 x kBinShards x ch waves take the cells k_bins_sort queued as heavy (four
+ * 4x4 waves each; slot i of shard s at 4 (i kBinShards + s)), the next
+ * kBinShards x cm the medium ones (one 8x8 wave each), the rest the plan's
+ * base tiles in plan order, skipping the ones a priority wave took. */
 struct BinsPlan {
     int32_t *cell_tile;   /* per cell: the plan's one tile inside it; -1 none (the cell is not rendered), -2 several */
     int32_t *taken;       /* per base tile: rendered by a priority wave this frame */
-    int32_t *prio;        /* e_h heavy, then e_m medium base-tile indices */
-    int32_t *phdr;        /* [0] heavy, [1] medium cells queued this frame */
-    int32_t e_h, e_m, nbase;
+    int32_t *prio;        /* base-tile indices: heavy kBinShards x ch, then medium kBinShards x cm */
+    int32_t *phdr;        /* cells queued this frame: counter bins_phdr_at(parity, heavy 0 / medium 1, shard) */
+    int32_t ch, cm, nbase;
     int32_t split, medium, quad;
+    int32_t par;          /* the frame's parity (which counters it uses) */
 };
 
-/* Per-frame counters of the device binning (crt_bins.hip). */
+/* Per-frame counters of the device binning (crt_bins.hip), two sets used by
+ * alternate frames: a frame's first kernel zeroes the other set for the next.
+ * Every counter has a 256-B line of its own (atomics on one line serialise,
+ * whatever word they name). */
+constexpr int kBinPad = 64;   /* int32 per counter */
+struct alignas(256) BinsCtr {
+    int32_t v;
+    int32_t pad[kBinPad - 1];
+};
 struct BinsHdr {
-    int32_t n_every, n_nonempty, total, done;
-    int32_t last_every, last_nonempty, last_total, pad;
+    BinsCtr n_every;
+    BinsCtr ne[kBinShards];    /* non-empty cells listed per shard */
+    BinsCtr rec[kBinShards];   /* records reserved per shard */
+};
+/* a plan's priority-list counters (BinsPlan::phdr): kind 0 heavy, 1 medium */
+__host__ __device__ constexpr int bins_phdr_at(int par, int kind, int sh) {
+    return ((par * 2 + kind) * kBinShards + sh) * kBinPad;
+}
+constexpr int kBinsPhdrInts = 4 * kBinShards * kBinPad;
+
+/* Where each shard's records go in the camera-bins record buffer. */
+struct BinsCaps {
+    int32_t base[kBinShards];
+    int32_t cap[kBinShards];
 };
 
 struct alignas(16) UnpackBucket {

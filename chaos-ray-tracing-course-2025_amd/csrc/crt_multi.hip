@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -109,6 +110,37 @@ int tree_mode(const crt_scene_desc *desc, int flags) {
         mode = nt >= CRT_SCENE_DEVICE_BUILD_MIN ? CRT_SCENE_TREE_DEVICE : CRT_SCENE_TREE_HOST;
     }
     return mode;
+}
+
+/* Estimated single-GPU frame (ms) of a scene, from what bounds it on one
+ * MI355X (build f9abbdcba9f8bfe1 / round 4 frames): camera rays of
+ * a frame without recursion ~0.05 ns each (C2: 2.07 M rays in ~0.1 ms),
+ * scattered rays (GI fan-out, reflect / refract chains) ~0.3 ns (C4: 345 M in
+ * 87 ms, C3: 3.2 M in 1.7 ms), both growing with the mesh once it leaves the
+ * caches (C5: 1 M triangles, 0.5 ns per camera ray). */
+double est_frame_ms(int64_t px, int64_t tris, bool gi, bool secondary, const crt_renderer_settings *st) {
+    double rays = 1.0;
+    if (gi && st->diffuse_reflection_ray_count > 0) {   /* the GI tree: sum of count^d over the traced depths */
+        double level = 1.0;
+        for (uint32_t d = 1; d <= std::min<uint32_t>(st->max_ray_depth, 8); ++d) {
+            level *= (double)st->diffuse_reflection_ray_count;
+            rays += level;
+        }
+    } else if (secondary) {
+        rays = 1.6;
+    }
+    const double ns = ((gi || secondary) ? 0.30 : 0.05) * (1.0 + (double)tris / 1e5);
+    return (double)px * rays * ns * 1e-6;
+}
+
+/* GPUs a frame is spread over when the caller leaves the choice: one unless
+ * the estimated frame is >= 2 ms (a shard then saves more than the copies and
+ * the unpack cost), else about one per 0.6 ms of it, at most `visible`.
+ * C2 / C3 stay on one GPU (8 shards: 1.04x / 1.12x), C4 / C5 spread (6.1x /
+ * 7.5x). */
+int auto_gpus(double est_ms, int visible) {
+    if (visible <= 1 || est_ms < 2.0) return 1;
+    return (int)std::max(1.0, std::min((double)visible, std::ceil(est_ms / 0.6)));
 }
 
 /* The replicas follow replica 0's measured plan (tuned once, there) and its
@@ -246,6 +278,52 @@ int crt_hip_scene_create_on(const crt_scene_desc *desc, const int32_t *devices, 
     if ((rc = upload_on(*hs, devices, count, out)) != CRT_OK) return rc;
     (*out)->info.create_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return CRT_OK;
+}
+
+int crt_auto_gpus(const crt_scene_desc *desc, const crt_renderer_settings *st, int visible) {
+    if (!desc || !st) return set_error(CRT_E_INVALID, "null argument");
+    if (const char *e = std::getenv("CRT_HIP_GPUS")) return std::max(1, std::min(visible, std::atoi(e)));
+    int64_t tris = 0;
+    for (int i = 0; i < desc->mesh_count && desc->meshes; ++i) tris += desc->meshes[i].index_count / 3;
+    bool diffuse = false, secondary = false;
+    for (int i = 0; i < desc->material_count && desc->materials; ++i) {
+        const int t = desc->materials[i].type;
+        diffuse = diffuse || t == CRT_MATERIAL_DIFFUSE;
+        secondary = secondary || t == CRT_MATERIAL_REFLECTIVE || t == CRT_MATERIAL_REFRACTIVE;
+    }
+    const int64_t px = (int64_t)std::max(0, desc->camera.width) * std::max(0, desc->camera.height);
+    return auto_gpus(est_frame_ms(px, tris, desc->gi_on && diffuse, secondary, st), visible);
+}
+
+int crt_auto_gpus_tree(const crt_tree_scene_desc *desc, const crt_renderer_settings *st, int visible) {
+    if (!desc || !st) return set_error(CRT_E_INVALID, "null argument");
+    if (const char *e = std::getenv("CRT_HIP_GPUS")) return std::max(1, std::min(visible, std::atoi(e)));
+    /* unique triangles ~ leaf copies / 4 (the reference tree duplicates straddling triangles) */
+    const int64_t copies = desc->leaf_offsets && desc->node_count > 0 ? desc->leaf_offsets[desc->node_count] : 0;
+    bool diffuse = false, secondary = false;
+    for (int i = 0; i < desc->material_count && desc->materials; ++i) {
+        const int t = desc->materials[i].type;
+        diffuse = diffuse || t == CRT_MATERIAL_DIFFUSE;
+        secondary = secondary || t == CRT_MATERIAL_REFLECTIVE || t == CRT_MATERIAL_REFRACTIVE;
+    }
+    const int64_t px = (int64_t)std::max(0, desc->width) * std::max(0, desc->height);
+    return auto_gpus(est_frame_ms(px, copies / 4, desc->gi_on && diffuse, secondary, st), visible);
+}
+
+static uint64_t first_n(int n) { return n >= 64 ? ~0ull : (1ull << n) - 1ull; }
+
+int crt_hip_scene_create_auto(const crt_scene_desc *desc, const crt_renderer_settings *st, int flags,
+                              crt_hip_scene **out) {
+    const int n = crt_auto_gpus(desc, st, std::max(1, crt_hip_device_count()));
+    if (n < 0) return n;
+    return crt_hip_scene_create_mask(desc, first_n(n), flags, out);
+}
+
+int crt_hip_scene_from_tree_auto(const crt_tree_scene_desc *desc, const crt_renderer_settings *st,
+                                 crt_hip_scene **out) {
+    const int n = crt_auto_gpus_tree(desc, st, std::max(1, crt_hip_device_count()));
+    if (n < 0) return n;
+    return crt_hip_scene_from_tree_mask(desc, first_n(n), out);
 }
 
 int crt_hip_scene_create_mask(const crt_scene_desc *desc, uint64_t gpu_mask, int flags, crt_hip_scene **out) {

@@ -16,19 +16,19 @@ namespace crt_amd {
  * BinsPlan): a quarter of a heavy cell, a medium cell, or the next base tile
  * no priority wave took.  false: nothing to do (an unused priority slot). */
 __device__ __forceinline__ bool bins_tile(const BinsPlan &bp, const Tile *__restrict__ tiles, int wave, Tile &tl) {
-    const int ph = 4 * bp.e_h, pm = ph + bp.e_m;
+    const int nh = 4 * kBinShards * bp.ch, nm = kBinShards * bp.cm;
     int k, q = -1;
-    if (wave < ph) {
-        const int s = wave >> 2;
-        if (s >= min(load_scalar(bp.phdr, 0), bp.e_h)) return false;
-        k = load_scalar(bp.prio, s);
+    if (wave < nh) {
+        const int slot = wave >> 2, sh = slot % kBinShards, i = slot / kBinShards;
+        if (i >= min(load_scalar(bp.phdr, bins_phdr_at(bp.par, 0, sh)), bp.ch)) return false;
+        k = load_scalar(bp.prio, sh * bp.ch + i);
         q = wave & 3;
-    } else if (wave < pm) {
-        const int s = wave - ph;
-        if (s >= min(load_scalar(bp.phdr, 1), bp.e_m)) return false;
-        k = load_scalar(bp.prio, bp.e_h + s);
+    } else if (wave < nh + nm) {
+        const int slot = wave - nh, sh = slot % kBinShards, i = slot / kBinShards;
+        if (i >= min(load_scalar(bp.phdr, bins_phdr_at(bp.par, 1, sh)), bp.cm)) return false;
+        k = load_scalar(bp.prio, kBinShards * bp.ch + sh * bp.cm + i);
     } else {
-        k = wave - pm;
+        k = wave - nh - nm;
         if (k >= bp.nbase || load_scalar(bp.taken, k) != 0) return false;
     }
     tl = tiles[k];

@@ -46,16 +46,22 @@ struct BinsDev {
     int nt = 0, tx = 0, ncell = 0;
     crt_amd::CamCand *tpl = nullptr;      /* per triangle: the records' static part */
     crt_amd::BinItem *items = nullptr;    /* per triangle: this frame's projection */
+    int32_t *tpref = nullptr;             /* per triangle: pair prefix inside its group of k_bins_project */
+    int32_t *gsum = nullptr;              /* per group: pairs */
+    int pair_blocks = 0;                  /* k_bins_pairs grid */
     int32_t *cnt = nullptr;               /* per cell: candidates (zero between frames) */
-    int32_t *keys = nullptr;              /* per cell: kBinCellCap triangle ids */
+    uint64_t *keys = nullptr;             /* per cell: kBinCellCap sort keys (dmin bits << 32 | triangle id) */
     int32_t *every = nullptr;             /* everywhere triangles */
-    int32_t *nonempty = nullptr;          /* cells with a candidate, in arrival order */
-    crt_amd::BinsHdr *hdr = nullptr;
+    int32_t *nonempty = nullptr;          /* cells with a candidate: kBinShards lists of cap_shard, arrival order */
+    int cap_shard = 0;
+    crt_amd::BinsHdr *hdr = nullptr;      /* two sets: frames alternate */
+    uint64_t frame = 0;                   /* frames binned (parity = frame & 1) */
+    crt_amd::BinsCaps caps{};             /* per shard: its region of recs */
     crt_amd::CamCand *recs = nullptr;     /* the lists */
     int32_t rec_cap = 0;
     int32_t *off = nullptr, *len = nullptr;   /* per cell */
     std::vector<int32_t> count;           /* per cell: list length of the sizing pass (-1 over the cap) */
-    int sort_blocks = 0;
+    int sort_blocks = 0;                  /* k_bins_sort waves */
     int64_t records = 0;                  /* records of the sizing pass */
     double setup_ms = 0.0;
     std::vector<void *> allocs;
@@ -142,6 +148,7 @@ struct crt_hip_scene {
     int32_t *d_next_px = nullptr;      /* pixel-refill list head (k_render_refill) */
     int gi_refill = 1;                 /* GI frames: persistent waves with pixel refill (env CRT_GI_REFILL, option "gi_refill") */
     int gi_machine = 1;                /* ... as per-lane state machines (k_render_gi; option "gi_machine") */
+    int rec_machine = 0;               /* recursion without GI through the same state machine (option "rec_machine") */
     int gi_blocks = 1024;              /* blocks of the k_render_gi grid (resident blocks per CU x CUs) */
     void *gi_frames = nullptr;         /* k_render_gi: frames below the LDS ones (grown on demand) */
     int64_t gi_frames_bytes = 0;
@@ -222,6 +229,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
                   hipStream_t stream, bool count, unsigned long long *stamps = nullptr);
 int render_into(crt_hip_scene *sc, const crt_renderer_settings *st, float *d_rgb, hipStream_t stream, bool count);
 bool camera_rays_fast(const HostScene &hs, bool planes_ok);
+bool rec_machine_on(const crt_hip_scene *sc, const crt_renderer_settings *st);
 int ensure_live_mask(crt_hip_scene *sc);
 std::vector<DBucket> compact_tiles(crt_hip_scene *sc, int shard, int shard_count, int64_t *px,
                                    std::vector<DBucket> *dead = nullptr);
@@ -234,7 +242,7 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
 /* crt_bins.hip: camera bins built on the device by every camera frame */
 int bins_setup(crt_hip_scene *sc, const HostScene &hs);
 int bins_plan(crt_hip_scene *sc, ShardPlan &plan);
-int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s);
+int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *par_out);
 void bins_free(crt_hip_scene *sc);
 /* crt_multi.hip: the frame over every replica of a multi-GPU scene into d_rgb
  * (on the scene's device) on `stream`; *overflow: some replica's recorded

@@ -126,7 +126,7 @@ static PyObject *render_scene_from_dict(PyObject *, PyObject *args) {
             crt_hip_scene_destroy(g_scene);
             g_scene = nullptr;
             g_scene_key.clear();
-            rc = crt_hip_scene_create_mask(desc, 0, CRT_SCENE_TREE_AUTO, &g_scene);   /* every visible GPU */
+            rc = crt_hip_scene_create_auto(desc, &st, CRT_SCENE_TREE_AUTO, &g_scene);   /* GPUs the frame pays for */
             if (rc == CRT_OK) g_scene_key = key;
         } else {
             rc = CRT_OK;

@@ -248,12 +248,15 @@ Image render_image(const Scene &scene, const RendererSettings &settings) {
     Cached *c = g_cache.find([&](const Cached &e) { return same_scene(e.flat, e.vertices, e.texels, *now); });
     if (!c) {
         std::unique_ptr<Cached> fresh(new Cached());
-        /* every visible GPU (CRT_HIP_GPUS=N limits it), as render_image spans
-         * every hardware thread (crt_renderer.cpp:176-196); CRT_HIP_DEVICE=K
-         * pins one device */
+        /* as many GPUs as the frame pays for (crt_hip_scene_from_tree_auto;
+         * CRT_HIP_GPUS=N sets the count), as render_image spans every hardware
+         * thread (crt_renderer.cpp:176-196); CRT_HIP_DEVICE=K pins one device */
+        const crt_renderer_settings st0{settings.max_ray_depth, settings.diffuse_reflection_ray_count,
+                                        settings.shadow_bias, settings.reflection_bias,
+                                        settings.diffuse_reflection_bias, settings.refraction_bias};
         const char *dev = std::getenv("CRT_HIP_DEVICE");
         const int urc = dev ? crt_hip_scene_from_tree(&now->desc, std::atoi(dev), &fresh->scene)
-                            : crt_hip_scene_from_tree_mask(&now->desc, 0, &fresh->scene);
+                            : crt_hip_scene_from_tree_auto(&now->desc, &st0, &fresh->scene);
         if (urc != CRT_OK) fail("scene upload");
         const float *vp = now->desc.vertices;
         fresh->vertices.assign(vp, vp + 9 * now->desc.vertex_count);

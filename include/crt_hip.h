@@ -297,6 +297,19 @@ int  crt_hip_scene_from_tree_on(const crt_tree_scene_desc *desc, const int32_t *
  * variable CRT_HIP_GPUS=N, else every visible device. */
 int  crt_hip_scene_create_mask(const crt_scene_desc *desc, uint64_t gpu_mask, int flags, crt_hip_scene **out);
 int  crt_hip_scene_from_tree_mask(const crt_tree_scene_desc *desc, uint64_t gpu_mask, crt_hip_scene **out);
+/* The GPU count a frame is spread over when the caller leaves the choice
+ * (the CLI, _crt and the crt::render_image shim): 1 unless the frame estimated
+ * from the scene and settings (pixels, GI fan-out, recursion, triangles) takes
+ * >= 2 ms on one GPU, else about one GPU per 0.6 ms of it, at most `visible`
+ * (C2 / C3 stay on one GPU, C4 / C5 spread).  CRT_HIP_GPUS=N
+ * overrides.  No GPU needed. */
+int  crt_auto_gpus(const crt_scene_desc *desc, const crt_renderer_settings *settings, int visible);
+int  crt_auto_gpus_tree(const crt_tree_scene_desc *desc, const crt_renderer_settings *settings, int visible);
+/* crt_hip_scene_create_mask / _from_tree_mask over the first crt_auto_gpus devices. */
+int  crt_hip_scene_create_auto(const crt_scene_desc *desc, const crt_renderer_settings *settings, int flags,
+                               crt_hip_scene **out);
+int  crt_hip_scene_from_tree_auto(const crt_tree_scene_desc *desc, const crt_renderer_settings *settings,
+                                  crt_hip_scene **out);
 /* Replica devices (devices may be NULL); returns the replica count. */
 int  crt_hip_scene_devices(const crt_hip_scene *scene, int32_t *devices, int32_t cap);
 /* Kernel ms of each replica's shard in the last render (blocks until done). */
@@ -387,6 +400,10 @@ int  crt_hip_trace_batch(crt_hip_scene *scene, const float *rays, int64_t n, crt
  * when the scene takes no camera bins). */
 int64_t crt_hip_camera_bins(crt_hip_scene *scene, int32_t *len_out, void *recs_out, int64_t cap);
 int64_t crt_host_camera_bins(const crt_host_scene *hs, int32_t *len_out, void *recs_out, int64_t cap);
+/* Diagnostics: device ms of one frame's camera binning alone (the two kernels
+ * every camera-bins frame runs before its render kernel), averaged over
+ * `frames` back-to-back frames on the scene's stream; 0 without camera bins. */
+int  crt_hip_bins_time(crt_hip_scene *scene, int32_t frames, double *ms);
 
 /* Work counters of one frame (instrumented variant of the render kernel). */
 int  crt_hip_count_work(crt_hip_scene *scene, const crt_renderer_settings *settings,
