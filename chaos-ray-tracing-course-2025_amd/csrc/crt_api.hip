@@ -187,6 +187,8 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
         if (m.type == CRT_MATERIAL_REFRACTIVE) sc->has_refractive = true;
         if (m.type == CRT_MATERIAL_DIFFUSE) sc->has_diffuse = true;
     }
+    const bool gi_tables = hs.gi_on && sc->has_diffuse, pow5_table = hs.refractions_on && sc->has_refractive;
+    start_host_tables(gi_tables, pow5_table);   /* background, overlapping the upload below */
     DeviceScene &ds = sc->ds;
     int rc;
     ds.prune_origin_max = hs.prune_origin_max;
@@ -297,6 +299,11 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
      * runtime's own initialisation (profiles/r03/cold): the device record, the
      * output image of crt_hip_render, and the runtime's staging for copies into
      * pageable host memory (allocated by the first such copy) */
+    /* the scene's libm tables on this device (GI angles, Fresnel pow5): a
+     * process-lifetime precompute of the host libm's values, kept out of the
+     * first frame (main.cpp:37-43 times that frame) */
+    if (gi_tables && (rc = ensure_gi_tables(sc.get())) != CRT_OK) return rc;
+    if (pow5_table && (rc = ensure_pow5_table(sc.get())) != CRT_OK) return rc;
     {
         const DeviceScene *d = nullptr;
         if ((rc = sync_device_record(sc.get(), &d)) != CRT_OK) return rc;
@@ -601,51 +608,52 @@ int crt_hip_profile_waves(crt_hip_scene *sc, const crt_renderer_settings *st, ui
     hipError_t e = rc == CRT_OK ? hipStreamSynchronize(sc->stream) : hipSuccess;
     if (rc == CRT_OK && e == hipSuccess)
         e = hipMemcpy(stamps, d, (size_t)nt * 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
-    /* each wave's tile: the plan's tiles in order, or (camera bins) the frame's
-     * priority lists ahead of the untaken tiles */
+    /* each wave's tile: the plan's tiles in order, or (camera bins) the
+     * frame's work lists, then the rest tiles */
     const ShardPlan &p = sc->full;
     const BinsPlan &bp = p.bp;
-    std::vector<int32_t> prio, taken, phdr(2 * kBinShards, 0), ph_all;
+    std::vector<BinsWork> work;
+    std::vector<int32_t> ph_all, rest;
+    int par = 0;
     if (rc == CRT_OK && e == hipSuccess && bp.cell_tile) {
-        const int par = (int)((sc->bins.frame - 1) & 1);   /* the parity the frame just used */
-        prio.resize((size_t)(kBinShards * (bp.ch + bp.cm)));
-        taken.resize((size_t)bp.nbase);
-        e = hipMemcpy(prio.data(), bp.prio, prio.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
-        if (e == hipSuccess) e = hipMemcpy(taken.data(), bp.taken, taken.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
+        par = (int)((sc->bins.frame - 1) & 1);   /* the parity the frame just used */
+        int64_t slots = 0;
+        for (int q = 0; q < kBinKinds; ++q) slots += (int64_t)kBinShards * bp.cap[q];
+        work.resize((size_t)std::max<int64_t>(1, slots));
         ph_all.resize((size_t)kBinsPhdrInts);
+        rest.resize((size_t)std::max(1, bp.nrest));
+        e = hipMemcpy(work.data(), bp.work, work.size() * sizeof(BinsWork), hipMemcpyDeviceToHost);
         if (e == hipSuccess) e = hipMemcpy(ph_all.data(), bp.phdr, ph_all.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
-        for (int kind = 0; kind < 2; ++kind)
-            for (int sh = 0; sh < kBinShards; ++sh)
-                phdr[(size_t)(kind * kBinShards + sh)] = ph_all[(size_t)bins_phdr_at(par, kind, sh)];
+        if (e == hipSuccess) e = hipMemcpy(rest.data(), bp.rest, rest.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
     }
     (void)hipFree(d);
     if (rc != CRT_OK) return rc;
     if (e != hipSuccess) return set_error(CRT_E_HIP, hipGetErrorString(e));
-    const int nh = 4 * kBinShards * bp.ch, nm = kBinShards * bp.cm;
     for (int k = 0; k < nt; ++k) {
         int x = -1, y = -1;
         if (!bp.cell_tile) {
             x = p.tiles[(size_t)k].x;
             y = p.tiles[(size_t)k].y;
-        } else if (k < nh) {
-            const int slot = k / 4, sh = slot % kBinShards, i2 = slot / kBinShards;
-            if (i2 < std::min(phdr[(size_t)sh], bp.ch)) {
-                const Tile &t = p.tiles[(size_t)prio[(size_t)(sh * bp.ch + i2)]];
-                x = t.x + (k & 1) * 4;
-                y = t.y + ((k >> 1) & 1) * 4;
-            }
-        } else if (k < nh + nm) {
-            const int slot = k - nh, sh = slot % kBinShards, i2 = slot / kBinShards;
-            if (i2 < std::min(phdr[(size_t)(kBinShards + sh)], bp.cm)) {
-                const Tile &t = p.tiles[(size_t)prio[(size_t)(kBinShards * bp.ch + sh * bp.cm + i2)]];
-                x = t.x;
-                y = t.y;
-            }
         } else {
-            const int b = k - nh - nm;
-            if (!taken[(size_t)b]) {
-                x = p.tiles[(size_t)b].x;
-                y = p.tiles[(size_t)b].y;
+            int kind = 0, slot = k >> 2, q = k & 3;
+            if (k >= 4 * kBinShards * bp.cap[0]) {
+                slot = k - 4 * kBinShards * bp.cap[0];
+                q = -1;
+                kind = 1;
+                while (kind < kBinKinds && slot >= kBinShards * bp.cap[kind]) slot -= kBinShards * bp.cap[kind++];
+            }
+            if (kind == kBinKinds) {
+                if (slot < bp.nrest) {
+                    x = p.tiles[(size_t)rest[(size_t)slot]].x;
+                    y = p.tiles[(size_t)rest[(size_t)slot]].y;
+                }
+            } else {
+                const int sh = slot % kBinShards, i2 = slot / kBinShards;
+                if (i2 < std::min(ph_all[(size_t)bins_phdr_at(par, kind, sh)], bp.cap[kind])) {
+                    const Tile &t = work[(size_t)(bp.wbase[kind] + sh * bp.cap[kind] + i2)].t;
+                    x = t.x + (q >= 0 ? (q & 1) * 4 : 0);
+                    y = t.y + (q >= 0 ? (q >> 1) * 4 : 0);
+                }
             }
         }
         tile_xy[2 * k] = x;

@@ -6,33 +6,43 @@
  * render_image call (crt_renderer.cpp:147-155, timed at main.cpp:37-39); the
  * lists that let a camera ray test only the triangles its 8x8 cell can hit
  * depend on the camera and the resolution, so they are rebuilt by every frame
- * that walks them, before its render kernel, in two launches:
+ * that walks them, before its render kernel:
  *
- *   k_bins_project  one thread per triangle: its hull's projection (bin_project:
- *                   pixel rectangle, dmin, everywhere); then every (triangle,
- *                   cell) pair of the block's 64 triangles, spread over the
- *                   block's 256 threads, takes a slot of its cell (atomic
- *                   count) and writes the triangle id there (kBinCellCap slots
- *                   per cell); the first pair of a cell appends the cell to the
- *                   frame's non-empty list.  Also clears the per-cell list
- *                   lengths and the tile plan's per-frame state.
- *   k_bins_sort     one wave per non-empty cell (every cell when some hull is
- *                   everywhere): its ids plus the everywhere ids, sorted by
- *                   (dmin, id) (bitonic, registers up to 64, LDS up to the cap),
- *                   written as CamCand records (static part from the per-triangle
- *                   template, dmin, the cell's pixel mask, and `rest`, the OR of
- *                   the masks from here to the list's end) into a range reserved
- *                   with one atomic; the cell's (offset, length); and the tile
- *                   plan's priority lists: a cell with bins_split or more
- *                   candidates is queued for four 4x4 waves, one with
- *                   kBinsMedium or more for an early 8x8 wave (the render's
- *                   other waves walk the remaining cells in frame order).
+ *   k_bins_project  one block per 32 triangles, 8 lanes each (one hull corner
+ *                   per lane): the hull's projection (pixel rectangle, dmin,
+ *                   everywhere); then the group's (triangle, cell) pairs, spread
+ *                   over the block's 256 threads, take a slot of their cell
+ *                   (atomic count) and write the key (dmin, id) there
+ *                   (kBinCellCap slots per cell); a cell's first pair appends
+ *                   it to its shard's non-empty list, its 17th to the long
+ *                   list.  A group with more than kExpand pairs queues the
+ *                   rest for k_bins_pairs, which spreads them over its grid
+ *                   (launched when the scene's sizing pass queued groups).
+ *                   Also zeroes this frame's per-cell lengths and the other
+ *                   parity's counts.
+ *   k_bins_sort     the long lists one a wave, the others four a wave (16
+ *                   lanes each): the cell's keys plus the everywhere ids
+ *                   ranked in LDS, written as CamCand records (static part
+ *                   from the per-triangle template, dmin, the cell's pixel
+ *                   mask, and `rest`, the OR of the masks from here to the
+ *                   list's end) into a range reserved with one atomic; the
+ *                   cell's (offset, length); and its entry in the tile plan's
+ *                   work lists by length (crt_kernel_common.h BinsPlan: heavy
+ *                   cells four 4x4 waves, then medium, light, BVH; empty cells
+ *                   get the background from the render's fill waves).
+ *
+ * Each step is a chain of dependent memory round trips (~1-2 us each at this
+ * size), not bandwidth: the kernels are shaped to issue what they can in one
+ * round (a cell's count, tile and first keys together; the record range's
+ * atomic with the templates' loads), and every per-frame counter has a
+ * 256-B line of its own, sharded by cell (device atomics on one line
+ * serialise).
  *
  * The lists equal the host checker's (crt_bvh_build.cpp build_camera_bins)
  * record for record (tests/test_gpu_bins.py); the records of different cells
  * sit in the buffer in no particular order (each cell's range is reserved by
  * an atomic), which no reader depends on.  Scene create runs k_bins_project
- * once to size the buffers (records, priority slots) and to decide whether the
+ * once to size the buffers (records, work lists, grids) and to decide whether the
  * scene takes bins at all (crt_bins.h caps); a frame whose lists would not fit
  * renders the cells that do not fit on the BVH walk — the same image.
  */
@@ -57,7 +67,7 @@ namespace crt_amd {
  * to 0, so the kernels stay on their control flow) */
 struct BinsDbg {
     int32_t code, idx, bound, pad;
-    int32_t nt, ncell, ne_cap, rec_cap, ntaken, prio_cap;
+    int32_t nt, ncell, rec_cap, ne_cap;
 };
 __device__ BinsDbg g_bins_dbg;
 __device__ int bins_ck(int64_t i, int64_t n, int code) {
@@ -81,7 +91,7 @@ __device__ int bins_ck(int64_t i, int64_t n, int code) {
  * at its start, after the projection, after the pair-count scan and at its end */
 __device__ unsigned long long g_bins_stamps[8192 * 4];
 #define BSTAMP(k) \
-    if (threadIdx.x == 0) g_bins_stamps[4 * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime()
+    if (threadIdx.x == 0 && blockIdx.x < 8192) g_bins_stamps[4 * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime()
 /* ... and per block of k_bins_sort: start, counters read, cell read, list written, end; the list length */
 __device__ unsigned long long g_bins_stamps4[16384 * 6];
 #define BSTAMP4(k) \
@@ -136,116 +146,62 @@ __device__ __forceinline__ uint64_t wave_suffix_or(uint64_t v, int lane) {
 
 }  // namespace
 
-/* Projection: 8 lanes per triangle (lane q projects hull corner q; the
- * bounds are reduced over the 8), the item, the triangle's (triangle, cell)
- * pair count np and its exclusive prefix inside the block's group of
- * kProjTris triangles, the group's sum; the everywhere list.  Also the
- * frame's resets: the other parity's counters, this frame's per-cell lengths
- * and the plan's taken flags. */
-__global__ __launch_bounds__(256) void k_bins_project(const CamCand *__restrict__ tpl, int nt, BinCamera cam,
-                                                      BinItem *__restrict__ items, int32_t *__restrict__ tpref,
-                                                      int32_t *__restrict__ gsum, int32_t *__restrict__ every,
-                                                      BinsHdr *__restrict__ hdr2, int par,
-                                                      int32_t *__restrict__ bin_len, int ncell,
-                                                      int32_t *__restrict__ taken, int ntaken,
-                                                      int32_t *__restrict__ phdr2) {
-    __shared__ int32_t npl[kProjTris];
-    const int tid = (int)threadIdx.x;
-    BSTAMP(0);
-    BinsHdr *hdr = hdr2 + par;
-    /* the other parity's counters start the next frame at zero (this frame
-     * does not touch them; the previous one is done with them) */
-    if (blockIdx.x == 0) {
-        BinsHdr *o = hdr2 + (par ^ 1);
-        if (tid == 0) o->n_every.v = 0;
-        if (tid < kBinShards) {
-            o->ne[tid].v = 0;
-            o->rec[tid].v = 0;
-        }
-        if (phdr2 && tid < 2 * kBinShards)
-            phdr2[BCK(bins_phdr_at(par ^ 1, tid / kBinShards, tid % kBinShards), kBinsPhdrInts, 1)] = 0;
-    }
-    /* this frame's per-cell lengths and plan state start empty (k_bins_sort fills them) */
-    const int g = (int)(blockIdx.x * blockDim.x) + tid, gn = (int)(gridDim.x * blockDim.x);
-    for (int i = g; i < ncell; i += gn) bin_len[BCK(i, BDBG(ncell), 2)] = 0;
-    for (int i = g; i < ntaken; i += gn) taken[BCK(i, BDBG(ntaken), 3)] = 0;
-    const int tl = tid >> 3, q = tid & 7;
-    const int t = (int)blockIdx.x * kProjTris + tl;
-    double lo[3] = {0.0, 0.0, 0.0}, hi[3] = {0.0, 0.0, 0.0};
-    double X0 = INFINITY, X1 = -INFINITY, Y0 = INFINITY, Y1 = -INFINITY;
-    int behind = 0;
-    if (t < nt) {
-        const float *b = reinterpret_cast<const float *>(tpl + BCK(t, BDBG(nt), 4));   /* lo_x, hi_x, lo_y, ... */
-        lo[0] = b[0]; hi[0] = b[1]; lo[1] = b[2]; hi[1] = b[3]; lo[2] = b[4]; hi[2] = b[5];
-        double X, Y;
-        if (bin_corner(lo, hi, q, cam, X, Y)) {
-            X0 = X1 = X;
-            Y0 = Y1 = Y;
-        } else {
-            behind = 1;
+/* (triangle, cell) pairs -> cell slots: the atomics of a thread's pairs in
+ * flight together; each pair writes its key (dmin, id) to its slot
+ * (kBinCellCap slots per cell), the first pair of a cell lists the cell in its
+ * shard's non-empty list, the 17th in its shard's list of long ones.  cell < 0:
+ * no pair. */
+constexpr int kSortGroup = 16;   /* k_bins_sort: lanes per cell of its first pass (longer lists: a wave each) */
+
+template <int U>
+__device__ __forceinline__ void bins_scatter(const int (&cell)[U], const uint64_t (&key)[U], int32_t *__restrict__ cnt,
+                                             uint64_t *__restrict__ keys, int32_t *__restrict__ nonempty,
+                                             int32_t *__restrict__ bigl, int cap_shard, BinsHdr *__restrict__ hdr) {
+    int slot[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        slot[u] = cell[u] >= 0 ? atomicAdd(&cnt[(size_t)BCK(cell[u], BDBG(ncell), 7) * kCntStride], 1) : kBinCellCap;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (cell[u] < 0) continue;
+        if (slot[u] < kBinCellCap)
+            keys[BCK((size_t)cell[u] * kBinCellCap + slot[u], (int64_t)BDBG(ncell) * kBinCellCap, 8)] = key[u];
+        if (slot[u] == 0) {
+            const int sh = cell[u] % kBinShards;
+            nonempty[BCK(sh * cap_shard + atomicAdd(&hdr->ne[BCK(sh, kBinShards, 9)].v, 1), BDBG(ne_cap), 10)] = cell[u];
+        } else if (slot[u] == kSortGroup) {   /* the cell's list outgrows a 16-lane group: a wave of its own */
+            const int sh = cell[u] % kBinShards;
+            bigl[BCK(sh * cap_shard + atomicAdd(&hdr->nb[sh].v, 1), BDBG(ne_cap), 13)] = cell[u];
         }
     }
-    for (int d = 1; d < 8; d <<= 1) {
-        X0 = fmin(X0, shfl_xor_f64(X0, d));
-        X1 = fmax(X1, shfl_xor_f64(X1, d));
-        Y0 = fmin(Y0, shfl_xor_f64(Y0, d));
-        Y1 = fmax(Y1, shfl_xor_f64(Y1, d));
-        behind |= __shfl_xor(behind, d);
-    }
-    if (q == 0) {
-        int np = 0;
-        if (t < nt) {
-            const BinItem it = bin_finish(behind != 0, X0, X1, Y0, Y1, bin_dmin(lo, hi, cam), cam);
-            items[BCK(t, BDBG(nt), 5)] = it;
-            if (it.every) {
-                const int k = atomicAdd(&hdr->n_every.v, 1);
-                if (k < kBinMaxEverywhere) every[BCK(k, kBinMaxEverywhere, 6)] = t;
-            } else if (it.px0 <= it.px1) {
-                np = ((it.px1 >> 3) - (it.px0 >> 3) + 1) * ((it.py1 >> 3) - (it.py0 >> 3) + 1);
-            }
-        }
-        npl[tl] = np;
-    }
-    BSTAMP(1);
-    __syncthreads();
-    if (tid < 64) {   /* wave 0: the group's exclusive prefix and sum */
-        const int np = tid < kProjTris ? npl[tid] : 0;
-        int incl = np;
-        for (int d = 1; d < 64; d <<= 1) {
-            const int v = __shfl_up(incl, d);
-            if (tid >= d) incl += v;
-        }
-        const int tt = (int)blockIdx.x * kProjTris + tid;
-        if (tid < kProjTris && tt < nt) tpref[BCK(tt, BDBG(nt), 33)] = incl - np;
-        if (tid == kProjTris - 1) gsum[blockIdx.x] = incl;
-    }
-    BSTAMP(2);
 }
 
-/* Scatter: every (triangle, cell) pair of the frame, spread evenly over the
- * grid (a triangle covering thousands of cells shares its pairs among many
- * blocks), takes a slot of its cell (atomic count; kBinCellCap slots per
- * cell) and writes the triangle id there; the first pair of a cell lists the
- * cell in its shard's non-empty list.  Each block scans the groups' sums in
- * LDS and finds each of its pairs' group, then its triangle (the group's
- * prefix), then its cell. */
-constexpr int kPairsPerThread = 2;
+/* the cell of pair j of an item's rectangle (row-major over its cells) */
+__device__ __forceinline__ int bins_pair_cell(const BinItem &it, int j, int tx) {
+    const int x0 = it.px0 >> 3, w = (it.px1 >> 3) - x0 + 1;
+    return ((it.py0 >> 3) + j / w) * tx + x0 + j % w;
+}
+
+constexpr int kPairsPerThread = 4;
+constexpr int kExpand = 256 * kPairsPerThread;
 constexpr int kMaxGroups = 8192;   /* 2^18 triangles (bins are built up to the BVH's limit) */
 
-__global__ __launch_bounds__(256) void k_bins_pairs(const BinItem *__restrict__ items,
-                                                    const int32_t *__restrict__ tpref,
-                                                    const int32_t *__restrict__ gsum, int ngroups, int nt, int tx,
-                                                    int32_t *__restrict__ cnt, uint64_t *__restrict__ keys,
-                                                    int32_t *__restrict__ nonempty, int cap_shard,
-                                                    BinsHdr *__restrict__ hdr2, int par) {
+/* The queued groups' pairs past the first kExpand, spread evenly over the
+ * blocks of k_bins_pairs (bid of nblk): each block scans the queued groups' remaining
+ * counts in LDS, finds each of its pairs' group, then its triangle (the
+ * group's prefixes), then its cell. */
+__device__ void bins_pairs(const BinItem *__restrict__ items, const int32_t *__restrict__ tpref,
+                           const int32_t *__restrict__ gsum, const int32_t *__restrict__ rem, int nt, int tx,
+                           int32_t *__restrict__ cnt, uint64_t *__restrict__ keys, int32_t *__restrict__ nonempty,
+                           int32_t *__restrict__ bigl, int cap_shard, BinsHdr *__restrict__ hdr, int bid, int nblk) {
     __shared__ int32_t gp[kMaxGroups + 1];
     __shared__ int32_t part[256];
     const int tid = (int)threadIdx.x;
-    BinsHdr *hdr = hdr2 + par;
-    /* exclusive prefix of the groups' sums: each thread sums a run, then the runs are scanned */
-    const int per = (ngroups + 255) / 256, g0 = tid * per, g1 = min(ngroups, g0 + per);
+    const int nq = hdr->nrem.v;
+    /* exclusive prefix of the queued groups' remaining counts: each thread sums a run, then the runs are scanned */
+    const int per = (nq + 255) / 256, g0 = tid * per, g1 = min(nq, g0 + per);
     int run = 0;
-    for (int k = g0; k < g1; ++k) run += gsum[k];
+    for (int k = g0; k < g1; ++k) run += gsum[BCK(rem[k], BDBG(nt), 36)] - kExpand;
     part[tid] = run;
     __syncthreads();
     if (tid < 64) {
@@ -269,31 +225,30 @@ __global__ __launch_bounds__(256) void k_bins_pairs(const BinItem *__restrict__ 
         int acc = part[tid];
         for (int k = g0; k < g1; ++k) {
             gp[k] = acc;
-            acc += gsum[k];
+            acc += gsum[rem[k]] - kExpand;
         }
     }
     __syncthreads();
     const int total = gp[kMaxGroups];
-    const int64_t G = gridDim.x;
-    const int p0 = (int)((int64_t)total * blockIdx.x / G), p1 = (int)((int64_t)total * (blockIdx.x + 1) / G);
-    for (int pb = p0 + tid; pb < p1; pb += 256 * kPairsPerThread) {
-        int cell[kPairsPerThread];
-        uint64_t key[kPairsPerThread];
+    const int p0 = (int)((int64_t)total * bid / nblk), p1 = (int)((int64_t)total * (bid + 1) / nblk);
+    for (int pb = p0 + tid; pb < p1; pb += 256 * 2) {
+        int cell[2];
+        uint64_t key[2];
 #pragma unroll
-        for (int u = 0; u < kPairsPerThread; ++u) {
+        for (int u = 0; u < 2; ++u) {
             const int p = pb + u * 256;
             cell[u] = -1;
             if (p >= p1) continue;
-            int lo = 0, hi = ngroups - 1;   /* the last group whose pairs start at or before p */
+            int lo = 0, hi = nq - 1;   /* the last queued group whose pairs start at or before p */
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
                 if (gp[mid] <= p) lo = mid;
                 else hi = mid - 1;
             }
-            const int r = p - gp[lo];
+            const int r = kExpand + p - gp[lo];   /* the pair inside its group */
             /* ... and the triangle inside the group: the group's prefixes in one
              * round of loads (kProjTris contiguous ints), the last one <= r */
-            const int a0 = lo * kProjTris, na = min(nt - a0, kProjTris);
+            const int a0 = rem[lo] * kProjTris, na = min(nt - a0, kProjTris);
             const int4 *tp4 = reinterpret_cast<const int4 *>(tpref + BCK(a0, BDBG(nt), 34));
             int4 v[kProjTris / 4];
 #pragma unroll
@@ -310,27 +265,143 @@ __global__ __launch_bounds__(256) void k_bins_pairs(const BinItem *__restrict__ 
                     }
             }
             const BinItem it = items[BCK(a, BDBG(nt), 35)];
-            const int j = r - pr, x0 = it.px0 >> 3, w = (it.px1 >> 3) - x0 + 1;
-            cell[u] = ((it.py0 >> 3) + j / w) * tx + x0 + j % w;
-            key[u] = bin_key(it.dmin, a);   /* the cell's sort key: (dmin, id) */
+            cell[u] = bins_pair_cell(it, r - pr, tx);
+            key[u] = bin_key(it.dmin, a);
         }
-        int slot[kPairsPerThread];
-#pragma unroll
-        for (int u = 0; u < kPairsPerThread; ++u)   /* the atomics in flight together */
-            slot[u] = cell[u] >= 0 ? atomicAdd(&cnt[(size_t)BCK(cell[u], BDBG(ncell), 7) * kCntStride], 1) : kBinCellCap;
-#pragma unroll
-        for (int u = 0; u < kPairsPerThread; ++u) {
-            if (cell[u] < 0) continue;
-            if (slot[u] < kBinCellCap)
-                keys[BCK((size_t)cell[u] * kBinCellCap + slot[u], (int64_t)BDBG(ncell) * kBinCellCap, 8)] = key[u];
-            if (slot[u] == 0) {   /* the cell's first candidate: list the cell in its shard */
-                const int sh = cell[u] % kBinShards;
-                nonempty[BCK(sh * cap_shard + atomicAdd(&hdr->ne[BCK(sh, kBinShards, 9)].v, 1), BDBG(ne_cap), 10)] =
-                    cell[u];
-            }
-        }
+        bins_scatter<2>(cell, key, cnt, keys, nonempty, bigl, cap_shard, hdr);
     }
 }
+
+
+/* Projection + scatter, one block per group of kProjTris triangles: 8 lanes
+ * per triangle (lane q projects hull corner q; the bounds are reduced over
+ * the 8) give the item; the group's pair counts are scanned in LDS and the
+ * block's 256 threads scatter the group's first kExpand (triangle, cell)
+ * pairs themselves — a group with more (a triangle covering thousands of
+ * cells) queues its rest for k_bins_pairs.
+ * Also the everywhere list, this frame's per-cell lengths (zero) and the other
+ * parity's counters (zero for the next frame). */
+__global__ __launch_bounds__(256) void k_bins_project(const CamCand *__restrict__ tpl, int nt, BinCamera cam,
+                                                      BinItem *__restrict__ items, int32_t *__restrict__ tpref,
+                                                      int32_t *__restrict__ gsum, int32_t *__restrict__ every,
+                                                      BinsHdr *__restrict__ hdr2, int par,
+                                                      int32_t *__restrict__ phdr2, int32_t *__restrict__ bin_len,
+                                                      int ncell, int tx, int32_t *__restrict__ cnt2,
+                                                      uint64_t *__restrict__ keys, int32_t *__restrict__ nonempty,
+                                                      int32_t *__restrict__ bigl, int cap_shard, int32_t *__restrict__ rem,
+                                                      int queue) {
+    __shared__ int32_t npl[kProjTris];
+    __shared__ int32_t spre[kProjTris + 1];
+    __shared__ BinItem sit[kProjTris];
+    const int tid = (int)threadIdx.x;
+    BSTAMP(0);
+    BinsHdr *hdr = hdr2 + par;
+    int32_t *cnt = cnt2 + (size_t)par * ncell * kCntStride;
+    /* the other parity's counters start the next frame at zero (this frame
+     * does not touch them; the previous one is done with them) */
+    if (blockIdx.x == 0) {
+        BinsHdr *o = hdr2 + (par ^ 1);
+        if (tid == 0) o->n_every.v = 0;
+        if (tid == 1) o->nrem.v = 0;
+        if (tid < kBinShards) {
+            o->ne[tid].v = 0;
+            o->nb[tid].v = 0;
+            o->rec[tid].v = 0;
+        }
+        if (phdr2 && tid < kBinKinds * kBinShards)
+            phdr2[BCK(bins_phdr_at(par ^ 1, tid / kBinShards, tid % kBinShards), kBinsPhdrInts, 1)] = 0;
+    }
+    /* this frame's per-cell lengths start empty (k_bins_sort sets the listed
+     * cells'); the other parity's counts start the next frame at zero */
+    for (int i = (int)(blockIdx.x * blockDim.x) + tid; i < ncell; i += (int)(gridDim.x * blockDim.x)) {
+        bin_len[BCK(i, BDBG(ncell), 2)] = 0;
+        cnt2[((size_t)(par ^ 1) * ncell + BCK(i, BDBG(ncell), 2)) * kCntStride] = 0;
+    }
+    const int tl = tid >> 3, q = tid & 7;
+    const int t0 = (int)blockIdx.x * kProjTris, t = t0 + tl;
+    double lo[3] = {0.0, 0.0, 0.0}, hi[3] = {0.0, 0.0, 0.0};
+    double X0 = INFINITY, X1 = -INFINITY, Y0 = INFINITY, Y1 = -INFINITY;
+    int behind = 0;
+    if (t < nt) {
+        const float *b = reinterpret_cast<const float *>(tpl + BCK(t, BDBG(nt), 4));   /* lo_x, hi_x, lo_y, ... */
+        lo[0] = b[0]; hi[0] = b[1]; lo[1] = b[2]; hi[1] = b[3]; lo[2] = b[4]; hi[2] = b[5];
+        double X, Y;
+        if (bin_corner(lo, hi, q, cam, X, Y)) {
+            X0 = X1 = X;
+            Y0 = Y1 = Y;
+        } else {
+            behind = 1;
+        }
+    }
+    for (int d = 1; d < 8; d <<= 1) {
+        X0 = fmin(X0, shfl_xor_f64(X0, d));
+        X1 = fmax(X1, shfl_xor_f64(X1, d));
+        Y0 = fmin(Y0, shfl_xor_f64(Y0, d));
+        Y1 = fmax(Y1, shfl_xor_f64(Y1, d));
+        behind |= __shfl_xor(behind, d);
+    }
+    if (q == 0) {
+        int np = 0;
+        BinItem it{};
+        it.px0 = 1;   /* no pixels */
+        if (t < nt) {
+            it = bin_finish(behind != 0, X0, X1, Y0, Y1, bin_dmin(lo, hi, cam), cam);
+            items[BCK(t, BDBG(nt), 5)] = it;
+            if (it.every) {
+                const int k = atomicAdd(&hdr->n_every.v, 1);
+                if (k < kBinMaxEverywhere) every[BCK(k, kBinMaxEverywhere, 6)] = t;
+            } else if (it.px0 <= it.px1) {
+                np = ((it.px1 >> 3) - (it.px0 >> 3) + 1) * ((it.py1 >> 3) - (it.py0 >> 3) + 1);
+            }
+        }
+        npl[tl] = np;
+        sit[tl] = it;
+    }
+    BSTAMP(1);
+    __syncthreads();
+    if (tid < 64) {   /* wave 0: the group's exclusive prefix and sum */
+        const int np = tid < kProjTris ? npl[tid] : 0;
+        int incl = np;
+        for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(incl, d);
+            if (tid >= d) incl += v;
+        }
+        const int tt = t0 + tid;
+        if (tid < kProjTris) spre[tid] = incl - np;
+        if (tid < kProjTris && tt < nt) tpref[BCK(tt, BDBG(nt), 33)] = incl - np;
+        if (tid == kProjTris - 1) {
+            spre[kProjTris] = incl;
+            gsum[blockIdx.x] = incl;
+        }
+    }
+    __syncthreads();
+    BSTAMP(2);
+    const int G = spre[kProjTris], E = min(G, kExpand);
+    if (tid == 0 && G > kExpand) {   /* the rest: k_bins_pairs (launched when the sizing pass queued groups) */
+        (void)BCK(queue ? 0 : -1, 1, 37);
+        rem[BCK(atomicAdd(&hdr->nrem.v, 1), BDBG(nt), 38)] = (int)blockIdx.x;
+    }
+    if (tid < E) {   /* pairs tid + 256 u of the group */
+        int cell[kPairsPerThread];
+        uint64_t key[kPairsPerThread];
+#pragma unroll
+        for (int u = 0; u < kPairsPerThread; ++u) {
+            const int p = tid + 256 * u;
+            cell[u] = -1;
+            if (p >= E) continue;
+            int a = 0;   /* the last triangle whose pairs start at or before p */
+#pragma unroll
+            for (int st = kProjTris / 2; st > 0; st >>= 1)
+                if (spre[a + st] <= p) a += st;
+            const BinItem it = sit[a];
+            cell[u] = bins_pair_cell(it, p - spre[a], tx);
+            key[u] = bin_key(it.dmin, t0 + a);   /* the cell's sort key: (dmin, id) */
+        }
+        bins_scatter<kPairsPerThread>(cell, key, cnt, keys, nonempty, bigl, cap_shard, hdr);
+    }
+    BSTAMP(3);
+}
+
 
 /* k_bins_sort: one wave per listed cell (every cell when some hull is
  * everywhere), four independent waves a block.  The cell's keys (its own
@@ -409,20 +480,23 @@ __device__ void bins_emit(const CamCand *__restrict__ tpl, const BinItem *__rest
     wave_lds_sync();   /* sk is reused by the wave's next cell */
 }
 
-/* n <= 64 (nearly every cell): one candidate per lane; its template and item
- * are loaded in list order while the keys are ranked, the record is written
- * straight to its ranked position, and only the masks and `rest` go through
- * LDS (sk[0..63] keys, [64..127] masks by rank, [128..191] rest by rank). */
-__device__ void bins_emit64(const CamCand *__restrict__ tpl, const BinItem *__restrict__ items,
-                            const uint64_t *__restrict__ own, int m, const int32_t *__restrict__ every, int n, int cx,
-                            int cy, CamCand *__restrict__ out, uint64_t *sk, int lane) {
+/* n <= 64 (nearly every cell): one candidate per lane (key: this lane's, in
+ * no order).  The cell's record range is reserved (lane 0's atomic on the
+ * shard's counter) while the lane's template and item load and the keys are
+ * ranked; the record is written straight to its ranked position, and only the
+ * masks and `rest` go through LDS (sk[0..63] keys, [64..127] masks by rank,
+ * [128..191] rest by rank).  Returns the range's start (-1: the shard's
+ * region is full, the cell walks the BVH). */
+__device__ int bins_emit64(const CamCand *__restrict__ tpl, const BinItem *__restrict__ items, uint64_t key, int n,
+                           int cx, int cy, CamCand *__restrict__ region, int cap, int32_t *__restrict__ ctr,
+                           uint64_t *sk, int lane) {
     const bool on = lane < n;
-    uint64_t key = ~0ull;
-    if (on) key = lane < m ? own[BCK(lane, kBinCellCap, 11)] : bin_key(0.0f, every[BCK(lane - m, kBinMaxEverywhere, 12)]);
+    int tick = 0;
+    if (lane == 0) tick = atomicAdd(ctr, n);
     const int t = (int)(uint32_t)key;
     BinItem it{};
     float4 q[6];
-    if (on) {   /* in flight during the ranking */
+    if (on) {   /* in flight with the atomic during the ranking */
         it = items[BCK(t, BDBG(nt), 19)];
         const float4 *src = reinterpret_cast<const float4 *>(tpl + BCK(t, BDBG(nt), 20));
 #pragma unroll
@@ -438,91 +512,238 @@ __device__ void bins_emit64(const CamCand *__restrict__ tpl, const BinItem *__re
     const uint64_t rest = wave_suffix_or(on ? sk[64 + lane] : 0ull, lane);   /* lane i: the rank-i record's rest */
     if (on) sk[128 + lane] = rest;
     wave_lds_sync();
-    if (on) {   /* dmin: float 6; mask: floats 20-21; rest: 22-23 */
+    int start = __shfl(tick, 0);
+    if (start > cap - n) start = -1;   /* does not fit: the cell walks the BVH */
+    if (on && start >= 0) {   /* dmin: float 6; mask: floats 20-21; rest: 22-23 */
         const uint64_t rr = sk[128 + rank];
         q[1].z = it.dmin;
         q[5].x = __uint_as_float((uint32_t)mask);
         q[5].y = __uint_as_float((uint32_t)(mask >> 32));
         q[5].z = __uint_as_float((uint32_t)rr);
         q[5].w = __uint_as_float((uint32_t)(rr >> 32));
-        float4 *dst = reinterpret_cast<float4 *>(out + rank);
+        float4 *dst = reinterpret_cast<float4 *>(region + start + rank);
 #pragma unroll
         for (int r = 0; r < 6; ++r) dst[r] = q[r];
     }
     wave_lds_sync();   /* sk is reused by the wave's next cell */
+    return start;
 }
 
-__global__ __launch_bounds__(64 * kSortWaves) void k_bins_sort(
+/* The queued groups' pairs past the first kExpand (bins_pairs), over this
+ * kernel's grid; launched only when the scene's sizing pass queued groups
+ * (the projection is the scene's fixed camera: every frame queues the same). */
+__global__ __launch_bounds__(256) void k_bins_pairs(const BinItem *__restrict__ items,
+                                                    const int32_t *__restrict__ tpref,
+                                                    const int32_t *__restrict__ gsum, const int32_t *__restrict__ rem,
+                                                    int nt, int tx, int32_t *__restrict__ cnt,
+                                                    uint64_t *__restrict__ keys, int32_t *__restrict__ nonempty,
+                                                    int32_t *__restrict__ bigl, int cap_shard, BinsHdr *__restrict__ hdr2,
+                                                    int par) {
+    bins_pairs(items, tpref, gsum, rem, nt, tx, cnt, keys, nonempty, bigl, cap_shard, hdr2 + par, (int)blockIdx.x,
+               (int)gridDim.x);
+}
+
+/* A cell into its work list (BinsPlan): one lane. */
+__device__ __forceinline__ void bins_list(const BinsPlan &bp, int kind, int sh, Tile t, int off, int len, int c) {
+    const int s2 = atomicAdd(&bp.phdr[bins_phdr_at(bp.par, kind, sh)], 1);
+    (void)BCK(s2, bp.cap[kind], 28);   /* the sizing pass's counts: every frame fits */
+    if (s2 < bp.cap[kind]) {
+        BinsWork w;
+        w.t = t;
+        w.off = off;
+        w.len = len;
+        w.cell = c;
+        w.pad = 0;
+        bp.work[bp.wbase[kind] + sh * bp.cap[kind] + s2] = w;
+    }
+}
+
+__device__ __forceinline__ int bins_kind(const BinsPlan &bp, int n, int start) {
+    return start < 0 ? 3 : n >= bp.split ? 0 : n >= bp.medium ? 1 : 2;
+}
+
+/* One cell's list by the whole wave (n > 16 candidates; n <= 64 in one pass,
+ * longer ones ranked from LDS); its (offset, length) and work-list entry.
+ * c, m, n, k wave-uniform. */
+__device__ void bins_sort_wave(const CamCand *__restrict__ tpl, const BinItem *__restrict__ items,
+                               const uint64_t *__restrict__ keys, const int32_t *__restrict__ every, int ev,
+                               BinsHdr *__restrict__ hdr, CamCand *__restrict__ recs, const BinsCaps &caps,
+                               int32_t *__restrict__ bin_off, int32_t *__restrict__ bin_len, int tx,
+                               const BinsPlan &bp, int c, int m, int n, int k, uint64_t *sk, int lane) {
+    const int sh = c % kBinShards;
+    Tile tl{};
+    if (k >= 0 && bp.work && lane == 0) tl = bp.tiles[k];   /* in flight with the list's loads */
+    int s2 = -1;
+    if (n <= kBinCellCap) {
+        const uint64_t *own = keys + (size_t)c * kBinCellCap;
+        if (n <= 64) {
+            const uint64_t kl = own[BCK(lane, kBinCellCap, 12)];
+            const int e = __shfl(ev, max(lane - m, 0));
+            const uint64_t key = lane < m ? kl : lane < n ? bin_key(0.0f, e) : ~0ull;
+            s2 = bins_emit64(tpl, items, key, n, c % tx, c / tx, recs + caps.base[BCK(sh, kBinShards, 24)], caps.cap[sh],
+                             &hdr->rec[sh].v, sk, lane);
+        } else {
+            if (lane == 0) s2 = atomicAdd(&hdr->rec[sh].v, n);
+            s2 = __shfl(s2, 0);
+            if (s2 > caps.cap[sh] - n) s2 = -1;   /* does not fit: the cell walks the BVH */
+            if (s2 >= 0) {
+                CamCand *out = recs + caps.base[BCK(sh, kBinShards, 24)] + s2;
+                if (n <= 128) bins_emit<2>(tpl, items, own, m, every, n, c % tx, c / tx, out, sk, lane);
+                else if (n <= 256) bins_emit<4>(tpl, items, own, m, every, n, c % tx, c / tx, out, sk, lane);
+                else bins_emit<kBinCellCap / 64>(tpl, items, own, m, every, n, c % tx, c / tx, out, sk, lane);
+            }
+        }
+    }
+    if (lane == 0) {
+        bin_off[BCK(c, BDBG(ncell), 26)] = s2 >= 0 ? caps.base[sh] + s2 : 0;
+        bin_len[BCK(c, BDBG(ncell), 27)] = s2 >= 0 ? n : -1;
+        if (k >= 0 && bp.work)
+            bins_list(bp, bins_kind(bp, n, s2), sh, tl, s2 >= 0 ? caps.base[sh] + s2 : 0, s2 >= 0 ? n : -1, c);
+    }
+}
+
+/* k_bins_sort: the frame's non-empty cells (every cell when some hull is
+ * everywhere).  The grid's first long_waves waves take the cells of more than
+ * 16 candidates (the scatter's long lists), one a wave; the others take the
+ * non-empty lists four cells a wave, 16 lanes each, skipping the long ones
+ * (a cell within 16 of its own but over 16 with the everywhere ids is
+ * finished by the whole wave after).  A cell's keys (its own from the
+ * scatter, then the everywhere ids at dmin 0) are ranked in LDS — each key's
+ * rank is the number of smaller keys (keys are distinct: they hold the id) —
+ * and each record written at its rank in a range reserved with one atomic:
+ * the static part from the triangle's template, dmin from the item, the
+ * cell's pixels inside the triangle's rectangle, and `rest` (the OR of the
+ * masks from here to the list's end).  Then the cell's (offset, length) and
+ * its work-list entry.  Slot i of a list set: shard i % kBinShards, entry
+ * i / kBinShards. */
+constexpr int kSortSlots = 64 / kSortGroup;   /* cells a wave of the first pass */
+
+#ifndef CRT_SORT_WAVES
+#define CRT_SORT_WAVES 1   /* min waves/SIMD asked of k_bins_sort (A/B builds) */
+#endif
+__global__ __launch_bounds__(64 * kSortWaves) __attribute__((amdgpu_waves_per_eu(CRT_SORT_WAVES))) void k_bins_sort(
     const CamCand *__restrict__ tpl, const BinItem *__restrict__ items, int32_t *__restrict__ cnt,
     const uint64_t *__restrict__ keys, const int32_t *__restrict__ every, const int32_t *__restrict__ nonempty,
-    int cap_shard, BinsHdr *__restrict__ hdr2, int par, CamCand *__restrict__ recs, BinsCaps caps,
-    int32_t *__restrict__ bin_off, int32_t *__restrict__ bin_len, int tx, int ncell, BinsPlan bp) {
+    const int32_t *__restrict__ bigl, int cap_shard, int long_waves, BinsHdr *__restrict__ hdr2, int par,
+    CamCand *__restrict__ recs, BinsCaps caps, int32_t *__restrict__ bin_off, int32_t *__restrict__ bin_len, int tx,
+    int ncell, BinsPlan bp) {
     __shared__ uint64_t sks[kSortWaves][kBinCellCap];
     const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    const int l = lane & (kSortGroup - 1), gq = lane / kSortGroup;
     uint64_t *sk = sks[wv];
-    const int wave = (int)blockIdx.x * kSortWaves + wv, nwaves = (int)gridDim.x * kSortWaves;
+    uint64_t *gk = sk + 3 * kSortGroup * gq;   /* the group's keys, masks by rank, rest by rank */
     BSTAMP4(0);
     BinsHdr *hdr = hdr2 + par;
-    int32_t *ph = bp.phdr;
+    const int wave = (int)blockIdx.x * kSortWaves + wv, nwaves = (int)gridDim.x * kSortWaves;
+    /* the everywhere count and ids (lane j: the j-th), the shards' list lengths (lane s: shard s) */
     const int n_every = hdr->n_every.v;
+    const int ev = lane < kBinMaxEverywhere ? every[lane] : 0;   /* valid below n_every */
+    const int nl = lane < kBinShards ? (wave < long_waves ? hdr->nb[lane].v : hdr->ne[lane].v) : 0;
     const bool all = n_every > 0;   /* everywhere hulls: every cell has a list */
-    int mx = lane < kBinShards ? hdr->ne[lane].v : 0;   /* the longest shard list, over the whole wave */
+    int mx = nl;   /* the longest shard list, over the whole wave */
     for (int d = 1; d < 64; d <<= 1) mx = max(mx, __shfl_xor(mx, d));
+    BSTAMP4(1);
+    if (wave < long_waves) {   /* the long lists, one a wave */
+        const int nslots = __builtin_amdgcn_readfirstlane(kBinShards * mx);
+        for (int i = wave; i < nslots; i += long_waves) {
+            const int sh0 = i % kBinShards, e = i / kBinShards;
+            if (e >= __shfl(nl, sh0)) continue;
+            const int c = __builtin_amdgcn_readfirstlane(bigl[BCK(sh0 * cap_shard + e, BDBG(ne_cap), 14)]);
+            const int m = cnt[(size_t)BCK(c, BDBG(ncell), 22) * kCntStride];
+            const int k = bp.cell_tile ? bp.cell_tile[BCK(c, BDBG(ncell), 23)] : -2;   /* -1: not rendered */
+            const int n = n_every > kBinMaxEverywhere ? kBinCellCap + 1 : m + n_every;
+            if (k != -1)
+                bins_sort_wave(tpl, items, keys, every, ev, hdr, recs, caps, bin_off, bin_len, tx, bp, c, m, n, k, sk,
+                               lane);
+        }
+        BSTAMP4(4);
+        return;
+    }
     const int nslots = __builtin_amdgcn_readfirstlane(all ? ncell : kBinShards * mx);   /* wave-uniform: the
                                                        loop body holds the wave's shuffles and LDS hand-offs */
-    BSTAMP4(1);
-    for (int i = wave; i < nslots; i += nwaves) {
-        int c = i;
-        if (!all) {   /* slot i: shard i % kBinShards, entry i / kBinShards */
-            const int sh = i % kBinShards, e = i / kBinShards;
-            if (e >= hdr->ne[sh].v) continue;
-            c = nonempty[BCK(sh * cap_shard + e, BDBG(ne_cap), 21)];
+    const int w1 = wave - long_waves, nw1 = nwaves - long_waves;
+    for (int base = w1 * kSortSlots; base < nslots; base += nw1 * kSortSlots) {
+        const int i = base + gq;
+        int c = -1;
+        if (i < nslots) {
+            if (all) {
+                c = i;
+            } else {
+                const int sh0 = i % kBinShards, e = i / kBinShards;
+                if (e < __shfl(nl, sh0)) c = nonempty[BCK(sh0 * cap_shard + e, BDBG(ne_cap), 21)];
+            }
         }
-        c = __builtin_amdgcn_readfirstlane(c);
-        const int sh = c % kBinShards;
-        const int m = cnt[(size_t)BCK(c, BDBG(ncell), 22) * kCntStride];
-        const int k = bp.cell_tile ? bp.cell_tile[BCK(c, BDBG(ncell), 23)] : -2;   /* -1: no tile of this plan reads the cell */
+        /* the group's cell: its count, tile and first 16 keys in one round of loads */
+        const bool cv = c >= 0;
+        const int m = cv ? cnt[(size_t)BCK(c, BDBG(ncell), 22) * kCntStride] : 0;
+        const int k = !cv ? -1 : bp.cell_tile ? bp.cell_tile[BCK(c, BDBG(ncell), 23)] : -2;   /* -1: not rendered */
+        const uint64_t kl = cv ? keys[BCK((size_t)c * kBinCellCap + l, (int64_t)BDBG(ncell) * kBinCellCap, 11)] : ~0ull;
         const int n = n_every > kBinMaxEverywhere ? kBinCellCap + 1 : m + n_every;
+        const int sh = cv ? c % kBinShards : 0;
+        const bool mine = k != -1 && m <= kSortGroup;   /* longer own lists: the long waves */
+        const bool small = mine && n <= kSortGroup;
+        /* ---- cells of at most 16 candidates: the group's 16 lanes ---- */
+        const bool on = small && l < n;
+        int tick = 0;
+        if (small && l == 0) tick = atomicAdd(&hdr->rec[sh].v, n);
+        const int e2 = __shfl(ev, max(l - m, 0));
+        const uint64_t key = !on ? ~0ull : l < m ? kl : bin_key(0.0f, e2);
+        const int t = (int)(uint32_t)key;
+        Tile tl{};
+        if (small && k >= 0 && bp.work) tl = bp.tiles[k];   /* the cell's tile (its list entry) */
+        BinItem it{};
+        float4 q[6];
+        if (on) {   /* in flight with the atomic and the tile during the ranking */
+            it = items[BCK(t, BDBG(nt), 19)];
+            const float4 *src = reinterpret_cast<const float4 *>(tpl + BCK(t, BDBG(nt), 20));
+#pragma unroll
+            for (int r = 0; r < 6; ++r) q[r] = load_global(src, r);
+        }
+        gk[l] = key;
+        wave_lds_sync();
+        int rank = 0;
+#pragma unroll
+        for (int j = 0; j < kSortGroup; ++j) rank += gk[j] < key ? 1 : 0;
+        const uint64_t mask = on ? bin_mask(it, c % tx, c / tx) : 0ull;
+        gk[kSortGroup + (on ? rank : l)] = mask;   /* positions past the list: 0 */
+        wave_lds_sync();
+        uint64_t rest = gk[kSortGroup + l];
+#pragma unroll
+        for (int d = 1; d < kSortGroup; d <<= 1) {
+            const uint64_t u = shfl_down_u64(rest, d);
+            if (l + d < kSortGroup) rest |= u;
+        }
+        gk[2 * kSortGroup + l] = rest;
+        wave_lds_sync();
+        int start = __shfl(tick, lane & ~(kSortGroup - 1));
+        if (start > caps.cap[sh] - n) start = -1;   /* does not fit: the cell walks the BVH */
+        if (on && start >= 0) {   /* dmin: float 6; mask: floats 20-21; rest: 22-23 */
+            const uint64_t rr = gk[2 * kSortGroup + rank];
+            q[1].z = it.dmin;
+            q[5].x = __uint_as_float((uint32_t)mask);
+            q[5].y = __uint_as_float((uint32_t)(mask >> 32));
+            q[5].z = __uint_as_float((uint32_t)rr);
+            q[5].w = __uint_as_float((uint32_t)(rr >> 32));
+            float4 *dst = reinterpret_cast<float4 *>(recs + caps.base[BCK(sh, kBinShards, 24)] + start + rank);
+#pragma unroll
+            for (int r = 0; r < 6; ++r) dst[r] = q[r];
+        }
+        if (small && l == 0) {
+            bin_off[BCK(c, BDBG(ncell), 26)] = start >= 0 ? caps.base[sh] + start : 0;
+            bin_len[BCK(c, BDBG(ncell), 27)] = start >= 0 ? n : -1;
+            if (k >= 0 && bp.work)
+                bins_list(bp, bins_kind(bp, n, start), sh, tl, start >= 0 ? caps.base[sh] + start : 0, start >= 0 ? n : -1, c);
+        }
+        wave_lds_sync();   /* sk is reused below */
         BSTAMP4(2);
-#ifdef CRT_BINS_STAMPS
-        if (lane == 0 && blockIdx.x < 16384) g_bins_stamps4[6 * blockIdx.x + 5] = (unsigned long long)n;
-#endif
-        int start = -1;
-        if (k != -1 && n <= kBinCellCap) {
-            if (lane == 0) start = atomicAdd(&hdr->rec[sh].v, n);
-            start = __shfl(start, 0);
-            if (start > caps.cap[sh] - n) start = -1;   /* does not fit: the cell walks the BVH */
-        }
-        if (start >= 0) {
-            const uint64_t *own = keys + (size_t)c * kBinCellCap;
-            CamCand *out = recs + caps.base[BCK(sh, kBinShards, 24)] + start;
-            if (n <= 64) bins_emit64(tpl, items, own, m, every, n, c % tx, c / tx, out, sk, lane);
-            else if (n <= 128) bins_emit<2>(tpl, items, own, m, every, n, c % tx, c / tx, out, sk, lane);
-            else if (n <= 256) bins_emit<4>(tpl, items, own, m, every, n, c % tx, c / tx, out, sk, lane);
-            else bins_emit<kBinCellCap / 64>(tpl, items, own, m, every, n, c % tx, c / tx, out, sk, lane);
-        }
-        BSTAMP4(3);
-        if (lane == 0) {
-            if (k != -1) {
-                bin_off[BCK(c, BDBG(ncell), 26)] = start >= 0 ? caps.base[sh] + start : 0;
-                bin_len[BCK(c, BDBG(ncell), 27)] = start >= 0 ? n : -1;
-            }
-            if (k >= 0 && start >= 0 && ph) {   /* the plan's priority lists */
-                if (n >= bp.split) {
-                    const int s2 = atomicAdd(&ph[bins_phdr_at(par, 0, sh)], 1);
-                    if (s2 < bp.ch) {
-                        bp.prio[BCK(sh * bp.ch + s2, BDBG(prio_cap), 28)] = k;
-                        bp.taken[BCK(k, BDBG(ntaken), 29)] = 1;
-                    }
-                } else if (n >= bp.medium) {
-                    const int s2 = atomicAdd(&ph[bins_phdr_at(par, 1, sh)], 1);
-                    if (s2 < bp.cm) {
-                        bp.prio[BCK(kBinShards * bp.ch + sh * bp.cm + s2, BDBG(prio_cap), 30)] = k;
-                        bp.taken[BCK(k, BDBG(ntaken), 31)] = 1;
-                    }
-                }
-            }
-            if (m) cnt[(size_t)BCK(c, BDBG(ncell), 32) * kCntStride] = 0;   /* next frame's counts start at zero */
+        /* ---- within 16 of its own, over 16 with the everywhere ids: the whole wave ---- */
+        uint64_t more = __ballot(l == 0 && mine && !small);
+        while (more) {
+            const int src = __builtin_ctzll(more);
+            more &= more - 1;
+            const int c2 = __builtin_amdgcn_readfirstlane(__shfl(c, src));
+            bins_sort_wave(tpl, items, keys, every, ev, hdr, recs, caps, bin_off, bin_len, tx, bp, c2,
+                           __shfl(m, src), __shfl(n, src), __shfl(k, src), sk, lane);
         }
     }
     BSTAMP4(4);
@@ -555,15 +776,19 @@ int bins_alloc(crt_hip_scene *sc, T **p, size_t n, bool zero = false) {
     return CRT_OK;
 }
 
-int launch_project(crt_hip_scene *sc, hipStream_t s, int par, int32_t *taken, int ntaken, int32_t *phdr) {
+int launch_project(crt_hip_scene *sc, hipStream_t s, int par, int32_t *phdr) {
     BinsDev &b = sc->bins;
     const int groups = (b.nt + kProjTris - 1) / kProjTris;
     hipLaunchKernelGGL(k_bins_project, dim3((unsigned)groups), dim3(256), 0, s, b.tpl, b.nt, b.cam, b.items, b.tpref,
-                       b.gsum, b.every, b.hdr, par, b.len, b.ncell, taken, ntaken, phdr);
+                       b.gsum, b.every, b.hdr, par, phdr, b.len, b.ncell, b.tx, b.cnt, b.keys, b.nonempty, b.bigl,
+                       b.cap_shard, b.rem, b.pair_blocks > 0 ? 1 : 0);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_bins_pairs, dim3((unsigned)b.pair_blocks), dim3(256), 0, s, b.items, b.tpref, b.gsum, groups,
-                       b.nt, b.tx, b.cnt, b.keys, b.nonempty, b.cap_shard, b.hdr, par);
-    HIP_TRY(hipGetLastError());
+    if (b.pair_blocks > 0) {
+        hipLaunchKernelGGL(k_bins_pairs, dim3((unsigned)b.pair_blocks), dim3(256), 0, s, b.items, b.tpref, b.gsum,
+                           b.rem, b.nt, b.tx, b.cnt + (size_t)par * b.ncell * kCntStride, b.keys, b.nonempty, b.bigl,
+                           b.cap_shard, b.hdr, par);
+        HIP_TRY(hipGetLastError());
+    }
     return CRT_OK;
 }
 
@@ -582,10 +807,8 @@ int bins_dbg_arm(crt_hip_scene *sc, const ShardPlan &plan) {
                                           " bound " + std::to_string(d.bound));
     d.nt = b.nt;
     d.ncell = b.ncell;
-    d.ne_cap = kBinShards * b.cap_shard;
     d.rec_cap = b.rec_cap;
-    d.ntaken = plan.bp.taken ? plan.bp.nbase : 0;
-    d.prio_cap = kBinShards * (plan.bp.ch + plan.bp.cm);
+    d.ne_cap = kBinShards * b.cap_shard;
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_bins_dbg), &d, sizeof d));
 #else
     (void)sc;
@@ -616,36 +839,39 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
     if ((rc = bins_alloc(sc, &b.items, (size_t)b.nt)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.tpref, (size_t)((b.nt + kProjTris - 1) / kProjTris) * kProjTris)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.gsum, (size_t)((b.nt + kProjTris - 1) / kProjTris))) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.rem, (size_t)((b.nt + kProjTris - 1) / kProjTris))) != CRT_OK) return rc;
     if ((b.nt + kProjTris - 1) / kProjTris > kMaxGroups) {   /* beyond the BVH's triangle limit: no bins */
         bins_free(sc);
         return CRT_OK;
     }
-    b.pair_blocks = 256;   /* the sizing pass's grid; resized from its pair count below */
-    if ((rc = bins_alloc(sc, &b.cnt, (size_t)b.ncell * kCntStride, true)) != CRT_OK) return rc;
+    b.pair_blocks = 256;   /* the sizing pass's grid; resized from its queued pairs below */
+    if ((rc = bins_alloc(sc, &b.cnt, (size_t)2 * b.ncell * kCntStride, true)) != CRT_OK) return rc;   /* two parities */
     if ((rc = bins_alloc(sc, &b.keys, (size_t)b.ncell * kBinCellCap)) != CRT_OK) return rc;   /* 64-bit keys */
     if ((rc = bins_alloc(sc, &b.every, (size_t)kBinMaxEverywhere)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.nonempty, (size_t)kBinShards * b.cap_shard)) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.bigl, (size_t)kBinShards * b.cap_shard)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.hdr, 2, true)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.off, (size_t)b.ncell, true)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.len, (size_t)b.ncell, true)) != CRT_OK) return rc;
     /* sizing pass: counts per cell of this camera */
     if ((rc = bins_dbg_arm(sc, ShardPlan{})) != CRT_OK) return rc;
-    if ((rc = launch_project(sc, sc->stream, 0, nullptr, 0, nullptr)) != CRT_OK) return rc;
-    std::vector<int32_t> cnt((size_t)b.ncell * kCntStride);
+    if ((rc = launch_project(sc, sc->stream, 0, nullptr)) != CRT_OK) return rc;
+    std::vector<int32_t> cnt((size_t)b.ncell * kCntStride), gsum((size_t)((b.nt + kProjTris - 1) / kProjTris));
     BinsHdr h;
     HIP_TRY(hipMemcpyAsync(cnt.data(), b.cnt, cnt.size() * sizeof(int32_t), hipMemcpyDeviceToHost, sc->stream));
+    HIP_TRY(hipMemcpyAsync(gsum.data(), b.gsum, gsum.size() * sizeof(int32_t), hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipMemcpyAsync(&h, b.hdr, sizeof h, hipMemcpyDeviceToHost, sc->stream));
     const int n_every = h.n_every.v;
     HIP_TRY(hipStreamSynchronize(sc->stream));
-    HIP_TRY(hipMemsetAsync(b.cnt, 0, cnt.size() * sizeof(int32_t), sc->stream));
+    HIP_TRY(hipMemsetAsync(b.cnt, 0, 2 * cnt.size() * sizeof(int32_t), sc->stream));
     HIP_TRY(hipMemsetAsync(b.hdr, 0, 2 * sizeof(BinsHdr), sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
     b.frame = 0;
     b.count.assign((size_t)b.ncell, 0);
-    int64_t pairs = 0;
-    for (int c = 0; c < b.ncell; ++c) pairs += cnt[(size_t)c * kCntStride];
-    b.pair_blocks = (int)std::max<int64_t>(32, std::min<int64_t>(2048, (pairs + 511) / 512));   /* ~2 pairs a thread */
-    int64_t total = 0, shard_rec[kBinShards] = {0}, shard_listed[kBinShards] = {0};
+    int64_t queued = 0;   /* pairs past the first kExpand of their group */
+    for (const int32_t g : gsum) queued += std::max(0, g - kExpand);
+    b.pair_blocks = queued ? (int)std::max<int64_t>(8, std::min<int64_t>(2048, (queued + 511) / 512)) : 0;
+    int64_t total = 0, shard_rec[kBinShards] = {0}, shard_listed[kBinShards] = {0}, shard_long[kBinShards] = {0};
     for (int c = 0; c < b.ncell; ++c) {
         const int64_t n = (int64_t)cnt[(size_t)c * kCntStride] + n_every;
         if (n > kBinCellCap || n_every > kBinMaxEverywhere) {
@@ -655,25 +881,32 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
             total += n;
             shard_rec[c % kBinShards] += n;
         }
-        shard_listed[c % kBinShards] += n > 0;
+        shard_listed[c % kBinShards] += cnt[(size_t)c * kCntStride] > 0;
+        shard_long[c % kBinShards] += cnt[(size_t)c * kCntStride] > kSortGroup;
     }
     if (n_every > kBinMaxEverywhere || total > kBinMeanCap * b.ncell || total >= INT32_MAX / 4) {
         bins_free(sc);   /* the scene walks the BVH */
         return CRT_OK;
     }
     /* each shard's records in a region of its own, sized from the pass with slack */
-    int64_t base = 0, most = 0;
+    int64_t base = 0;
     for (int s2 = 0; s2 < kBinShards; ++s2) {
         const int64_t cap = shard_rec[s2] + shard_rec[s2] / 8 + 256;
         b.caps.base[s2] = (int32_t)base;
         b.caps.cap[s2] = (int32_t)cap;
         base += cap;
-        most = std::max(most, shard_listed[s2]);
     }
     b.rec_cap = (int32_t)base;
     if ((rc = bins_alloc(sc, &b.recs, (size_t)b.rec_cap)) != CRT_OK) return rc;
-    /* one wave per listed cell (every cell when some hull is everywhere) */
-    b.sort_blocks = (int)std::max<int64_t>(64, std::min<int64_t>(16384, n_every > 0 ? b.ncell : kBinShards * most));
+    /* k_bins_sort's grid: a wave per long list (at least kBinShards waves),
+     * then the listed cells (every cell when some hull is everywhere),
+     * kSortSlots a wave */
+    const int64_t most = *std::max_element(shard_listed, shard_listed + kBinShards);
+    const int64_t most_long = *std::max_element(shard_long, shard_long + kBinShards);
+    const int64_t slots = n_every > 0 ? b.ncell : kBinShards * most;
+    b.long_waves = (int)std::max<int64_t>(kBinShards, kBinShards * most_long);
+    const int64_t waves = b.long_waves + (slots + kSortSlots - 1) / kSortSlots;
+    b.sort_blocks = (int)((waves + kSortWaves - 1) / kSortWaves);
     b.records = total;
     b.setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     sc->ds.bins = b.recs;
@@ -683,49 +916,63 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
     return CRT_OK;
 }
 
-/* A plan's camera-bins dispatch (BinsPlan): the base tiles stay in plan order;
- * the render grid puts the heavy-split and the medium waves before them, per
- * shard ch / cm slots.  Capacities from the sizing pass's counts, with slack. */
+/* A plan's camera-bins dispatch (BinsPlan): the work lists' capacities from
+ * the sizing pass's counts (per kind, the fullest shard), the cells the plan
+ * renders as one tile each, and the `rest` tiles. */
 int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
     BinsDev &b = sc->bins;
     const int nb = plan.ntiles;
     std::vector<int32_t> cell_tile((size_t)b.ncell, -1);
+    std::vector<uint8_t> inside((size_t)nb, 0);
     for (int k = 0; k < nb; ++k) {
         const Tile &t = plan.tiles[(size_t)k];
         if ((t.x & 7) + t.w > 8 || (t.y & 7) + t.h > 8) continue;   /* not inside one cell: BVH walk */
+        inside[(size_t)k] = 1;
         int32_t &e = cell_tile[(size_t)(t.y >> 3) * b.tx + (t.x >> 3)];
-        e = e == -1 ? k : -2;   /* several tiles in one cell: none of them split */
-    }
-    int heavy[kBinShards] = {0}, medium[kBinShards] = {0};
-    for (int c = 0; c < b.ncell; ++c) {
-        if (cell_tile[(size_t)c] < 0) continue;
-        const int n = b.count[(size_t)c];
-        if (n >= sc->bins_split) ++heavy[c % kBinShards];
-        else if (n >= kBinsMedium) ++medium[c % kBinShards];
+        e = e == -1 ? k : -2;   /* several tiles in one cell: each reads the cell's list */
     }
     BinsPlan &bp = plan.bp;
-    const int mh = *std::max_element(heavy, heavy + kBinShards), mm = *std::max_element(medium, medium + kBinShards);
-    bp.ch = mh + mh / 4 + (mh > 0 ? 1 : 0);
-    bp.cm = mm + mm / 4 + (mm > 0 ? 1 : 0);
+    bp = BinsPlan{};
     bp.split = sc->bins_split;
     bp.medium = kBinsMedium;
     bp.quad = sc->bins_quad;
-    bp.nbase = nb;
-    bp.par = 0;
-    std::vector<void *> ps(4, nullptr);
-    const size_t sizes[4] = {(size_t)b.ncell, (size_t)std::max(1, nb),
-                             (size_t)std::max(1, kBinShards * (bp.ch + bp.cm)), (size_t)kBinsPhdrInts};
-    for (int i = 0; i < 4; ++i) {
-        HIP_TRY(hipMalloc(&ps[(size_t)i], sizes[i] * sizeof(int32_t)));
-        sc->plan_allocs.push_back(ps[(size_t)i]);
-        HIP_TRY(hipMemset(ps[(size_t)i], 0, sizes[i] * sizeof(int32_t)));
+    int per[kBinKinds][kBinShards] = {};
+    for (int c = 0; c < b.ncell; ++c) {
+        if (cell_tile[(size_t)c] < 0) continue;
+        const int n = b.count[(size_t)c];
+        if (n == 0) continue;   /* the background: a fill wave */
+        ++per[n < 0 ? 3 : n >= bp.split ? 0 : n >= bp.medium ? 1 : 2][c % kBinShards];
     }
-    HIP_TRY(hipMemcpy(ps[0], cell_tile.data(), cell_tile.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-    bp.cell_tile = static_cast<int32_t *>(ps[0]);
-    bp.taken = static_cast<int32_t *>(ps[1]);
-    bp.prio = static_cast<int32_t *>(ps[2]);
-    bp.phdr = static_cast<int32_t *>(ps[3]);
-    plan.waves = 4 * kBinShards * bp.ch + kBinShards * bp.cm + nb;
+    std::vector<int32_t> rest;
+    for (int k = 0; k < nb; ++k) {
+        const Tile &t = plan.tiles[(size_t)k];
+        if (!inside[(size_t)k] || cell_tile[(size_t)(t.y >> 3) * b.tx + (t.x >> 3)] == -2) rest.push_back(k);
+    }
+    int64_t slots = 0;
+    for (int q = 0; q < kBinKinds; ++q) {
+        bp.cap[q] = *std::max_element(per[q], per[q] + kBinShards);
+        bp.wbase[q] = (int32_t)slots;
+        slots += (int64_t)kBinShards * bp.cap[q];
+    }
+    bp.nrest = (int32_t)rest.size();
+    bp.ncell = b.ncell;
+    bp.nfill = (b.ncell + 15) / 16;   /* 16 cells a fill wave */
+    void *p[4] = {nullptr, nullptr, nullptr, nullptr};
+    const size_t sizes[4] = {(size_t)b.ncell * sizeof(int32_t), (size_t)std::max<int64_t>(1, slots) * sizeof(BinsWork),
+                             (size_t)kBinsPhdrInts * sizeof(int32_t), std::max<size_t>(1, rest.size()) * sizeof(int32_t)};
+    for (int i = 0; i < 4; ++i) {
+        HIP_TRY(hipMalloc(&p[i], sizes[i]));
+        sc->plan_allocs.push_back(p[i]);
+        HIP_TRY(hipMemset(p[i], 0, sizes[i]));
+    }
+    HIP_TRY(hipMemcpy(p[0], cell_tile.data(), sizes[0], hipMemcpyHostToDevice));
+    if (!rest.empty()) HIP_TRY(hipMemcpy(p[3], rest.data(), rest.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    bp.cell_tile = static_cast<int32_t *>(p[0]);
+    bp.tiles = plan.d_tiles;
+    bp.work = static_cast<BinsWork *>(p[1]);
+    bp.phdr = static_cast<int32_t *>(p[2]);
+    bp.rest = static_cast<int32_t *>(p[3]);
+    plan.waves = 4 * kBinShards * bp.cap[0] + kBinShards * (bp.cap[1] + bp.cap[2] + bp.cap[3]) + bp.nrest + bp.nfill;
     return CRT_OK;
 }
 
@@ -738,12 +985,15 @@ int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *p
         const int rc0 = bins_dbg_arm(sc, plan);
         if (rc0 != CRT_OK) return rc0;
     }
-    int rc = launch_project(sc, s, par, plan.bp.taken, plan.bp.taken ? plan.bp.nbase : 0, plan.bp.phdr);
+    int rc = launch_project(sc, s, par, plan.bp.phdr);
     if (rc != CRT_OK) return rc;
     BinsPlan bp = plan.bp;
     bp.par = par;
-    hipLaunchKernelGGL(k_bins_sort, dim3((unsigned)((b.sort_blocks + kSortWaves - 1) / kSortWaves)), dim3(64 * kSortWaves), 0, s, b.tpl, b.items, b.cnt, b.keys,
-                       b.every, b.nonempty, b.cap_shard, b.hdr, par, b.recs, b.caps, b.off, b.len, b.tx, b.ncell, bp);
+    hipLaunchKernelGGL(k_bins_sort, dim3((unsigned)b.sort_blocks), dim3(64 * kSortWaves), 0, s, b.tpl, b.items,
+                       b.cnt + (size_t)par * b.ncell * kCntStride,
+                       b.keys, b.every, b.nonempty, b.bigl, b.cap_shard, b.long_waves, b.hdr, par, b.recs, b.caps, b.off,
+                       b.len, b.tx, b.ncell,
+                       bp);
     HIP_TRY(hipGetLastError());
     if (par_out) *par_out = par;
 #ifdef CRT_BINS_STAMPS
@@ -759,7 +1009,7 @@ int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *p
                     std::fprintf(f, "%llu %llu %llu %llu\n", st[4 * i], st[4 * i + 1], st[4 * i + 2], st[4 * i + 3]);
                 std::fclose(f);
             }
-            const int ns = std::min((b.sort_blocks + kSortWaves - 1) / kSortWaves, 16384);
+            const int ns = std::min(b.sort_blocks, 16384);
             std::vector<unsigned long long> s4((size_t)ns * 6);
             HIP_TRY(hipMemcpyFromSymbol(s4.data(), HIP_SYMBOL(g_bins_stamps4), s4.size() * sizeof(unsigned long long)));
             if (FILE *f = std::fopen((std::string(fn) + ".sort").c_str(), "w")) {
@@ -820,7 +1070,8 @@ int crt_hip_bins_time(crt_hip_scene *sc, int32_t frames, double *ms) {
     int rc = CRT_OK;
     for (int w = 0; w < 3 && rc == CRT_OK; ++w) rc = bins_enqueue(sc, sc->full, sc->stream, nullptr);   /* warm */
     hipError_t e = rc == CRT_OK ? hipEventRecord(e0, sc->stream) : hipSuccess;
-    for (int f = 0; f < frames && rc == CRT_OK && e == hipSuccess; ++f) rc = bins_enqueue(sc, sc->full, sc->stream, nullptr);
+    for (int f = 0; f < frames && rc == CRT_OK && e == hipSuccess; ++f)
+        rc = bins_enqueue(sc, sc->full, sc->stream, nullptr);
     if (rc == CRT_OK && e == hipSuccess) e = hipEventRecord(e1, sc->stream);
     if (rc == CRT_OK && e == hipSuccess) e = hipEventSynchronize(e1);
     float f = 0.f;

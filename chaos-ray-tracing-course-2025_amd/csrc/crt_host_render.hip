@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -31,13 +32,24 @@ std::vector<float> g_gi_host;
 
 constexpr int64_t kGiN = int64_t(1) << 23;
 
+/* Host threads for the table builds: the process's CPU quota (OMP_NUM_THREADS
+ * when set, as on the GPU boxes), at most 64. */
+unsigned table_threads() {
+    unsigned n = std::thread::hardware_concurrency();
+    if (const char *e = std::getenv("OMP_NUM_THREADS")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v > 0) n = (unsigned)v;
+    }
+    return std::max(1u, std::min(64u, n));
+}
+
 void build_gi_host_tables() {
     if (!g_gi_host.empty()) return;
     g_gi_host.resize((size_t)(4 * kGiN));
     /* (cos, sin) pairs: one 8-B read per angle (the tables are 64 MB each and
      * read at random: one cache line per angle instead of two) */
     float *pi2 = g_gi_host.data(), *tau2 = pi2 + 2 * kGiN;
-    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned nt = table_threads();
     std::vector<std::thread> pool;
     for (unsigned w = 0; w < nt; ++w) {
         pool.emplace_back([=]() {
@@ -129,9 +141,8 @@ int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool 
         plan.packed_pixels = total;
     }
     if (bins_active(sc) && !tiles.empty()) {
-        /* camera bins: the tiles stay in plan order; each frame's binning
-         * queues its heavy and medium cells for the waves dispatched first
-         * (crt_bins.hip bins_plan) */
+        /* camera bins: each frame's binning lists the cells by list length
+         * for the render grid, heaviest first (crt_bins.hip bins_plan) */
         plan.cost.clear();
     } else if (!sc->calib.empty() && !tiles.empty()) {
         /* measured costs: split as calibrated, heaviest first */
@@ -325,7 +336,7 @@ void build_pow5_host_table() {
     if (!g_pow5_host.empty()) return;
     g_pow5_host.resize((size_t)kPow5N);
     float *t = g_pow5_host.data();
-    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned nt = table_threads();
     std::vector<std::thread> pool;
     for (unsigned w = 0; w < nt; ++w) {
         pool.emplace_back([=]() {
@@ -339,12 +350,25 @@ void build_pow5_host_table() {
     for (auto &th : pool) th.join();
 }
 
+/* The host tables are built once per process, in the background from the
+ * first scene create that needs them (start_host_tables), overlapping the
+ * rest of the create; the device copy waits for them (ensure_*). */
+std::mutex g_fut_mu;
+std::shared_future<void> g_gi_fut, g_pow5_fut;
+
+void start_host_tables(bool gi, bool pow5) {
+    std::lock_guard<std::mutex> g(g_fut_mu);
+    if (gi && !g_gi_fut.valid()) g_gi_fut = std::async(std::launch::async, build_gi_host_tables).share();
+    if (pow5 && !g_pow5_fut.valid()) g_pow5_fut = std::async(std::launch::async, build_pow5_host_table).share();
+}
+
 int ensure_pow5_table(crt_hip_scene *sc) {
     if (sc->ds.pow5) return CRT_OK;
+    start_host_tables(false, true);
     std::lock_guard<std::mutex> g(g_pow5_mu);
     float *&d = g_pow5[sc->device];
     if (!d) {
-        build_pow5_host_table();
+        g_pow5_fut.wait();
         void *p = nullptr;
         HIP_TRY(hipMalloc(&p, (size_t)kPow5N * sizeof(float)));
         HIP_TRY(hipMemcpy(p, g_pow5_host.data(), (size_t)kPow5N * sizeof(float), hipMemcpyHostToDevice));
@@ -356,10 +380,11 @@ int ensure_pow5_table(crt_hip_scene *sc) {
 
 int ensure_gi_tables(crt_hip_scene *sc) {
     if (sc->ds.gi_pi) return CRT_OK;
+    start_host_tables(true, false);
     std::lock_guard<std::mutex> g(g_gi_mu);
     GiTables &t = g_gi[sc->device];
     if (!t.d) {
-        build_gi_host_tables();
+        g_gi_fut.wait();
         void *p = nullptr;
         HIP_TRY(hipMalloc(&p, (size_t)(4 * kGiN) * sizeof(float)));
         HIP_TRY(hipMemcpy(p, g_gi_host.data(), (size_t)(4 * kGiN) * sizeof(float), hipMemcpyHostToDevice));

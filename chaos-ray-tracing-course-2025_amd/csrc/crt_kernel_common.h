@@ -25,23 +25,38 @@ struct alignas(16) Tile {
  * device-scope atomic on one word serialises at ~88 per microsecond. */
 constexpr int kBinShards = 16;
 
-/* Camera-bins dispatch of a tile plan (crt_bins.hip): the render grid's first
- * 4 x kBinShards x ch waves take the cells k_bins_sort queued as heavy (four
- * 4x4 waves each; slot i of shard s at 4 (i kBinShards + s)), the next
- * kBinShards x cm the medium ones (one 8x8 wave each), the rest the plan's
- * base tiles in plan order, skipping the ones a priority wave took. */
+/* Camera-bins dispatch of a tile plan (crt_bins.hip).  Every frame's
+ * k_bins_sort puts each cell the plan renders as one tile into a work list by
+ * its list length n — heavy (n >= split: four 4x4 waves, four lanes a pixel),
+ * medium (n >= kBinsMedium), light (n >= 1), bvh (over the cap: the BVH walk) —
+ * with the tile and the cell's (offset, length).  The render grid is the lists
+ * in that order (kind q: kBinShards x cap[q] slots, slot i of shard s at
+ * i kBinShards + s; heavy slots four waves each), then the plan's `rest` tiles
+ * (not inside one cell, or sharing a cell), which read the cell's list
+ * themselves, then the fill waves: 16 cells each, the background written to
+ * the tiles of the cells with no candidate (every pixel misses).  The lists'
+ * capacities are the scene's sizing-pass counts: the camera is the scene's, so
+ * every frame fills them alike. */
+constexpr int kBinKinds = 4;   /* heavy, medium, light, bvh */
+struct alignas(16) BinsWork {
+    Tile t;
+    int32_t off, len;   /* the cell's records (len -1: the BVH walk) */
+    int32_t cell, pad;
+};
 struct BinsPlan {
     int32_t *cell_tile;   /* per cell: the plan's one tile inside it; -1 none (the cell is not rendered), -2 several */
-    int32_t *taken;       /* per base tile: rendered by a priority wave this frame */
-    int32_t *prio;        /* base-tile indices: heavy kBinShards x ch, then medium kBinShards x cm */
-    int32_t *phdr;        /* cells queued this frame: counter bins_phdr_at(parity, heavy 0 / medium 1, shard) */
-    int32_t ch, cm, nbase;
+    const Tile *tiles;    /* the plan's tiles */
+    BinsWork *work;       /* the lists: kind q, shard s, entry i at wbase[q] + s cap[q] + i */
+    int32_t *phdr;        /* entries listed this frame: counter bins_phdr_at(parity, kind, shard) */
+    const int32_t *rest;  /* tiles the lists do not hold */
+    int32_t cap[kBinKinds], wbase[kBinKinds];
+    int32_t nrest, nfill, ncell;
     int32_t split, medium, quad;
     int32_t par;          /* the frame's parity (which counters it uses) */
 };
 
-/* Per-frame counters of the device binning (crt_bins.hip), two sets used by
- * alternate frames: a frame's first kernel zeroes the other set for the next.
+/* The device binning's per-frame counters, two sets (frames alternate; a
+ * frame's first kernel zeroes the other set for the next frame).
  * Every counter has a 256-B line of its own (atomics on one line serialise,
  * whatever word they name). */
 constexpr int kBinPad = 64;   /* int32 per counter */
@@ -51,14 +66,16 @@ struct alignas(256) BinsCtr {
 };
 struct BinsHdr {
     BinsCtr n_every;
+    BinsCtr nrem;              /* groups whose pairs past the first kExpand k_bins_pairs scatters */
     BinsCtr ne[kBinShards];    /* non-empty cells listed per shard */
+    BinsCtr nb[kBinShards];    /* cells of more than 16 candidates listed per shard */
     BinsCtr rec[kBinShards];   /* records reserved per shard */
 };
-/* a plan's priority-list counters (BinsPlan::phdr): kind 0 heavy, 1 medium */
+/* a plan's work-list counters (BinsPlan::phdr) */
 __host__ __device__ constexpr int bins_phdr_at(int par, int kind, int sh) {
-    return ((par * 2 + kind) * kBinShards + sh) * kBinPad;
+    return ((par * kBinKinds + kind) * kBinShards + sh) * kBinPad;
 }
-constexpr int kBinsPhdrInts = 4 * kBinShards * kBinPad;
+constexpr int kBinsPhdrInts = 2 * kBinKinds * kBinShards * kBinPad;
 
 /* Where each shard's records go in the camera-bins record buffer. */
 struct BinsCaps {

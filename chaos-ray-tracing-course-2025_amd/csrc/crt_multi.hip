@@ -272,6 +272,14 @@ int crt_hip_scene_create_on(const crt_scene_desc *desc, const int32_t *devices, 
     const int mode = tree_mode(desc, flags);
     if (mode != CRT_SCENE_TREE_HOST && mode != CRT_SCENE_TREE_DEVICE) return set_error(CRT_E_INVALID, "bad tree build flag");
     const auto t0 = std::chrono::steady_clock::now();
+    {   /* the libm tables this scene's frames read: built in the background from here on (crt_host_render.hip) */
+        bool diffuse = false, refractive = false;
+        for (int i = 0; i < desc->material_count && desc->materials; ++i) {
+            diffuse = diffuse || desc->materials[i].type == CRT_MATERIAL_DIFFUSE;
+            refractive = refractive || desc->materials[i].type == CRT_MATERIAL_REFRACTIVE;
+        }
+        start_host_tables(desc->gi_on && diffuse, desc->refractions_on && refractive);
+    }
     std::unique_ptr<HostScene> hs(new HostScene());
     int rc = prepare_scene(desc, *hs, mode == CRT_SCENE_TREE_HOST);
     if (rc != CRT_OK) return rc;

@@ -13,28 +13,42 @@
 namespace crt_amd {
 
 /* The tile a wave of a camera-bins grid renders (crt_kernel_common.h
- * BinsPlan): a quarter of a heavy cell, a medium cell, or the next base tile
- * no priority wave took.  false: nothing to do (an unused priority slot). */
-__device__ __forceinline__ bool bins_tile(const BinsPlan &bp, const Tile *__restrict__ tiles, int wave, Tile &tl) {
-    const int nh = 4 * kBinShards * bp.ch, nm = kBinShards * bp.cm;
-    int k, q = -1;
-    if (wave < nh) {
-        const int slot = wave >> 2, sh = slot % kBinShards, i = slot / kBinShards;
-        if (i >= min(load_scalar(bp.phdr, bins_phdr_at(bp.par, 0, sh)), bp.ch)) return false;
-        k = load_scalar(bp.prio, sh * bp.ch + i);
-        q = wave & 3;
-    } else if (wave < nh + nm) {
-        const int slot = wave - nh, sh = slot % kBinShards, i = slot / kBinShards;
-        if (i >= min(load_scalar(bp.phdr, bins_phdr_at(bp.par, 1, sh)), bp.cm)) return false;
-        k = load_scalar(bp.prio, kBinShards * bp.ch + sh * bp.cm + i);
-    } else {
-        k = wave - nh - nm;
-        if (k >= bp.nbase || load_scalar(bp.taken, k) != 0) return false;
+ * BinsPlan): a quarter of a heavy cell, a medium, light or bvh cell of this
+ * frame's work lists (with the cell's list: off, len), or a rest tile (len
+ * -2: the wave reads its cell's list).  The list's count and the entry are
+ * loaded together.  Returns 0: nothing to do (an unused list slot), 1: the
+ * tile, 2: a fill wave (off: its index). */
+__device__ __forceinline__ int bins_tile(const BinsPlan &bp, const Tile *__restrict__ tiles, int wave, Tile &tl,
+                                         int &off, int &len) {
+    int kind = 0, slot = wave >> 2, q = wave & 3;
+    if (wave >= 4 * kBinShards * bp.cap[0]) {
+        slot = wave - 4 * kBinShards * bp.cap[0];
+        q = -1;
+        kind = 1;
+        while (kind < kBinKinds && slot >= kBinShards * bp.cap[kind]) {
+            slot -= kBinShards * bp.cap[kind];
+            ++kind;
+        }
+        if (kind == kBinKinds) {
+            if (slot >= bp.nrest) {
+                off = slot - bp.nrest;
+                return 2;
+            }
+            tl = tiles[load_scalar(bp.rest, slot)];
+            len = -2;
+            return 1;
+        }
     }
-    tl = tiles[k];
+    const int sh = slot % kBinShards, i = slot / kBinShards;
+    const int n = load_scalar(bp.phdr, bins_phdr_at(bp.par, kind, sh));
+    const BinsWork w = bp.work[bp.wbase[kind] + sh * bp.cap[kind] + i];
+    if (i >= min(n, bp.cap[kind])) return 0;
+    tl = w.t;
+    off = w.off;
+    len = w.len;
     if (q >= 0) {
         const int xx = (q & 1) * 4, yy = (q >> 1) * 4;
-        if (xx >= tl.w || yy >= tl.h) return false;
+        if (xx >= tl.w || yy >= tl.h) return 0;
         tl.x += xx;
         tl.y += yy;
         tl.w = min(4, tl.w - xx);
@@ -42,7 +56,56 @@ __device__ __forceinline__ bool bins_tile(const BinsPlan &bp, const Tile *__rest
         tl.out_base += (int64_t)yy * tl.out_stride + xx;
         tl.prio = bp.quad ? 3 : 1;
     }
-    return true;
+    return 1;
+}
+
+/* A fill wave of the camera-bins grid: of its 16 cells, the ones the plan
+ * renders as one tile whose list is empty get the background (every camera
+ * ray of the cell misses: no triangle's hull projects there).  A full 8x8
+ * tile on 16-B aligned rows is written as 48 float4, else pixel by pixel.
+ * Work-count frames count these rays as traversals (the reference traces
+ * them; they test nothing). */
+__device__ void bins_fill(const DeviceScene &s, const BinsPlan &bp, const Tile *__restrict__ tiles, int fw,
+                          float *__restrict__ out, unsigned long long *__restrict__ counters) {
+    const int lane = (int)__lane_id();
+    const int c = fw * 16 + (lane & 15);
+    bool e = false;
+    int k = -1;
+    if (lane < 16 && c < bp.ncell) {   /* the cell's tile and list length in one round of loads */
+        k = bp.cell_tile[c];
+        e = s.bin_len[c] == 0 && k >= 0;
+    }
+    Tile t{};
+    if (e) t = tiles[k];
+    const float bg[3] = {s.background[0], s.background[1], s.background[2]};
+    uint64_t todo = __ballot(e);
+    while (todo) {
+        const int j = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        const int w = __shfl(t.w, j), h = __shfl(t.h, j), stride = __shfl(t.out_stride, j);
+        const int64_t base = ((int64_t)(uint32_t)__shfl((int)(uint32_t)t.out_base, j)) |
+                             ((int64_t)__shfl((int)(t.out_base >> 32), j) << 32);
+        if (w == 8 && h == 8 && (base & 3) == 0 && (stride & 3) == 0) {
+            if (lane < 48) {   /* row lane / 6, float4 lane % 6 of its 24 floats */
+                const int row = lane / 6, q4 = lane % 6;
+                float4 v;
+                v.x = bg[(4 * q4) % 3];
+                v.y = bg[(4 * q4 + 1) % 3];
+                v.z = bg[(4 * q4 + 2) % 3];
+                v.w = bg[(4 * q4 + 3) % 3];
+                *reinterpret_cast<float4 *>(out + 3 * (base + (int64_t)row * stride) + 4 * q4) = v;
+            }
+        } else {
+            const int x = lane & 7, y = lane >> 3;
+            if (x < w && y < h) {
+                float *o = out + 3 * (base + (int64_t)y * stride + x);
+                o[0] = bg[0];
+                o[1] = bg[1];
+                o[2] = bg[2];
+            }
+        }
+        if (counters && lane == 0) atomicAdd(&counters[0], (unsigned long long)(w * h));
+    }
 }
 
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW>
@@ -61,8 +124,11 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
     /* diagnostic build only (stamps != nullptr): wave start / end in s_memrealtime ticks (100 MHz) */
     if (stamps && lane == 0) stamps[2 * wave] = __builtin_amdgcn_s_memrealtime();
     Tile tl;
+    int bin_beg = 0, bin_len = -2;   /* camera bins: the cell's list from the work list (-2: read it below) */
     if constexpr (TRAV == 15 && !FULL && !SHADOW) {
-        if (!bins_tile(bp, tiles, wave, tl)) return;
+        const int r = bins_tile(bp, tiles, wave, tl, bin_beg, bin_len);
+        if (r == 2) bins_fill(s, bp, tiles, bin_beg, out, COUNT ? counters : nullptr);
+        if (r != 1) return;
     } else {
         (void)bp;
         tl = tiles[wave];
@@ -122,9 +188,10 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
         /* a tile inside one 8x8 camera-bins cell: the cell's candidate list */
         const int tx0 = uniform_i(tl.x), ty0 = uniform_i(tl.y), tw = uniform_i(tl.w), th = uniform_i(tl.h);
         const int cell = (ty0 >> 3) * s.bin_tx + (tx0 >> 3);
-        const int len = (tx0 & 7) + tw <= 8 && (ty0 & 7) + th <= 8 ? load_scalar(s.bin_len, cell) : -1;
+        const bool one = (tx0 & 7) + tw <= 8 && (ty0 & 7) + th <= 8;
+        const int len = uniform_i(bin_len != -2 ? bin_len : one ? load_scalar(s.bin_len, cell) : -1);
         if (len >= 0) {   /* -1: not inside one cell, or the cell's list is over the cap: the BVH walk below */
-            const int beg = load_scalar(s.bin_off, cell), end = beg + len;
+            const int beg = uniform_i(bin_len != -2 ? bin_beg : load_scalar(s.bin_off, cell)), end = beg + len;
             __shared__ CamCand stage[4 * kBinChunk];
             if ((tl.prio & 2) && tw <= 4 && th <= 4) {
                 /* a split tile of a long list: four lanes per pixel (trace_bins_lanes) */

@@ -28,7 +28,7 @@ namespace crt_amd {
 struct ShardPlan {
     Tile *d_tiles = nullptr;
     int ntiles = 0;
-    int waves = 0;               /* waves of the render grid (camera bins: priority waves + ntiles) */
+    int waves = 0;               /* waves of the render grid (camera bins: the work lists' slots + rest tiles) */
     BinsPlan bp{};               /* camera-bins dispatch (crt_bins.hip bins_plan); cell_tile null otherwise */
     int64_t packed_pixels = 0;
     std::vector<Tile> tiles;     /* host copy, dispatch order */
@@ -48,12 +48,15 @@ struct BinsDev {
     crt_amd::BinItem *items = nullptr;    /* per triangle: this frame's projection */
     int32_t *tpref = nullptr;             /* per triangle: pair prefix inside its group of k_bins_project */
     int32_t *gsum = nullptr;              /* per group: pairs */
-    int pair_blocks = 0;                  /* k_bins_pairs grid */
-    int32_t *cnt = nullptr;               /* per cell: candidates (zero between frames) */
+    int32_t *rem = nullptr;               /* groups queued for k_bins_pairs */
+    int pair_blocks = 0;                  /* k_bins_pairs grid (0: not launched; the sizing pass queued none) */
+    int32_t *cnt = nullptr;               /* per cell: candidates; two parities (a frame zeroes the other's) */
     uint64_t *keys = nullptr;             /* per cell: kBinCellCap sort keys (dmin bits << 32 | triangle id) */
     int32_t *every = nullptr;             /* everywhere triangles */
     int32_t *nonempty = nullptr;          /* cells with a candidate: kBinShards lists of cap_shard, arrival order */
+    int32_t *bigl = nullptr;              /* cells of more than 16 candidates: kBinShards lists of cap_shard */
     int cap_shard = 0;
+    int long_waves = 0;                   /* k_bins_sort waves for the long lists */
     crt_amd::BinsHdr *hdr = nullptr;      /* two sets: frames alternate */
     uint64_t frame = 0;                   /* frames binned (parity = frame & 1) */
     crt_amd::BinsCaps caps{};             /* per shard: its region of recs */
@@ -61,7 +64,7 @@ struct BinsDev {
     int32_t rec_cap = 0;
     int32_t *off = nullptr, *len = nullptr;   /* per cell */
     std::vector<int32_t> count;           /* per cell: list length of the sizing pass (-1 over the cap) */
-    int sort_blocks = 0;                  /* k_bins_sort waves */
+    int sort_blocks = 0;                  /* k_bins_sort blocks */
     int64_t records = 0;                  /* records of the sizing pass */
     double setup_ms = 0.0;
     std::vector<void *> allocs;
@@ -222,6 +225,9 @@ int sync_device_record(crt_hip_scene *sc, const DeviceScene **out);
 int check_settings(const crt_renderer_settings *st);
 int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t stream, bool render = false);
 void warm_code_objects(int device, hipStream_t stream);
+void start_host_tables(bool gi, bool pow5);
+int ensure_gi_tables(crt_hip_scene *sc);
+int ensure_pow5_table(crt_hip_scene *sc);
 /* camera frames of this scene walk the camera bins (walk 15): built, enabled,
  * and the default camera walk selected */
 inline bool bins_active(const crt_hip_scene *sc) { return sc->ds.bins && sc->bins_on && sc->traversal == 14; }

@@ -21,17 +21,25 @@ print("lib", N.LIB_PATH, N.build_id(), flush=True)
 cases = [("14-01-acceleration-tree__scene1", None), ("14-01-acceleration-tree__scene1", (333, 177)),
          ("12-01-textures__scene4", (640, 360)), ("09-02-diffuse-smooth-shading__scene3", (480, 270)),
          ("13-01-optimizations__scene0", (640, 360))]
+from test_gpu_bins import floor_scene, wall_scene  # noqa: E402
+
+cases += [("14-01-acceleration-tree__scene1", (3840, 2160)), ("wall", (640, 360)), ("wall", (1920, 1080)), ("floor", (400, 240))]
 st = N.RendererSettings.default()
 for name, size in cases:
-    sc = load_npz(ROOT / "tests" / "golden" / "scenes" / f"{name}.npz")
-    if size:
-        sc.set_resolution(*size)
+    if name == "wall":
+        sc = wall_scene(N, *size)
+    elif name == "floor":
+        sc = floor_scene(N, *size)
+    else:
+        sc = load_npz(ROOT / "tests" / "golden" / "scenes" / f"{name}.npz")
+        if size:
+            sc.set_resolution(*size)
     hl, hr = N.HostScene(sc).camera_bins()
     g = N.HipScene(sc)
     for _ in range(3):
         dl, dr = g.camera_bins()
         assert np.array_equal(hl, dl) and hr.tobytes() == dr.tobytes(), name
-    want = pyoracle.OracleScene(sc).render(st) if size else None
+    want = pyoracle.OracleScene(sc).render(st) if size and size[0] <= 640 else None
     for _ in range(3):
         img = g.render(st)
         if want is not None:

@@ -34,6 +34,20 @@ def floor_scene(N, w, h, n=600, seed=5, cam=(0.0, 0.3, 0.0), rot=None, fov=70.0)
     return N.SyntheticScene(pos, idx, width=w, height=h, camera_location=cam, camera_rotation=rot, fov_degrees=fov)
 
 
+def wall_scene(N, w, h, n=400, seed=9):
+    """A triangle cloud in front of two large walls, wholly in front of the
+    camera: each wall triangle covers thousands of cells, so its group has more
+    pairs than k_bins_project scatters itself and queues the rest for
+    k_bins_pairs."""
+    rng = np.random.default_rng(seed)
+    c = rng.uniform([-2.0, -1.0, -6.0], [2.0, 1.0, -3.0], (n, 3)).astype(np.float32)
+    v = (c[:, None, :] + rng.uniform(-0.2, 0.2, (n, 3, 3))).astype(np.float32).reshape(-1, 3)
+    wall = np.array([[-30, -20, -9], [30, -20, -9], [30, 20, -9], [-30, 20, -9]], np.float32)
+    b = len(v)
+    idx = np.concatenate([np.arange(b, dtype=np.int32), np.array([b, b + 1, b + 2, b, b + 2, b + 3], np.int32)])
+    return N.SyntheticScene(np.concatenate([v, wall], 0), idx, width=w, height=h, fov_degrees=80.0)
+
+
 CASES = [("14-01-acceleration-tree__scene1", None), ("14-01-acceleration-tree__scene1", (333, 177)),
          ("14-01-acceleration-tree__scene1", (3840, 2160)), ("14-01-acceleration-tree__scene0", None),
          ("12-01-textures__scene4", None), ("12-01-textures__scene3", (517, 301)),
@@ -66,6 +80,16 @@ def test_device_bins_everywhere_and_overflow(N):
     sc = floor_scene(N, 400, 240)
     ln = _compare(N, sc)
     assert (ln >= 2).all() or (ln < 0).any()   # the floor is in every cell's list
+
+
+@pytest.mark.parametrize("size", [(640, 360), (1920, 1080)])
+def test_device_bins_queued_groups(N, oracle, size):
+    """Groups with more pairs than the projection block scatters (the walls)."""
+    sc = wall_scene(N, *size)
+    _compare(N, sc)
+    if size[0] <= 640:
+        st = N.RendererSettings.default()
+        assert np.array_equal(bits(N.HipScene(sc).render(st)), bits(oracle.OracleScene(sc).render(st)))
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
