@@ -277,9 +277,13 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
     warm_code_objects(sc->device, sc->stream);
     /* camera bins (crt_bins.hip), rebuilt on the device by every camera frame
      * of scenes whose camera rays the tile kernels trace without recursion
-     * (no reflective / refractive material, no GI with a diffuse one) */
-    if (hs.bnode_count > 0 && hs.tree_on_host && !sc->has_secondary && !(hs.gi_on && sc->has_diffuse))
+     * (no reflective / refractive material, no GI with a diffuse one); on a
+     * scene without the BVH (> 2^18 triangles) only when no cell's list is
+     * over the cap (those cells walk the BVH) */
+    if (!sc->has_secondary && !(hs.gi_on && sc->has_diffuse)) {
         if ((rc = bins_setup(sc.get(), hs)) != CRT_OK) return rc;
+        if (ds.bins) sc->traversal = 14;   /* bins off: the BVH walk, or the kd walk without a BVH */
+    }
     HIP_TRY(hipEventCreate(&sc->ev_start));
     HIP_TRY(hipEventCreate(&sc->ev_stop));
     void *p = nullptr;

@@ -840,7 +840,7 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
     if ((rc = bins_alloc(sc, &b.tpref, (size_t)((b.nt + kProjTris - 1) / kProjTris) * kProjTris)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.gsum, (size_t)((b.nt + kProjTris - 1) / kProjTris))) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.rem, (size_t)((b.nt + kProjTris - 1) / kProjTris))) != CRT_OK) return rc;
-    if ((b.nt + kProjTris - 1) / kProjTris > kMaxGroups) {   /* beyond the BVH's triangle limit: no bins */
+    if ((int64_t)b.ncell * kBinMeanCap / kExpand > kMaxGroups) {   /* k_bins_pairs could queue more groups than it scans */
         bins_free(sc);
         return CRT_OK;
     }
@@ -884,8 +884,11 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
         shard_listed[c % kBinShards] += cnt[(size_t)c * kCntStride] > 0;
         shard_long[c % kBinShards] += cnt[(size_t)c * kCntStride] > kSortGroup;
     }
-    if (n_every > kBinMaxEverywhere || total > kBinMeanCap * b.ncell || total >= INT32_MAX / 4) {
-        bins_free(sc);   /* the scene walks the BVH */
+    bool over = false;   /* some cell over the cap: it walks the BVH */
+    for (int c = 0; c < b.ncell; ++c) over = over || b.count[(size_t)c] < 0;
+    if (n_every > kBinMaxEverywhere || total > kBinMeanCap * b.ncell || total >= INT32_MAX / 4 ||
+        (over && !sc->ds.bnodes)) {
+        bins_free(sc);   /* the scene walks the BVH (or the kd tree) */
         return CRT_OK;
     }
     /* each shard's records in a region of its own, sized from the pass with slack */
@@ -946,6 +949,7 @@ int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
     std::vector<int32_t> rest;
     for (int k = 0; k < nb; ++k) {
         const Tile &t = plan.tiles[(size_t)k];
+        if (!inside[(size_t)k] && !sc->ds.bnodes) return CRT_OK;   /* no BVH for it: not a bins plan (the kd walk) */
         if (!inside[(size_t)k] || cell_tile[(size_t)(t.y >> 3) * b.tx + (t.x >> 3)] == -2) rest.push_back(k);
     }
     int64_t slots = 0;

@@ -882,30 +882,26 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         if (trav == 10 || trav == 14) CRT_LAUNCH_T(true, MAXF, 10, COUNT);                                  \
         else CRT_LAUNCH_T(true, MAXF, 4, COUNT);                                                           \
     } while (0)
-    if (!full) {
+    if (!full && bins_active(sc) && plan.bp.cell_tile) {
+        /* this frame's camera bins, then the render over the bins plan's grid */
+        int par = 0;
+        const int rc = bins_enqueue(sc, plan, stream, &par);
+        if (rc != CRT_OK) return rc;
+        BinsPlan bp = plan.bp;
+        bp.par = par;
+        const unsigned bb = (unsigned)((plan.waves + 3) / 4);
+#define CRT_LAUNCH_B(COUNT)                                                                                 \
+    hipLaunchKernelGGL((k_render_tiles<false, 0, 15, 15, COUNT>), dim3(bb), dim3(256), 0, stream, d_scene, ds, \
+                       plan.d_tiles, plan.waves, d_out, cnt, stamps, bp)
+        if (count) CRT_LAUNCH_B(true); else CRT_LAUNCH_B(false);
+#undef CRT_LAUNCH_B
+    } else if (!full) {
         switch (trav) {
         case 7: if (count) CRT_LAUNCH_T(false, 0, 7, true); else CRT_LAUNCH_T(false, 0, 7, false); break;
         case 8: if (count) CRT_LAUNCH_T(false, 0, 8, true); else CRT_LAUNCH_T(false, 0, 8, false); break;
         case 12: if (count) CRT_LAUNCH_T(false, 0, 12, true); else CRT_LAUNCH_T(false, 0, 12, false); break;
         case 13: if (count) CRT_LAUNCH_T(false, 0, 13, true); else CRT_LAUNCH_T(false, 0, 13, false); break;
-        case 14:
-            if (bins_active(sc) && plan.bp.cell_tile) {
-                /* this frame's camera bins, then the render over the bins plan's grid */
-                int par = 0;
-                const int rc = bins_enqueue(sc, plan, stream, &par);
-                if (rc != CRT_OK) return rc;
-                BinsPlan bp = plan.bp;
-                bp.par = par;
-                const unsigned bb = (unsigned)((plan.waves + 3) / 4);
-#define CRT_LAUNCH_B(COUNT)                                                                                 \
-    hipLaunchKernelGGL((k_render_tiles<false, 0, 15, 15, COUNT>), dim3(bb), dim3(256), 0, stream, d_scene, ds, \
-                       plan.d_tiles, plan.waves, d_out, cnt, stamps, bp)
-                if (count) CRT_LAUNCH_B(true); else CRT_LAUNCH_B(false);
-#undef CRT_LAUNCH_B
-            } else {
-                if (count) CRT_LAUNCH_T(false, 0, 14, true); else CRT_LAUNCH_T(false, 0, 14, false);
-            }
-            break;
+        case 14: if (count) CRT_LAUNCH_T(false, 0, 14, true); else CRT_LAUNCH_T(false, 0, 14, false); break;
         default: return set_error(CRT_E_INVALID, "no such camera walk");
         }
     } else if (rec_machine || (gi && (trav == 4 || trav == 10 || trav == 14) && sc->gi_refill && sc->d_next_px && !stamps &&
