@@ -251,6 +251,7 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
         if ((rc = upload(sc.get(), hs.btri_id, &ds.btri_id)) != CRT_OK) return rc;
         ds.bnode_count = hs.bnode_count;
         if ((rc = upload(sc.get(), hs.ktopo, &ds.ktopo)) != CRT_OK) return rc;
+        if ((rc = upload(sc.get(), hs.ktopo2, &ds.ktopo2)) != CRT_OK) return rc;
     }
     sc->camera_fast = camera_rays_fast(hs, ds.planes_ok != 0);
     if (ds.bnodes) sc->traversal = 14;   /* camera rays through the BVH too */

@@ -43,6 +43,9 @@
 #ifndef CRT_BVH_PREFETCH
 #define CRT_BVH_PREFETCH 1
 #endif
+#ifndef CRT_PROOF_TOPO2
+#define CRT_PROOF_TOPO2 1    /* 0: the proof's descent loads one KTopo a level even where KTopo2 exists */
+#endif
 
 namespace crt_amd {
 
@@ -345,6 +348,53 @@ CRT_HD bool topo_level(const KTopo *topo, Vec p, TopoWalk &w) {
     return true;
 }
 
+/* KTopo2 entry LO + k, k < N (N a power of two): a tree of selects on the
+ * record's registers (a dynamic index would put the record in scratch) */
+template <int LO, int N>
+CRT_HD KTopo topo2_pick(const KTopo2 &r, int k) {
+    if constexpr (N == 1) {
+        (void)k;
+        return r.t[LO];
+    } else {
+        const KTopo a = topo2_pick<LO, N / 2>(r, k), b = topo2_pick<LO + N / 2, N / 2>(r, k);
+        const bool hi = (k & (N / 2)) != 0;
+        return KTopo{hi ? b.a : a.a, hi ? b.b : a.b};
+    }
+}
+
+/* topo_level with the child's record from the node's KTopo2 (r, loaded at
+ * the treelet's root; q: the current node's heap position there, LV its
+ * level below the root + 1) instead of a load */
+template <int AX, int LV>
+CRT_HD bool topo_level2(const KTopo2 &r, int &q, Vec p, TopoWalk &w) {
+    if (w.tp.b >= 0 || w.depth >= 62) return false;
+    DNode lo, hi;
+    topo_halves<AX>(w.cell, lo, hi);
+    const bool first_up = w.tp.b == -2;
+    const DNode n1 = cell_sel(first_up, hi, lo), n2 = cell_sel(first_up, lo, hi);
+    int ci = w.i + 1;
+    bool up = first_up, second = false;
+    if (w.tp.a >= 0 && !cell_holds(n1, p)) {
+        if (cell_holds(n2, p) || cell_excess(n2, p) < cell_excess(n1, p)) {
+            ci = w.tp.a;
+            up = !first_up;
+            second = true;
+        }
+    }
+    if (up) w.upper |= 1ull << w.depth;
+    ++w.depth;
+    const float old = up ? cell_plane(w.cell, AX) : cell_plane(w.cell, 3 + AX);
+    const float mid = up ? cell_plane(hi, AX) : cell_plane(lo, 3 + AX);
+    const int f = up ? AX : 3 + AX;
+    if (!(mid == old)) w.df = (w.df & ~(0xffull << (8 * f))) | ((uint64_t)w.depth << (8 * f));
+    w.cell = cell_sel(up, hi, lo);
+    w.i = ci;
+    q = 2 * q + (second ? 1 : 0);
+    /* level LV's entries: positions 2^LV .. 2^(LV+1) - 1, entries from 2^LV - 2 */
+    w.tp = topo2_pick<(1 << LV) - 2, (1 << LV)>(r, q - (1 << LV));
+    return true;
+}
+
 /* Step 2 on the topology records (crt_layout.h KTopo): verify_kd's descent
  * and proof with the cells computed in registers — one dependent 8-B load
  * per level (verify_kd: one or two 32-B loads), and the full tests of the
@@ -352,7 +402,7 @@ CRT_HD bool topo_level(const KTopo *topo, Vec p, TopoWalk &w) {
  * Levels go three at a time (axes 0, 1, 2). */
 template <bool COUNT>
 CRT_HD int verify_topo(const KTopo *topo, const DNode *nodes, const int32_t *slot_tri, int tri, Vec o, Vec d,
-                       const RayRcp &rr, Vec p, WalkCounts &c) {
+                       const RayRcp &rr, Vec p, WalkCounts &c, const KTopo2 *topo2 = nullptr) {
     TopoWalk w;
     w.cell = CRT_LDG(nodes, 0);                /* the root cell */
     w.tp = CRT_LDG(topo, 0);
@@ -360,7 +410,23 @@ CRT_HD int verify_topo(const KTopo *topo, const DNode *nodes, const int32_t *slo
     w.depth = 0;
     w.upper = 0;
     w.df = 0;
-    while (topo_level<0>(topo, p, w) && topo_level<1>(topo, p, w) && topo_level<2>(topo, p, w)) {
+    if (topo2) {   /* two levels a load (the axes cycle with depth: six levels a round) */
+        for (;;) {
+            KTopo2 r;
+            int q;
+#define CRT_TOPO2_PAIR(A0, A1)                                                                     \
+    if (w.tp.b >= 0 || w.depth >= 62) break;                                                       \
+    r = CRT_LDG(topo2, w.i);                                                                       \
+    q = 1;                                                                                         \
+    if (!(topo_level2<A0, 1>(r, q, p, w) && topo_level2<A1, 2>(r, q, p, w))) break;
+            CRT_TOPO2_PAIR(0, 1)
+            CRT_TOPO2_PAIR(2, 0)
+            CRT_TOPO2_PAIR(1, 2)
+#undef CRT_TOPO2_PAIR
+        }
+    } else {
+        while (topo_level<0>(topo, p, w) && topo_level<1>(topo, p, w) && topo_level<2>(topo, p, w)) {
+        }
     }
     if (w.tp.b < 0) return -1;                 /* an interior node at depth 62 */
     int slot = -1;
@@ -482,13 +548,14 @@ template <bool COUNT>
 CRT_HD int resolve_closest(const DNode *nodes, const PNode *pnodes, int n, const DTriGeo *slots,
                            const uint8_t *slot_cull, const int32_t *slot_tri, const KTopo *ktopo, bool planes_ok,
                            Vec o, Vec d, const PruneRay &pr, int tri, float t, bool tie, float &best_t, WalkCounts &c,
-                           bool *fb = nullptr) {
+                           bool *fb = nullptr, const KTopo2 *ktopo2 = nullptr) {
     best_t = 0.0f;
     if (tri < 0) return -1;
     const RayRcp rr = make_ray_rcp(o, d, planes_ok);
     if (!tie) {
         const Vec p = vadd(o, vscale(d, t));
-        const int slot = CRT_PROOF_TOPO && ktopo ? verify_topo<COUNT>(ktopo, nodes, slot_tri, tri, o, d, rr, p, c)
+        const int slot = CRT_PROOF_TOPO && ktopo ? verify_topo<COUNT>(ktopo, nodes, slot_tri, tri, o, d, rr, p, c,
+                                                                      CRT_PROOF_TOPO2 ? ktopo2 : nullptr)
                                                  : verify_kd<COUNT>(nodes, slot_tri, tri, o, d, rr, p, c);
         if (slot >= 0) {
             best_t = t;
@@ -508,7 +575,8 @@ CRT_HD int trace_bvh_exact(const BNode *bnodes, int bn, const DTriGeo *btri, con
                            const DNode *nodes, const PNode *pnodes, int n, const DTriGeo *slots,
                            const uint8_t *slot_cull, const int32_t *slot_tri, const KTopo *ktopo,
                            float prune_origin_max, bool planes_ok,
-                           Vec o, Vec d, float &best_t, WalkCounts &c, bool *fb = nullptr) {
+                           Vec o, Vec d, float &best_t, WalkCounts &c, bool *fb = nullptr,
+                           const KTopo2 *ktopo2 = nullptr) {
     best_t = 0.0f;
     if (fb) *fb = false;
     if (isnan(o.x) || isnan(o.y) || isnan(o.z) || isnan(d.x) || isnan(d.y) || isnan(d.z)) return -1;
@@ -518,7 +586,7 @@ CRT_HD int trace_bvh_exact(const BNode *bnodes, int bn, const DTriGeo *btri, con
     float t = 0.0f;
     const int tri = walk_bvh<COUNT, PF>(bnode_order(bnodes, bn, oct), bn, btri, btri_id, o, d, pr, t, tie, c);
     return resolve_closest<COUNT>(nodes, pnodes, n, slots, slot_cull, slot_tri, ktopo, planes_ok, o, d, pr, tri, t, tie,
-                                  best_t, c, fb);
+                                  best_t, c, fb, ktopo2);
 }
 
 /* The same answer for a camera ray of cell [beg, end) through the camera bins. */
@@ -526,7 +594,7 @@ template <bool COUNT>
 CRT_HD int trace_bins_exact(const CamCand *cands, int beg, int end, int bit, const DNode *nodes, const PNode *pnodes, int n,
                             const DTriGeo *slots, const uint8_t *slot_cull, const int32_t *slot_tri,
                             const KTopo *ktopo, float prune_origin_max, bool planes_ok, Vec o, Vec d, float &best_t,
-                            WalkCounts &c, bool *fb = nullptr) {
+                            WalkCounts &c, bool *fb = nullptr, const KTopo2 *ktopo2 = nullptr) {
     best_t = 0.0f;
     if (fb) *fb = false;
     if (isnan(o.x) || isnan(o.y) || isnan(o.z) || isnan(d.x) || isnan(d.y) || isnan(d.z)) return -1;
@@ -535,7 +603,7 @@ CRT_HD int trace_bins_exact(const CamCand *cands, int beg, int end, int bit, con
     float t = 0.0f;
     const int tri = walk_bins<COUNT>(cands, beg, end, bit, o, d, pr, t, tie, c);
     return resolve_closest<COUNT>(nodes, pnodes, n, slots, slot_cull, slot_tri, ktopo, planes_ok, o, d, pr, tri, t, tie,
-                                  best_t, c, fb);
+                                  best_t, c, fb, ktopo2);
 }
 
 }  // namespace crt_amd

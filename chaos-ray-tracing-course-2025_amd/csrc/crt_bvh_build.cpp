@@ -279,10 +279,24 @@ int build_proof_tables(HostScene &hs) {
         if (c2 < nd.a) ok = ok && cell_equal(nodes[(size_t)c2], first_lo ? hi_half : lo_half);
         if (!ok) {
             hs.ktopo.clear();   /* not the reference's halving: the proof descends the nodes (verify_kd) */
+            hs.ktopo2.clear();
             return CRT_OK;
         }
         t.a = c2 < nd.a ? c2 : -1;
         t.b = first_lo ? -1 : -2;
+    }
+    /* two levels a record (crt_layout.h KTopo2) */
+    hs.ktopo2.assign((size_t)n, KTopo2{});
+    for (int32_t i = 0; i < n; ++i) {
+        int32_t idx[8];
+        idx[1] = i;
+        for (int q = 2; q < 8; ++q) {
+            const int32_t par = idx[q >> 1];
+            int32_t c = -1;
+            if (par >= 0 && hs.ktopo[(size_t)par].b < 0) c = (q & 1) ? hs.ktopo[(size_t)par].a : par + 1;
+            idx[q] = c;
+            hs.ktopo2[(size_t)i].t[q - 2] = c >= 0 ? hs.ktopo[(size_t)c] : KTopo{0, 0};
+        }
     }
     return CRT_OK;
 }

@@ -184,7 +184,8 @@ __device__ __forceinline__ int gi_walk_finish(const DeviceScene &s, const GiWalk
     int slot = -1;
     if (!w.tie) {
         const Vec p = vadd(o, vscale(d, w.t));
-        slot = CRT_PROOF_TOPO && s.ktopo ? verify_topo<COUNT>(s.ktopo, s.nodes, s.slot_tri, w.tri, o, d, rr, p, wc)
+        slot = CRT_PROOF_TOPO && s.ktopo ? verify_topo<COUNT>(s.ktopo, s.nodes, s.slot_tri, w.tri, o, d, rr, p, wc,
+                                                                   CRT_PROOF_TOPO2 ? s.ktopo2 : nullptr)
                                          : verify_kd<COUNT>(s.nodes, s.slot_tri, w.tri, o, d, rr, p, wc);
         t = w.t;
     }

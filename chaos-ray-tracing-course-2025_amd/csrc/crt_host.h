@@ -87,6 +87,7 @@ struct HostScene {
     std::vector<int32_t> btri_id;   /* triangle id | back_face_culling << 31 */
     /* the BVH proof's tree topology (crt_layout.h KTopo; build_proof_tables) */
     std::vector<KTopo> ktopo;
+    std::vector<KTopo2> ktopo2;   /* per node: its children and grandchildren (verify_topo) */
 
 
     /* root cell (crt_acceleration_tree.cpp:89-94); tree_on_host = false when

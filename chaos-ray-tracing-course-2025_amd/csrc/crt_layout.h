@@ -53,6 +53,17 @@ struct KTopo {
 };
 static_assert(sizeof(KTopo) == 8, "KTopo must be 8 B");
 
+/* verify_topo's descent two levels a load: for node i, the KTopo records of
+ * its children and grandchildren in heap order (the node is position 1,
+ * position q's children are 2q and 2q + 1: first child i + 1, second child
+ * KTopo::a), entry q - 2 for q = 2..7; absent ones {0, 0}.  64 B.  (Three
+ * levels in one 128-B line took 30 more VGPRs in the camera kernel: one wave
+ * less per SIMD.) */
+struct alignas(64) KTopo2 {
+    KTopo t[8];
+};
+static_assert(sizeof(KTopo2) == 64, "KTopo2 must be 64 B");
+
 /* Node record of the pruned walks: the reference cell (the box the
  * reference's six-face test runs on — it decides which leaf copies are
  * eligible, crt_intersection.cpp:121) plus a conservative hull of every
@@ -164,8 +175,10 @@ struct DeviceScene {
     int32_t bnode_count;
     const DTriGeo *btri;
     const int32_t *btri_id;
-    /* the proof's tree topology (KTopo); null when the tree lives on the device only */
+    /* the proof's tree topology (KTopo, and per node its two levels below,
+     * KTopo2); null when the tree lives on the device only */
     const KTopo *ktopo;
+    const KTopo2 *ktopo2;
     /* camera bins (crt_bvh.h walk_bins), rebuilt on the device by every camera
      * frame (crt_bins.hip): per 8x8 cell of the frame (bin_tx cells a row),
      * candidates bins[bin_off[c] .. bin_off[c] + bin_len[c]), bin_len -1: the

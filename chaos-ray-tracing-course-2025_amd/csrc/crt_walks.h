@@ -812,7 +812,7 @@ __device__ __forceinline__ int trace_lane_bvh(const DeviceScene &s, bool active,
     WalkCounts wc = {0u, 0u};
     const int best = trace_bvh_exact<COUNT, PF>(s.bnodes, s.bnode_count, s.btri, s.btri_id, s.nodes, s.pnodes,
                                             s.node_count, s.slots, s.slot_cull, s.slot_tri, s.ktopo, s.prune_origin_max,
-                                            s.planes_ok != 0, o, d, best_t, wc);
+                                            s.planes_ok != 0, o, d, best_t, wc, nullptr, s.ktopo2);
     if (COUNT) {
         c.nodes += wc.nodes;
         c.tris += wc.tris;
@@ -963,7 +963,8 @@ __device__ int trace_bvh_window(const DeviceScene &s, int sl, bool act, Vec o, V
         WalkCounts pc = {0u, 0u};
         if (!tie) {
             const Vec p = vadd(o, vscale(d, t));
-            slot = CRT_PROOF_TOPO && s.ktopo ? verify_topo<COUNT>(s.ktopo, s.nodes, s.slot_tri, tri, o, d, rr, p, pc)
+            slot = CRT_PROOF_TOPO && s.ktopo ? verify_topo<COUNT>(s.ktopo, s.nodes, s.slot_tri, tri, o, d, rr, p, pc,
+                                                                 CRT_PROOF_TOPO2 ? s.ktopo2 : nullptr)
                                              : verify_kd<COUNT>(s.nodes, s.slot_tri, tri, o, d, rr, p, pc);
             if (slot >= 0) best_t = t;
         }
@@ -1103,7 +1104,7 @@ __device__ int trace_bins_wave(const DeviceScene &s, CamCand *stage, int beg, in
     int slot = -1;
     if (act && !nan_ray)
         slot = resolve_closest<COUNT>(s.nodes, s.pnodes, s.node_count, s.slots, s.slot_cull, s.slot_tri, s.ktopo,
-                                      s.planes_ok != 0, o, d, pr, best, bt, tie, best_t, wc);
+                                      s.planes_ok != 0, o, d, pr, best, bt, tie, best_t, wc, nullptr, s.ktopo2);
     if (COUNT) {
         c.nodes += wc.nodes;
         c.tris += wc.tris;
@@ -1191,7 +1192,7 @@ __device__ int trace_bins_lanes(const DeviceScene &s, CamCand *stage, int beg, i
     if (act && !nan_ray && sl == 0 && holders != 0u)
         slot = resolve_closest<COUNT>(s.nodes, s.pnodes, s.node_count, s.slots, s.slot_cull, s.slot_tri, s.ktopo,
                                       s.planes_ok != 0, o, d, pr, gbest, g, __builtin_popcount(holders) > 1 || ties != 0u,
-                                      best_t, wc);
+                                      best_t, wc, nullptr, s.ktopo2);
     if (COUNT) {
         c.nodes += wc.nodes;
         c.tris += wc.tris;
