@@ -627,7 +627,8 @@ int crt_hip_profile_waves(crt_hip_scene *sc, const crt_renderer_settings *st, ui
         work.resize((size_t)std::max<int64_t>(1, slots));
         ph_all.resize((size_t)kBinsPhdrInts);
         rest.resize((size_t)std::max(1, bp.nrest));
-        e = hipMemcpy(work.data(), bp.work, work.size() * sizeof(BinsWork), hipMemcpyDeviceToHost);
+        e = hipMemcpy(work.data(), bp.work + (size_t)par * bp.wslots, work.size() * sizeof(BinsWork),
+                      hipMemcpyDeviceToHost);
         if (e == hipSuccess) e = hipMemcpy(ph_all.data(), bp.phdr, ph_all.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
         if (e == hipSuccess) e = hipMemcpy(rest.data(), bp.rest, rest.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
     }

@@ -308,8 +308,10 @@ __global__ __launch_bounds__(256) void k_bins_project(const CamCand *__restrict_
             o->nb[tid].v = 0;
             o->rec[tid].v = 0;
         }
+        /* this frame's work-list counters (k_bins_sort appends after this
+         * kernel; the render two frames back, same parity, is done with them) */
         if (phdr2 && tid < kBinKinds * kBinShards)
-            phdr2[BCK(bins_phdr_at(par ^ 1, tid / kBinShards, tid % kBinShards), kBinsPhdrInts, 1)] = 0;
+            phdr2[BCK(bins_phdr_at(par, tid / kBinShards, tid % kBinShards), kBinsPhdrInts, 1)] = 0;
     }
     /* this frame's per-cell lengths start empty (k_bins_sort sets the listed
      * cells'); the other parity's counts start the next frame at zero */
@@ -756,7 +758,13 @@ __global__ void k_warm_bins() {}
 
 void bins_free(crt_hip_scene *sc) {
     BinsDev &b = sc->bins;
+    if (b.stream) (void)hipStreamSynchronize(b.stream);
     for (void *p : b.allocs) (void)hipFree(p);
+    for (int i = 0; i < 2; ++i) {
+        if (b.bdone[i]) (void)hipEventDestroy(b.bdone[i]);
+        if (b.rdone[i]) (void)hipEventDestroy(b.rdone[i]);
+    }
+    if (b.stream) (void)hipStreamDestroy(b.stream);
     b = BinsDev{};
     sc->ds.bins = nullptr;
     sc->ds.bin_off = nullptr;
@@ -780,7 +788,8 @@ int launch_project(crt_hip_scene *sc, hipStream_t s, int par, int32_t *phdr) {
     BinsDev &b = sc->bins;
     const int groups = (b.nt + kProjTris - 1) / kProjTris;
     hipLaunchKernelGGL(k_bins_project, dim3((unsigned)groups), dim3(256), 0, s, b.tpl, b.nt, b.cam, b.items, b.tpref,
-                       b.gsum, b.every, b.hdr, par, phdr, b.len, b.ncell, b.tx, b.cnt, b.keys, b.nonempty, b.bigl,
+                       b.gsum, b.every, b.hdr, par, phdr, b.len + (size_t)par * b.ncell, b.ncell, b.tx, b.cnt, b.keys,
+                       b.nonempty, b.bigl,
                        b.cap_shard, b.rem, b.pair_blocks > 0 ? 1 : 0);
     HIP_TRY(hipGetLastError());
     if (b.pair_blocks > 0) {
@@ -807,7 +816,7 @@ int bins_dbg_arm(crt_hip_scene *sc, const ShardPlan &plan) {
                                           " bound " + std::to_string(d.bound));
     d.nt = b.nt;
     d.ncell = b.ncell;
-    d.rec_cap = b.rec_cap;
+    d.rec_cap = 2 * b.rec_cap;
     d.ne_cap = kBinShards * b.cap_shard;
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_bins_dbg), &d, sizeof d));
 #else
@@ -851,8 +860,8 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
     if ((rc = bins_alloc(sc, &b.nonempty, (size_t)kBinShards * b.cap_shard)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.bigl, (size_t)kBinShards * b.cap_shard)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.hdr, 2, true)) != CRT_OK) return rc;
-    if ((rc = bins_alloc(sc, &b.off, (size_t)b.ncell, true)) != CRT_OK) return rc;
-    if ((rc = bins_alloc(sc, &b.len, (size_t)b.ncell, true)) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.off, (size_t)2 * b.ncell, true)) != CRT_OK) return rc;   /* two parities */
+    if ((rc = bins_alloc(sc, &b.len, (size_t)2 * b.ncell, true)) != CRT_OK) return rc;
     /* sizing pass: counts per cell of this camera */
     if ((rc = bins_dbg_arm(sc, ShardPlan{})) != CRT_OK) return rc;
     if ((rc = launch_project(sc, sc->stream, 0, nullptr)) != CRT_OK) return rc;
@@ -900,7 +909,20 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
         base += cap;
     }
     b.rec_cap = (int32_t)base;
-    if ((rc = bins_alloc(sc, &b.recs, (size_t)b.rec_cap)) != CRT_OK) return rc;
+    if ((int64_t)2 * base >= INT32_MAX) {   /* record offsets are int32 */
+        bins_free(sc);
+        return CRT_OK;
+    }
+    if ((rc = bins_alloc(sc, &b.recs, (size_t)2 * b.rec_cap)) != CRT_OK) return rc;   /* two parities */
+    /* the frames pipeline: the binning's stream and the parities' events
+     * (recorded once, so the first two frames find their lists free) */
+    HIP_TRY(hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) {
+        HIP_TRY(hipEventCreateWithFlags(&b.bdone[i], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&b.rdone[i], hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(b.rdone[i], sc->stream));
+        HIP_TRY(hipEventRecord(b.bdone[i], sc->stream));
+    }
     /* k_bins_sort's grid: a wave per long list (at least kBinShards waves),
      * then the listed cells (every cell when some hull is everywhere),
      * kSortSlots a wave */
@@ -962,7 +984,8 @@ int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
     bp.ncell = b.ncell;
     bp.nfill = (b.ncell + 15) / 16;   /* 16 cells a fill wave */
     void *p[4] = {nullptr, nullptr, nullptr, nullptr};
-    const size_t sizes[4] = {(size_t)b.ncell * sizeof(int32_t), (size_t)std::max<int64_t>(1, slots) * sizeof(BinsWork),
+    bp.wslots = (int32_t)slots;
+    const size_t sizes[4] = {(size_t)b.ncell * sizeof(int32_t), (size_t)std::max<int64_t>(1, 2 * slots) * sizeof(BinsWork),
                              (size_t)kBinsPhdrInts * sizeof(int32_t), std::max<size_t>(1, rest.size()) * sizeof(int32_t)};
     for (int i = 0; i < 4; ++i) {
         HIP_TRY(hipMalloc(&p[i], sizes[i]));
@@ -980,8 +1003,13 @@ int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
     return CRT_OK;
 }
 
-/* The frame's lists, on `s`, before its render kernel; returns the frame's
- * parity (the render reads that set of the plan's counters). */
+/* The frame's lists, before its render on `s`; returns the frame's parity
+ * (the render reads that set of lists and records rdone[parity] after it).
+ * While the previous frame still renders (frames issued back to back), the
+ * binning runs on the binning's own stream — after the render two frames back
+ * (same parity) is done with the set and after the previous binning — and `s`
+ * waits for it: frame k + 1's binning overlaps frame k's render.  Otherwise
+ * (one frame at a time) `s` takes the binning itself: no cross-stream hop. */
 int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *par_out) {
     BinsDev &b = sc->bins;
     const int par = (int)(b.frame++ & 1);
@@ -989,16 +1017,30 @@ int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *p
         const int rc0 = bins_dbg_arm(sc, plan);
         if (rc0 != CRT_OK) return rc0;
     }
-    int rc = launch_project(sc, s, par, plan.bp.phdr);
+    /* the previous frame still renders: overlap it.  The binnings share their
+     * scratch (items, keys, counts, lists), so they stay in order: the
+     * binning stream also waits for the previous frame's binning, wherever
+     * it ran */
+    const bool overlap = hipEventQuery(b.rdone[par ^ 1]) == hipErrorNotReady;
+    const hipStream_t bs = overlap ? b.stream : s;
+    if (overlap) {
+        HIP_TRY(hipStreamWaitEvent(b.stream, b.rdone[par], 0));
+        HIP_TRY(hipStreamWaitEvent(b.stream, b.bdone[par ^ 1], 0));
+    }
+    int rc = launch_project(sc, bs, par, plan.bp.phdr);
     if (rc != CRT_OK) return rc;
     BinsPlan bp = plan.bp;
     bp.par = par;
-    hipLaunchKernelGGL(k_bins_sort, dim3((unsigned)b.sort_blocks), dim3(64 * kSortWaves), 0, s, b.tpl, b.items,
+    if (bp.work) bp.work += (size_t)par * bp.wslots;
+    BinsCaps caps = b.caps;   /* this parity's half of the record buffer */
+    for (int i = 0; i < kBinShards; ++i) caps.base[i] += par * b.rec_cap;
+    hipLaunchKernelGGL(k_bins_sort, dim3((unsigned)b.sort_blocks), dim3(64 * kSortWaves), 0, bs, b.tpl, b.items,
                        b.cnt + (size_t)par * b.ncell * kCntStride,
-                       b.keys, b.every, b.nonempty, b.bigl, b.cap_shard, b.long_waves, b.hdr, par, b.recs, b.caps, b.off,
-                       b.len, b.tx, b.ncell,
-                       bp);
+                       b.keys, b.every, b.nonempty, b.bigl, b.cap_shard, b.long_waves, b.hdr, par, b.recs, caps,
+                       b.off + (size_t)par * b.ncell, b.len + (size_t)par * b.ncell, b.tx, b.ncell, bp);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(b.bdone[par], bs));
+    if (overlap) HIP_TRY(hipStreamWaitEvent(s, b.bdone[par], 0));
     if (par_out) *par_out = par;
 #ifdef CRT_BINS_STAMPS
     if (const char *fn = std::getenv("CRT_BINS_STAMPS_FILE")) {
@@ -1046,10 +1088,13 @@ int64_t crt_hip_camera_bins(crt_hip_scene *sc, int32_t *len_out, void *recs_out,
     int rc = bins_enqueue(sc, none, sc->stream, nullptr);
     if (rc != CRT_OK) return rc;
     if ((rc = bins_dbg_arm(sc, none)) != CRT_OK) return rc;   /* diagnostic builds: this frame's violations */
+    const int par = (int)((b.frame - 1) & 1);   /* the parity that frame used */
     std::vector<int32_t> off((size_t)b.ncell), len((size_t)b.ncell);
-    std::vector<CamCand> recs((size_t)b.rec_cap);   /* every shard's region */
-    HIP_TRY(hipMemcpyAsync(off.data(), b.off, off.size() * sizeof(int32_t), hipMemcpyDeviceToHost, sc->stream));
-    HIP_TRY(hipMemcpyAsync(len.data(), b.len, len.size() * sizeof(int32_t), hipMemcpyDeviceToHost, sc->stream));
+    std::vector<CamCand> recs((size_t)2 * b.rec_cap);   /* both parities' regions (offsets are absolute) */
+    HIP_TRY(hipMemcpyAsync(off.data(), b.off + (size_t)par * b.ncell, off.size() * sizeof(int32_t),
+                           hipMemcpyDeviceToHost, sc->stream));
+    HIP_TRY(hipMemcpyAsync(len.data(), b.len + (size_t)par * b.ncell, len.size() * sizeof(int32_t),
+                           hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipMemcpyAsync(recs.data(), b.recs, recs.size() * sizeof(CamCand), hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
     int64_t total = 0;

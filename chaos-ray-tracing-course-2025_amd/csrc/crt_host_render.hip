@@ -889,12 +889,15 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         if (rc != CRT_OK) return rc;
         BinsPlan bp = plan.bp;
         bp.par = par;
+        bp.work += (size_t)par * bp.wslots;   /* this frame's parity of the work lists */
         const unsigned bb = (unsigned)((plan.waves + 3) / 4);
 #define CRT_LAUNCH_B(COUNT)                                                                                 \
     hipLaunchKernelGGL((k_render_tiles<false, 0, 15, 15, COUNT>), dim3(bb), dim3(256), 0, stream, d_scene, ds, \
                        plan.d_tiles, plan.waves, d_out, cnt, stamps, bp)
         if (count) CRT_LAUNCH_B(true); else CRT_LAUNCH_B(false);
 #undef CRT_LAUNCH_B
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(sc->bins.rdone[par], stream));   /* this parity's lists are free again */
     } else if (!full) {
         switch (trav) {
         case 7: if (count) CRT_LAUNCH_T(false, 0, 7, true); else CRT_LAUNCH_T(false, 0, 7, false); break;

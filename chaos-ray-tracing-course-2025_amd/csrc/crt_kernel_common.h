@@ -51,6 +51,7 @@ struct BinsPlan {
     const int32_t *rest;  /* tiles the lists do not hold */
     int32_t cap[kBinKinds], wbase[kBinKinds];
     int32_t nrest, nfill, ncell;
+    int32_t wslots;       /* work-list slots of one parity (work: two parities; the frame's at par * wslots) */
     int32_t split, medium, quad;
     int32_t par;          /* the frame's parity (which counters it uses) */
 };

@@ -182,7 +182,10 @@ struct DeviceScene {
     /* camera bins (crt_bvh.h walk_bins), rebuilt on the device by every camera
      * frame (crt_bins.hip): per 8x8 cell of the frame (bin_tx cells a row),
      * candidates bins[bin_off[c] .. bin_off[c] + bin_len[c]), bin_len -1: the
-     * cell's pixels walk the BVH; null when the scene takes no bins */
+     * cell's pixels walk the BVH; two sets by frame parity (frame k + 1 bins
+     * while frame k renders): a frame's per-cell entries at parity * ncell,
+     * its records anywhere in `bins` (offsets absolute); null when the scene
+     * takes no bins */
     const CamCand *bins;
     const int32_t *bin_off;
     const int32_t *bin_len;

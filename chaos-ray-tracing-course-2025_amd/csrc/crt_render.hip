@@ -71,9 +71,9 @@ __device__ void bins_fill(const DeviceScene &s, const BinsPlan &bp, const Tile *
     const int c = fw * 16 + (lane & 15);
     bool e = false;
     int k = -1;
-    if (lane < 16 && c < bp.ncell) {   /* the cell's tile and list length in one round of loads */
+    if (lane < 16 && c < bp.ncell) {   /* the cell's tile and list length (this frame's parity) in one round of loads */
         k = bp.cell_tile[c];
-        e = s.bin_len[c] == 0 && k >= 0;
+        e = s.bin_len[(size_t)bp.par * bp.ncell + c] == 0 && k >= 0;
     }
     Tile t{};
     if (e) t = tiles[k];
@@ -189,9 +189,10 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
         const int tx0 = uniform_i(tl.x), ty0 = uniform_i(tl.y), tw = uniform_i(tl.w), th = uniform_i(tl.h);
         const int cell = (ty0 >> 3) * s.bin_tx + (tx0 >> 3);
         const bool one = (tx0 & 7) + tw <= 8 && (ty0 & 7) + th <= 8;
-        const int len = uniform_i(bin_len != -2 ? bin_len : one ? load_scalar(s.bin_len, cell) : -1);
+        const int pc = bp.par * bp.ncell + cell;   /* this frame's parity of the per-cell lists */
+        const int len = uniform_i(bin_len != -2 ? bin_len : one ? load_scalar(s.bin_len, pc) : -1);
         if (len >= 0) {   /* -1: not inside one cell, or the cell's list is over the cap: the BVH walk below */
-            const int beg = uniform_i(bin_len != -2 ? bin_beg : load_scalar(s.bin_off, cell)), end = beg + len;
+            const int beg = uniform_i(bin_len != -2 ? bin_beg : load_scalar(s.bin_off, pc)), end = beg + len;
             __shared__ CamCand stage[4 * kBinChunk];
             if ((tl.prio & 2) && tw <= 4 && th <= 4) {
                 /* a split tile of a long list: four lanes per pixel (trace_bins_lanes) */

@@ -60,14 +60,20 @@ struct BinsDev {
     crt_amd::BinsHdr *hdr = nullptr;      /* two sets: frames alternate */
     uint64_t frame = 0;                   /* frames binned (parity = frame & 1) */
     crt_amd::BinsCaps caps{};             /* per shard: its region of recs */
-    crt_amd::CamCand *recs = nullptr;     /* the lists */
+    crt_amd::CamCand *recs = nullptr;     /* the lists, two parities (rec_cap each) */
     int32_t rec_cap = 0;
-    int32_t *off = nullptr, *len = nullptr;   /* per cell */
+    int32_t *off = nullptr, *len = nullptr;   /* per cell, two parities (ncell each) */
     std::vector<int32_t> count;           /* per cell: list length of the sizing pass (-1 over the cap) */
     int sort_blocks = 0;                  /* k_bins_sort blocks */
     int64_t records = 0;                  /* records of the sizing pass */
     double setup_ms = 0.0;
     std::vector<void *> allocs;
+    /* frames pipeline: frame k's binning runs on `stream` (its kernels in
+     * order) while frame k - 1 renders; the lists the render reads are
+     * double-buffered by frame parity, bdone[p] = parity p's lists built,
+     * rdone[p] = parity p's render done with them */
+    hipStream_t stream = nullptr;
+    hipEvent_t bdone[2] = {nullptr, nullptr}, rdone[2] = {nullptr, nullptr};
 };
 
 
