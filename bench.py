@@ -50,7 +50,7 @@ import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
-PKG = ROOT / "chaos-ray-tracing-course-2025_amd"
+PKG = Path(os.environ["CRT_PKG"]).resolve() if os.environ.get("CRT_PKG") else ROOT / "chaos-ray-tracing-course-2025_amd"   # CRT_PKG: A/B builds
 for _p in (str(PKG), str(ROOT)):
     if _p not in sys.path:
         sys.path.insert(0, _p)

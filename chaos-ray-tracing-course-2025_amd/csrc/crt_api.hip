@@ -275,6 +275,8 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
     ds.refractions_on = hs.refractions_on;
 
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
+    if (sc->has_secondary && !(hs.gi_on && sc->has_diffuse))   /* the wavefront path's frame sets (render_wavefront) */
+        if ((rc = wf_streams(sc->wf, sc->stream)) != CRT_OK) return rc;
     warm_code_objects(sc->device, sc->stream);
     /* camera bins (crt_bins.hip), rebuilt on the device by every camera frame
      * of scenes whose camera rays the tile kernels trace without recursion

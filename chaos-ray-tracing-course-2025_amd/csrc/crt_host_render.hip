@@ -543,9 +543,9 @@ DSettings to_dsettings(const crt_renderer_settings *st) {
     return d;
 }
 
-int wf_grow_ids(WfBuffers &w, int64_t need, int64_t used, hipStream_t stream) {
+int wf_grow_ids(WfBuffers &wb, WfSet &w, int64_t need, int64_t used, hipStream_t stream) {
     if (need <= w.cap) return CRT_OK;
-    wf_graphs_clear(w);
+    wf_graphs_clear(wb);
     const int64_t cap = std::max<int64_t>(need, 2 * w.cap);
     void *pn = nullptr, *pc = nullptr;
     HIP_TRY(hipMalloc(&pn, (size_t)cap * sizeof(WNode)));
@@ -563,9 +563,9 @@ int wf_grow_ids(WfBuffers &w, int64_t need, int64_t used, hipStream_t stream) {
     return CRT_OK;
 }
 
-int wf_grow_queue(WfBuffers &w, int k, int64_t need) {
+int wf_grow_queue(WfBuffers &wb, WfSet &w, int k, int64_t need) {
     if (need <= w.qcap[k]) return CRT_OK;
-    wf_graphs_clear(w);
+    wf_graphs_clear(wb);
     const int64_t cap = std::max<int64_t>(need, 2 * w.qcap[k]);
     if (w.q[k]) (void)hipFree(w.q[k]);
     w.q[k] = nullptr;
@@ -576,35 +576,65 @@ int wf_grow_queue(WfBuffers &w, int k, int64_t need) {
     return CRT_OK;
 }
 
-void wf_free(WfBuffers &w) {
-    wf_graphs_clear(w);
-    for (void *p : {(void *)w.nodes, (void *)w.cols, (void *)w.q[0], (void *)w.q[1], (void *)w.counts, (void *)w.d_flag})
-        if (p) (void)hipFree(p);
-    if (w.h_flag) (void)hipHostFree(w.h_flag);
-    if (w.flag_ev) (void)hipEventDestroy(w.flag_ev);
-    w = WfBuffers{};
+void wf_free(WfBuffers &wb) {
+    wf_graphs_clear(wb);
+    for (WfSet &w : wb.set) {
+        if (w.stream) (void)hipStreamSynchronize(w.stream);
+        for (void *p : {(void *)w.nodes, (void *)w.cols, (void *)w.q[0], (void *)w.q[1], (void *)w.counts, (void *)w.d_flag})
+            if (p) (void)hipFree(p);
+        if (w.h_flag) (void)hipHostFree(w.h_flag);
+        for (hipEvent_t e : {w.flag_ev, w.free_ev, w.done_ev})
+            if (e) (void)hipEventDestroy(e);
+        if (w.stream) (void)hipStreamDestroy(w.stream);
+    }
+    wb = WfBuffers{};
 }
 
-/* The last recorded-size frame's overflow flag, if its copy has landed
- * (wait: block until it has).  Returns true when that frame overflowed; the
- * recorded sizes are then dropped, so the next frame reads its sizes back. */
-bool wf_overflowed(WfBuffers &w, bool wait) {
-    if (!w.flag_pending) return false;
-    if (wait) {
-        if (hipEventSynchronize(w.flag_ev) != hipSuccess) return false;
-    } else if (hipEventQuery(w.flag_ev) != hipSuccess) {
-        return false;
+/* The last recorded-size frames' overflow flags, if their copies have landed
+ * (wait: block until they have).  Returns true when one of them overflowed;
+ * the recorded sizes are then dropped, so the next frame reads its sizes back. */
+bool wf_overflowed(WfBuffers &wb, bool wait) {
+    bool any = false;
+    for (WfSet &w : wb.set) {
+        if (!w.flag_pending) continue;
+        if (wait) {
+            if (hipEventSynchronize(w.flag_ev) != hipSuccess) continue;
+        } else if (hipEventQuery(w.flag_ev) != hipSuccess) {
+            continue;
+        }
+        w.flag_pending = false;
+        any = any || *w.h_flag != 0;
     }
-    w.flag_pending = false;
-    if (*w.h_flag == 0) return false;
+    if (!any) return false;
     /* consumed: frames still in flight were queued with the same stale sizes
-     * and are covered by this report; re-arm the device flag behind them */
+     * and are covered by this report; re-arm the device flags behind them */
     (void)hipDeviceSynchronize();
-    (void)hipMemset(w.d_flag, 0, sizeof(int32_t));
-    *w.h_flag = 0;
-    w.recs.clear();
-    wf_graphs_clear(w);
+    for (WfSet &w : wb.set) {
+        if (w.d_flag) (void)hipMemset(w.d_flag, 0, sizeof(int32_t));
+        if (w.h_flag) *w.h_flag = 0;
+        w.flag_pending = false;
+    }
+    wb.recs.clear();
+    wf_graphs_clear(wb);
     return true;
+}
+
+/* The sets' streams and events, created together (the runtime deals a
+ * process's streams round robin over the device's hardware queues: streams
+ * created back to back land on distinct queues, so the sets' levels can run
+ * side by side — created at different times, two landed on one queue and ran
+ * one after the other); free_ev recorded once on `stream`.  Called at scene
+ * upload for scenes that take the wavefront path, so the first frame does
+ * not pay for it. */
+int wf_streams(WfBuffers &wb, hipStream_t stream) {
+    if (wb.set[0].stream) return CRT_OK;
+    for (WfSet &w : wb.set) HIP_TRY(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
+    for (WfSet &w : wb.set) {
+        HIP_TRY(hipEventCreateWithFlags(&w.free_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&w.done_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(w.free_ev, stream));
+    }
+    return CRT_OK;
 }
 
 /* One frame of the wavefront path (see k_wf_level).  A level's size is
@@ -616,19 +646,40 @@ bool wf_overflowed(WfBuffers &w, bool wait) {
  * each level may queue exactly the recorded size of the next, and a level
  * that would queue more sets an overflow flag instead (checked behind the
  * frame: crt_hip_render re-renders that frame with read-backs, the device-side
- * entry points report it on the next call). */
+ * entry points report it on the next call).
+ *
+ * Recorded-size frames take kWfSets buffer sets in turn, each set's levels
+ * and compose on a stream of its own (after the set's previous frame wrote
+ * its pixels), the pixels on the caller's stream (after the set's levels):
+ * consecutive frames' levels overlap — a level's few, long walks leave most
+ * of the GPU idle — while the frame's only write the caller sees stays in
+ * the caller's stream order. */
 int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_settings *st, const ShardPlan &plan,
                      float *d_out, hipStream_t stream, bool count, const DeviceScene *d_scene, int sec, int primary) {
-    WfBuffers &w = sc->wf;
+    WfBuffers &wb = sc->wf;
     /* levels 0..max_ray_depth are traced (a child deeper than max_ray_depth is
      * never queued, crt_renderer.cpp:47-48), so the loop below always drains
      * the queue: counts[max_ray_depth] is written by nobody and stays 0 */
     if (ds.max_ray_depth > (uint32_t)kWfMaxDepth)
         return set_error(CRT_E_UNSUPPORTED, "max_ray_depth > " + std::to_string(kWfMaxDepth) +
                                                 " with reflective/refractive materials is not supported");
-    if (wf_overflowed(w, false))
+    if (wf_overflowed(wb, false))
         return set_error(CRT_E_STATE, "a wavefront level outgrew its recorded size in the previous frame; "
                                          "that frame is wrong (sizes are now read back again)");
+    const int64_t n0 = (int64_t)plan.ntiles * 64;
+    const auto rit = wb.recs.find((const void *)plan.d_tiles);
+    const bool replay = !count && sc->wf_replay && rit != wb.recs.end() && rit->second.ntiles == plan.ntiles &&
+                        std::memcmp(&rit->second.st, st, sizeof *st) == 0;
+    const int si = replay ? (int)(wb.frame++ % kWfSets) : 0;
+    WfSet &w = wb.set[si];
+    {
+        const int rc0 = wf_streams(wb, stream);
+        if (rc0 != CRT_OK) return rc0;
+    }
+    /* where the levels run: a recorded-size frame on its set's stream, after
+     * the set's previous frame; a frame with read-backs on the caller's */
+    const hipStream_t ls = replay ? w.stream : stream;
+    HIP_TRY(hipStreamWaitEvent(ls, w.free_ev, 0));
     const int kMaxLevels = (int)ds.max_ray_depth + 2;
     if (!w.counts || w.count_cap < kMaxLevels) {
         if (w.counts) (void)hipFree(w.counts);
@@ -637,22 +688,18 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         HIP_TRY(hipMalloc(&p, (size_t)kMaxLevels * sizeof(int32_t)));
         w.counts = static_cast<int32_t *>(p);
         w.count_cap = kMaxLevels;
-        wf_graphs_clear(w);
+        wf_graphs_clear(wb);
     }
     if (!w.d_flag) {
         void *p = nullptr;
         HIP_TRY(hipMalloc(&p, sizeof(int32_t)));
         w.d_flag = static_cast<int32_t *>(p);
-        HIP_TRY(hipMemsetAsync(w.d_flag, 0, sizeof(int32_t), stream));
+        HIP_TRY(hipMemsetAsync(w.d_flag, 0, sizeof(int32_t), ls));
         HIP_TRY(hipHostMalloc(&p, sizeof(int32_t), hipHostMallocDefault));
         w.h_flag = static_cast<int32_t *>(p);
         *w.h_flag = 0;
         HIP_TRY(hipEventCreateWithFlags(&w.flag_ev, hipEventDisableTiming));
     }
-    const int64_t n0 = (int64_t)plan.ntiles * 64;
-    const auto rit = w.recs.find((const void *)plan.d_tiles);
-    const bool replay = !count && sc->wf_replay && rit != w.recs.end() && rit->second.ntiles == plan.ntiles &&
-                        std::memcmp(&rit->second.st, st, sizeof *st) == 0;
     static const std::vector<int32_t> kNone;
     const std::vector<int32_t> &rec = replay ? rit->second.sizes : kNone;
     int rc;
@@ -666,33 +713,51 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         qneed = std::max<int64_t>(mx, 1);
         ids = tot;
     }
-    if ((rc = wf_grow_ids(w, ids, 0, stream)) != CRT_OK) return rc;
-    if ((rc = wf_grow_queue(w, 0, qneed)) != CRT_OK) return rc;
-    if (replay && (rc = wf_grow_queue(w, 1, qneed)) != CRT_OK) return rc;
-    /* a recorded-size frame is a fixed launch sequence: replayed from a HIP
-     * graph captured the first time (one launch instead of ~2 per level) */
+    if ((rc = wf_grow_ids(wb, w, ids, 0, ls)) != CRT_OK) return rc;
+    if ((rc = wf_grow_queue(wb, w, 0, qneed)) != CRT_OK) return rc;
+    if (replay && (rc = wf_grow_queue(wb, w, 1, qneed)) != CRT_OK) return rc;
+    /* the pixels on the caller's stream once the levels are done; the set is
+     * free again after them */
+    auto finish = [&]() -> int {
+        if (replay) {
+            HIP_TRY(hipEventRecord(w.done_ev, ls));
+            HIP_TRY(hipStreamWaitEvent(stream, w.done_ev, 0));
+        }
+        hipLaunchKernelGGL(k_wf_pixels, dim3((unsigned)((plan.ntiles + 3) / 4)), dim3(256), 0, stream, w.nodes, w.cols,
+                           plan.d_tiles, plan.ntiles, d_out);
+        HIP_TRY(hipGetLastError());
+        if (replay)   /* the device flag is sticky: a later frame's copy cannot hide an earlier overflow */
+            HIP_TRY(hipMemcpyAsync(w.h_flag, w.d_flag, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipEventRecord(w.free_ev, stream));
+        if (replay) {
+            HIP_TRY(hipEventRecord(w.flag_ev, stream));
+            w.flag_pending = true;
+        }
+        return CRT_OK;
+    };
+    /* a recorded-size frame's levels are a fixed launch sequence: replayed
+     * from a HIP graph captured the first time (one launch instead of ~2 per
+     * level) */
     if (replay && sc->wf_graph) {
-        for (const auto &g : w.graphs)
-            if (g.tiles == (const void *)plan.d_tiles && g.out == d_out && g.stream == stream &&
-                g.scene == (const void *)d_scene && std::memcmp(&g.st, st, sizeof *st) == 0) {
-                HIP_TRY(hipGraphLaunch(g.exec, stream));
-                HIP_TRY(hipEventRecord(w.flag_ev, stream));
-                w.flag_pending = true;
-                return CRT_OK;
+        for (const auto &g : wb.graphs)
+            if (g.tiles == (const void *)plan.d_tiles && g.stream == ls && g.scene == (const void *)d_scene &&
+                std::memcmp(&g.st, st, sizeof *st) == 0) {
+                HIP_TRY(hipGraphLaunch(g.exec, ls));
+                return finish();
             }
     }
     const bool capture = replay && sc->wf_graph;
-    if (capture) HIP_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
+    if (capture) HIP_TRY(hipStreamBeginCapture(ls, hipStreamCaptureModeRelaxed));
     auto cap_of = [](int64_t c) { return (int32_t)std::min<int64_t>(c, INT32_MAX); };
     std::vector<int32_t> sizes;
     auto enqueue = [&]() -> int {
-    HIP_TRY(hipMemsetAsync(w.counts, 0, kMaxLevels * sizeof(int32_t), stream));
+    HIP_TRY(hipMemsetAsync(w.counts, 0, kMaxLevels * sizeof(int32_t), ls));
     unsigned long long *cnt = sc->d_counters;
     WLevel lv{nullptr, 0, 0, w.q[0], w.counts, (int32_t)n0, w.nodes, w.cols, 64,
               replay ? (rec.empty() ? 0 : rec[0]) : cap_of(w.qcap[0]), w.d_flag};
     const int blocks0 = (plan.ntiles + 3) / 4;
 #define CRT_WF0(T, COUNT)                                                                                   \
-    hipLaunchKernelGGL((k_wf_level<T, true, COUNT>), dim3(blocks0), dim3(256), 0, stream, d_scene, ds,      \
+    hipLaunchKernelGGL((k_wf_level<T, true, COUNT>), dim3(blocks0), dim3(256), 0, ls, d_scene, ds,          \
                        plan.d_tiles, plan.ntiles, lv, cnt)
     if (primary == 14) {   /* level 0 on the BVH (camera bins there measured neutral, profiles/r03/ab_level0_bins) */
         if (count) CRT_WF0(14, true); else CRT_WF0(14, false);
@@ -717,12 +782,12 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
             n = rec[L - 1];
             out_cap = L < (int)rec.size() ? rec[L] : 0;
         } else {
-            HIP_TRY(hipMemcpyAsync(&n, w.counts + (L - 1), sizeof n, hipMemcpyDeviceToHost, stream));
-            HIP_TRY(hipStreamSynchronize(stream));
+            HIP_TRY(hipMemcpyAsync(&n, w.counts + (L - 1), sizeof n, hipMemcpyDeviceToHost, ls));
+            HIP_TRY(hipStreamSynchronize(ls));
             if (n == 0) break;
             if (base + 3 * (int64_t)n > INT32_MAX) return set_error(CRT_E_UNSUPPORTED, "wavefront ray ids exceed 2^31");
-            if ((rc = wf_grow_ids(w, base + 3 * (int64_t)n, base, stream)) != CRT_OK) return rc;
-            if ((rc = wf_grow_queue(w, cur ^ 1, 2 * (int64_t)n)) != CRT_OK) return rc;
+            if ((rc = wf_grow_ids(wb, w, base + 3 * (int64_t)n, base, ls)) != CRT_OK) return rc;
+            if ((rc = wf_grow_queue(wb, w, cur ^ 1, 2 * (int64_t)n)) != CRT_OK) return rc;
             out_cap = cap_of(w.qcap[cur ^ 1]);
             sizes.push_back(n);
         }
@@ -736,7 +801,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         const int64_t waves = ((int64_t)n + rpw_l - 1) / rpw_l;
         const int blocks = (int)((waves + 3) / 4);
 #define CRT_WF(SEC, COUNT)                                                                                  \
-    hipLaunchKernelGGL((k_wf_level<SEC, false, COUNT>), dim3(blocks), dim3(256), 0, stream, d_scene, ds,     \
+    hipLaunchKernelGGL((k_wf_level<SEC, false, COUNT>), dim3(blocks), dim3(256), 0, ls, d_scene, ds,         \
                        plan.d_tiles, plan.ntiles, l, cnt)
         if (sec == 14) {
             if (count) CRT_WF(14, true); else CRT_WF(14, false);
@@ -752,19 +817,15 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         cur ^= 1;
     }
     for (auto it = levels.rbegin(); it != levels.rend(); ++it)
-        hipLaunchKernelGGL(k_wf_compose, dim3((unsigned)((it->second + 255) / 256)), dim3(256), 0, stream, w.nodes,
+        hipLaunchKernelGGL(k_wf_compose, dim3((unsigned)((it->second + 255) / 256)), dim3(256), 0, ls, w.nodes,
                            w.cols, (int32_t)it->first, (int32_t)it->second);
-    hipLaunchKernelGGL(k_wf_pixels, dim3(blocks0), dim3(256), 0, stream, w.nodes, w.cols, plan.d_tiles,
-                       plan.ntiles, d_out);
     HIP_TRY(hipGetLastError());
-    if (replay)   /* the device flag is sticky: a later frame's copy cannot hide an earlier overflow */
-        HIP_TRY(hipMemcpyAsync(w.h_flag, w.d_flag, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
     return CRT_OK;
     };
     rc = enqueue();
     if (capture) {
         hipGraph_t graph = nullptr;
-        const hipError_t e = hipStreamEndCapture(stream, &graph);
+        const hipError_t e = hipStreamEndCapture(ls, &graph);
         if (rc != CRT_OK) {
             if (graph) (void)hipGraphDestroy(graph);
             return rc;
@@ -774,16 +835,14 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
         (void)hipGraphDestroy(graph);
         if (ei != hipSuccess) return set_error(CRT_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
-        w.graphs.push_back(WfBuffers::Graph{(const void *)plan.d_tiles, *st, d_out, stream, (const void *)d_scene, exec});
-        HIP_TRY(hipGraphLaunch(exec, stream));
+        wb.graphs.push_back(WfBuffers::Graph{(const void *)plan.d_tiles, *st, nullptr, ls, (const void *)d_scene, exec});
+        HIP_TRY(hipGraphLaunch(exec, ls));
     } else if (rc != CRT_OK) {
         return rc;
     }
-    if (replay) {
-        HIP_TRY(hipEventRecord(w.flag_ev, stream));
-        w.flag_pending = true;
-    } else if (!count && sc->wf_replay) {
-        WfBuffers::Rec &r = w.recs[(const void *)plan.d_tiles];
+    if ((rc = finish()) != CRT_OK) return rc;
+    if (!replay && !count && sc->wf_replay) {
+        WfBuffers::Rec &r = wb.recs[(const void *)plan.d_tiles];
         if (sc->wf_replay == 2)
             for (int32_t &n : sizes) n = n > 1 ? n - 1 : n;
         r.sizes.swap(sizes);

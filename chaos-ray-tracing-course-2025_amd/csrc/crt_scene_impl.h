@@ -77,8 +77,11 @@ struct BinsDev {
 };
 
 
-/* Device buffers of the wavefront path, grown on demand (kept across frames). */
-struct WfBuffers {
+/* One frame's buffers of the wavefront path, grown on demand (kept across
+ * frames).  kWfSets sets: recorded-size frames take them in turn, each on a
+ * stream of its own, so frame k + 1's levels run while frame k's do
+ * (render_wavefront); frames with read-backs use set 0 on the caller's stream. */
+struct WfSet {
     crt_amd::WNode *nodes = nullptr;
     crt_amd::DVec4 *cols = nullptr;
     int64_t cap = 0;             /* ray ids */
@@ -86,6 +89,24 @@ struct WfBuffers {
     int64_t qcap[2] = {0, 0};
     int32_t *counts = nullptr;   /* children queued per level; counts[count_cap - 1]: overflow flag */
     int count_cap = 0;
+    /* overflow flag of recorded-size frames: device word, copied into pinned
+     * host memory behind each such frame and read once that copy is done */
+    int32_t *d_flag = nullptr;
+    int32_t *h_flag = nullptr;
+    hipEvent_t flag_ev = nullptr;
+    bool flag_pending = false;
+    hipStream_t stream = nullptr;     /* the set's levels (recorded-size frames) */
+    hipEvent_t free_ev = nullptr;     /* the set's last frame has written its pixels */
+    hipEvent_t done_ev = nullptr;     /* the set's levels of the current frame are done */
+};
+
+#ifndef CRT_WF_SETS
+#define CRT_WF_SETS 2            /* wavefront frames in flight (A/B builds: 3) */
+#endif
+constexpr int kWfSets = CRT_WF_SETS;
+struct WfBuffers {
+    WfSet set[kWfSets];
+    uint64_t frame = 0;          /* recorded-size frames issued (set = frame % kWfSets) */
     /* Level sizes of the last frame traced with host read-backs, and what they
      * depend on (settings, tile list): a frame's level sizes are a function of
      * its rays alone, so later frames with the same key launch every level
@@ -96,12 +117,6 @@ struct WfBuffers {
         int ntiles = 0;
     };
     std::map<const void *, Rec> recs;   /* by tile list (device pointer; cleared when plans are freed) */
-    /* overflow flag of recorded-size frames: device word, copied into pinned
-     * host memory behind each such frame and read once that copy is done */
-    int32_t *d_flag = nullptr;
-    int32_t *h_flag = nullptr;
-    hipEvent_t flag_ev = nullptr;
-    bool flag_pending = false;
     /* recorded-size frames captured as HIP graphs, by everything their
      * launches bake in (cleared whenever a buffer, tile list or record changes) */
     struct Graph {
@@ -225,6 +240,7 @@ namespace crt_amd {
 void wf_graphs_clear(WfBuffers &w);
 void wf_free(WfBuffers &w);
 bool wf_overflowed(WfBuffers &w, bool wait);
+int wf_streams(WfBuffers &wb, hipStream_t stream);
 int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool full_frame, ShardPlan &plan);
 void free_plans(crt_hip_scene *sc);
 int sync_device_record(crt_hip_scene *sc, const DeviceScene **out);
