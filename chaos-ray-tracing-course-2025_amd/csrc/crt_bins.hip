@@ -918,8 +918,8 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
      * (recorded once, so the first two frames find their lists free) */
     HIP_TRY(hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) {
-        HIP_TRY(hipEventCreateWithFlags(&b.bdone[i], hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&b.rdone[i], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&b.bdone[i], CRT_PIPE_EV_FLAGS));
+        HIP_TRY(hipEventCreateWithFlags(&b.rdone[i], CRT_PIPE_EV_FLAGS));
         HIP_TRY(hipEventRecord(b.rdone[i], sc->stream));
         HIP_TRY(hipEventRecord(b.bdone[i], sc->stream));
     }

@@ -630,8 +630,8 @@ int wf_streams(WfBuffers &wb, hipStream_t stream) {
     if (wb.set[0].stream) return CRT_OK;
     for (WfSet &w : wb.set) HIP_TRY(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
     for (WfSet &w : wb.set) {
-        HIP_TRY(hipEventCreateWithFlags(&w.free_ev, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&w.done_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&w.free_ev, CRT_PIPE_EV_FLAGS));
+        HIP_TRY(hipEventCreateWithFlags(&w.done_ev, CRT_PIPE_EV_FLAGS));
         HIP_TRY(hipEventRecord(w.free_ev, stream));
     }
     return CRT_OK;

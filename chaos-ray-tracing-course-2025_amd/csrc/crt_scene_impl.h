@@ -40,6 +40,13 @@ struct ShardPlan {
 
 using namespace crt_amd;
 
+/* Flags of the events that order the frames pipelines' streams on one device
+ * (camera bins, wavefront sets): no timing, and no system-scope fence — the
+ * work they order is on the same device, and kernel ends release to it. */
+#ifndef CRT_PIPE_EV_FLAGS
+#define CRT_PIPE_EV_FLAGS (hipEventDisableTiming | hipEventDisableSystemFence)
+#endif
+
 /* Device buffers of the camera bins (crt_bins.hip), per scene. */
 struct BinsDev {
     crt_amd::BinCamera cam{};

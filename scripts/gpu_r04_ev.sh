@@ -1,0 +1,9 @@
+# pipeline events with / without the system-scope fence: C2 and C3 bench lines
+set -e
+export TMPDIR=/tmp
+for v in main evfence main evfence; do
+  if [ $v = main ]; then P=$PWD/chaos-ray-tracing-course-2025_amd; else P=$PWD/abtest/$v; fi
+  CRT_PKG=$P timeout -k 10 300 python bench.py --steps 100 --no-cpu-baseline --no-e2e > gpurun_out/r04_ev_$v.json 2>/dev/null
+  CRT_PKG=$P timeout -k 10 300 python bench.py --config c3 --steps 20 --warmup 3 --no-cpu-baseline --no-e2e > gpurun_out/r04_ev3_$v.json 2>/dev/null
+  echo "$v c2 $(python3 -c "import json; d=json.loads(open('gpurun_out/r04_ev_$v.json').read().strip().splitlines()[-1]); print(d['ms_per_step'])") c3 $(python3 -c "import json; d=json.loads(open('gpurun_out/r04_ev3_$v.json').read().strip().splitlines()[-1]); print(d['ms_per_step'])")"
+done
