@@ -578,15 +578,17 @@ int wf_grow_queue(WfBuffers &wb, WfSet &w, int k, int64_t need) {
 
 void wf_free(WfBuffers &wb) {
     wf_graphs_clear(wb);
+    for (hipStream_t st : wb.streams)
+        if (st) (void)hipStreamSynchronize(st);
     for (WfSet &w : wb.set) {
-        if (w.stream) (void)hipStreamSynchronize(w.stream);
         for (void *p : {(void *)w.nodes, (void *)w.cols, (void *)w.q[0], (void *)w.q[1], (void *)w.counts, (void *)w.d_flag})
             if (p) (void)hipFree(p);
         if (w.h_flag) (void)hipHostFree(w.h_flag);
         for (hipEvent_t e : {w.flag_ev, w.free_ev, w.done_ev})
             if (e) (void)hipEventDestroy(e);
-        if (w.stream) (void)hipStreamDestroy(w.stream);
     }
+    for (hipStream_t st : wb.streams)
+        if (st) (void)hipStreamDestroy(st);
     wb = WfBuffers{};
 }
 
@@ -627,8 +629,8 @@ bool wf_overflowed(WfBuffers &wb, bool wait) {
  * upload for scenes that take the wavefront path, so the first frame does
  * not pay for it. */
 int wf_streams(WfBuffers &wb, hipStream_t stream) {
-    if (wb.set[0].stream) return CRT_OK;
-    for (WfSet &w : wb.set) HIP_TRY(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
+    if (wb.streams[0]) return CRT_OK;
+    for (hipStream_t &st : wb.streams) HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     for (WfSet &w : wb.set) {
         HIP_TRY(hipEventCreateWithFlags(&w.free_ev, CRT_PIPE_EV_FLAGS));
         HIP_TRY(hipEventCreateWithFlags(&w.done_ev, CRT_PIPE_EV_FLAGS));
@@ -648,12 +650,15 @@ int wf_streams(WfBuffers &wb, hipStream_t stream) {
  * frame: crt_hip_render re-renders that frame with read-backs, the device-side
  * entry points report it on the next call).
  *
- * Recorded-size frames take kWfSets buffer sets in turn, each set's levels
- * and compose on a stream of its own (after the set's previous frame wrote
+ * Recorded-size frames take up to kWfSets buffer sets in turn, set i's levels
+ * and compose on stream i % kWfStreams (after the set's previous frame wrote
  * its pixels), the pixels on the caller's stream (after the set's levels):
  * consecutive frames' levels overlap — a level's few, long walks leave most
  * of the GPU idle — while the frame's only write the caller sees stays in
- * the caller's stream order. */
+ * the caller's stream order.  More frames in flight kept paying: C3 back to
+ * back 1.20 ms with 2 sets/2 streams, 1.07 with 4/4, 0.93 with 8/8, 0.89
+ * with 12/12, 0.90 with 16/16; sets sharing streams were slower
+ * (profiles/r04/ab_wf_sets.txt). */
 int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_settings *st, const ShardPlan &plan,
                      float *d_out, hipStream_t stream, bool count, const DeviceScene *d_scene, int sec, int primary) {
     WfBuffers &wb = sc->wf;
@@ -670,7 +675,21 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
     const auto rit = wb.recs.find((const void *)plan.d_tiles);
     const bool replay = !count && sc->wf_replay && rit != wb.recs.end() && rit->second.ntiles == plan.ntiles &&
                         std::memcmp(&rit->second.st, st, sizeof *st) == 0;
-    const int si = replay ? (int)(wb.frame++ % kWfSets) : 0;
+    /* sets in use: as many as CRT_WF_SET_BUDGET holds of this frame size
+     * (rays x (node + colour) + two queues), 2 <= sets <= kWfSets; each set
+     * waits for its own previous frame, so the count may change between frames */
+    int si = 0;
+    if (replay) {
+        int64_t tot = n0, mx = 1;
+        for (int32_t n : rit->second.sizes) {
+            tot += n;
+            mx = std::max<int64_t>(mx, n);
+        }
+        const int64_t set_bytes = tot * (int64_t)(sizeof(WNode) + sizeof(DVec4)) + 2 * mx * (int64_t)sizeof(WRay);
+        const int64_t fit = CRT_WF_SET_BUDGET / std::max<int64_t>(set_bytes, 1);
+        const int nsets = (int)std::min<int64_t>(kWfSets, std::max<int64_t>(2, fit));
+        si = (int)(wb.frame++ % (uint64_t)nsets);
+    }
     WfSet &w = wb.set[si];
     {
         const int rc0 = wf_streams(wb, stream);
@@ -678,7 +697,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
     }
     /* where the levels run: a recorded-size frame on its set's stream, after
      * the set's previous frame; a frame with read-backs on the caller's */
-    const hipStream_t ls = replay ? w.stream : stream;
+    const hipStream_t ls = replay ? wb.streams[si % kWfStreams] : stream;
     HIP_TRY(hipStreamWaitEvent(ls, w.free_ev, 0));
     const int kMaxLevels = (int)ds.max_ray_depth + 2;
     if (!w.counts || w.count_cap < kMaxLevels) {
@@ -740,7 +759,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
      * level) */
     if (replay && sc->wf_graph) {
         for (const auto &g : wb.graphs)
-            if (g.tiles == (const void *)plan.d_tiles && g.stream == ls && g.scene == (const void *)d_scene &&
+            if (g.tiles == (const void *)plan.d_tiles && g.stream == ls && g.set == si && g.scene == (const void *)d_scene &&
                 std::memcmp(&g.st, st, sizeof *st) == 0) {
                 HIP_TRY(hipGraphLaunch(g.exec, ls));
                 return finish();
@@ -835,7 +854,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
         (void)hipGraphDestroy(graph);
         if (ei != hipSuccess) return set_error(CRT_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
-        wb.graphs.push_back(WfBuffers::Graph{(const void *)plan.d_tiles, *st, nullptr, ls, (const void *)d_scene, exec});
+        wb.graphs.push_back(WfBuffers::Graph{(const void *)plan.d_tiles, *st, nullptr, ls, si, (const void *)d_scene, exec});
         HIP_TRY(hipGraphLaunch(exec, ls));
     } else if (rc != CRT_OK) {
         return rc;

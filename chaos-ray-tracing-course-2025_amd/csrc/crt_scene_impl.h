@@ -85,9 +85,10 @@ struct BinsDev {
 
 
 /* One frame's buffers of the wavefront path, grown on demand (kept across
- * frames).  kWfSets sets: recorded-size frames take them in turn, each on a
- * stream of its own, so frame k + 1's levels run while frame k's do
- * (render_wavefront); frames with read-backs use set 0 on the caller's stream. */
+ * frames).  Up to kWfSets sets: recorded-size frames take them in turn, set
+ * i's levels on stream i % kWfStreams, so the levels of several consecutive
+ * frames run side by side (render_wavefront); frames with read-backs use set
+ * 0 on the caller's stream. */
 struct WfSet {
     crt_amd::WNode *nodes = nullptr;
     crt_amd::DVec4 *cols = nullptr;
@@ -102,18 +103,27 @@ struct WfSet {
     int32_t *h_flag = nullptr;
     hipEvent_t flag_ev = nullptr;
     bool flag_pending = false;
-    hipStream_t stream = nullptr;     /* the set's levels (recorded-size frames) */
     hipEvent_t free_ev = nullptr;     /* the set's last frame has written its pixels */
     hipEvent_t done_ev = nullptr;     /* the set's levels of the current frame are done */
 };
 
 #ifndef CRT_WF_SETS
-#define CRT_WF_SETS 2            /* wavefront frames in flight (A/B builds: 3) */
+#define CRT_WF_SETS 12           /* wavefront frame buffer sets, at most (A/B builds: 2, 4, 8, 16) */
+#endif
+#ifndef CRT_WF_STREAMS
+#define CRT_WF_STREAMS CRT_WF_SETS
+#endif
+#ifndef CRT_WF_SET_BUDGET
+#define CRT_WF_SET_BUDGET (16ll << 30)   /* bytes all sets of one frame size may take together */
 #endif
 constexpr int kWfSets = CRT_WF_SETS;
+constexpr int kWfStreams = CRT_WF_STREAMS;    /* set i's levels run on stream i % kWfStreams */
+static_assert(kWfSets % kWfStreams == 0, "buffer sets share streams evenly");
+static_assert(kWfSets >= 2, "frames in flight need two sets at least");
 struct WfBuffers {
     WfSet set[kWfSets];
-    uint64_t frame = 0;          /* recorded-size frames issued (set = frame % kWfSets) */
+    hipStream_t streams[kWfStreams] = {};
+    uint64_t frame = 0;          /* recorded-size frames issued (set = frame % sets in use) */
     /* Level sizes of the last frame traced with host read-backs, and what they
      * depend on (settings, tile list): a frame's level sizes are a function of
      * its rays alone, so later frames with the same key launch every level
@@ -131,6 +141,7 @@ struct WfBuffers {
         crt_renderer_settings st;
         const float *out;
         hipStream_t stream;
+        int set;                 /* the buffer set whose pointers the graph holds */
         const void *scene;
         hipGraphExec_t exec;
     };

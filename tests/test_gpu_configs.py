@@ -277,19 +277,21 @@ def test_c3_recorded_sizes_overflow(N, devbuf):
 
 
 def test_c3_frames_pipelined(N, devbuf):
-    """Recorded-size wavefront frames issued back to back alternate between
-    two buffer sets, each set's levels on a stream of its own, so frame k + 1's
-    levels run beside frame k's (crt_host_render.hip render_wavefront); the
-    pixels stay in the caller's stream order.  Twelve frames into two
-    alternating buffers, then a host frame: all equal the read-back frame."""
+    """Recorded-size wavefront frames issued back to back take four buffer
+    sets in turn, set i's levels on stream i % 2, so frame k + 1's levels run
+    beside frame k's and frame k + 2's right behind frame k's
+    (crt_host_render.hip render_wavefront; each set replays a graph captured
+    on its own buffers); the pixels stay in the caller's stream order.
+    Twelve frames into four rotating buffers, then a host frame: all equal
+    the read-back frame."""
     sc = scene_npz("11-01-refractive__scene8").set_resolution(480, 270)
     st = N.RendererSettings.default(max_ray_depth=8)
     ref = N.HipScene(sc, wf_replay=0).render(st)
     g = N.HipScene(sc)
     assert np.array_equal(bits(g.render(st)), bits(ref))   # records the level sizes
-    d = [devbuf.alloc(ref.nbytes) for _ in range(2)]
+    d = [devbuf.alloc(ref.nbytes) for _ in range(4)]
     for k in range(12):
-        g.render_device(st, d[k % 2])
-    for k in range(2):
+        g.render_device(st, d[k % 4])
+    for k in range(4):
         assert np.array_equal(bits(devbuf.download(d[k], ref.shape, np.float32)), bits(ref))
     assert np.array_equal(bits(g.render(st)), bits(ref))
