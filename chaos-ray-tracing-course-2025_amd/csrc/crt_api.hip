@@ -623,7 +623,7 @@ int crt_hip_profile_waves(crt_hip_scene *sc, const crt_renderer_settings *st, ui
     std::vector<int32_t> ph_all, rest;
     int par = 0;
     if (rc == CRT_OK && e == hipSuccess && bp.cell_tile) {
-        par = (int)((sc->bins.frame - 1) & 1);   /* the parity the frame just used */
+        par = (int)((sc->bins.frame - 1) % kBinSets);   /* the set the frame just used */
         int64_t slots = 0;
         for (int q = 0; q < kBinKinds; ++q) slots += (int64_t)kBinShards * bp.cap[q];
         work.resize((size_t)std::max<int64_t>(1, slots));

@@ -297,10 +297,10 @@ __global__ __launch_bounds__(256) void k_bins_project(const CamCand *__restrict_
     BSTAMP(0);
     BinsHdr *hdr = hdr2 + par;
     int32_t *cnt = cnt2 + (size_t)par * ncell * kCntStride;
-    /* the other parity's counters start the next frame at zero (this frame
+    /* the next set's counters start the next frame at zero (this frame
      * does not touch them; the previous one is done with them) */
     if (blockIdx.x == 0) {
-        BinsHdr *o = hdr2 + (par ^ 1);
+        BinsHdr *o = hdr2 + (par + 1) % kBinSets;
         if (tid == 0) o->n_every.v = 0;
         if (tid == 1) o->nrem.v = 0;
         if (tid < kBinShards) {
@@ -309,15 +309,15 @@ __global__ __launch_bounds__(256) void k_bins_project(const CamCand *__restrict_
             o->rec[tid].v = 0;
         }
         /* this frame's work-list counters (k_bins_sort appends after this
-         * kernel; the render two frames back, same parity, is done with them) */
+         * kernel; the render kBinSets frames back, same set, is done with them) */
         if (phdr2 && tid < kBinKinds * kBinShards)
             phdr2[BCK(bins_phdr_at(par, tid / kBinShards, tid % kBinShards), kBinsPhdrInts, 1)] = 0;
     }
     /* this frame's per-cell lengths start empty (k_bins_sort sets the listed
-     * cells'); the other parity's counts start the next frame at zero */
+     * cells'); the next set's counts start the next frame at zero */
     for (int i = (int)(blockIdx.x * blockDim.x) + tid; i < ncell; i += (int)(gridDim.x * blockDim.x)) {
         bin_len[BCK(i, BDBG(ncell), 2)] = 0;
-        cnt2[((size_t)(par ^ 1) * ncell + BCK(i, BDBG(ncell), 2)) * kCntStride] = 0;
+        cnt2[((size_t)((par + 1) % kBinSets) * ncell + BCK(i, BDBG(ncell), 2)) * kCntStride] = 0;
     }
     const int tl = tid >> 3, q = tid & 7;
     const int t0 = (int)blockIdx.x * kProjTris, t = t0 + tl;
@@ -760,7 +760,7 @@ void bins_free(crt_hip_scene *sc) {
     BinsDev &b = sc->bins;
     if (b.stream) (void)hipStreamSynchronize(b.stream);
     for (void *p : b.allocs) (void)hipFree(p);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kBinSets; ++i) {
         if (b.bdone[i]) (void)hipEventDestroy(b.bdone[i]);
         if (b.rdone[i]) (void)hipEventDestroy(b.rdone[i]);
     }
@@ -816,7 +816,7 @@ int bins_dbg_arm(crt_hip_scene *sc, const ShardPlan &plan) {
                                           " bound " + std::to_string(d.bound));
     d.nt = b.nt;
     d.ncell = b.ncell;
-    d.rec_cap = 2 * b.rec_cap;
+    d.rec_cap = kBinSets * b.rec_cap;
     d.ne_cap = kBinShards * b.cap_shard;
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_bins_dbg), &d, sizeof d));
 #else
@@ -854,14 +854,14 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
         return CRT_OK;
     }
     b.pair_blocks = 256;   /* the sizing pass's grid; resized from its queued pairs below */
-    if ((rc = bins_alloc(sc, &b.cnt, (size_t)2 * b.ncell * kCntStride, true)) != CRT_OK) return rc;   /* two parities */
+    if ((rc = bins_alloc(sc, &b.cnt, (size_t)kBinSets * b.ncell * kCntStride, true)) != CRT_OK) return rc;   /* per set */
     if ((rc = bins_alloc(sc, &b.keys, (size_t)b.ncell * kBinCellCap)) != CRT_OK) return rc;   /* 64-bit keys */
     if ((rc = bins_alloc(sc, &b.every, (size_t)kBinMaxEverywhere)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.nonempty, (size_t)kBinShards * b.cap_shard)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.bigl, (size_t)kBinShards * b.cap_shard)) != CRT_OK) return rc;
-    if ((rc = bins_alloc(sc, &b.hdr, 2, true)) != CRT_OK) return rc;
-    if ((rc = bins_alloc(sc, &b.off, (size_t)2 * b.ncell, true)) != CRT_OK) return rc;   /* two parities */
-    if ((rc = bins_alloc(sc, &b.len, (size_t)2 * b.ncell, true)) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.hdr, kBinSets, true)) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.off, (size_t)kBinSets * b.ncell, true)) != CRT_OK) return rc;   /* per set */
+    if ((rc = bins_alloc(sc, &b.len, (size_t)kBinSets * b.ncell, true)) != CRT_OK) return rc;
     /* sizing pass: counts per cell of this camera */
     if ((rc = bins_dbg_arm(sc, ShardPlan{})) != CRT_OK) return rc;
     if ((rc = launch_project(sc, sc->stream, 0, nullptr)) != CRT_OK) return rc;
@@ -872,8 +872,8 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
     HIP_TRY(hipMemcpyAsync(&h, b.hdr, sizeof h, hipMemcpyDeviceToHost, sc->stream));
     const int n_every = h.n_every.v;
     HIP_TRY(hipStreamSynchronize(sc->stream));
-    HIP_TRY(hipMemsetAsync(b.cnt, 0, 2 * cnt.size() * sizeof(int32_t), sc->stream));
-    HIP_TRY(hipMemsetAsync(b.hdr, 0, 2 * sizeof(BinsHdr), sc->stream));
+    HIP_TRY(hipMemsetAsync(b.cnt, 0, kBinSets * cnt.size() * sizeof(int32_t), sc->stream));
+    HIP_TRY(hipMemsetAsync(b.hdr, 0, kBinSets * sizeof(BinsHdr), sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
     b.frame = 0;
     b.count.assign((size_t)b.ncell, 0);
@@ -909,15 +909,15 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
         base += cap;
     }
     b.rec_cap = (int32_t)base;
-    if ((int64_t)2 * base >= INT32_MAX) {   /* record offsets are int32 */
+    if ((int64_t)kBinSets * base >= INT32_MAX) {   /* record offsets are int32 */
         bins_free(sc);
         return CRT_OK;
     }
-    if ((rc = bins_alloc(sc, &b.recs, (size_t)2 * b.rec_cap)) != CRT_OK) return rc;   /* two parities */
-    /* the frames pipeline: the binning's stream and the parities' events
-     * (recorded once, so the first two frames find their lists free) */
+    if ((rc = bins_alloc(sc, &b.recs, (size_t)kBinSets * b.rec_cap)) != CRT_OK) return rc;   /* per set */
+    /* the frames pipeline: the binning's stream and the sets' events
+     * (recorded once, so the first frames find their lists free) */
     HIP_TRY(hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking));
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kBinSets; ++i) {
         HIP_TRY(hipEventCreateWithFlags(&b.bdone[i], CRT_PIPE_EV_FLAGS));
         HIP_TRY(hipEventCreateWithFlags(&b.rdone[i], CRT_PIPE_EV_FLAGS));
         HIP_TRY(hipEventRecord(b.rdone[i], sc->stream));
@@ -985,7 +985,7 @@ int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
     bp.nfill = (b.ncell + 15) / 16;   /* 16 cells a fill wave */
     void *p[4] = {nullptr, nullptr, nullptr, nullptr};
     bp.wslots = (int32_t)slots;
-    const size_t sizes[4] = {(size_t)b.ncell * sizeof(int32_t), (size_t)std::max<int64_t>(1, 2 * slots) * sizeof(BinsWork),
+    const size_t sizes[4] = {(size_t)b.ncell * sizeof(int32_t), (size_t)std::max<int64_t>(1, kBinSets * slots) * sizeof(BinsWork),
                              (size_t)kBinsPhdrInts * sizeof(int32_t), std::max<size_t>(1, rest.size()) * sizeof(int32_t)};
     for (int i = 0; i < 4; ++i) {
         HIP_TRY(hipMalloc(&p[i], sizes[i]));
@@ -1003,16 +1003,18 @@ int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
     return CRT_OK;
 }
 
-/* The frame's lists, before its render on `s`; returns the frame's parity
- * (the render reads that set of lists and records rdone[parity] after it).
+/* The frame's lists, before its render on `s`; returns the frame's set
+ * (the render reads that set of lists and records rdone[set] after it).
  * While the previous frame still renders (frames issued back to back), the
- * binning runs on the binning's own stream — after the render two frames back
- * (same parity) is done with the set and after the previous binning — and `s`
- * waits for it: frame k + 1's binning overlaps frame k's render.  Otherwise
- * (one frame at a time) `s` takes the binning itself: no cross-stream hop. */
+ * binning runs on the binning's own stream — after the render kBinSets frames
+ * back (same set) is done with the set and after the previous binning — and
+ * `s` waits for it: the next frames' binnings overlap frame k's render.
+ * Otherwise (one frame at a time) `s` takes the binning itself: no
+ * cross-stream hop. */
 int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *par_out) {
     BinsDev &b = sc->bins;
-    const int par = (int)(b.frame++ & 1);
+    const int par = (int)(b.frame++ % kBinSets);
+    const int prev = (par + kBinSets - 1) % kBinSets;
     {
         const int rc0 = bins_dbg_arm(sc, plan);
         if (rc0 != CRT_OK) return rc0;
@@ -1021,18 +1023,18 @@ int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *p
      * scratch (items, keys, counts, lists), so they stay in order: the
      * binning stream also waits for the previous frame's binning, wherever
      * it ran */
-    const bool overlap = hipEventQuery(b.rdone[par ^ 1]) == hipErrorNotReady;
+    const bool overlap = hipEventQuery(b.rdone[prev]) == hipErrorNotReady;
     const hipStream_t bs = overlap ? b.stream : s;
     if (overlap) {
         HIP_TRY(hipStreamWaitEvent(b.stream, b.rdone[par], 0));
-        HIP_TRY(hipStreamWaitEvent(b.stream, b.bdone[par ^ 1], 0));
+        HIP_TRY(hipStreamWaitEvent(b.stream, b.bdone[prev], 0));
     }
     int rc = launch_project(sc, bs, par, plan.bp.phdr);
     if (rc != CRT_OK) return rc;
     BinsPlan bp = plan.bp;
     bp.par = par;
     if (bp.work) bp.work += (size_t)par * bp.wslots;
-    BinsCaps caps = b.caps;   /* this parity's half of the record buffer */
+    BinsCaps caps = b.caps;   /* this set's part of the record buffer */
     for (int i = 0; i < kBinShards; ++i) caps.base[i] += par * b.rec_cap;
     hipLaunchKernelGGL(k_bins_sort, dim3((unsigned)b.sort_blocks), dim3(64 * kSortWaves), 0, bs, b.tpl, b.items,
                        b.cnt + (size_t)par * b.ncell * kCntStride,
@@ -1088,9 +1090,9 @@ int64_t crt_hip_camera_bins(crt_hip_scene *sc, int32_t *len_out, void *recs_out,
     int rc = bins_enqueue(sc, none, sc->stream, nullptr);
     if (rc != CRT_OK) return rc;
     if ((rc = bins_dbg_arm(sc, none)) != CRT_OK) return rc;   /* diagnostic builds: this frame's violations */
-    const int par = (int)((b.frame - 1) & 1);   /* the parity that frame used */
+    const int par = (int)((b.frame - 1) % kBinSets);   /* the set that frame used */
     std::vector<int32_t> off((size_t)b.ncell), len((size_t)b.ncell);
-    std::vector<CamCand> recs((size_t)2 * b.rec_cap);   /* both parities' regions (offsets are absolute) */
+    std::vector<CamCand> recs((size_t)kBinSets * b.rec_cap);   /* every set's region (offsets are absolute) */
     HIP_TRY(hipMemcpyAsync(off.data(), b.off + (size_t)par * b.ncell, off.size() * sizeof(int32_t),
                            hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipMemcpyAsync(len.data(), b.len + (size_t)par * b.ncell, len.size() * sizeof(int32_t),

@@ -967,7 +967,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         if (rc != CRT_OK) return rc;
         BinsPlan bp = plan.bp;
         bp.par = par;
-        bp.work += (size_t)par * bp.wslots;   /* this frame's parity of the work lists */
+        bp.work += (size_t)par * bp.wslots;   /* this frame's set of the work lists */
         const unsigned bb = (unsigned)((plan.waves + 3) / 4);
 #define CRT_LAUNCH_B(COUNT)                                                                                 \
     hipLaunchKernelGGL((k_render_tiles<false, 0, 15, 15, COUNT>), dim3(bb), dim3(256), 0, stream, d_scene, ds, \

@@ -51,7 +51,7 @@ struct BinsPlan {
     const int32_t *rest;  /* tiles the lists do not hold */
     int32_t cap[kBinKinds], wbase[kBinKinds];
     int32_t nrest, nfill, ncell;
-    int32_t wslots;       /* work-list slots of one parity (work: two parities; the frame's at par * wslots) */
+    int32_t wslots;       /* work-list slots of one set (work: kBinSets sets; the frame's at par * wslots) */
     int32_t split, medium, quad;
     int32_t par;          /* the frame's parity (which counters it uses) */
 };
@@ -72,11 +72,19 @@ struct BinsHdr {
     BinsCtr nb[kBinShards];    /* cells of more than 16 candidates listed per shard */
     BinsCtr rec[kBinShards];   /* records reserved per shard */
 };
+/* Sets of per-frame lists (records, per-cell off/len, work lists and their
+ * counters, the binning's counts): frame k takes set k % kBinSets, so the
+ * binnings of the next kBinSets - 1 frames may run while frame k renders. */
+#ifndef CRT_BIN_SETS
+#define CRT_BIN_SETS 3
+#endif
+constexpr int kBinSets = CRT_BIN_SETS;
+static_assert(kBinSets >= 2, "a frame's binning clears the next frame's set");
 /* a plan's work-list counters (BinsPlan::phdr) */
 __host__ __device__ constexpr int bins_phdr_at(int par, int kind, int sh) {
     return ((par * kBinKinds + kind) * kBinShards + sh) * kBinPad;
 }
-constexpr int kBinsPhdrInts = 2 * kBinKinds * kBinShards * kBinPad;
+constexpr int kBinsPhdrInts = kBinSets * kBinKinds * kBinShards * kBinPad;
 
 /* Where each shard's records go in the camera-bins record buffer. */
 struct BinsCaps {

@@ -57,30 +57,30 @@ struct BinsDev {
     int32_t *gsum = nullptr;              /* per group: pairs */
     int32_t *rem = nullptr;               /* groups queued for k_bins_pairs */
     int pair_blocks = 0;                  /* k_bins_pairs grid (0: not launched; the sizing pass queued none) */
-    int32_t *cnt = nullptr;               /* per cell: candidates; two parities (a frame zeroes the other's) */
+    int32_t *cnt = nullptr;               /* per cell: candidates; kBinSets sets (a frame zeroes the next one's) */
     uint64_t *keys = nullptr;             /* per cell: kBinCellCap sort keys (dmin bits << 32 | triangle id) */
     int32_t *every = nullptr;             /* everywhere triangles */
     int32_t *nonempty = nullptr;          /* cells with a candidate: kBinShards lists of cap_shard, arrival order */
     int32_t *bigl = nullptr;              /* cells of more than 16 candidates: kBinShards lists of cap_shard */
     int cap_shard = 0;
     int long_waves = 0;                   /* k_bins_sort waves for the long lists */
-    crt_amd::BinsHdr *hdr = nullptr;      /* two sets: frames alternate */
-    uint64_t frame = 0;                   /* frames binned (parity = frame & 1) */
+    crt_amd::BinsHdr *hdr = nullptr;      /* kBinSets sets: frames take them in turn */
+    uint64_t frame = 0;                   /* frames binned (set = frame % kBinSets) */
     crt_amd::BinsCaps caps{};             /* per shard: its region of recs */
-    crt_amd::CamCand *recs = nullptr;     /* the lists, two parities (rec_cap each) */
+    crt_amd::CamCand *recs = nullptr;     /* the lists, kBinSets sets (rec_cap each) */
     int32_t rec_cap = 0;
-    int32_t *off = nullptr, *len = nullptr;   /* per cell, two parities (ncell each) */
+    int32_t *off = nullptr, *len = nullptr;   /* per cell, kBinSets sets (ncell each) */
     std::vector<int32_t> count;           /* per cell: list length of the sizing pass (-1 over the cap) */
     int sort_blocks = 0;                  /* k_bins_sort blocks */
     int64_t records = 0;                  /* records of the sizing pass */
     double setup_ms = 0.0;
     std::vector<void *> allocs;
     /* frames pipeline: frame k's binning runs on `stream` (its kernels in
-     * order) while frame k - 1 renders; the lists the render reads are
-     * double-buffered by frame parity, bdone[p] = parity p's lists built,
-     * rdone[p] = parity p's render done with them */
+     * order) while frame k - 1 renders; the lists the render reads come in
+     * kBinSets sets taken in turn, bdone[p] = set p's lists built, rdone[p] =
+     * set p's render done with them */
     hipStream_t stream = nullptr;
-    hipEvent_t bdone[2] = {nullptr, nullptr}, rdone[2] = {nullptr, nullptr};
+    hipEvent_t bdone[crt_amd::kBinSets] = {}, rdone[crt_amd::kBinSets] = {};
 };
 
 

@@ -127,17 +127,17 @@ def test_bins_frames_repeat_bit_exact(N, oracle, devbuf):
 
 
 def test_bins_frames_pipelined_bit_exact(N, oracle, devbuf):
-    """Frames issued back to back without a host wait: frame k + 1's binning
-    runs on the binning stream while frame k renders (crt_bins.hip
-    bins_enqueue), on double-buffered lists.  Forty frames into two
-    alternating buffers, then a host frame: all equal the oracle."""
+    """Frames issued back to back without a host wait: the next frames'
+    binnings run on the binning stream while frame k renders (crt_bins.hip
+    bins_enqueue), on kBinSets (3) sets of lists taken in turn.  Forty frames
+    into three rotating buffers, then a host frame: all equal the oracle."""
     sc = scene_npz("14-01-acceleration-tree__scene1").set_resolution(960, 540)
     st = N.RendererSettings.default()
     want = bits(oracle.OracleScene(sc).render(st))
     g = N.HipScene(sc)
-    d = [devbuf.alloc(960 * 540 * 3 * 4) for _ in range(2)]
+    d = [devbuf.alloc(960 * 540 * 3 * 4) for _ in range(3)]
     for k in range(40):
-        g.render_device(st, d[k % 2])
-    for k in range(2):
+        g.render_device(st, d[k % 3])
+    for k in range(3):
         assert np.array_equal(bits(devbuf.download(d[k], (540, 960, 3), np.float32)), want)
     assert np.array_equal(bits(g.render(st)), want)
