@@ -554,13 +554,13 @@ def main():
                 torch.cuda.synchronize()
                 ser.append(e0.elapsed_time(e1))
             one_ms = statistics.median(ser)
-            bins = {"rebuilt_every_frame": True, "frames_in_flight": 2, "bins_ms": round(b_ms, 5),
+            bins = {"rebuilt_every_frame": True, "list_sets": 3, "bins_ms": round(b_ms, 5),
                     "frame_ms_one_at_a_time": round(one_ms, 5),
                     "frame_ms_bins_off": round(off_ms, 5),
                     "value_bins_off": round(rays_per_frame / (off_ms * 1e-3) / 1e6, 3),
                     "note": "frame = device binning (k_bins_project [+ k_bins_pairs] + k_bins_sort) + render; frames "
-                            "back to back (ms_per_step): frame k+1's binning overlaps frame k's render (double-"
-                            "buffered lists); frame_ms_one_at_a_time: a host sync after every frame; bins_ms = the "
+                            "back to back (ms_per_step): the next frames' binnings overlap frame k's render (3 "
+                            "sets of lists, crt_kernel_common.h kBinSets); frame_ms_one_at_a_time: a host sync after every frame; bins_ms = the "
                             "binning alone (HIP events, 50 frames); bins off = the BVH walk for every camera ray"}
 
     check = None
