@@ -82,8 +82,10 @@ PNODE_BYTES, SLOT_BYTES = 64, 48                     # device records (crt_layou
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    # a C2 frame is ~0.06 ms: 200 frames (12 ms) keep the pipeline's fill and
+    # drain (the first frame runs alone) under 1 % of the timed region
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--config", choices=sorted(CONFIGS), default="c2",
                    help="BASELINE config (c2 = the headline metric workload)")
     p.add_argument("--width", type=int, default=None, help="override the config's image width")

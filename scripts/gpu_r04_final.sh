@@ -32,12 +32,12 @@ if [[ $STEPS == *pmc* ]]; then
   grep -h '"build_id"' profiles/r04/pmc_c*.json | head -4
 fi
 if [[ $STEPS == *bench* ]]; then
-  run bench_c2 600 python bench.py --steps 50 --warmup 5
+  run bench_c2 600 python bench.py
   run bench_c3 600 python bench.py --config c3 --steps 20 --warmup 3
   run bench_c4 900 python bench.py --config c4 --steps 8 --warmup 2
   run bench_c5 600 python bench.py --config c5 --steps 10 --warmup 2
 fi
-[[ $STEPS == *trace* ]] && run trace_bench_c2 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_bench_c2" -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-e2e
+[[ $STEPS == *trace* ]] && run trace_bench_c2 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_bench_c2" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-e2e
 if [[ $STEPS == *shards* ]]; then
   for c in c2 c3 c4 c5; do
     r=20; [ $c = c4 ] && r=3; [ $c = c5 ] && r=5
