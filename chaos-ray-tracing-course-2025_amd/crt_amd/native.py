@@ -129,7 +129,8 @@ class SceneInfo(C.Structure):
                 ("height", C.c_int32), ("bucket_size", C.c_int32), ("gi_on", C.c_int32),
                 ("reflections_on", C.c_int32), ("refractions_on", C.c_int32), ("tree_on_device", C.c_int32),
                 ("tree_build_ms", C.c_double), ("prep_ms", C.c_double), ("bvh_ms", C.c_double),
-                ("bins_ms", C.c_double), ("upload_ms", C.c_double), ("create_ms", C.c_double)]
+                ("bins_ms", C.c_double), ("upload_ms", C.c_double), ("create_ms", C.c_double),
+                ("wf_sets", C.c_int32), ("pad0", C.c_int32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -253,7 +253,10 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
         if ((rc = upload(sc.get(), hs.ktopo, &ds.ktopo)) != CRT_OK) return rc;
         if ((rc = upload(sc.get(), hs.ktopo2, &ds.ktopo2)) != CRT_OK) return rc;
     }
-    sc->camera_fast = camera_rays_fast(hs, ds.planes_ok != 0);
+    sc->cam = host_camera(hs);
+    sc->fov_radians = hs.fov_radians;
+    sc->prune_origin_max = hs.prune_origin_max;
+    sc->camera_fast = camera_rays_fast(sc->cam, ds.planes_ok != 0);
     if (ds.bnodes) sc->traversal = 14;   /* camera rays through the BVH too */
     if ((rc = upload(sc.get(), hs.tri_attr, &ds.tri_attr)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.vnormal, &ds.vnormal)) != CRT_OK) return rc;
@@ -263,12 +266,6 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
     if ((rc = upload(sc.get(), hs.texels, &ds.texels)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.lights, &ds.lights)) != CRT_OK) return rc;
     ds.light_count = (int32_t)hs.lights.size();
-    std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
-    std::memcpy(ds.cam_rot, hs.cam_rot, sizeof ds.cam_rot);
-    ds.width = hs.width;
-    ds.height = hs.height;
-    ds.aspect = hs.aspect;
-    ds.tan_half_fov = hs.tan_half_fov;
     std::memcpy(ds.background, hs.background, sizeof ds.background);
     ds.gi_on = hs.gi_on;
     ds.reflections_on = hs.reflections_on;
@@ -383,6 +380,8 @@ int crt_hip_scene_tree(const crt_hip_scene *sc, float *bounds, int32_t *children
 int crt_hip_scene_info(const crt_hip_scene *sc, crt_scene_info *out) {
     if (!sc || !out) return set_error(CRT_E_INVALID, "null argument");
     *out = sc->info;
+    out->wf_sets = 0;
+    for (const WfSet &w : sc->wf.set) out->wf_sets += w.nodes ? 1 : 0;
     return CRT_OK;
 }
 

@@ -19,7 +19,7 @@
  *                   rest for k_bins_pairs, which spreads them over its grid
  *                   (launched when the scene's sizing pass queued groups).
  *                   Also zeroes this frame's per-cell lengths and the other
- *                   parity's counts.
+ *                   set's counts (kBinSets sets taken in turn).
  *   k_bins_sort     the long lists one a wave, the others four a wave (16
  *                   lanes each): the cell's keys plus the everywhere ids
  *                   ranked in LDS, written as CamCand records (static part
@@ -197,7 +197,7 @@ __device__ void bins_pairs(const BinItem *__restrict__ items, const int32_t *__r
     __shared__ int32_t gp[kMaxGroups + 1];
     __shared__ int32_t part[256];
     const int tid = (int)threadIdx.x;
-    const int nq = hdr->nrem.v;
+    const int nq = min(hdr->nrem.v, kMaxGroups);   /* k_bins_project queues no more (the rest scatter themselves) */
     /* exclusive prefix of the queued groups' remaining counts: each thread sums a run, then the runs are scanned */
     const int per = (nq + 255) / 256, g0 = tid * per, g1 = min(nq, g0 + per);
     int run = 0;
@@ -280,7 +280,7 @@ __device__ void bins_pairs(const BinItem *__restrict__ items, const int32_t *__r
  * pairs themselves — a group with more (a triangle covering thousands of
  * cells) queues its rest for k_bins_pairs.
  * Also the everywhere list, this frame's per-cell lengths (zero) and the other
- * parity's counters (zero for the next frame). */
+ * set's counters (zero for the next frame). */
 __global__ __launch_bounds__(256) void k_bins_project(const CamCand *__restrict__ tpl, int nt, BinCamera cam,
                                                       BinItem *__restrict__ items, int32_t *__restrict__ tpref,
                                                       int32_t *__restrict__ gsum, int32_t *__restrict__ every,
@@ -376,27 +376,42 @@ __global__ __launch_bounds__(256) void k_bins_project(const CamCand *__restrict_
             gsum[blockIdx.x] = incl;
         }
     }
+    /* the group's pairs past kExpand go to k_bins_pairs when it is launched
+     * (queue) and holds a slot for the group (its LDS scan takes kMaxGroups);
+     * otherwise the block scatters them itself, kExpand a round */
+    __shared__ int s_queued;
+    const int G = spre[kProjTris];
+    if (tid == 0) {
+        int qd = 0;
+        if (G > kExpand && queue) {
+            const int k = atomicAdd(&hdr->nrem.v, 1);
+            if (k < kMaxGroups) {
+                rem[BCK(k, BDBG(nt), 38)] = (int)blockIdx.x;
+                qd = 1;
+            }
+        }
+        s_queued = qd;
+    }
     __syncthreads();
     BSTAMP(2);
-    const int G = spre[kProjTris], E = min(G, kExpand);
-    if (tid == 0 && G > kExpand) {   /* the rest: k_bins_pairs (launched when the sizing pass queued groups) */
-        (void)BCK(queue ? 0 : -1, 1, 37);
-        rem[BCK(atomicAdd(&hdr->nrem.v, 1), BDBG(nt), 38)] = (int)blockIdx.x;
-    }
-    if (tid < E) {   /* pairs tid + 256 u of the group */
-        int cell[kPairsPerThread];
+    const int lim = s_queued ? kExpand : G;
+    for (int base = 0; base < lim; base += kExpand) {
+        const int E = min(lim - base, kExpand);
+        if (tid >= E) break;
+        int cell[kPairsPerThread];   /* pairs base + tid + 256 u of the group */
         uint64_t key[kPairsPerThread];
 #pragma unroll
         for (int u = 0; u < kPairsPerThread; ++u) {
             const int p = tid + 256 * u;
             cell[u] = -1;
             if (p >= E) continue;
-            int a = 0;   /* the last triangle whose pairs start at or before p */
+            const int pg = base + p;
+            int a = 0;   /* the last triangle whose pairs start at or before pg */
 #pragma unroll
             for (int st = kProjTris / 2; st > 0; st >>= 1)
-                if (spre[a + st] <= p) a += st;
+                if (spre[a + st] <= pg) a += st;
             const BinItem it = sit[a];
-            cell[u] = bins_pair_cell(it, p - spre[a], tx);
+            cell[u] = bins_pair_cell(it, pg - spre[a], tx);
             key[u] = bin_key(it.dmin, t0 + a);   /* the cell's sort key: (dmin, id) */
         }
         bins_scatter<kPairsPerThread>(cell, key, cnt, keys, nonempty, bigl, cap_shard, hdr);
@@ -849,10 +864,6 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
     if ((rc = bins_alloc(sc, &b.tpref, (size_t)((b.nt + kProjTris - 1) / kProjTris) * kProjTris)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.gsum, (size_t)((b.nt + kProjTris - 1) / kProjTris))) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.rem, (size_t)((b.nt + kProjTris - 1) / kProjTris))) != CRT_OK) return rc;
-    if ((int64_t)b.ncell * kBinMeanCap / kExpand > kMaxGroups) {   /* k_bins_pairs could queue more groups than it scans */
-        bins_free(sc);
-        return CRT_OK;
-    }
     b.pair_blocks = 256;   /* the sizing pass's grid; resized from its queued pairs below */
     if ((rc = bins_alloc(sc, &b.cnt, (size_t)kBinSets * b.ncell * kCntStride, true)) != CRT_OK) return rc;   /* per set */
     if ((rc = bins_alloc(sc, &b.keys, (size_t)b.ncell * kBinCellCap)) != CRT_OK) return rc;   /* 64-bit keys */
@@ -1009,8 +1020,8 @@ int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
  * binning runs on the binning's own stream — after the render kBinSets frames
  * back (same set) is done with the set and after the previous binning — and
  * `s` waits for it: the next frames' binnings overlap frame k's render.
- * Otherwise (one frame at a time) `s` takes the binning itself: no
- * cross-stream hop. */
+ * Otherwise (one frame at a time) `s` takes the binning itself, after the
+ * same two events. */
 int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *par_out) {
     BinsDev &b = sc->bins;
     const int par = (int)(b.frame++ % kBinSets);
@@ -1019,16 +1030,16 @@ int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *p
         const int rc0 = bins_dbg_arm(sc, plan);
         if (rc0 != CRT_OK) return rc0;
     }
-    /* the previous frame still renders: overlap it.  The binnings share their
-     * scratch (items, keys, counts, lists), so they stay in order: the
-     * binning stream also waits for the previous frame's binning, wherever
-     * it ran */
+    /* the previous frame still renders: overlap it.  Wherever the binning
+     * runs, it waits for the render kBinSets frames back (same set of lists)
+     * and for the previous binning (the binnings share their scratch: items,
+     * keys, counts, lists) — whichever streams those ran on, so a caller that
+     * issues frames on different streams cannot reopen a scratch race; a wait
+     * on an event already reached on the same stream costs nothing */
     const bool overlap = hipEventQuery(b.rdone[prev]) == hipErrorNotReady;
     const hipStream_t bs = overlap ? b.stream : s;
-    if (overlap) {
-        HIP_TRY(hipStreamWaitEvent(b.stream, b.rdone[par], 0));
-        HIP_TRY(hipStreamWaitEvent(b.stream, b.bdone[prev], 0));
-    }
+    HIP_TRY(hipStreamWaitEvent(bs, b.rdone[par], 0));
+    HIP_TRY(hipStreamWaitEvent(bs, b.bdone[prev], 0));
     int rc = launch_project(sc, bs, par, plan.bp.phdr);
     if (rc != CRT_OK) return rc;
     BinsPlan bp = plan.bp;

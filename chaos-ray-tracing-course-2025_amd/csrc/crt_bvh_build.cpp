@@ -304,15 +304,20 @@ int build_proof_tables(HostScene &hs) {
 /* Camera bins (crt_bins.h): the host restatement of the device binning
  * (crt_bins.hip), used as its checker and by the CPU walk checks. */
 bool bin_camera(const HostScene &hs, BinCamera &cam) {
-    const int W = hs.width, H = hs.height;
-    if (W <= 0 || H <= 0 || hs.tri_attr.empty()) return false;
+    if (hs.tri_attr.empty()) return false;
+    return bin_camera_of(host_camera(hs), hs.prune_origin_max, cam);
+}
+
+bool bin_camera_of(const DCamera &c, float prune_origin_max, BinCamera &cam) {
+    const int W = c.width, H = c.height;
+    if (W <= 0 || H <= 0) return false;
     for (int k = 0; k < 3; ++k) {
-        cam.o[k] = hs.cam_loc[k];
-        if (!(std::fabs(cam.o[k]) <= (double)hs.prune_origin_max)) return false;
+        cam.o[k] = c.loc[k];
+        if (!(std::fabs(cam.o[k]) <= (double)prune_origin_max)) return false;
     }
     double M[3][3];
     for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) M[i][j] = hs.cam_rot[3 * i + j];
+        for (int j = 0; j < 3; ++j) M[i][j] = c.rot[3 * i + j];
     const double det = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) -
                        M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) +
                        M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]);
@@ -322,8 +327,8 @@ bool bin_camera(const HostScene &hs, BinCamera &cam) {
             const int i1 = (j + 1) % 3, i2 = (j + 2) % 3, j1 = (i + 1) % 3, j2 = (i + 2) % 3;
             cam.Mi[i][j] = (M[i1][j1] * M[i2][j2] - M[i1][j2] * M[i2][j1]) / det;
         }
-    cam.sx = (double)hs.aspect * (double)hs.tan_half_fov;
-    cam.sy = hs.tan_half_fov;
+    cam.sx = (double)c.aspect * (double)c.tan_half_fov;
+    cam.sy = c.tan_half_fov;
     if (!(cam.sx > 0.0) || !(cam.sy > 0.0) || !std::isfinite(cam.sx) || !std::isfinite(cam.sy)) return false;
     cam.W = W;
     cam.H = H;

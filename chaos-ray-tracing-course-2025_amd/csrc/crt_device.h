@@ -52,17 +52,17 @@ CRT_HD int node_depth(const DNode &n) { return n.b < 0 ? -n.b - 1 : (int)((unsig
 
 /* Camera::generate_ray (crt_camera.cpp:7-35). aspect and tan_half_fov are the
  * per-frame constants float(W)/H and std::tan(fov*0.5f), computed on the host. */
-CRT_HD void camera_ray(const DeviceScene &s, int x, int y, Vec &o, Vec &d) {
+CRT_HD void camera_ray(const DCamera &c, int x, int y, Vec &o, Vec &d) {
     float dx = x + 0.5f, dy = y + 0.5f;
-    dx /= (float)s.width;
-    dy /= (float)s.height;
+    dx /= (float)c.width;
+    dy /= (float)c.height;
     dx = (2.0f * dx) - 1.0f;
     dy = 1.0f - (2.0f * dy);
-    dx *= s.aspect;
-    dx *= s.tan_half_fov;
-    dy *= s.tan_half_fov;
-    o = vec(s.cam_loc[0], s.cam_loc[1], s.cam_loc[2]);
-    d = vnormalize(vec_mat(vec(dx, dy, -1.0f), s.cam_rot));
+    dx *= c.aspect;
+    dx *= c.tan_half_fov;
+    dy *= c.tan_half_fov;
+    o = vec(c.loc[0], c.loc[1], c.loc[2]);
+    d = vnormalize(vec_mat(vec(dx, dy, -1.0f), c.rot));
 }
 
 /* ray_intersect_aabb_p (crt_intersection.cpp:14-45): for extent ∈ {min,max},

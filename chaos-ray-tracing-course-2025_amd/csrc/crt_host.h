@@ -108,6 +108,17 @@ struct HostScene {
     int32_t max_leaf_size = 0;
 };
 
+/* The camera of hs as the kernels see it (crt_layout.h DCamera). */
+DCamera host_camera(const HostScene &hs);
+/* A camera from the reference's Camera fields (crt_camera.h:16-21: location,
+ * rotation, the stored m_fov_radians, resolution), with the per-frame
+ * constants float(W)/H and std::tan(fov * 0.5f) of crt_camera.cpp:23,26-27
+ * computed once by this process's libm.  false: non-positive resolution. */
+bool make_camera(const float loc[3], const float rot[9], float fov_radians, int32_t width, int32_t height,
+                 DCamera &out);
+/* crt_camera.h:20 (crt_json.cpp camera "fov"): m_fov_radians from degrees, float ops. */
+inline float fov_degrees_to_radians(float deg) { return deg * 3.14159265358979323846f / 180.0f; }
+
 /* The secondary-ray BVH over hs's triangles (crt_bvh_build.cpp); needs the
  * mesh prep and prune_G. */
 int build_bvh(HostScene &hs);
@@ -130,6 +141,9 @@ int build_camera_bins(const HostScene &hs, std::vector<CamCand> &bins, std::vect
 /* The projection constants of hs's camera (false: no bins — the camera is too
  * far for the hull margins, its matrix singular or the field of view bad). */
 bool bin_camera(const HostScene &hs, BinCamera &cam);
+/* Same for any camera of a scene (prune_origin_max: the hull margins' origin
+ * bound, crt_scene_build.cpp). */
+bool bin_camera_of(const DCamera &c, float prune_origin_max, BinCamera &cam);
 /* Per-triangle static part of the candidate records (hull box, id, geometry). */
 void bin_templates(const HostScene &hs, std::vector<CamCand> &tpl);
 
@@ -142,6 +156,10 @@ int prepare_scene_from_tree(const crt_tree_scene_desc *desc, HostScene &out);
  * and its triangle count added to the 8x8 tiles its image overlaps.  Used only
  * to dispatch expensive tiles first (results do not depend on it). */
 std::vector<float> tile_work_estimate(const HostScene &hs, int tiles_x, int tiles_y);
+/* Same from the tree in the reference's numbering, for any camera. */
+std::vector<float> tile_work_estimate_of(const DCamera &c, const std::vector<float> &ref_bounds,
+                                         const std::vector<int32_t> &ref_children,
+                                         const std::vector<int64_t> &ref_leaf_off, int tiles_x, int tiles_y);
 
 /* The reference bucket grid (crt_renderer.cpp:160-174) dealt round-robin to
  * shard_count shards; returns the buckets of `shard` with packed offsets and

@@ -87,8 +87,28 @@ void warm_code_objects(int device, hipStream_t stream) {
 }
 
 void wf_graphs_clear(WfBuffers &w) {
+    if (w.graphs.empty()) return;
+    /* a graph may still run on its set's stream: let the sets' streams drain */
+    for (hipStream_t st : w.streams)
+        if (st) (void)hipStreamSynchronize(st);
     for (auto &g : w.graphs) (void)hipGraphExecDestroy(g.exec);
     w.graphs.clear();
+}
+
+/* Set si is about to regrow its buffers: its last frame (levels and pixels)
+ * must be done with them, and the graphs captured on them go. */
+int wf_set_release(WfBuffers &wb, int si) {
+    WfSet &w = wb.set[si];
+    if (w.free_ev) HIP_TRY(hipEventSynchronize(w.free_ev));
+    for (size_t i = 0; i < wb.graphs.size();) {
+        if (wb.graphs[i].set == si) {
+            (void)hipGraphExecDestroy(wb.graphs[i].exec);
+            wb.graphs.erase(wb.graphs.begin() + (std::ptrdiff_t)i);
+        } else {
+            ++i;
+        }
+    }
+    return CRT_OK;
 }
 
 
@@ -100,15 +120,15 @@ void wf_graphs_clear(WfBuffers &w) {
  * finite and bounded, w = v R is finite; with sigma_min(R) >= |det R| /
  * |R|_F^2 far above the rounding of v R (and above 2^-50, so |w|^2 stays
  * normal), w cannot round to 0 — then each |d_i| = |w_i| / |w| <= 1. */
-bool camera_rays_fast(const HostScene &hs, bool planes_ok) {
+bool camera_rays_fast(const DCamera &c, bool planes_ok) {
     if (!planes_ok) return false;
     for (int k = 0; k < 3; ++k)
-        if (!coord_ok(hs.cam_loc[k])) return false;
-    const double ta = std::fabs((double)hs.tan_half_fov), aa = std::fabs((double)hs.aspect) * ta;
+        if (!coord_ok(c.loc[k])) return false;
+    const double ta = std::fabs((double)c.tan_half_fov), aa = std::fabs((double)c.aspect) * ta;
     if (!std::isfinite(ta) || !std::isfinite(aa) || ta > 0x1p40 || aa > 0x1p40) return false;
     double R[9], fro = 0.0, mx = 0.0;
     for (int k = 0; k < 9; ++k) {
-        R[k] = hs.cam_rot[k];
+        R[k] = c.rot[k];
         if (!std::isfinite(R[k]) || std::fabs(R[k]) > 0x1p40) return false;
         fro += R[k] * R[k];
         mx = std::max(mx, std::fabs(R[k]));
@@ -247,11 +267,11 @@ int probe_tiles(crt_hip_scene *sc, const DeviceScene *d_scene, int walk, const s
         const Tile *t = static_cast<const Tile *>(dt);
         uint32_t *c = static_cast<uint32_t *>(dc);
         switch (walk) {
-        case 7: hipLaunchKernelGGL(k_probe_tiles<7>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
-        case 12: hipLaunchKernelGGL(k_probe_tiles<12>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
-        case 13: hipLaunchKernelGGL(k_probe_tiles<13>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
-        case 14: hipLaunchKernelGGL(k_probe_tiles<14>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
-        default: hipLaunchKernelGGL(k_probe_tiles<8>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
+        case 7: hipLaunchKernelGGL(k_probe_tiles<7>, grid, dim3(256), 0, stream, d_scene, sc->cam, t, n, c); break;
+        case 12: hipLaunchKernelGGL(k_probe_tiles<12>, grid, dim3(256), 0, stream, d_scene, sc->cam, t, n, c); break;
+        case 13: hipLaunchKernelGGL(k_probe_tiles<13>, grid, dim3(256), 0, stream, d_scene, sc->cam, t, n, c); break;
+        case 14: hipLaunchKernelGGL(k_probe_tiles<14>, grid, dim3(256), 0, stream, d_scene, sc->cam, t, n, c); break;
+        default: hipLaunchKernelGGL(k_probe_tiles<8>, grid, dim3(256), 0, stream, d_scene, sc->cam, t, n, c); break;
         }
         e = hipGetLastError();
     }
@@ -532,8 +552,9 @@ int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t
     return make_tile_plan(sc, all, true, sc->full);
 }
 
-DSettings to_dsettings(const crt_renderer_settings *st) {
+DSettings to_dsettings(const crt_hip_scene *sc, const crt_renderer_settings *st) {
     DSettings d;
+    d.cam = sc->cam;
     d.max_ray_depth = st->max_ray_depth;
     d.diffuse_reflection_ray_count = st->diffuse_reflection_ray_count;
     d.shadow_bias = st->shadow_bias;
@@ -543,9 +564,13 @@ DSettings to_dsettings(const crt_renderer_settings *st) {
     return d;
 }
 
-int wf_grow_ids(WfBuffers &wb, WfSet &w, int64_t need, int64_t used, hipStream_t stream) {
+int wf_grow_ids(WfBuffers &wb, int si, int64_t need, int64_t used, hipStream_t stream) {
+    WfSet &w = wb.set[si];
     if (need <= w.cap) return CRT_OK;
-    wf_graphs_clear(wb);
+    {   /* (mid-frame regrowth of a read-back frame: its stream waited for free_ev and was synchronised) */
+        const int rc = wf_set_release(wb, si);
+        if (rc != CRT_OK) return rc;
+    }
     const int64_t cap = std::max<int64_t>(need, 2 * w.cap);
     void *pn = nullptr, *pc = nullptr;
     HIP_TRY(hipMalloc(&pn, (size_t)cap * sizeof(WNode)));
@@ -563,9 +588,13 @@ int wf_grow_ids(WfBuffers &wb, WfSet &w, int64_t need, int64_t used, hipStream_t
     return CRT_OK;
 }
 
-int wf_grow_queue(WfBuffers &wb, WfSet &w, int k, int64_t need) {
+int wf_grow_queue(WfBuffers &wb, int si, int k, int64_t need) {
+    WfSet &w = wb.set[si];
     if (need <= w.qcap[k]) return CRT_OK;
-    wf_graphs_clear(wb);
+    {
+        const int rc = wf_set_release(wb, si);
+        if (rc != CRT_OK) return rc;
+    }
     const int64_t cap = std::max<int64_t>(need, 2 * w.qcap[k]);
     if (w.q[k]) (void)hipFree(w.q[k]);
     w.q[k] = nullptr;
@@ -678,6 +707,10 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
     /* sets in use: as many as CRT_WF_SET_BUDGET holds of this frame size
      * (rays x (node + colour) + two queues), 2 <= sets <= kWfSets; each set
      * waits for its own previous frame, so the count may change between frames */
+    {
+        const int rc0 = wf_streams(wb, stream);
+        if (rc0 != CRT_OK) return rc0;
+    }
     int si = 0;
     if (replay) {
         int64_t tot = n0, mx = 1;
@@ -687,27 +720,35 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         }
         const int64_t set_bytes = tot * (int64_t)(sizeof(WNode) + sizeof(DVec4)) + 2 * mx * (int64_t)sizeof(WRay);
         const int64_t fit = CRT_WF_SET_BUDGET / std::max<int64_t>(set_bytes, 1);
-        const int nsets = (int)std::min<int64_t>(kWfSets, std::max<int64_t>(2, fit));
-        si = (int)(wb.frame++ % (uint64_t)nsets);
+        const int nsets = (int)std::min<int64_t>(kWfSets, std::max<int64_t>(1, fit));
+        /* the first set whose last frame is done (a caller that waits for each
+         * frame stays on set 0: one set's buffers and one graph); with every
+         * set busy (frames back to back), the one issued longest ago */
+        si = -1;
+        for (int k = 0; k < nsets && si < 0; ++k)
+            if (hipEventQuery(wb.set[k].free_ev) == hipSuccess) si = k;
+        if (si < 0) {
+            si = 0;
+            for (int k = 1; k < nsets; ++k)
+                if (wb.set[k].seq < wb.set[si].seq) si = k;
+        }
+        wb.set[si].seq = ++wb.frame;
     }
     WfSet &w = wb.set[si];
-    {
-        const int rc0 = wf_streams(wb, stream);
-        if (rc0 != CRT_OK) return rc0;
-    }
     /* where the levels run: a recorded-size frame on its set's stream, after
      * the set's previous frame; a frame with read-backs on the caller's */
     const hipStream_t ls = replay ? wb.streams[si % kWfStreams] : stream;
     HIP_TRY(hipStreamWaitEvent(ls, w.free_ev, 0));
     const int kMaxLevels = (int)ds.max_ray_depth + 2;
     if (!w.counts || w.count_cap < kMaxLevels) {
+        int rc0 = wf_set_release(wb, si);
+        if (rc0 != CRT_OK) return rc0;
         if (w.counts) (void)hipFree(w.counts);
         w.counts = nullptr;
         void *p = nullptr;
         HIP_TRY(hipMalloc(&p, (size_t)kMaxLevels * sizeof(int32_t)));
         w.counts = static_cast<int32_t *>(p);
         w.count_cap = kMaxLevels;
-        wf_graphs_clear(wb);
     }
     if (!w.d_flag) {
         void *p = nullptr;
@@ -732,9 +773,9 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         qneed = std::max<int64_t>(mx, 1);
         ids = tot;
     }
-    if ((rc = wf_grow_ids(wb, w, ids, 0, ls)) != CRT_OK) return rc;
-    if ((rc = wf_grow_queue(wb, w, 0, qneed)) != CRT_OK) return rc;
-    if (replay && (rc = wf_grow_queue(wb, w, 1, qneed)) != CRT_OK) return rc;
+    if ((rc = wf_grow_ids(wb, si, ids, 0, ls)) != CRT_OK) return rc;
+    if ((rc = wf_grow_queue(wb, si, 0, qneed)) != CRT_OK) return rc;
+    if (replay && (rc = wf_grow_queue(wb, si, 1, qneed)) != CRT_OK) return rc;
     /* the pixels on the caller's stream once the levels are done; the set is
      * free again after them */
     auto finish = [&]() -> int {
@@ -805,8 +846,8 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
             HIP_TRY(hipStreamSynchronize(ls));
             if (n == 0) break;
             if (base + 3 * (int64_t)n > INT32_MAX) return set_error(CRT_E_UNSUPPORTED, "wavefront ray ids exceed 2^31");
-            if ((rc = wf_grow_ids(wb, w, base + 3 * (int64_t)n, base, ls)) != CRT_OK) return rc;
-            if ((rc = wf_grow_queue(wb, w, cur ^ 1, 2 * (int64_t)n)) != CRT_OK) return rc;
+            if ((rc = wf_grow_ids(wb, si, base + 3 * (int64_t)n, base, ls)) != CRT_OK) return rc;
+            if ((rc = wf_grow_queue(wb, si, cur ^ 1, 2 * (int64_t)n)) != CRT_OK) return rc;
             out_cap = cap_of(w.qcap[cur ^ 1]);
             sizes.push_back(n);
         }
@@ -890,7 +931,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         const int rc = sync_device_record(sc, &d_scene);
         if (rc != CRT_OK) return rc;
     }
-    const DSettings ds = to_dsettings(st);
+    const DSettings ds = to_dsettings(sc, st);
     /* Walks: camera rays take the packet walk (traversal 7, or 8 pruned).
      * Secondary rays scatter and take the cooperative walk: pruned (10) for
      * reflect/refract levels (C3), reference order (4) for GI fan-out — the
@@ -1073,7 +1114,7 @@ int ensure_live_mask(crt_hip_scene *sc) {
     const int64_t npx = (int64_t)sc->info.width * sc->info.height;
     uint8_t *d = nullptr;
     HIP_TRY(hipMalloc(&d, (size_t)npx));
-    hipLaunchKernelGGL(k_live_pixels, dim3((unsigned)((npx + 255) / 256)), dim3(256), 0, sc->stream, d_scene, d);
+    hipLaunchKernelGGL(k_live_pixels, dim3((unsigned)((npx + 255) / 256)), dim3(256), 0, sc->stream, d_scene, sc->cam, d);
     hipError_t e = hipGetLastError();
     std::vector<uint8_t> m((size_t)npx);
     if (e == hipSuccess) e = hipMemcpyAsync(m.data(), d, (size_t)npx, hipMemcpyDeviceToHost, sc->stream);

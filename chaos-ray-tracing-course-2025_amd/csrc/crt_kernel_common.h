@@ -47,17 +47,18 @@ struct BinsPlan {
     int32_t *cell_tile;   /* per cell: the plan's one tile inside it; -1 none (the cell is not rendered), -2 several */
     const Tile *tiles;    /* the plan's tiles */
     BinsWork *work;       /* the lists: kind q, shard s, entry i at wbase[q] + s cap[q] + i */
-    int32_t *phdr;        /* entries listed this frame: counter bins_phdr_at(parity, kind, shard) */
+    int32_t *phdr;        /* entries listed this frame: counter bins_phdr_at(set, kind, shard) */
     const int32_t *rest;  /* tiles the lists do not hold */
     int32_t cap[kBinKinds], wbase[kBinKinds];
     int32_t nrest, nfill, ncell;
     int32_t wslots;       /* work-list slots of one set (work: kBinSets sets; the frame's at par * wslots) */
     int32_t split, medium, quad;
-    int32_t par;          /* the frame's parity (which counters it uses) */
+    int32_t par;          /* the frame's set, frame % kBinSets (which counters and lists it uses) */
 };
 
-/* The device binning's per-frame counters, two sets (frames alternate; a
- * frame's first kernel zeroes the other set for the next frame).
+/* The device binning's per-frame counters, kBinSets sets taken in turn
+ * (frame k uses set k % kBinSets; its first kernel zeroes set (k + 1) %
+ * kBinSets for the next frame).
  * Every counter has a 256-B line of its own (atomics on one line serialise,
  * whatever word they name). */
 constexpr int kBinPad = 64;   /* int32 per counter */

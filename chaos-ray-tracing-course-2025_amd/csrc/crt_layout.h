@@ -182,8 +182,9 @@ struct DeviceScene {
     /* camera bins (crt_bvh.h walk_bins), rebuilt on the device by every camera
      * frame (crt_bins.hip): per 8x8 cell of the frame (bin_tx cells a row),
      * candidates bins[bin_off[c] .. bin_off[c] + bin_len[c]), bin_len -1: the
-     * cell's pixels walk the BVH; two sets by frame parity (frame k + 1 bins
-     * while frame k renders): a frame's per-cell entries at parity * ncell,
+     * cell's pixels walk the BVH; kBinSets sets taken in turn (the next
+     * frames bin while frame k renders): a frame's per-cell entries at
+     * set * ncell (set = frame % kBinSets),
      * its records anywhere in `bins` (offsets absolute); null when the scene
      * takes no bins */
     const CamCand *bins;
@@ -204,18 +205,26 @@ struct DeviceScene {
     /* powf(x, 5.0f) of the host's libm for every x = k * 2^-24 in [-1, 1]
      * (2^25 + 1 floats, index k + 2^24): the Fresnel term's exact values */
     const float *pow5;
-    /* camera (crt_camera.cpp:7-35), per-frame constants precomputed on host */
-    float cam_loc[3];
-    float cam_rot[9];
-    int32_t width, height;
     int32_t planes_ok;      /* every node plane is 0 or |p| in [2^-40, 2^62] (crt_device.h coord_ok) */
-    float aspect;           /* float(width) / height            (crt_camera.cpp:23) */
-    float tan_half_fov;     /* std::tan(fov_radians * 0.5f)     (crt_camera.cpp:26-27) */
     float background[3];
     int32_t gi_on, reflections_on, refractions_on;
 };
 
-/* Renderer settings as the kernels see them (crt_renderer.h:18-25). */
+/* The camera as the kernels see it (crt_camera.cpp:7-35): the frame's
+ * constants, float(width) / height and std::tan(fov_radians * 0.5f) computed
+ * on the host with the reference's libm. */
+struct DCamera {
+    float loc[3];
+    float rot[9];           /* row-major, ray_dir = v * R (crt_matrix.h:66-74) */
+    int32_t width, height;
+    float aspect;           /* float(width) / height            (crt_camera.cpp:23) */
+    float tan_half_fov;     /* std::tan(fov_radians * 0.5f)     (crt_camera.cpp:26-27) */
+};
+
+/* A frame's constants as the kernels see them, passed by value with every
+ * launch: the renderer settings (crt_renderer.h:18-25) and the camera — so a
+ * frame renders with the camera current when it was issued, whatever
+ * crt_hip_scene_set_camera does while it is in flight. */
 struct DSettings {
     uint32_t max_ray_depth;
     uint32_t diffuse_reflection_ray_count;
@@ -223,6 +232,7 @@ struct DSettings {
     float reflection_bias;
     float diffuse_reflection_bias;
     float refraction_bias;
+    DCamera cam;
 };
 
 /* A bucket of the reference grid (crt_renderer.cpp:160-174). */

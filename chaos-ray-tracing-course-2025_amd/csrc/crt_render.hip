@@ -71,7 +71,7 @@ __device__ void bins_fill(const DeviceScene &s, const BinsPlan &bp, const Tile *
     const int c = fw * 16 + (lane & 15);
     bool e = false;
     int k = -1;
-    if (lane < 16 && c < bp.ncell) {   /* the cell's tile and list length (this frame's parity) in one round of loads */
+    if (lane < 16 && c < bp.ncell) {   /* the cell's tile and list length (this frame's set) in one round of loads */
         k = bp.cell_tile[c];
         e = s.bin_len[(size_t)bp.par * bp.ncell + c] == 0 && k >= 0;
     }
@@ -147,7 +147,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             const bool act = r < npx;
             const int px = act ? r % tw : 0, py = act ? r / tw : 0;
             Vec o, d;
-            camera_ray(s, tl.x + px, tl.y + py, o, d);
+            camera_ray(st.cam, tl.x + px, tl.y + py, o, d);
             LaneCounts cw = {};
             float t;
             const int slot = R == 4 ? trace_window<COUNT, 4>(s, r, sl, act, o, d, t, cw)
@@ -189,7 +189,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
         const int tx0 = uniform_i(tl.x), ty0 = uniform_i(tl.y), tw = uniform_i(tl.w), th = uniform_i(tl.h);
         const int cell = (ty0 >> 3) * s.bin_tx + (tx0 >> 3);
         const bool one = (tx0 & 7) + tw <= 8 && (ty0 & 7) + th <= 8;
-        const int pc = bp.par * bp.ncell + cell;   /* this frame's parity of the per-cell lists */
+        const int pc = bp.par * bp.ncell + cell;   /* this frame's set of the per-cell lists */
         const int len = uniform_i(bin_len != -2 ? bin_len : one ? load_scalar(s.bin_len, pc) : -1);
         if (len >= 0) {   /* -1: not inside one cell, or the cell's list is over the cap: the BVH walk below */
             const int beg = uniform_i(bin_len != -2 ? bin_beg : load_scalar(s.bin_off, pc)), end = beg + len;
@@ -199,7 +199,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
                 const int p = lane >> 2, sl = lane & 3, lx = p & 3, ly = p >> 2;
                 const bool act = lx < tw && ly < th;
                 Vec o, d;
-                camera_ray(s, tx0 + (act ? lx : 0), ty0 + (act ? ly : 0), o, d);
+                camera_ray(st.cam, tx0 + (act ? lx : 0), ty0 + (act ? ly : 0), o, d);
                 LaneCounts cw = {};
                 float t;
                 const int bit = 8 * ((ty0 & 7) + ly) + (tx0 & 7) + lx;
@@ -225,7 +225,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             const int lx = lane & 7, ly = lane >> 3;
             const bool act = lx < tw && ly < th;
             Vec o, d;
-            camera_ray(s, tx0 + (act ? lx : 0), ty0 + (act ? ly : 0), o, d);
+            camera_ray(st.cam, tx0 + (act ? lx : 0), ty0 + (act ? ly : 0), o, d);
             LaneCounts cw = {};
             float t;
             const int bit = 8 * ((ty0 & 7) + ly) + (tx0 & 7) + lx;
@@ -261,7 +261,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             const bool act = r < npx;
             const int px = act ? r % tw : 0, py = act ? r / tw : 0;
             Vec o, d;
-            camera_ray(s, tl.x + px, tl.y + py, o, d);
+            camera_ray(st.cam, tl.x + px, tl.y + py, o, d);
             LaneCounts cw = {};
             float t;
             const int slot = K == 16 ? trace_bvh_window<COUNT, 16>(s, sl, act, o, d, t, cw)
@@ -331,7 +331,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
  * (what the wave pays: the union of its lanes' visit sets), for per-lane
  * walks the largest lane's node + triangle tests. */
 template <int TRAV>
-__global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restrict__ scene,
+__global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restrict__ scene, DCamera cam,
                                                      const Tile *__restrict__ tiles, int ntiles,
                                                      uint32_t *__restrict__ wave_cost) {
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restri
     const int lx = lane & 7, ly = lane >> 3;
     const bool has_px = lx < tl.w && ly < tl.h;
     Vec o, d;
-    camera_ray(s, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), o, d);
+    camera_ray(cam, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), o, d);
     LaneCounts cnt = {};
     constexpr bool kCoop = kIsCoop<TRAV>;
     __shared__ CoopLds coop[kCoop ? 4 : 1];

@@ -450,7 +450,7 @@ int prepare_scene_(const crt_scene_desc *d, HostScene &hs, bool build_tree_on_ho
     hs.width = d->camera.width;
     hs.height = d->camera.height;
     /* crt_camera.h:20, crt_camera.cpp:23,26-27 — same float expressions, once. */
-    hs.fov_radians = d->camera.fov_degrees * 3.14159265358979323846f / 180.0f;
+    hs.fov_radians = fov_degrees_to_radians(d->camera.fov_degrees);
     hs.aspect = float(hs.width) / hs.height;
     hs.tan_half_fov = std::tan(hs.fov_radians * 0.5f);
     hs.bucket_size = d->bucket_size;
@@ -686,33 +686,64 @@ int prepare_scene_from_tree(const crt_tree_scene_desc *d, HostScene &hs) {
     return maybe_build_bvh(hs);
 }
 
+DCamera host_camera(const HostScene &hs) {
+    DCamera c{};
+    std::memcpy(c.loc, hs.cam_loc, sizeof c.loc);
+    std::memcpy(c.rot, hs.cam_rot, sizeof c.rot);
+    c.width = hs.width;
+    c.height = hs.height;
+    c.aspect = hs.aspect;
+    c.tan_half_fov = hs.tan_half_fov;
+    return c;
+}
+
+bool make_camera(const float loc[3], const float rot[9], float fov_radians, int32_t width, int32_t height,
+                 DCamera &out) {
+    if (width <= 0 || height <= 0) return false;
+    std::memcpy(out.loc, loc, sizeof out.loc);
+    std::memcpy(out.rot, rot, sizeof out.rot);
+    out.width = width;
+    out.height = height;
+    /* crt_camera.cpp:23,26-27 — the same float expressions prepare_scene uses */
+    out.aspect = float(width) / height;
+    out.tan_half_fov = std::tan(fov_radians * 0.5f);
+    return true;
+}
+
 std::vector<float> tile_work_estimate(const HostScene &hs, int tiles_x, int tiles_y) {
+    return tile_work_estimate_of(host_camera(hs), hs.ref_bounds, hs.ref_children, hs.ref_leaf_off, tiles_x, tiles_y);
+}
+
+std::vector<float> tile_work_estimate_of(const DCamera &cam, const std::vector<float> &ref_bounds,
+                                         const std::vector<int32_t> &ref_children,
+                                         const std::vector<int64_t> &ref_leaf_off, int tiles_x, int tiles_y) {
     std::vector<float> w((size_t)tiles_x * tiles_y, 0.f);
-    const size_t n = hs.ref_children.size() / 2;
-    const float *R = hs.cam_rot;
-    const float sx = hs.aspect * hs.tan_half_fov, sy = hs.tan_half_fov;
+    const size_t n = ref_children.size() / 2;
+    if (ref_leaf_off.size() < n + 1 || ref_bounds.size() < 6 * n) return w;
+    const float *R = cam.rot;
+    const float sx = cam.aspect * cam.tan_half_fov, sy = cam.tan_half_fov;
     for (size_t i = 0; i < n; ++i) {
-        const int64_t cnt = hs.ref_leaf_off[i + 1] - hs.ref_leaf_off[i];
+        const int64_t cnt = ref_leaf_off[i + 1] - ref_leaf_off[i];
         if (cnt == 0) continue;
-        const float *b = &hs.ref_bounds[6 * i];
+        const float *b = &ref_bounds[6 * i];
         float x0 = 1e30f, x1 = -1e30f, y0 = 1e30f, y1 = -1e30f;
         bool behind = false;
         for (int c = 0; c < 8; ++c) {
-            const float v[3] = {b[(c & 1) ? 3 : 0] - hs.cam_loc[0], b[(c & 2) ? 4 : 1] - hs.cam_loc[1],
-                                b[(c & 4) ? 5 : 2] - hs.cam_loc[2]};
+            const float v[3] = {b[(c & 1) ? 3 : 0] - cam.loc[0], b[(c & 2) ? 4 : 1] - cam.loc[1],
+                                b[(c & 4) ? 5 : 2] - cam.loc[2]};
             /* camera space = world * R^T (ray dir = cam * R, crt_camera.cpp:31) */
             const float cx = v[0] * R[0] + v[1] * R[1] + v[2] * R[2];
             const float cy = v[0] * R[3] + v[1] * R[4] + v[2] * R[5];
             const float cz = v[0] * R[6] + v[1] * R[7] + v[2] * R[8];
             if (!(cz < -1e-6f)) { behind = true; break; }
-            const float px = (cx / -cz / sx + 1.0f) * 0.5f * hs.width;
-            const float py = (1.0f - cy / -cz / sy) * 0.5f * hs.height;
+            const float px = (cx / -cz / sx + 1.0f) * 0.5f * cam.width;
+            const float py = (1.0f - cy / -cz / sy) * 0.5f * cam.height;
             x0 = std::min(x0, px); x1 = std::max(x1, px);
             y0 = std::min(y0, py); y1 = std::max(y1, py);
         }
         int tx0 = 0, tx1 = tiles_x - 1, ty0 = 0, ty1 = tiles_y - 1;
         if (!behind) {
-            if (x1 < 0 || y1 < 0 || x0 >= hs.width || y0 >= hs.height) continue;
+            if (x1 < 0 || y1 < 0 || x0 >= cam.width || y0 >= cam.height) continue;
             tx0 = std::max(0, (int)(x0 / 8)); tx1 = std::min(tiles_x - 1, (int)(x1 / 8));
             ty0 = std::max(0, (int)(y0 / 8)); ty1 = std::min(tiles_y - 1, (int)(y1 / 8));
         }

@@ -104,6 +104,7 @@ struct WfSet {
     hipEvent_t flag_ev = nullptr;
     bool flag_pending = false;
     hipEvent_t free_ev = nullptr;     /* the set's last frame has written its pixels */
+    uint64_t seq = 0;                 /* WfBuffers::frame of the set's last frame */
     hipEvent_t done_ev = nullptr;     /* the set's levels of the current frame are done */
 };
 
@@ -123,7 +124,7 @@ static_assert(kWfSets >= 2, "frames in flight need two sets at least");
 struct WfBuffers {
     WfSet set[kWfSets];
     hipStream_t streams[kWfStreams] = {};
-    uint64_t frame = 0;          /* recorded-size frames issued (set = frame % sets in use) */
+    uint64_t frame = 0;          /* recorded-size frames issued */
     /* Level sizes of the last frame traced with host read-backs, and what they
      * depend on (settings, tile list): a frame's level sizes are a function of
      * its rays alone, so later frames with the same key launch every level
@@ -199,6 +200,11 @@ struct crt_hip_scene {
     int traversal = 8;             /* 7 reference order | 8 pruned (default), see trace<> (env CRT_TRAVERSAL) */
     int shadows = 0;               /* option "shadows": trace the shadow rays (k_render_tiles<..., SHADOW>) */
     int trace_walk = 1;            /* crt_hip_trace_batch: 0 reference-order walk, 1 pruned per-lane walk */
+    /* the camera frames are issued with (crt_hip_scene_set_camera), passed to
+     * every launch by value in DSettings */
+    DCamera cam{};
+    float fov_radians = 0.f;
+    float prune_origin_max = 0.f;  /* the hull margins' origin bound (bins need the camera inside it) */
     bool camera_fast = false;      /* every camera ray takes the fast box path (camera_rays_fast) */
     /* estimate plan (no calibration): a tile is split into 4x4 (2x2) pixel
      * waves when its work estimate exceeds split4 (split16) times the mean work
@@ -274,7 +280,7 @@ inline bool bins_active(const crt_hip_scene *sc) { return sc->ds.bins && sc->bin
 int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const ShardPlan &plan, float *d_out,
                   hipStream_t stream, bool count, unsigned long long *stamps = nullptr);
 int render_into(crt_hip_scene *sc, const crt_renderer_settings *st, float *d_rgb, hipStream_t stream, bool count);
-bool camera_rays_fast(const HostScene &hs, bool planes_ok);
+bool camera_rays_fast(const DCamera &c, bool planes_ok);
 bool rec_machine_on(const crt_hip_scene *sc, const crt_renderer_settings *st);
 int ensure_live_mask(crt_hip_scene *sc);
 std::vector<DBucket> compact_tiles(crt_hip_scene *sc, int shard, int shard_count, int64_t *px,

@@ -73,13 +73,14 @@ __global__ __launch_bounds__(256) void k_unpack(const UnpackBucket *__restrict__
  * first, :114-121).  A ray that fails it is a miss, i.e. shade_ray returns the
  * background colour (crt_renderer.cpp:142-144) — so dead pixels need neither
  * rendering nor transport. */
-__global__ __launch_bounds__(256) void k_live_pixels(const DeviceScene *__restrict__ scene, uint8_t *__restrict__ live) {
+__global__ __launch_bounds__(256) void k_live_pixels(const DeviceScene *__restrict__ scene, DCamera cam,
+                                                     uint8_t *__restrict__ live) {
     const DeviceScene &s = *scene;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)s.width * s.height) return;
-    const int x = (int)(i % s.width), y = (int)(i / s.width);
+    if (i >= (int64_t)cam.width * cam.height) return;
+    const int x = (int)(i % cam.width), y = (int)(i / cam.width);
     Vec o, d;
-    camera_ray(s, x, y, o, d);
+    camera_ray(cam, x, y, o, d);
     bool hit = false;
     if (s.node_count > 0) {
         const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);

@@ -142,6 +142,9 @@ typedef struct crt_scene_info {
     double  bins_ms;           /* camera-bins setup: templates, buffers, the sizing pass (device) */
     double  upload_ms;         /* upload to every device (incl. device tree build and bins setup) */
     double  create_ms;         /* the whole crt_hip_scene_create* call */
+    int32_t wf_sets;           /* wavefront frame buffer sets holding buffers (1 for a caller that waits for
+                                * each frame; up to 12 for frames issued back to back) */
+    int32_t pad0;
 } crt_scene_info;
 
 typedef struct crt_render_stats {

@@ -54,7 +54,17 @@ class DeviceBuffers:
         self.hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
         self.hip.hipFree.argtypes = [C.c_void_p]
         self.hip.hipDeviceSynchronize.argtypes = []
+        self.hip.hipStreamCreateWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_uint]
+        self.hip.hipStreamDestroy.argtypes = [C.c_void_p]
         self.ptrs = []
+        self.streams = []
+
+    def stream(self) -> int:
+        """A non-blocking HIP stream (hipStreamNonBlocking), destroyed on close."""
+        s = self.C.c_void_p()
+        assert self.hip.hipStreamCreateWithFlags(self.C.byref(s), 1) == 0
+        self.streams.append(s)
+        return s.value
 
     def alloc(self, nbytes: int) -> int:
         p = self.C.c_void_p()
@@ -78,9 +88,14 @@ class DeviceBuffers:
         assert self.hip.hipDeviceSynchronize() == 0
 
     def close(self):
+        if self.ptrs or self.streams:
+            self.hip.hipDeviceSynchronize()
         for p in self.ptrs:
             self.hip.hipFree(p)
         self.ptrs = []
+        for s in self.streams:
+            self.hip.hipStreamDestroy(s)
+        self.streams = []
 
 
 @pytest.fixture

@@ -141,3 +141,38 @@ def test_bins_frames_pipelined_bit_exact(N, oracle, devbuf):
     for k in range(3):
         assert np.array_equal(bits(devbuf.download(d[k], (540, 960, 3), np.float32)), want)
     assert np.array_equal(bits(g.render(st)), want)
+
+
+def test_bins_frames_pipelined_full_size_every_frame(N, oracle, devbuf):
+    """The bench's own C2 mode at the benched size: 1920x1080 frames issued back
+    to back with no host wait (the next frames' binnings overlap frame k's
+    render, kBinSets sets of lists in turn), each into a buffer of its own, and
+    every one of the 24 frames compared with the oracle's frame."""
+    sc = scene_npz("14-01-acceleration-tree__scene1")
+    st = N.RendererSettings.default()
+    want = bits(oracle.OracleScene(sc).render(st))
+    g = N.HipScene(sc)
+    nb = 1920 * 1080 * 3 * 4
+    d = [devbuf.alloc(nb) for _ in range(24)]
+    for k in range(24):
+        g.render_device(st, d[k])
+    bad = [k for k in range(24) if not np.array_equal(bits(devbuf.download(d[k], (1080, 1920, 3), np.float32)), want)]
+    assert not bad, f"frames {bad} differ from the oracle"
+
+
+def test_bins_frames_on_alternating_streams(N, oracle, devbuf):
+    """Frames issued on two caller streams in turn, no host wait: a binning
+    waits for the render kBinSets frames back and for the previous binning
+    whichever stream they ran on (crt_bins.hip bins_enqueue), so the shared
+    binning scratch is never rewritten under a render.  30 frames, each into a
+    buffer of its own, every one equal to the oracle."""
+    sc = scene_npz("14-01-acceleration-tree__scene1").set_resolution(960, 540)
+    st = N.RendererSettings.default()
+    want = bits(oracle.OracleScene(sc).render(st))
+    g = N.HipScene(sc)
+    streams = [devbuf.stream(), devbuf.stream()]
+    d = [devbuf.alloc(960 * 540 * 3 * 4) for _ in range(30)]
+    for k in range(30):
+        g.render_device(st, d[k], streams[k % 2])
+    bad = [k for k in range(30) if not np.array_equal(bits(devbuf.download(d[k], (540, 960, 3), np.float32)), want)]
+    assert not bad, f"frames {bad} differ from the oracle"

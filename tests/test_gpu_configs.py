@@ -277,13 +277,12 @@ def test_c3_recorded_sizes_overflow(N, devbuf):
 
 
 def test_c3_frames_pipelined(N, devbuf):
-    """Recorded-size wavefront frames issued back to back take four buffer
-    sets in turn, set i's levels on stream i % 2, so frame k + 1's levels run
-    beside frame k's and frame k + 2's right behind frame k's
-    (crt_host_render.hip render_wavefront; each set replays a graph captured
-    on its own buffers); the pixels stay in the caller's stream order.
-    Twelve frames into four rotating buffers, then a host frame: all equal
-    the read-back frame."""
+    """Recorded-size wavefront frames issued back to back take the free buffer
+    sets (up to 12, each set's levels on a stream of its own), so frame k + 1's
+    levels run beside frame k's (crt_host_render.hip render_wavefront; each set
+    replays a graph captured on its own buffers); the pixels stay in the
+    caller's stream order.  Twelve frames into four rotating buffers, then a
+    host frame: all equal the read-back frame."""
     sc = scene_npz("11-01-refractive__scene8").set_resolution(480, 270)
     st = N.RendererSettings.default(max_ray_depth=8)
     ref = N.HipScene(sc, wf_replay=0).render(st)
@@ -295,3 +294,36 @@ def test_c3_frames_pipelined(N, devbuf):
     for k in range(4):
         assert np.array_equal(bits(devbuf.download(d[k], ref.shape, np.float32)), bits(ref))
     assert np.array_equal(bits(g.render(st)), bits(ref))
+
+
+def test_c3_frames_pipelined_full_size_every_frame(N, oracle, devbuf):
+    """The bench's own C3 mode at the benched size: 1920x1080 depth-8 frames
+    issued back to back (levels of up to 12 frames side by side on the sets'
+    streams), each into a buffer of its own; every one of the 24 frames equal
+    to the oracle's frame."""
+    h = HASHES["C3"]
+    sc = scene_npz(h["scene"])
+    st = N.RendererSettings.default(**h["settings"])
+    want = bits(oracle.OracleScene(sc).render(st))
+    g = N.HipScene(sc)
+    assert np.array_equal(bits(g.render(st)), want)   # records the level sizes
+    nb = 1920 * 1080 * 3 * 4
+    d = [devbuf.alloc(nb) for _ in range(24)]
+    for k in range(24):
+        g.render_device(st, d[k])
+    bad = [k for k in range(24) if not np.array_equal(bits(devbuf.download(d[k], (1080, 1920, 3), np.float32)), want)]
+    assert not bad, f"frames {bad} differ from the oracle"
+    assert g.info()["wf_sets"] >= 2   # the frames did run on several sets
+
+
+def test_c3_blocking_frames_stay_on_one_set(N):
+    """A caller that waits for every frame (the CLI, _crt, the shim: the
+    reference's blocking render_image) finds set 0 free each time and never
+    allocates another set's buffers or captures another graph."""
+    sc = scene_npz("11-01-refractive__scene8").set_resolution(480, 270)
+    st = N.RendererSettings.default(max_ray_depth=8)
+    g = N.HipScene(sc)
+    first = g.render(st)
+    for _ in range(20):
+        assert np.array_equal(bits(g.render(st)), bits(first))
+    assert g.info()["wf_sets"] <= 2, g.info()["wf_sets"]

@@ -376,17 +376,12 @@ extern "C" int bins_sim_check(const crt_scene_desc *desc, uint64_t *out) {
     out[4] = off.size() - 1;
     out[5] = bins.size();
     DeviceScene ds{};
-    std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
-    std::memcpy(ds.cam_rot, hs.cam_rot, sizeof ds.cam_rot);
-    ds.width = hs.width;
-    ds.height = hs.height;
-    ds.aspect = hs.aspect;
-    ds.tan_half_fov = hs.tan_half_fov;
+    const DCamera cam = host_camera(hs);
     const int tx = (hs.width + 7) / 8;
     for (int y = 0; y < hs.height; ++y)
         for (int x = 0; x < hs.width; ++x) {
             Vec o, d;
-            camera_ray(ds, x, y, o, d);
+            camera_ray(cam, x, y, o, d);
             const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
             WalkCounts w = {0u, 0u}, wb = {0u, 0u};
             float t1 = 0.f, t2 = 0.f;
@@ -428,18 +423,13 @@ extern "C" int bins_sim_lanes_check(const crt_scene_desc *desc, int K, uint64_t 
     out[0] = out[1] = out[2] = 0;
     if (bins.empty()) return CRT_OK;
     DeviceScene ds{};
-    std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
-    std::memcpy(ds.cam_rot, hs.cam_rot, sizeof ds.cam_rot);
-    ds.width = hs.width;
-    ds.height = hs.height;
-    ds.aspect = hs.aspect;
-    ds.tan_half_fov = hs.tan_half_fov;
+    const DCamera cam = host_camera(hs);
     const int tx = (hs.width + 7) / 8;
     constexpr int kChunk = 32;   /* crt_walks.h kBinChunk */
     for (int y = 0; y < hs.height; ++y)
         for (int x = 0; x < hs.width; ++x) {
             Vec o, d;
-            camera_ray(ds, x, y, o, d);
+            camera_ray(cam, x, y, o, d);
             const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
             const int cell = (y / 8) * tx + x / 8, bit = 8 * (y % 8) + x % 8;
             if (over[(size_t)cell]) continue;
@@ -529,18 +519,13 @@ extern "C" int bins_sim_diffs(const crt_scene_desc *desc, int64_t *rows, int cap
     if ((rc = build_camera_bins(hs, bins, off, &over)) != CRT_OK) return rc;
     if (bins.empty()) return 0;
     DeviceScene ds{};
-    std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
-    std::memcpy(ds.cam_rot, hs.cam_rot, sizeof ds.cam_rot);
-    ds.width = hs.width;
-    ds.height = hs.height;
-    ds.aspect = hs.aspect;
-    ds.tan_half_fov = hs.tan_half_fov;
+    const DCamera cam = host_camera(hs);
     const int tx = (hs.width + 7) / 8;
     int n = 0;
     for (int y = 0; y < hs.height && n < cap; ++y)
         for (int x = 0; x < hs.width && n < cap; ++x) {
             Vec o, d;
-            camera_ray(ds, x, y, o, d);
+            camera_ray(cam, x, y, o, d);
             const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
             WalkCounts w = {0u, 0u};
             float t1 = 0.f, t2 = 0.f;
@@ -580,12 +565,7 @@ extern "C" int bins_sim_cells(const crt_scene_desc *desc, int64_t *out) {
     if ((rc = build_camera_bins(hs, bins, off, &over)) != CRT_OK) return rc;
     if (bins.empty()) return -1;
     DeviceScene ds{};
-    std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
-    std::memcpy(ds.cam_rot, hs.cam_rot, sizeof ds.cam_rot);
-    ds.width = hs.width;
-    ds.height = hs.height;
-    ds.aspect = hs.aspect;
-    ds.tan_half_fov = hs.tan_half_fov;
+    const DCamera cam = host_camera(hs);
     const int tx = (hs.width + 7) / 8, ty = (hs.height + 7) / 8;
     for (int cy = 0; cy < ty; ++cy)
         for (int cx = 0; cx < tx; ++cx) {
@@ -596,7 +576,7 @@ extern "C" int bins_sim_cells(const crt_scene_desc *desc, int64_t *out) {
             for (int y = 8 * cy; y < std::min(hs.height, 8 * cy + 8); ++y)
                 for (int x = 8 * cx; x < std::min(hs.width, 8 * cx + 8); ++x) {
                     Vec o, d;
-                    camera_ray(ds, x, y, o, d);
+                    camera_ray(cam, x, y, o, d);
                     const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
                     const int bit = 8 * (y - 8 * cy) + (x - 8 * cx);
                     int best = -1;
@@ -677,12 +657,7 @@ extern "C" int bins_fuzz(const crt_scene_desc *desc, int nthreads, uint64_t *out
         planes_ok = planes_ok && ok(n.lo_x) && ok(n.lo_y) && ok(n.lo_z) && ok(n.hi_x) && ok(n.hi_y) && ok(n.hi_z) &&
                     n.lo_x <= n.hi_x && n.lo_y <= n.hi_y && n.lo_z <= n.hi_z;
     DeviceScene ds{};
-    std::memcpy(ds.cam_loc, hs.cam_loc, sizeof ds.cam_loc);
-    std::memcpy(ds.cam_rot, hs.cam_rot, sizeof ds.cam_rot);
-    ds.width = hs.width;
-    ds.height = hs.height;
-    ds.aspect = hs.aspect;
-    ds.tan_half_fov = hs.tan_half_fov;
+    const DCamera cam = host_camera(hs);
     const int W = hs.width, H = hs.height, tx = (W + 7) / 8;
     std::vector<int32_t> res_slot((size_t)W * H);
     std::vector<float> res_t((size_t)W * H);
@@ -693,7 +668,7 @@ extern "C" int bins_fuzz(const crt_scene_desc *desc, int nthreads, uint64_t *out
         for (int y = th; y < H; y += nth)
             for (int x = 0; x < W; ++x) {
                 Vec o, d;
-                camera_ray(ds, x, y, o, d);
+                camera_ray(cam, x, y, o, d);
                 const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
                 WalkCounts w = {0u, 0u};
                 float t1 = 0.f, t2 = 0.f;
