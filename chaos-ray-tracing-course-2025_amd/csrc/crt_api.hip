@@ -253,10 +253,10 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
         if ((rc = upload(sc.get(), hs.ktopo, &ds.ktopo)) != CRT_OK) return rc;
         if ((rc = upload(sc.get(), hs.ktopo2, &ds.ktopo2)) != CRT_OK) return rc;
     }
-    sc->cam = host_camera(hs);
+    ds.cam = host_camera(hs);
     sc->fov_radians = hs.fov_radians;
     sc->prune_origin_max = hs.prune_origin_max;
-    sc->camera_fast = camera_rays_fast(sc->cam, ds.planes_ok != 0);
+    sc->camera_fast = camera_rays_fast(ds.cam, ds.planes_ok != 0);
     if (ds.bnodes) sc->traversal = 14;   /* camera rays through the BVH too */
     if ((rc = upload(sc.get(), hs.tri_attr, &ds.tri_attr)) != CRT_OK) return rc;
     if ((rc = upload(sc.get(), hs.vnormal, &ds.vnormal)) != CRT_OK) return rc;
@@ -310,7 +310,7 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
     if (pow5_table && (rc = ensure_pow5_table(sc.get())) != CRT_OK) return rc;
     {
         const DeviceScene *d = nullptr;
-        if ((rc = sync_device_record(sc.get(), &d)) != CRT_OK) return rc;
+        if ((rc = sync_device_record(sc.get(), &d, sc->stream)) != CRT_OK) return rc;
         if (!sc->grid_empty && primary) {
             const size_t bytes = (size_t)hs.width * hs.height * 3 * sizeof(float);
             HIP_TRY(hipMalloc(&sc->d_out, bytes));
@@ -402,6 +402,10 @@ void crt_hip_scene_destroy(crt_hip_scene *sc) {
     if (sc->h_stage) (void)hipHostFree(sc->h_stage);
     for (hipEvent_t e : sc->stage_ev)
         if (e) (void)hipEventDestroy(e);
+    for (int j = 0; j < kRecRing; ++j) {
+        if (sc->rec_up[j]) (void)hipEventDestroy(sc->rec_up[j]);
+        if (sc->rec_use[j]) (void)hipEventDestroy(sc->rec_use[j]);
+    }
     if (sc->ev_start) (void)hipEventDestroy(sc->ev_start);
     if (sc->ev_stop) (void)hipEventDestroy(sc->ev_stop);
     if (sc->stream) (void)hipStreamDestroy(sc->stream);
@@ -624,7 +628,7 @@ int crt_hip_profile_waves(crt_hip_scene *sc, const crt_renderer_settings *st, ui
     if (rc == CRT_OK && e == hipSuccess && bp.cell_tile) {
         par = (int)((sc->bins.frame - 1) % kBinSets);   /* the set the frame just used */
         int64_t slots = 0;
-        for (int q = 0; q < kBinKinds; ++q) slots += (int64_t)kBinShards * bp.cap[q];
+        slots = (int64_t)kBinKinds * kBinShards * bp.ecap;
         work.resize((size_t)std::max<int64_t>(1, slots));
         ph_all.resize((size_t)kBinsPhdrInts);
         rest.resize((size_t)std::max(1, bp.nrest));
@@ -643,11 +647,11 @@ int crt_hip_profile_waves(crt_hip_scene *sc, const crt_renderer_settings *st, ui
             y = p.tiles[(size_t)k].y;
         } else {
             int kind = 0, slot = k >> 2, q = k & 3;
-            if (k >= 4 * kBinShards * bp.cap[0]) {
-                slot = k - 4 * kBinShards * bp.cap[0];
+            if (k >= 4 * kBinShards * bp.gcap[0]) {
+                slot = k - 4 * kBinShards * bp.gcap[0];
                 q = -1;
                 kind = 1;
-                while (kind < kBinKinds && slot >= kBinShards * bp.cap[kind]) slot -= kBinShards * bp.cap[kind++];
+                while (kind < kBinKinds && slot >= kBinShards * bp.gcap[kind]) slot -= kBinShards * bp.gcap[kind++];
             }
             if (kind == kBinKinds) {
                 if (slot < bp.nrest) {
@@ -656,8 +660,8 @@ int crt_hip_profile_waves(crt_hip_scene *sc, const crt_renderer_settings *st, ui
                 }
             } else {
                 const int sh = slot % kBinShards, i2 = slot / kBinShards;
-                if (i2 < std::min(ph_all[(size_t)bins_phdr_at(par, kind, sh)], bp.cap[kind])) {
-                    const Tile &t = work[(size_t)(bp.wbase[kind] + sh * bp.cap[kind] + i2)].t;
+                if (i2 < std::min(ph_all[(size_t)bins_phdr_at(par, kind, sh)], bp.ecap)) {
+                    const Tile &t = work[(size_t)(bp.wbase[kind] + sh * bp.ecap + i2)].t;
                     x = t.x + (q >= 0 ? (q & 1) * 4 : 0);
                     y = t.y + (q >= 0 ? (q >> 1) * 4 : 0);
                 }

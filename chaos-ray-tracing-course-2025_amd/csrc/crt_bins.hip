@@ -380,6 +380,7 @@ __global__ __launch_bounds__(256) void k_bins_project(const CamCand *__restrict_
      * (queue) and holds a slot for the group (its LDS scan takes kMaxGroups);
      * otherwise the block scatters them itself, kExpand a round */
     __shared__ int s_queued;
+    __syncthreads();   /* spre: wave 0's scan */
     const int G = spre[kProjTris];
     if (tid == 0) {
         int qd = 0;
@@ -563,15 +564,15 @@ __global__ __launch_bounds__(256) void k_bins_pairs(const BinItem *__restrict__ 
 /* A cell into its work list (BinsPlan): one lane. */
 __device__ __forceinline__ void bins_list(const BinsPlan &bp, int kind, int sh, Tile t, int off, int len, int c) {
     const int s2 = atomicAdd(&bp.phdr[bins_phdr_at(bp.par, kind, sh)], 1);
-    (void)BCK(s2, bp.cap[kind], 28);   /* the sizing pass's counts: every frame fits */
-    if (s2 < bp.cap[kind]) {
+    (void)BCK(s2, bp.ecap, 28);   /* a list holds every cell of its shard */
+    if (s2 < bp.ecap) {
         BinsWork w;
         w.t = t;
         w.off = off;
         w.len = len;
         w.cell = c;
         w.pad = 0;
-        bp.work[bp.wbase[kind] + sh * bp.cap[kind] + s2] = w;
+        bp.work[bp.wbase[kind] + sh * bp.ecap + s2] = w;
     }
 }
 
@@ -911,10 +912,12 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
         bins_free(sc);   /* the scene walks the BVH (or the kd tree) */
         return CRT_OK;
     }
-    /* each shard's records in a region of its own, sized from the pass with slack */
+    /* each shard's records in a region of its own, sized from the pass with
+     * room for a camera that moves (crt_hip_scene_set_camera): a cell whose
+     * list does not fit walks the BVH */
     int64_t base = 0;
     for (int s2 = 0; s2 < kBinShards; ++s2) {
-        const int64_t cap = shard_rec[s2] + shard_rec[s2] / 8 + 256;
+        const int64_t cap = 2 * shard_rec[s2] + 1024;
         b.caps.base[s2] = (int32_t)base;
         b.caps.cap[s2] = (int32_t)cap;
         base += cap;
@@ -985,11 +988,15 @@ int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
         if (!inside[(size_t)k] && !sc->ds.bnodes) return CRT_OK;   /* no BVH for it: not a bins plan (the kd walk) */
         if (!inside[(size_t)k] || cell_tile[(size_t)(t.y >> 3) * b.tx + (t.x >> 3)] == -2) rest.push_back(k);
     }
+    /* the lists hold every cell of a shard (a moved camera may list any cell
+     * of any kind); the grid takes the sizing pass's counts, at least one
+     * slot per shard and kind */
+    bp.ecap = b.cap_shard;
     int64_t slots = 0;
     for (int q = 0; q < kBinKinds; ++q) {
-        bp.cap[q] = *std::max_element(per[q], per[q] + kBinShards);
+        bp.gcap[q] = std::max(1, *std::max_element(per[q], per[q] + kBinShards));
         bp.wbase[q] = (int32_t)slots;
-        slots += (int64_t)kBinShards * bp.cap[q];
+        slots += (int64_t)kBinShards * bp.ecap;
     }
     bp.nrest = (int32_t)rest.size();
     bp.ncell = b.ncell;
@@ -1010,7 +1017,7 @@ int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
     bp.work = static_cast<BinsWork *>(p[1]);
     bp.phdr = static_cast<int32_t *>(p[2]);
     bp.rest = static_cast<int32_t *>(p[3]);
-    plan.waves = 4 * kBinShards * bp.cap[0] + kBinShards * (bp.cap[1] + bp.cap[2] + bp.cap[3]) + bp.nrest + bp.nfill;
+    plan.waves = 4 * kBinShards * bp.gcap[0] + kBinShards * (bp.gcap[1] + bp.gcap[2] + bp.gcap[3]) + bp.nrest + bp.nfill;
     return CRT_OK;
 }
 

@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRT_GIM_WAV
                         opx = (int)(tl.out_base + (int64_t)ly * tl.out_stride + lx);
                         px = (uint32_t)(tl.x + lx);
                         py = (uint32_t)(tl.y + ly);
-                        camera_ray(st.cam, (int)px, (int)py, o, d);
+                        camera_ray(s.cam, (int)px, (int)py, o, d);
                         depth = 0;
                         rng = make_pcg(px, py);
                         if (COUNT) ++cnt.traversals;

@@ -267,11 +267,11 @@ int probe_tiles(crt_hip_scene *sc, const DeviceScene *d_scene, int walk, const s
         const Tile *t = static_cast<const Tile *>(dt);
         uint32_t *c = static_cast<uint32_t *>(dc);
         switch (walk) {
-        case 7: hipLaunchKernelGGL(k_probe_tiles<7>, grid, dim3(256), 0, stream, d_scene, sc->cam, t, n, c); break;
-        case 12: hipLaunchKernelGGL(k_probe_tiles<12>, grid, dim3(256), 0, stream, d_scene, sc->cam, t, n, c); break;
-        case 13: hipLaunchKernelGGL(k_probe_tiles<13>, grid, dim3(256), 0, stream, d_scene, sc->cam, t, n, c); break;
-        case 14: hipLaunchKernelGGL(k_probe_tiles<14>, grid, dim3(256), 0, stream, d_scene, sc->cam, t, n, c); break;
-        default: hipLaunchKernelGGL(k_probe_tiles<8>, grid, dim3(256), 0, stream, d_scene, sc->cam, t, n, c); break;
+        case 7: hipLaunchKernelGGL(k_probe_tiles<7>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
+        case 12: hipLaunchKernelGGL(k_probe_tiles<12>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
+        case 13: hipLaunchKernelGGL(k_probe_tiles<13>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
+        case 14: hipLaunchKernelGGL(k_probe_tiles<14>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
+        default: hipLaunchKernelGGL(k_probe_tiles<8>, grid, dim3(256), 0, stream, d_scene, t, n, c); break;
         }
         e = hipGetLastError();
     }
@@ -415,23 +415,60 @@ int ensure_gi_tables(crt_hip_scene *sc) {
     return CRT_OK;
 }
 
-/* Device copy of sc->ds for the render kernels.  Re-uploaded only when the
- * host record changed (first GI frame, new resolution); kernels of earlier
- * frames may still read the old copy, so the device is drained first. */
-int sync_device_record(crt_hip_scene *sc, const DeviceScene **out) {
-    if (!sc->d_ds || std::memcmp(&sc->ds_uploaded, &sc->ds, sizeof(DeviceScene)) != 0) {
-        if (!sc->d_ds) {
-            void *p = nullptr;
-            HIP_TRY(hipMalloc(&p, sizeof(DeviceScene)));
-            sc->allocs.push_back(p);
-            sc->d_ds = static_cast<DeviceScene *>(p);
-        } else {
-            HIP_TRY(hipDeviceSynchronize());
+/* Device copy of sc->ds for the render kernels.  When the host record
+ * changed (a new camera, the first GI frame's tables) the next slot of a ring
+ * of kRecRing records takes it, written on `stream` by a one-thread kernel
+ * (the record travels as its by-value argument: no host sync, no staging),
+ * after the frames that last read that slot (rec_use); frames issued before
+ * keep reading their own slot.  Work on another stream that reads the record
+ * waits for rec_up of its slot (wait_device_record). */
+int sync_device_record(crt_hip_scene *sc, const DeviceScene **out, hipStream_t stream) {
+    if (!sc->d_ring) {
+        void *p = nullptr;
+        HIP_TRY(hipMalloc(&p, kRecRing * sizeof(DeviceScene)));
+        sc->allocs.push_back(p);
+        sc->d_ring = static_cast<DeviceScene *>(p);
+        for (int j = 0; j < kRecRing; ++j) {
+            HIP_TRY(hipEventCreateWithFlags(&sc->rec_up[j], CRT_PIPE_EV_FLAGS));
+            HIP_TRY(hipEventCreateWithFlags(&sc->rec_use[j], CRT_PIPE_EV_FLAGS));
         }
-        HIP_TRY(hipMemcpy(sc->d_ds, &sc->ds, sizeof(DeviceScene), hipMemcpyHostToDevice));
+    }
+    if (sc->ring_cur < 0 || std::memcmp(&sc->ds_uploaded, &sc->ds, sizeof(DeviceScene)) != 0) {
+        const int j = (sc->ring_cur + 1) % kRecRing;
+        if (sc->rec_used[j]) HIP_TRY(hipStreamWaitEvent(stream, sc->rec_use[j], 0));
+        hipLaunchKernelGGL(k_put_record, dim3(1), dim3(64), 0, stream, sc->d_ring + j, sc->ds);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(sc->rec_up[j], stream));
+        sc->ring_cur = j;
+        sc->rec_up_stream = stream;
+        sc->d_ds = sc->d_ring + j;
         std::memcpy(&sc->ds_uploaded, &sc->ds, sizeof(DeviceScene));
+        ++sc->records_written;
+    } else {
+        const int rc = wait_device_record(sc, stream);
+        if (rc != CRT_OK) return rc;
     }
     *out = sc->d_ds;
+    return CRT_OK;
+}
+
+/* `stream` will read the current record: after its write (nothing to wait
+ * for on the stream that wrote it, or once the write is done). */
+int wait_device_record(crt_hip_scene *sc, hipStream_t stream) {
+    if (sc->ring_cur < 0 || stream == sc->rec_up_stream) return CRT_OK;
+    if (hipEventQuery(sc->rec_up[sc->ring_cur]) == hipSuccess) {
+        sc->rec_up_stream = nullptr;   /* written: every stream may read it */
+        return CRT_OK;
+    }
+    HIP_TRY(hipStreamWaitEvent(stream, sc->rec_up[sc->ring_cur], 0));
+    return CRT_OK;
+}
+
+/* The frame issued on `stream` is the current record's last reader so far. */
+int used_device_record(crt_hip_scene *sc, hipStream_t stream) {
+    if (sc->ring_cur < 0) return CRT_OK;
+    HIP_TRY(hipEventRecord(sc->rec_use[sc->ring_cur], stream));
+    sc->rec_used[sc->ring_cur] = true;
     return CRT_OK;
 }
 
@@ -495,7 +532,7 @@ int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t
         return CRT_OK;
     }
     const DeviceScene *d_scene = nullptr;
-    int rc = sync_device_record(sc, &d_scene);
+    int rc = sync_device_record(sc, &d_scene, stream);
     if (rc != CRT_OK) return rc;
     HIP_TRY(hipDeviceSynchronize());   /* earlier frames may still read the old tile lists */
     int64_t px = 0;
@@ -552,9 +589,8 @@ int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t
     return make_tile_plan(sc, all, true, sc->full);
 }
 
-DSettings to_dsettings(const crt_hip_scene *sc, const crt_renderer_settings *st) {
+DSettings to_dsettings(const crt_renderer_settings *st) {
     DSettings d;
-    d.cam = sc->cam;
     d.max_ray_depth = st->max_ray_depth;
     d.diffuse_reflection_ray_count = st->diffuse_reflection_ray_count;
     d.shadow_bias = st->shadow_bias;
@@ -739,6 +775,10 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
      * the set's previous frame; a frame with read-backs on the caller's */
     const hipStream_t ls = replay ? wb.streams[si % kWfStreams] : stream;
     HIP_TRY(hipStreamWaitEvent(ls, w.free_ev, 0));
+    if (replay) {   /* the scene record this frame reads was written on another stream */
+        const int rc0 = wait_device_record(sc, ls);
+        if (rc0 != CRT_OK) return rc0;
+    }
     const int kMaxLevels = (int)ds.max_ray_depth + 2;
     if (!w.counts || w.count_cap < kMaxLevels) {
         int rc0 = wf_set_release(wb, si);
@@ -928,10 +968,10 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     if (plan.ntiles == 0) return CRT_OK;
     const DeviceScene *d_scene = nullptr;
     {
-        const int rc = sync_device_record(sc, &d_scene);
+        const int rc = sync_device_record(sc, &d_scene, stream);
         if (rc != CRT_OK) return rc;
     }
-    const DSettings ds = to_dsettings(sc, st);
+    const DSettings ds = to_dsettings(st);
     /* Walks: camera rays take the packet walk (traversal 7, or 8 pruned).
      * Secondary rays scatter and take the cooperative walk: pruned (10) for
      * reflect/refract levels (C3), reference order (4) for GI fan-out — the
@@ -1097,7 +1137,7 @@ int render_into(crt_hip_scene *sc, const crt_renderer_settings *st, float *d_rgb
     if (rc != CRT_OK) return rc;
     if (sc->record_events) HIP_TRY(hipEventRecord(sc->ev_stop, stream));
     sc->events_valid = sc->record_events != 0;
-    return CRT_OK;
+    return used_device_record(sc, stream);
 }
 
 }  // namespace crt_amd
@@ -1109,12 +1149,12 @@ namespace crt_amd {
 int ensure_live_mask(crt_hip_scene *sc) {
     if (!sc->live_mask.empty() || sc->grid_empty) return CRT_OK;
     const DeviceScene *d_scene = nullptr;
-    int rc = sync_device_record(sc, &d_scene);
+    int rc = sync_device_record(sc, &d_scene, sc->stream);
     if (rc != CRT_OK) return rc;
     const int64_t npx = (int64_t)sc->info.width * sc->info.height;
     uint8_t *d = nullptr;
     HIP_TRY(hipMalloc(&d, (size_t)npx));
-    hipLaunchKernelGGL(k_live_pixels, dim3((unsigned)((npx + 255) / 256)), dim3(256), 0, sc->stream, d_scene, sc->cam, d);
+    hipLaunchKernelGGL(k_live_pixels, dim3((unsigned)((npx + 255) / 256)), dim3(256), 0, sc->stream, d_scene, d);
     hipError_t e = hipGetLastError();
     std::vector<uint8_t> m((size_t)npx);
     if (e == hipSuccess) e = hipMemcpyAsync(m.data(), d, (size_t)npx, hipMemcpyDeviceToHost, sc->stream);
@@ -1158,7 +1198,7 @@ int render_shard_t(crt_hip_scene *sc, const crt_renderer_settings *st, int shard
     if (rc != CRT_OK) return rc;
     if (sc->record_events) HIP_TRY(hipEventRecord(sc->ev_stop, s));
     sc->events_valid = sc->record_events != 0;
-    return CRT_OK;
+    return used_device_record(sc, s);
 }
 
 /* write_ppm's conversion of one component on the host (k_quantize). */

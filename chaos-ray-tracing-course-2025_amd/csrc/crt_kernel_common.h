@@ -34,9 +34,11 @@ constexpr int kBinShards = 16;
  * i kBinShards + s; heavy slots four waves each), then the plan's `rest` tiles
  * (not inside one cell, or sharing a cell), which read the cell's list
  * themselves, then the fill waves: 16 cells each, the background written to
- * the tiles of the cells with no candidate (every pixel misses).  The lists'
- * capacities are the scene's sizing-pass counts: the camera is the scene's, so
- * every frame fills them alike. */
+ * the tiles of the cells with no candidate (every pixel misses).  Each list
+ * holds up to ecap entries per shard (every cell of the shard fits); the grid
+ * has gcap[q] slots per shard and kind, the scene's sizing-pass counts (at
+ * least 1): a frame whose camera lists more cells of a kind than the grid
+ * holds has each slot's wave take the entries gcap[q] apart in turn. */
 constexpr int kBinKinds = 4;   /* heavy, medium, light, bvh */
 struct alignas(16) BinsWork {
     Tile t;
@@ -46,10 +48,11 @@ struct alignas(16) BinsWork {
 struct BinsPlan {
     int32_t *cell_tile;   /* per cell: the plan's one tile inside it; -1 none (the cell is not rendered), -2 several */
     const Tile *tiles;    /* the plan's tiles */
-    BinsWork *work;       /* the lists: kind q, shard s, entry i at wbase[q] + s cap[q] + i */
+    BinsWork *work;       /* the lists: kind q, shard s, entry i at wbase[q] + s ecap + i */
     int32_t *phdr;        /* entries listed this frame: counter bins_phdr_at(set, kind, shard) */
     const int32_t *rest;  /* tiles the lists do not hold */
-    int32_t cap[kBinKinds], wbase[kBinKinds];
+    int32_t gcap[kBinKinds], wbase[kBinKinds];   /* grid slots per shard; each kind's first entry */
+    int32_t ecap;         /* entries per shard and kind (the shard's cells) */
     int32_t nrest, nfill, ncell;
     int32_t wslots;       /* work-list slots of one set (work: kBinSets sets; the frame's at par * wslots) */
     int32_t split, medium, quad;

@@ -96,7 +96,7 @@ __global__ void k_render_gi(const DeviceScene *__restrict__ scene, DSettings st,
                             int ntiles, float *__restrict__ out, int32_t *__restrict__ next_px,
                             unsigned long long *__restrict__ counters, float4 *__restrict__ gframes);
 template <int TRAV>
-__global__ void k_probe_tiles(const DeviceScene *__restrict__ scene, DCamera cam, const Tile *__restrict__ tiles, int ntiles,
+__global__ void k_probe_tiles(const DeviceScene *__restrict__ scene, const Tile *__restrict__ tiles, int ntiles,
                               uint32_t *__restrict__ wave_cost);
 template <int TRAV, bool LEVEL0, bool COUNT>
 __global__ void k_wf_level(const DeviceScene *__restrict__ scene, DSettings st, const Tile *__restrict__ tiles,
@@ -109,7 +109,8 @@ __global__ void k_trace_rays(DeviceScene s, const float *__restrict__ rays, int6
 template <class T>
 __global__ void k_unpack(const UnpackBucket *__restrict__ buckets, const T *__restrict__ src, T *__restrict__ dst,
                          int width, Rgb<T> bg);
-__global__ void k_live_pixels(const DeviceScene *__restrict__ scene, DCamera cam, uint8_t *__restrict__ live);
+__global__ void k_live_pixels(const DeviceScene *__restrict__ scene, uint8_t *__restrict__ live);
+__global__ void k_put_record(DeviceScene *__restrict__ dst, DeviceScene v);
 __global__ void k_quantize(const float *__restrict__ src, uint8_t *__restrict__ dst, int64_t n, float maxf, int maxi);
 __global__ void k_warm_render();
 __global__ void k_warm_gi();
@@ -142,7 +143,7 @@ __global__ void k_warm_bins();
 #define CRT_GIM_SIG(C) void k_render_gi<C>(const DeviceScene *__restrict__, DSettings, const Tile *__restrict__, int, \
     float *__restrict__, int32_t *__restrict__, unsigned long long *__restrict__, float4 *__restrict__);
 #define CRT_PROBE_INSTANCES(X) X(7) X(8) X(12) X(13) X(14)
-#define CRT_PROBE_SIG(T) void k_probe_tiles<T>(const DeviceScene *__restrict__, DCamera, const Tile *__restrict__, int, \
+#define CRT_PROBE_SIG(T) void k_probe_tiles<T>(const DeviceScene *__restrict__, const Tile *__restrict__, int, \
     uint32_t *__restrict__);
 #define CRT_WF_INSTANCES(X) X(4, false, false) X(4, false, true) X(10, false, false) X(10, false, true)        \
     X(14, false, false) X(14, false, true) X(7, true, false) X(7, true, true) X(8, true, false) X(8, true, true) \

@@ -158,6 +158,17 @@ struct DLight {
     float px, py, pz;
 };
 
+/* The camera as the kernels see it (crt_camera.cpp:7-35): the frame's
+ * constants, float(width) / height and std::tan(fov_radians * 0.5f) computed
+ * on the host with the reference's libm. */
+struct DCamera {
+    float loc[3];
+    float rot[9];           /* row-major, ray_dir = v * R (crt_matrix.h:66-74) */
+    int32_t width, height;
+    float aspect;           /* float(width) / height            (crt_camera.cpp:23) */
+    float tan_half_fov;     /* std::tan(fov_radians * 0.5f)     (crt_camera.cpp:26-27) */
+};
+
 /* Everything a render kernel needs, passed by value. */
 struct DeviceScene {
     const DNode *nodes;
@@ -205,26 +216,16 @@ struct DeviceScene {
     /* powf(x, 5.0f) of the host's libm for every x = k * 2^-24 in [-1, 1]
      * (2^25 + 1 floats, index k + 2^24): the Fresnel term's exact values */
     const float *pow5;
+    /* the camera frames are rendered with: a device scene record is one of a
+     * ring of records (crt_host_render.hip sync_device_record), so a frame
+     * keeps the camera it was issued with while the next frames move it */
+    DCamera cam;
     int32_t planes_ok;      /* every node plane is 0 or |p| in [2^-40, 2^62] (crt_device.h coord_ok) */
     float background[3];
     int32_t gi_on, reflections_on, refractions_on;
 };
 
-/* The camera as the kernels see it (crt_camera.cpp:7-35): the frame's
- * constants, float(width) / height and std::tan(fov_radians * 0.5f) computed
- * on the host with the reference's libm. */
-struct DCamera {
-    float loc[3];
-    float rot[9];           /* row-major, ray_dir = v * R (crt_matrix.h:66-74) */
-    int32_t width, height;
-    float aspect;           /* float(width) / height            (crt_camera.cpp:23) */
-    float tan_half_fov;     /* std::tan(fov_radians * 0.5f)     (crt_camera.cpp:26-27) */
-};
-
-/* A frame's constants as the kernels see them, passed by value with every
- * launch: the renderer settings (crt_renderer.h:18-25) and the camera — so a
- * frame renders with the camera current when it was issued, whatever
- * crt_hip_scene_set_camera does while it is in flight. */
+/* Renderer settings as the kernels see them (crt_renderer.h:18-25). */
 struct DSettings {
     uint32_t max_ray_depth;
     uint32_t diffuse_reflection_ray_count;
@@ -232,7 +233,6 @@ struct DSettings {
     float reflection_bias;
     float diffuse_reflection_bias;
     float refraction_bias;
-    DCamera cam;
 };
 
 /* A bucket of the reference grid (crt_renderer.cpp:160-174). */

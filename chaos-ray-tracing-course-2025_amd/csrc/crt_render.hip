@@ -16,20 +16,22 @@ namespace crt_amd {
  * BinsPlan): a quarter of a heavy cell, a medium, light or bvh cell of this
  * frame's work lists (with the cell's list: off, len), or a rest tile (len
  * -2: the wave reads its cell's list).  The list's count and the entry are
- * loaded together.  Returns 0: nothing to do (an unused list slot), 1: the
+ * loaded together.  rep: the slot's rep-th entry (entries gcap apart).
+ * Returns 0: nothing to do (an unused list slot, or no further entry), 1: the
  * tile, 2: a fill wave (off: its index). */
-__device__ __forceinline__ int bins_tile(const BinsPlan &bp, const Tile *__restrict__ tiles, int wave, Tile &tl,
-                                         int &off, int &len) {
+__device__ __forceinline__ int bins_tile(const BinsPlan &bp, const Tile *__restrict__ tiles, int wave, int rep,
+                                         Tile &tl, int &off, int &len) {
     int kind = 0, slot = wave >> 2, q = wave & 3;
-    if (wave >= 4 * kBinShards * bp.cap[0]) {
-        slot = wave - 4 * kBinShards * bp.cap[0];
+    if (wave >= 4 * kBinShards * bp.gcap[0]) {
+        slot = wave - 4 * kBinShards * bp.gcap[0];
         q = -1;
         kind = 1;
-        while (kind < kBinKinds && slot >= kBinShards * bp.cap[kind]) {
-            slot -= kBinShards * bp.cap[kind];
+        while (kind < kBinKinds && slot >= kBinShards * bp.gcap[kind]) {
+            slot -= kBinShards * bp.gcap[kind];
             ++kind;
         }
         if (kind == kBinKinds) {
+            if (rep > 0) return 0;
             if (slot >= bp.nrest) {
                 off = slot - bp.nrest;
                 return 2;
@@ -39,10 +41,11 @@ __device__ __forceinline__ int bins_tile(const BinsPlan &bp, const Tile *__restr
             return 1;
         }
     }
-    const int sh = slot % kBinShards, i = slot / kBinShards;
+    const int sh = slot % kBinShards, i = slot / kBinShards + rep * bp.gcap[kind];
     const int n = load_scalar(bp.phdr, bins_phdr_at(bp.par, kind, sh));
-    const BinsWork w = bp.work[bp.wbase[kind] + sh * bp.cap[kind] + i];
-    if (i >= min(n, bp.cap[kind])) return 0;
+    if (i >= bp.ecap) return 0;
+    const BinsWork w = bp.work[bp.wbase[kind] + sh * bp.ecap + i];
+    if (i >= n) return 0;
     tl = w.t;
     off = w.off;
     len = w.len;
@@ -108,31 +111,15 @@ __device__ void bins_fill(const DeviceScene &s, const BinsPlan &bp, const Tile *
     }
 }
 
+/* One tile of a render grid (k_render_tiles): camera bins cell (len >= 0:
+ * the cell's list from its work-list entry; -2: read it here; -1: the BVH
+ * walk), a split tile's window walk, or the frame-stack walk of an 8x8 tile. */
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW>
-__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT_WINDOW_WAVES : TRAV == 12 ? CRT_PACKET_WAVES : (TRAV == 14 || TRAV == 15) && !FULL ? CRT_BVH_WAVES : (FULL && MAXF == 4 ? CRT_GI_WAVES : 1)))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
-                                                  const Tile *__restrict__ tiles,
-                                                      int ntiles, float *__restrict__ out,
-                                                      unsigned long long *__restrict__ counters,
-                                                      unsigned long long *__restrict__ stamps, BinsPlan bp) {
-    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    const int lane = (int)(threadIdx.x & 63);
-    if (wave >= ntiles) return;
-    /* The scene record is read through a pointer (not a by-value kernel
-     * argument): its fields are then loaded where they are used, so shading
-     * constants are not held in SGPRs across the tree walk (6 -> more waves/SIMD). */
-    const DeviceScene &s = *scene;
-    /* diagnostic build only (stamps != nullptr): wave start / end in s_memrealtime ticks (100 MHz) */
-    if (stamps && lane == 0) stamps[2 * wave] = __builtin_amdgcn_s_memrealtime();
-    Tile tl;
-    int bin_beg = 0, bin_len = -2;   /* camera bins: the cell's list from the work list (-2: read it below) */
-    if constexpr (TRAV == 15 && !FULL && !SHADOW) {
-        const int r = bins_tile(bp, tiles, wave, tl, bin_beg, bin_len);
-        if (r == 2) bins_fill(s, bp, tiles, bin_beg, out, COUNT ? counters : nullptr);
-        if (r != 1) return;
-    } else {
-        (void)bp;
-        tl = tiles[wave];
-    }
+__device__ __forceinline__ void render_tile(const DeviceScene &s, const DSettings &st, Tile tl, int bin_beg,
+                                            int bin_len, float *__restrict__ out,
+                                            unsigned long long *__restrict__ counters,
+                                            unsigned long long *__restrict__ stamps, const BinsPlan &bp, int wave,
+                                            int lane) {
     /* the heaviest tiles set the frame length (their walks are long chains of
      * dependent loads): they get issue priority over the light waves that
      * share their SIMD (s_setprio; scheduling only, results unchanged) */
@@ -147,7 +134,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             const bool act = r < npx;
             const int px = act ? r % tw : 0, py = act ? r / tw : 0;
             Vec o, d;
-            camera_ray(st.cam, tl.x + px, tl.y + py, o, d);
+            camera_ray(s.cam, tl.x + px, tl.y + py, o, d);
             LaneCounts cw = {};
             float t;
             const int slot = R == 4 ? trace_window<COUNT, 4>(s, r, sl, act, o, d, t, cw)
@@ -199,7 +186,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
                 const int p = lane >> 2, sl = lane & 3, lx = p & 3, ly = p >> 2;
                 const bool act = lx < tw && ly < th;
                 Vec o, d;
-                camera_ray(st.cam, tx0 + (act ? lx : 0), ty0 + (act ? ly : 0), o, d);
+                camera_ray(s.cam, tx0 + (act ? lx : 0), ty0 + (act ? ly : 0), o, d);
                 LaneCounts cw = {};
                 float t;
                 const int bit = 8 * ((ty0 & 7) + ly) + (tx0 & 7) + lx;
@@ -225,7 +212,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             const int lx = lane & 7, ly = lane >> 3;
             const bool act = lx < tw && ly < th;
             Vec o, d;
-            camera_ray(st.cam, tx0 + (act ? lx : 0), ty0 + (act ? ly : 0), o, d);
+            camera_ray(s.cam, tx0 + (act ? lx : 0), ty0 + (act ? ly : 0), o, d);
             LaneCounts cw = {};
             float t;
             const int bit = 8 * ((ty0 & 7) + ly) + (tx0 & 7) + lx;
@@ -261,7 +248,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
             const bool act = r < npx;
             const int px = act ? r % tw : 0, py = act ? r / tw : 0;
             Vec o, d;
-            camera_ray(st.cam, tl.x + px, tl.y + py, o, d);
+            camera_ray(s.cam, tl.x + px, tl.y + py, o, d);
             LaneCounts cw = {};
             float t;
             const int slot = K == 16 ? trace_bvh_window<COUNT, 16>(s, sl, act, o, d, t, cw)
@@ -325,13 +312,48 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
     }
 }
 
+
+template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW>
+__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT_WINDOW_WAVES : TRAV == 12 ? CRT_PACKET_WAVES : (TRAV == 14 || TRAV == 15) && !FULL ? CRT_BVH_WAVES : (FULL && MAXF == 4 ? CRT_GI_WAVES : 1)))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
+                                                  const Tile *__restrict__ tiles,
+                                                      int ntiles, float *__restrict__ out,
+                                                      unsigned long long *__restrict__ counters,
+                                                      unsigned long long *__restrict__ stamps, BinsPlan bp) {
+    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int lane = (int)(threadIdx.x & 63);
+    if (wave >= ntiles) return;
+    /* The scene record is read through a pointer (not a by-value kernel
+     * argument): its fields are then loaded where they are used, so shading
+     * constants are not held in SGPRs across the tree walk (6 -> more waves/SIMD). */
+    const DeviceScene &s = *scene;
+    /* diagnostic build only (stamps != nullptr): wave start / end in s_memrealtime ticks (100 MHz) */
+    if (stamps && lane == 0) stamps[2 * wave] = __builtin_amdgcn_s_memrealtime();
+    if constexpr (TRAV == 15 && !FULL && !SHADOW) {
+        /* camera bins: the wave's work-list slot, and the entries a grid's
+         * capacity further on when this frame's list outgrew the grid (the
+         * camera moved since the sizing pass) */
+        for (int rep = 0;; ++rep) {
+            Tile tl;
+            int bin_beg = 0, bin_len = -2;   /* the cell's list from the work list (-2: read it in render_tile) */
+            const int r = bins_tile(bp, tiles, wave, rep, tl, bin_beg, bin_len);
+            if (r == 2) bins_fill(s, bp, tiles, bin_beg, out, COUNT ? counters : nullptr);
+            if (r != 1) return;
+            render_tile<FULL, MAXF, TRAV, SEC, COUNT, SHADOW>(s, st, tl, bin_beg, bin_len, out, counters, stamps, bp,
+                                                              wave, lane);
+        }
+    } else {
+        render_tile<FULL, MAXF, TRAV, SEC, COUNT, SHADOW>(s, st, tiles[wave], 0, -2, out, counters, stamps, bp, wave,
+                                                          lane);
+    }
+}
+
 /* Calibration probe (measured-cost tile plan): the camera rays of a tile
  * list traced with the frame's primary walk, no shading.  Each wave writes
  * its cost: for the packet walks the wave's node + triangle + edge steps
  * (what the wave pays: the union of its lanes' visit sets), for per-lane
  * walks the largest lane's node + triangle tests. */
 template <int TRAV>
-__global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restrict__ scene, DCamera cam,
+__global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restrict__ scene,
                                                      const Tile *__restrict__ tiles, int ntiles,
                                                      uint32_t *__restrict__ wave_cost) {
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -342,7 +364,7 @@ __global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restri
     const int lx = lane & 7, ly = lane >> 3;
     const bool has_px = lx < tl.w && ly < tl.h;
     Vec o, d;
-    camera_ray(cam, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), o, d);
+    camera_ray(s.cam, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), o, d);
     LaneCounts cnt = {};
     constexpr bool kCoop = kIsCoop<TRAV>;
     __shared__ CoopLds coop[kCoop ? 4 : 1];

@@ -58,7 +58,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(MAXF == 4 ? (TRA
                     if (lx < tl.w && ly < tl.h) {   /* slots outside a partial tile: retry next pass */
                         has = true;
                         opx = tl.out_base + (int64_t)ly * tl.out_stride + lx;
-                        camera_ray(st.cam, tl.x + lx, tl.y + ly, o, d);
+                        camera_ray(s.cam, tl.x + lx, tl.y + ly, o, d);
                         depth = 0;
                         rng = make_pcg((uint32_t)(tl.x + lx), (uint32_t)(tl.y + ly));
                         sp = 0;

@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         if (tl.prio & 1) __builtin_amdgcn_s_setprio(3);
         const int lx = lane & 7, ly = lane >> 3;
         has = lx < tl.w && ly < tl.h;
-        if (has) camera_ray(st.cam, tl.x + lx, tl.y + ly, o, d);
+        if (has) camera_ray(s.cam, tl.x + lx, tl.y + ly, o, d);
     } else {
         const int ray0 = (gid >> 6) * lv.rpw;
         if (ray0 >= lv.n) return;          /* whole wave past the queue */

@@ -149,6 +149,9 @@ struct WfBuffers {
     std::vector<Graph> graphs;
 };
 
+/* Device scene records in flight (crt_host_render.hip sync_device_record). */
+constexpr int kRecRing = 16;
+
 /* Deepest recursion the wavefront path accepts (levels are launched one by one). */
 constexpr int kWfMaxDepth = 4096;
 
@@ -169,7 +172,14 @@ struct crt_hip_scene {
     bool has_refractive = false;   /* Fresnel term: needs the powf table (fresnel_of) */
     DeviceScene ds{};
     DeviceScene ds_uploaded{};   /* what d_ds holds */
-    DeviceScene *d_ds = nullptr;
+    DeviceScene *d_ds = nullptr;     /* the current record: a slot of d_ring (sync_device_record) */
+    DeviceScene *d_ring = nullptr;
+    int ring_cur = -1;
+    hipStream_t rec_up_stream = nullptr;   /* where the current record was written (null: done) */
+    hipEvent_t rec_up[kRecRing] = {};    /* slot written */
+    hipEvent_t rec_use[kRecRing] = {};   /* the last frame that read the slot is done */
+    bool rec_used[kRecRing] = {};
+    int64_t records_written = 0;
     crt_wave_counts wave_counts{};   /* from the last crt_hip_count_work */
     std::vector<void *> allocs;
     hipStream_t stream = nullptr;
@@ -200,10 +210,7 @@ struct crt_hip_scene {
     int traversal = 8;             /* 7 reference order | 8 pruned (default), see trace<> (env CRT_TRAVERSAL) */
     int shadows = 0;               /* option "shadows": trace the shadow rays (k_render_tiles<..., SHADOW>) */
     int trace_walk = 1;            /* crt_hip_trace_batch: 0 reference-order walk, 1 pruned per-lane walk */
-    /* the camera frames are issued with (crt_hip_scene_set_camera), passed to
-     * every launch by value in DSettings */
-    DCamera cam{};
-    float fov_radians = 0.f;
+    float fov_radians = 0.f;       /* the camera's (ds.cam: the rest) */
     float prune_origin_max = 0.f;  /* the hull margins' origin bound (bins need the camera inside it) */
     bool camera_fast = false;      /* every camera ray takes the fast box path (camera_rays_fast) */
     /* estimate plan (no calibration): a tile is split into 4x4 (2x2) pixel
@@ -267,7 +274,9 @@ bool wf_overflowed(WfBuffers &w, bool wait);
 int wf_streams(WfBuffers &wb, hipStream_t stream);
 int make_tile_plan(crt_hip_scene *sc, const std::vector<DBucket> &buckets, bool full_frame, ShardPlan &plan);
 void free_plans(crt_hip_scene *sc);
-int sync_device_record(crt_hip_scene *sc, const DeviceScene **out);
+int sync_device_record(crt_hip_scene *sc, const DeviceScene **out, hipStream_t stream);
+int wait_device_record(crt_hip_scene *sc, hipStream_t stream);
+int used_device_record(crt_hip_scene *sc, hipStream_t stream);
 int check_settings(const crt_renderer_settings *st);
 int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t stream, bool render = false);
 void warm_code_objects(int device, hipStream_t stream);

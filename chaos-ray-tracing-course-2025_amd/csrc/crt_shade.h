@@ -341,7 +341,7 @@ template <int TRAV, bool COUNT>
 __device__ Vec shade_shadowed(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt, CoopLds *L,
                               bool has_px) {
     Vec o, d;
-    camera_ray(st.cam, x, y, o, d);
+    camera_ray(s.cam, x, y, o, d);
     float t;
     const int slot = trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
     return shade_hit_shadowed<COUNT>(s, st, has_px, o, d, slot, t, cnt);
@@ -351,7 +351,7 @@ template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW = fals
 __device__ Vec shade_pixel(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt, CoopLds *L,
                            bool has_px) {
     Vec o, d;
-    camera_ray(st.cam, x, y, o, d);
+    camera_ray(s.cam, x, y, o, d);
     uint32_t depth = 0;
     Pcg32 rng;
     if (FULL) rng = make_pcg((uint32_t)x, (uint32_t)y);

@@ -68,19 +68,25 @@ __global__ __launch_bounds__(256) void k_unpack(const UnpackBucket *__restrict__
     }
 }
 
+/* One device scene record into its ring slot (sync_device_record): the
+ * record is this launch's by-value argument, so the write is ordered on the
+ * launch's stream like any kernel. */
+__global__ void k_put_record(DeviceScene *__restrict__ dst, DeviceScene v) {
+    if (threadIdx.x == 0) *dst = v;
+}
+
 /* Live pixels for the compact shards: the camera ray passes the reference's
  * six-face test on the root cell (crt_intersection.cpp:14-45, node 0 popped
  * first, :114-121).  A ray that fails it is a miss, i.e. shade_ray returns the
  * background colour (crt_renderer.cpp:142-144) — so dead pixels need neither
  * rendering nor transport. */
-__global__ __launch_bounds__(256) void k_live_pixels(const DeviceScene *__restrict__ scene, DCamera cam,
-                                                     uint8_t *__restrict__ live) {
+__global__ __launch_bounds__(256) void k_live_pixels(const DeviceScene *__restrict__ scene, uint8_t *__restrict__ live) {
     const DeviceScene &s = *scene;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)cam.width * cam.height) return;
-    const int x = (int)(i % cam.width), y = (int)(i / cam.width);
+    if (i >= (int64_t)s.cam.width * s.cam.height) return;
+    const int x = (int)(i % s.cam.width), y = (int)(i / s.cam.width);
     Vec o, d;
-    camera_ray(cam, x, y, o, d);
+    camera_ray(s.cam, x, y, o, d);
     bool hit = false;
     if (s.node_count > 0) {
         const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
