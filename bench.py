@@ -113,6 +113,10 @@ def parse(argv=None):
                    help="trace the shadow rays (option \"shadows\": the course's earlier renderer, dead code at HEAD; "
                         "a separate report, never the HEAD-parity headline): rays = camera + shadow rays")
     p.add_argument("--no-secondary", action="store_true", help="N>1: skip the secondary frames-mode measurement")
+    p.add_argument("--camera-orbit", type=int, default=60, metavar="POSES",
+                   help="N=1: also time frames with a new camera pose every frame (crt_hip_scene_set_camera; the pose "
+                        "swings around the scene's centre over POSES frames), reported beside the fixed-camera line "
+                        "as config.camera_orbit; 0 skips it")
     p.add_argument("--event-every", type=int, default=5,
                    help="bracket every k-th render of the timed region with HIP events (kernel time sample; "
                         "an event pair between two renders costs ~7 us of a ~165 us C2 step)")
@@ -572,6 +576,51 @@ def main():
                             "sets of lists, crt_kernel_common.h kBinSets); frame_ms_one_at_a_time: a host sync after every frame; bins_ms = the "
                             "binning alone (HIP events, 50 frames); bins off = the BVH walk for every camera ray"}
 
+    # moving camera: a new pose before every frame, frames back to back
+    # (the binning of each frame runs with its own pose; frames in flight keep
+    # theirs), then the last orbit frame against a blocking render of its pose
+    orbit = None
+    if mode == "single" and a.camera_orbit > 0 and "scene" in cfg and not a.shadows:
+        from crt_amd.camera import orbit_poses
+        fov = float(scene.a["cam_fov"][0])
+        cams = [N.CameraDesc(N.Vec3(*[float(v) for v in loc]), (N.C.c_float * 9)(*[float(v) for v in rot]), W, H, fov)
+                for loc, rot in orbit_poses(scene.a, a.camera_orbit)]
+        home = N.CameraDesc(N.Vec3(*[float(v) for v in scene.a["cam_loc"]]),
+                            (N.C.c_float * 9)(*[float(v) for v in scene.a["cam_rot"]]), W, H, fov)
+        moves0 = gpu.info()["view_rebuilds"]
+
+        def orbit_step(k):
+            gpu.set_camera_desc(cams[k % len(cams)])
+            gpu.render_device(settings, frame.data_ptr(), sptr)
+
+        for k in range(a.warmup):
+            orbit_step(k)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(a.steps):
+            orbit_step(k)
+        torch.cuda.synchronize()
+        o_el = time.perf_counter() - t0
+        o_ms = o_el / a.steps * 1e3
+        o_check = None
+        if a.check:
+            o_last = frame.clone()
+            gpu.set_camera_desc(cams[(a.steps - 1) % len(cams)])
+            o_want = gpu.render(settings)
+            o_check = ("bit-identical" if np.array_equal(o_last.view(H, W, 3).cpu().numpy().view(np.uint32),
+                                                         o_want.view(np.uint32)) else "DIFFERS")
+        gpu.set_camera_desc(home)
+        orbit = {"poses": len(cams), "frames": a.steps, "ms_per_step": round(o_ms, 5),
+                 "value": round(npx / (o_ms * 1e-3) / 1e6, 3), "unit": "Mrays/s (camera rays: one per pixel)",
+                 "vs_fixed_camera": round(o_ms / (elapsed / a.steps * 1e3), 4),
+                 "view_rebuilds": gpu.info()["view_rebuilds"] - moves0, "check": o_check,
+                 "note": "crt_hip_scene_set_camera before every frame (yaw 20 deg sin, pitch 6 deg cos around the "
+                         "scene's centre), frames issued back to back into HBM; the camera bins are rebuilt for "
+                         "every pose inside its frame"}
+        if o_check == "DIFFERS":
+            print("check: orbit frame DIFFERS from the blocking render of its pose", flush=True)
+            raise SystemExit(1)
+
     check = None
     if a.check and rank == 0:
         # the reference's blocking call (crt_hip_render, one frame with nothing
@@ -681,6 +730,7 @@ def main():
                        "cold_cli": cold,
                        "check": check, "build_id": build_id,
                        "camera_bins": bins,
+                       "camera_orbit": orbit,
                        "scene_create_ms": {"wall": round(create_wall_ms, 3),
                                            **{k: round(v, 3) for k, v in gpu.info().items()
                                               if k in ("prep_ms", "tree_build_ms", "bvh_ms", "bins_ms", "upload_ms",

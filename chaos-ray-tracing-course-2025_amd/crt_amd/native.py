@@ -130,7 +130,9 @@ class SceneInfo(C.Structure):
                 ("reflections_on", C.c_int32), ("refractions_on", C.c_int32), ("tree_on_device", C.c_int32),
                 ("tree_build_ms", C.c_double), ("prep_ms", C.c_double), ("bvh_ms", C.c_double),
                 ("bins_ms", C.c_double), ("upload_ms", C.c_double), ("create_ms", C.c_double),
-                ("wf_sets", C.c_int32), ("pad0", C.c_int32)]
+                ("wf_sets", C.c_int32), ("pad0", C.c_int32), ("camera_moves", C.c_int64),
+                ("view_rebuilds", C.c_int64), ("records_written", C.c_int64), ("multi_probe", C.c_int32),
+                ("pad1", C.c_int32), ("multi_probe_ms", C.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -185,6 +187,7 @@ EXPORTS = [
     ("crt_hip_scene_create_mask", C.c_int, [C.POINTER(SceneDesc), C.c_uint64, C.c_int, C.POINTER(_P)]),
     ("crt_hip_scene_from_tree_mask", C.c_int, [C.POINTER(TreeSceneDesc), C.c_uint64, C.POINTER(_P)]),
     ("crt_hip_scene_devices", C.c_int, [_P, _P, C.c_int32]),
+    ("crt_multi_probe_verdict", C.c_int, [_P, _P, C.c_int64, C.c_int]),
     ("crt_auto_gpus", C.c_int, [C.POINTER(SceneDesc), C.POINTER(RendererSettings), C.c_int]),
     ("crt_auto_gpus_tree", C.c_int, [C.POINTER(TreeSceneDesc), C.POINTER(RendererSettings), C.c_int]),
     ("crt_hip_scene_create_auto", C.c_int, [C.POINTER(SceneDesc), C.POINTER(RendererSettings), C.c_int, C.POINTER(_P)]),
@@ -192,6 +195,9 @@ EXPORTS = [
                                                C.POINTER(_P)]),
     ("crt_hip_last_replica_ms", C.c_int, [_P, _P, C.c_int32]),
     ("crt_hip_scene_from_tree", C.c_int, [C.POINTER(TreeSceneDesc), C.c_int, C.POINTER(_P)]),
+    ("crt_hip_render_image_tree", C.c_int, [C.POINTER(TreeSceneDesc), C.POINTER(RendererSettings), _P]),
+    ("crt_hip_render_image_tree_stats", C.c_int, [C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    ("crt_hip_render_image_tree_reset", None, []),
     ("crt_host_scene_from_tree", C.c_int, [C.POINTER(TreeSceneDesc), C.POINTER(_P)]),
     ("crt_hip_scene_tree", C.c_int, [_P, _P, _P, _P, _P]),
     ("crt_hip_scene_upload", C.c_int, [_P, C.c_int, C.POINTER(_P)]),
@@ -222,6 +228,10 @@ EXPORTS = [
     ("crt_hip_plan_info", C.c_int, [_P, _P]),
     ("crt_hip_wave_counts", C.c_int, [_P, C.POINTER(WaveCounts)]),
     ("crt_hip_scene_set_option", C.c_int, [_P, C.c_char_p, C.c_int]),
+    ("crt_hip_scene_set_camera", C.c_int, [_P, C.POINTER(CameraDesc)]),
+    ("crt_hip_scene_set_camera_rad", C.c_int, [_P, C.POINTER(Vec3), C.POINTER(C.c_float), C.c_float, C.c_int32,
+                                               C.c_int32]),
+    ("crt_hip_scene_camera", C.c_int, [_P, C.POINTER(CameraDesc), C.POINTER(C.c_float)]),
     ("crt_hip_profile_waves", C.c_int, [_P, C.POINTER(RendererSettings), _P, C.c_int64, _P]),
     ("crt_hip_plan_tiles", C.c_int, [_P, C.POINTER(RendererSettings), _P, _P, C.c_int64]),
     ("crt_renderer_settings_default", None, [C.POINTER(RendererSettings)]),
@@ -387,6 +397,16 @@ class TreeScene:
         self._desc.width, self._desc.height = width, height
         return self
 
+    def set_camera(self, location=None, rotation=None, fov_radians=None) -> "TreeScene":
+        """The reference Camera's transform and stored m_fov_radians."""
+        if location is not None:
+            self._desc.camera_location = Vec3(*(float(x) for x in location))
+        if rotation is not None:
+            self._desc.camera_rotation = (C.c_float * 9)(*(float(x) for x in np.ravel(rotation)))
+        if fov_radians is not None:
+            self._desc.fov_radians = float(fov_radians)
+        return self
+
     def tree_desc_ptr(self):
         return C.pointer(self._desc)
 
@@ -529,6 +549,37 @@ class HipScene:
         out = np.zeros(n, np.float64)
         _check(min(int(lib().crt_hip_last_replica_ms(self._h, out.ctypes.data, n)), 0))
         return [float(x) for x in out]
+
+    def set_camera(self, location=None, rotation=None, fov_degrees=None, width=None, height=None) -> "HipScene":
+        """A new camera for the next frames (crt_hip_scene_set_camera); omitted
+        fields keep the current camera's."""
+        cur = CameraDesc()
+        _check(lib().crt_hip_scene_camera(self._h, C.byref(cur), None))
+        loc = location if location is not None else (cur.location.x, cur.location.y, cur.location.z)
+        rot = rotation if rotation is not None else tuple(cur.rotation)
+        cam = CameraDesc(Vec3(*[float(v) for v in loc]), (C.c_float * 9)(*[float(v) for v in np.ravel(rot)]),
+                         int(width if width is not None else cur.width), int(height if height is not None else cur.height),
+                         float(fov_degrees if fov_degrees is not None else cur.fov_degrees))
+        _check(lib().crt_hip_scene_set_camera(self._h, C.byref(cam)))
+        return self
+
+    def set_camera_desc(self, cam: CameraDesc) -> None:
+        """crt_hip_scene_set_camera with a prepared CameraDesc (no read-back of the current camera)."""
+        _check(lib().crt_hip_scene_set_camera(self._h, C.byref(cam)))
+
+    def set_camera_rad(self, location, rotation, fov_radians: float, width: int, height: int) -> "HipScene":
+        """Same with the reference Camera's stored m_fov_radians (crt_hip_scene_set_camera_rad)."""
+        rot = (C.c_float * 9)(*[float(v) for v in np.ravel(rotation)])
+        _check(lib().crt_hip_scene_set_camera_rad(self._h, C.byref(Vec3(*[float(v) for v in location])), rot,
+                                                  float(fov_radians), int(width), int(height)))
+        return self
+
+    def camera(self) -> dict:
+        cur = CameraDesc()
+        fov = C.c_float()
+        _check(lib().crt_hip_scene_camera(self._h, C.byref(cur), C.byref(fov)))
+        return {"location": (cur.location.x, cur.location.y, cur.location.z), "rotation": tuple(cur.rotation),
+                "width": cur.width, "height": cur.height, "fov_radians": fov.value}
 
     def set_option(self, name: str, value: int) -> "HipScene":
         """Walk selection (crt_hip_scene_set_option): traversal / secondary / wavefront / trace_walk."""
@@ -711,6 +762,23 @@ class HipScene:
             self.close()
         except Exception:
             pass
+
+
+def render_image_tree(tree_scene: "TreeScene", settings: RendererSettings | None = None) -> np.ndarray:
+    """crt::render_image's body for the reference's built Scene
+    (crt_hip_render_image_tree: cached device scenes, camera moves in place):
+    float32 [H, W, 3], top row first."""
+    st = settings or RendererSettings.default()
+    d = tree_scene.tree_desc_ptr().contents
+    out = np.empty((d.height, d.width, 3), np.float32)
+    _check(lib().crt_hip_render_image_tree(tree_scene.tree_desc_ptr(), C.byref(st), out.ctypes.data))
+    return out
+
+
+def render_image_tree_stats() -> dict:
+    c, m, r = C.c_int64(), C.c_int64(), C.c_int64()
+    _check(lib().crt_hip_render_image_tree_stats(C.byref(c), C.byref(m), C.byref(r)))
+    return {"creates": c.value, "camera_moves": m.value, "reuses": r.value}
 
 
 def shard_plan(width: int, height: int, bucket_size: int, shard: int, shard_count: int) -> np.ndarray:

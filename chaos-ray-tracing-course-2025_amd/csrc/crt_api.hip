@@ -382,6 +382,9 @@ int crt_hip_scene_info(const crt_hip_scene *sc, crt_scene_info *out) {
     *out = sc->info;
     out->wf_sets = 0;
     for (const WfSet &w : sc->wf.set) out->wf_sets += w.nodes ? 1 : 0;
+    out->camera_moves = sc->camera_moves;
+    out->view_rebuilds = sc->view_rebuilds;
+    out->records_written = sc->records_written;
     return CRT_OK;
 }
 
@@ -813,6 +816,126 @@ static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
         return set_error(CRT_E_INVALID, "unknown option: " + k);
     }
     /* tile plans depend on the walk (tile splitting): rebuild on next use */
+    return CRT_OK;
+}
+
+/* ---- the camera (crt_hip_scene_set_camera) ---- */
+
+namespace {
+
+/* Device buffers and plans derived from the view, rebuilt with the device
+ * drained: the resolution changed, the camera bins must be built or dropped
+ * for the new camera, or the compact shards' live mask (a function of the
+ * camera) is in use. */
+int rebuild_view(crt_hip_scene *sc, const DCamera &c, bool resized, bool bins_ok, bool primary) {
+    HIP_TRY(hipDeviceSynchronize());
+    sc->ds.cam = c;
+    if (resized) {
+        sc->info.width = c.width;
+        sc->info.height = c.height;
+        sc->calib.clear();   /* per 8x8 tile of the old frame */
+        sc->calib_walk = -1;
+        sc->calib_deferred_walk = -1;
+        if (!sc->ref_children.empty())
+            sc->tile_work = tile_work_estimate_of(c, sc->ref_bounds, sc->ref_children, sc->ref_leaf_off,
+                                                  (c.width + 7) / 8, (c.height + 7) / 8);
+        else
+            sc->tile_work.clear();
+    }
+    sc->live_mask.clear();
+    for (auto &kv : sc->compact_unpack) (void)hipFree(kv.second.first);
+    sc->compact_unpack.clear();
+    if (resized) {
+        for (auto &kv : sc->unpack_plans) (void)hipFree(kv.second.first);
+        sc->unpack_plans.clear();
+    }
+    free_plans(sc);   /* full frame, shards, compact shards; wavefront sizes and graphs */
+    if (sc->bins.tpl && (resized || (sc->ds.bins != nullptr) != bins_ok)) {
+        bins_free_view(sc);
+        int rc;
+        if (bins_ok && (rc = bins_view(sc)) != CRT_OK) return rc;
+    } else if (sc->ds.bins) {
+        (void)bin_camera_of(c, sc->prune_origin_max, sc->bins.cam);
+    }
+    int64_t px = 0;
+    const std::vector<DBucket> all = shard_buckets(c.width, c.height, sc->info.bucket_size, 0, 1, &px);
+    sc->grid_empty = all.empty();
+    if (resized && primary) {
+        const size_t bytes = (size_t)c.width * c.height * 3 * sizeof(float);
+        if (sc->d_out) (void)hipFree(sc->d_out);
+        sc->d_out = nullptr;
+        HIP_TRY(hipMalloc(&sc->d_out, bytes));
+        if (sc->h_stage) (void)hipHostFree(sc->h_stage);
+        sc->h_stage = nullptr;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&sc->h_stage), bytes, hipHostMallocDefault));
+    }
+    return make_tile_plan(sc, all, true, sc->full);
+}
+
+/* One replica (primary: the handle's first, which owns the output image). */
+int set_camera_one(crt_hip_scene *sc, const DCamera &c, float fov_radians, bool primary) {
+    HIP_TRY(hipSetDevice(sc->device));
+    if (std::memcmp(&sc->ds.cam, &c, sizeof c) == 0 && sc->fov_radians == fov_radians) return CRT_OK;
+    const bool resized = c.width != sc->ds.cam.width || c.height != sc->ds.cam.height;
+    BinCamera bc;
+    const bool bins_ok = sc->bins.tpl && bin_camera_of(c, sc->prune_origin_max, bc);
+    sc->fov_radians = fov_radians;
+    sc->camera_fast = camera_rays_fast(c, sc->ds.planes_ok != 0);
+    ++sc->camera_moves;
+    if (resized || (sc->bins.tpl && (sc->ds.bins != nullptr) != bins_ok) || !sc->live_mask.empty() ||
+        !sc->compact_unpack.empty()) {
+        ++sc->view_rebuilds;
+        return rebuild_view(sc, c, resized, bins_ok, primary);
+    }
+    /* the camera alone: frames in flight keep their device record and their
+     * binning's camera (both taken by value when a frame is issued); the next
+     * frames take these */
+    sc->ds.cam = c;
+    if (sc->ds.bins) sc->bins.cam = bc;
+    if (!sc->wf.recs.empty() || !sc->wf.graphs.empty()) {   /* level sizes are the old camera's rays */
+        wf_graphs_clear(sc->wf);
+        sc->wf.recs.clear();
+    }
+    return CRT_OK;
+}
+
+int set_camera_all(crt_hip_scene *sc, const crt_vec3 *location, const float *rotation, float fov_radians,
+                   int32_t width, int32_t height) {
+    if (!sc || !location || !rotation) return set_error(CRT_E_INVALID, "null argument");
+    if (width <= 0 || height <= 0) return set_error(CRT_E_INVALID, "image width/height must be positive");
+    const float loc[3] = {location->x, location->y, location->z};
+    DCamera c{};
+    if (!make_camera(loc, rotation, fov_radians, width, height, c))
+        return set_error(CRT_E_INVALID, "bad camera");
+    int rc = set_camera_one(sc, c, fov_radians, true);
+    for (size_t i = 0; rc == CRT_OK && i < sc->replicas.size(); ++i) rc = set_camera_one(sc->replicas[i], c, fov_radians, false);
+    HIP_TRY(hipSetDevice(sc->device));
+    return rc;
+}
+
+}  // namespace
+
+int crt_hip_scene_set_camera(crt_hip_scene *sc, const crt_camera_desc *camera) {
+    if (!sc || !camera) return set_error(CRT_E_INVALID, "null argument");
+    return set_camera_all(sc, &camera->location, camera->rotation, fov_degrees_to_radians(camera->fov_degrees),
+                          camera->width, camera->height);
+}
+
+int crt_hip_scene_set_camera_rad(crt_hip_scene *sc, const crt_vec3 *location, const float *rotation,
+                                 float fov_radians, int32_t width, int32_t height) {
+    return set_camera_all(sc, location, rotation, fov_radians, width, height);
+}
+
+int crt_hip_scene_camera(const crt_hip_scene *sc, crt_camera_desc *camera, float *fov_radians) {
+    if (!sc) return set_error(CRT_E_INVALID, "null argument");
+    if (camera) {
+        camera->location = crt_vec3{sc->ds.cam.loc[0], sc->ds.cam.loc[1], sc->ds.cam.loc[2]};
+        std::memcpy(camera->rotation, sc->ds.cam.rot, sizeof camera->rotation);
+        camera->width = sc->ds.cam.width;
+        camera->height = sc->ds.cam.height;
+        camera->fov_degrees = sc->fov_radians * 180.0f / 3.14159265358979323846f;
+    }
+    if (fov_radians) *fov_radians = sc->fov_radians;
     return CRT_OK;
 }
 

@@ -772,28 +772,53 @@ __global__ void k_warm_bins() {}
 
 /* ---- host side ---- */
 
-void bins_free(crt_hip_scene *sc) {
+/* The buffers of the current camera view (all but the per-triangle ones);
+ * the scene then walks without bins until bins_view builds them again. */
+void bins_free_view(crt_hip_scene *sc) {
     BinsDev &b = sc->bins;
     if (b.stream) (void)hipStreamSynchronize(b.stream);
     for (void *p : b.allocs) (void)hipFree(p);
+    b.allocs.clear();
     for (int i = 0; i < kBinSets; ++i) {
         if (b.bdone[i]) (void)hipEventDestroy(b.bdone[i]);
         if (b.rdone[i]) (void)hipEventDestroy(b.rdone[i]);
+        b.bdone[i] = b.rdone[i] = nullptr;
     }
     if (b.stream) (void)hipStreamDestroy(b.stream);
-    b = BinsDev{};
+    b.stream = nullptr;
+    b.cam = BinCamera{};
+    b.tx = b.ncell = b.cap_shard = b.long_waves = b.sort_blocks = b.pair_blocks = 0;
+    b.cnt = nullptr;
+    b.keys = nullptr;
+    b.every = b.nonempty = b.bigl = nullptr;
+    b.hdr = nullptr;
+    b.frame = 0;
+    b.caps = BinsCaps{};
+    b.recs = nullptr;
+    b.rec_cap = 0;
+    b.off = b.len = nullptr;
+    b.count.clear();
+    b.records = 0;
     sc->ds.bins = nullptr;
     sc->ds.bin_off = nullptr;
     sc->ds.bin_len = nullptr;
+    sc->ds.bin_tx = 0;
+}
+
+void bins_free(crt_hip_scene *sc) {
+    bins_free_view(sc);
+    BinsDev &b = sc->bins;
+    for (void *p : b.keep) (void)hipFree(p);
+    b = BinsDev{};
 }
 
 namespace {
 
 template <class T>
-int bins_alloc(crt_hip_scene *sc, T **p, size_t n, bool zero = false) {
+int bins_alloc(crt_hip_scene *sc, T **p, size_t n, bool zero = false, bool keep = false) {
     void *q = nullptr;
     HIP_TRY(hipMalloc(&q, std::max<size_t>(1, n) * sizeof(T)));
-    sc->bins.allocs.push_back(q);
+    (keep ? sc->bins.keep : sc->bins.allocs).push_back(q);
     if (zero) HIP_TRY(hipMemset(q, 0, std::max<size_t>(1, n) * sizeof(T)));
     sc->info.device_bytes += (int64_t)(n * sizeof(T));
     *p = static_cast<T *>(q);
@@ -848,23 +873,40 @@ int bins_dbg_arm(crt_hip_scene *sc, const ShardPlan &plan) {
  * bins. */
 int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
     BinsDev &b = sc->bins;
-    BinCamera cam;
-    if (!bin_camera(hs, cam)) return CRT_OK;
+    if (hs.tri_attr.empty()) return CRT_OK;
     const auto t0 = std::chrono::steady_clock::now();
-    b.cam = cam;
+    /* per triangle, kept for every view: the records' static parts and the
+     * projection's scratch */
     b.nt = (int)hs.tri_attr.size();
-    b.tx = cam.tx;
-    b.ncell = cam.tx * cam.ty;
-    b.cap_shard = (b.ncell + kBinShards - 1) / kBinShards;
     std::vector<CamCand> tpl;
     bin_templates(hs, tpl);
     int rc;
-    if ((rc = bins_alloc(sc, &b.tpl, tpl.size())) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.tpl, tpl.size(), false, true)) != CRT_OK) return rc;
     HIP_TRY(hipMemcpy(b.tpl, tpl.data(), tpl.size() * sizeof(CamCand), hipMemcpyHostToDevice));
-    if ((rc = bins_alloc(sc, &b.items, (size_t)b.nt)) != CRT_OK) return rc;
-    if ((rc = bins_alloc(sc, &b.tpref, (size_t)((b.nt + kProjTris - 1) / kProjTris) * kProjTris)) != CRT_OK) return rc;
-    if ((rc = bins_alloc(sc, &b.gsum, (size_t)((b.nt + kProjTris - 1) / kProjTris))) != CRT_OK) return rc;
-    if ((rc = bins_alloc(sc, &b.rem, (size_t)((b.nt + kProjTris - 1) / kProjTris))) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.items, (size_t)b.nt, false, true)) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.tpref, (size_t)((b.nt + kProjTris - 1) / kProjTris) * kProjTris, false, true)) != CRT_OK)
+        return rc;
+    if ((rc = bins_alloc(sc, &b.gsum, (size_t)((b.nt + kProjTris - 1) / kProjTris), false, true)) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.rem, (size_t)((b.nt + kProjTris - 1) / kProjTris), false, true)) != CRT_OK) return rc;
+    rc = bins_view(sc);
+    b.setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+/* The buffers of the scene's current camera and resolution (sc->ds.cam),
+ * sized by one projection pass of that camera; leaves sc->ds.bins null when
+ * this view takes no bins (bin_camera_of fails: the camera outside the hull
+ * margins' origin bound, a singular rotation; or the lists would be too long). */
+int bins_view(crt_hip_scene *sc) {
+    BinsDev &b = sc->bins;
+    if (!b.tpl) return CRT_OK;
+    BinCamera cam;
+    if (!bin_camera_of(sc->ds.cam, sc->prune_origin_max, cam)) return CRT_OK;
+    b.cam = cam;
+    b.tx = cam.tx;
+    b.ncell = cam.tx * cam.ty;
+    b.cap_shard = (b.ncell + kBinShards - 1) / kBinShards;
+    int rc;
     b.pair_blocks = 256;   /* the sizing pass's grid; resized from its queued pairs below */
     if ((rc = bins_alloc(sc, &b.cnt, (size_t)kBinSets * b.ncell * kCntStride, true)) != CRT_OK) return rc;   /* per set */
     if ((rc = bins_alloc(sc, &b.keys, (size_t)b.ncell * kBinCellCap)) != CRT_OK) return rc;   /* 64-bit keys */
@@ -909,7 +951,7 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
     for (int c = 0; c < b.ncell; ++c) over = over || b.count[(size_t)c] < 0;
     if (n_every > kBinMaxEverywhere || total > kBinMeanCap * b.ncell || total >= INT32_MAX / 4 ||
         (over && !sc->ds.bnodes)) {
-        bins_free(sc);   /* the scene walks the BVH (or the kd tree) */
+        bins_free_view(sc);   /* the scene walks the BVH (or the kd tree) */
         return CRT_OK;
     }
     /* each shard's records in a region of its own, sized from the pass with
@@ -924,7 +966,7 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
     }
     b.rec_cap = (int32_t)base;
     if ((int64_t)kBinSets * base >= INT32_MAX) {   /* record offsets are int32 */
-        bins_free(sc);
+        bins_free_view(sc);
         return CRT_OK;
     }
     if ((rc = bins_alloc(sc, &b.recs, (size_t)kBinSets * b.rec_cap)) != CRT_OK) return rc;   /* per set */
@@ -947,7 +989,6 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
     const int64_t waves = b.long_waves + (slots + kSortSlots - 1) / kSortSlots;
     b.sort_blocks = (int)((waves + kSortWaves - 1) / kSortWaves);
     b.records = total;
-    b.setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     sc->ds.bins = b.recs;
     sc->ds.bin_off = b.off;
     sc->ds.bin_len = b.len;

@@ -50,6 +50,65 @@ void enable_peers(int a, int b) {
     (void)hipGetLastError();   /* hipErrorPeerAccessAlreadyEnabled is not an error here */
 }
 
+/* The multi-device probe's verdict (crt_multi_probe_verdict). */
+int probe_verdict(const float *multi, const float *single, int64_t n, int render_status) {
+    if (render_status != CRT_OK) return 2;
+    if (n > 0 && std::memcmp(multi, single, (size_t)n * sizeof(float)) != 0) return 1;
+    return 0;
+}
+
+/* A handle over >= 2 distinct devices renders a 64x36 probe frame of its
+ * scene through every replica (shards dealt over the devices, peer copies
+ * into device 0, cross-device event waits: the path no single-GPU test
+ * exercises) and through device 0 alone, before its first real frame; on any
+ * error or a differing bit the replicas go and the handle renders on one GPU
+ * (crt_scene_info.multi_probe = -1 / -2, the reason in crt_hip_last_error()).
+ * CRT_MULTI_PROBE=0 skips it, =force runs it also over repeated devices;
+ * CRT_MULTI_PROBE_INJECT=1 flips one bit of the multi-device image (tests). */
+int multi_probe(crt_hip_scene *sc) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const DCamera full = sc->ds.cam;
+    const float fov = sc->fov_radians;
+    const crt_vec3 loc{full.loc[0], full.loc[1], full.loc[2]};
+    const int pw = std::min(64, full.width), ph = std::min(36, full.height);
+    crt_renderer_settings st;
+    crt_renderer_settings_default(&st);
+    std::vector<float> multi((size_t)pw * ph * 3, 0.f), single((size_t)pw * ph * 3, 0.f);
+    int rc = crt_hip_scene_set_camera_rad(sc, &loc, full.rot, fov, pw, ph);
+    if (rc == CRT_OK) rc = crt_hip_render(sc, &st, multi.data(), nullptr);
+    if (rc == CRT_OK) {
+        std::vector<crt_hip_scene *> reps;
+        reps.swap(sc->replicas);   /* device 0 alone */
+        rc = crt_hip_render(sc, &st, single.data(), nullptr);
+        sc->replicas.swap(reps);
+    }
+    std::string why = rc != CRT_OK ? std::string(crt_hip_last_error()) : std::string();
+    if (rc == CRT_OK) {
+        if (const char *e = std::getenv("CRT_MULTI_PROBE_INJECT"))
+            if (std::atoi(e) == 1 && !multi.empty()) reinterpret_cast<uint32_t *>(multi.data())[0] ^= 1u;
+    }
+    const int verdict = probe_verdict(multi.data(), single.data(), (int64_t)multi.size(), rc);
+    /* back to the scene's own camera, then drop the replicas if the probe failed */
+    (void)hipGetLastError();
+    const int rc2 = crt_hip_scene_set_camera_rad(sc, &loc, full.rot, fov, full.width, full.height);
+    sc->info.multi_probe_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (verdict == 0 && rc2 == CRT_OK) {
+        sc->info.multi_probe = 1;
+        return CRT_OK;
+    }
+    multi_free(sc);
+    HIP_TRY(hipSetDevice(sc->device));
+    if (rc2 != CRT_OK) {   /* one GPU: its camera back, plans and buffers of its size */
+        const int rc3 = crt_hip_scene_set_camera_rad(sc, &loc, full.rot, fov, full.width, full.height);
+        if (rc3 != CRT_OK) return rc3;
+    }
+    sc->info.multi_probe = verdict == 1 ? -1 : -2;
+    set_error(CRT_E_STATE, verdict == 1 ? "multi-GPU probe: the replicas' 64x36 frame differs from device 0's; "
+                                          "rendering on one GPU"
+                                        : "multi-GPU probe failed (" + why + "); rendering on one GPU");
+    return CRT_OK;
+}
+
 /* One prepared host scene uploaded to every listed device. */
 int upload_on(const HostScene &hs, const int32_t *devices, int32_t count, crt_hip_scene **out) {
     *out = nullptr;
@@ -70,6 +129,14 @@ int upload_on(const HostScene &hs, const int32_t *devices, int32_t count, crt_hi
     if (count > 1) {
         HIP_TRY(hipSetDevice(devices[0]));
         HIP_TRY(hipEventCreateWithFlags(&sc->mg_done, hipEventDisableTiming));   /* "gather unpacked" */
+        bool distinct = false;
+        for (int32_t i = 1; i < count; ++i) distinct = distinct || devices[i] != devices[0];
+        const char *e = std::getenv("CRT_MULTI_PROBE");
+        const bool force = e && std::strcmp(e, "force") == 0, off = e && std::strcmp(e, "0") == 0;
+        if (!off && (distinct || force) && !sc->grid_empty) {
+            const int rc2 = multi_probe(sc.get());
+            if (rc2 != CRT_OK) return rc2;
+        }
     }
     sc->info.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     *out = sc.release();
@@ -258,6 +325,11 @@ void multi_free(crt_hip_scene *sc) {
 }  // namespace crt_amd
 
 extern "C" {
+
+int crt_multi_probe_verdict(const float *multi, const float *single, int64_t n, int render_status) {
+    if (n < 0 || (n > 0 && (!multi || !single))) return set_error(CRT_E_INVALID, "bad argument");
+    return probe_verdict(multi, single, n, render_status);
+}
 
 int crt_hip_device_count(void) {
     int n = 0;

@@ -74,7 +74,8 @@ struct BinsDev {
     int sort_blocks = 0;                  /* k_bins_sort blocks */
     int64_t records = 0;                  /* records of the sizing pass */
     double setup_ms = 0.0;
-    std::vector<void *> allocs;
+    std::vector<void *> allocs;           /* the view's buffers (bins_free_view) */
+    std::vector<void *> keep;             /* per triangle: templates, items and the projection's scratch */
     /* frames pipeline: frame k's binning runs on `stream` (its kernels in
      * order) while frame k - 1 renders; the lists the render reads come in
      * kBinSets sets taken in turn, bdone[p] = set p's lists built, rdone[p] =
@@ -211,6 +212,8 @@ struct crt_hip_scene {
     int shadows = 0;               /* option "shadows": trace the shadow rays (k_render_tiles<..., SHADOW>) */
     int trace_walk = 1;            /* crt_hip_trace_batch: 0 reference-order walk, 1 pruned per-lane walk */
     float fov_radians = 0.f;       /* the camera's (ds.cam: the rest) */
+    int64_t camera_moves = 0;      /* crt_hip_scene_set_camera calls that changed the camera */
+    int64_t view_rebuilds = 0;     /* ... of them that rebuilt plans and buffers with the device drained */
     float prune_origin_max = 0.f;  /* the hull margins' origin bound (bins need the camera inside it) */
     bool camera_fast = false;      /* every camera ray takes the fast box path (camera_rays_fast) */
     /* estimate plan (no calibration): a tile is split into 4x4 (2x2) pixel
@@ -302,6 +305,8 @@ int scene_upload_buffers(crt_hip_scene *sc, const HostScene &hs);
 int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **out);
 /* crt_bins.hip: camera bins built on the device by every camera frame */
 int bins_setup(crt_hip_scene *sc, const HostScene &hs);
+int bins_view(crt_hip_scene *sc);
+void bins_free_view(crt_hip_scene *sc);
 int bins_plan(crt_hip_scene *sc, ShardPlan &plan);
 int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *par_out);
 void bins_free(crt_hip_scene *sc);

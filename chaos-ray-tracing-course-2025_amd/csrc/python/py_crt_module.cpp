@@ -18,16 +18,71 @@
 #include <Python.h>
 #include <structmember.h>
 
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../../include/crt_hip.h"
 
-/* the device scene of the last rendered dict (render_scene_from_dict) */
+/* the device scene of the last rendered dict (render_scene_from_dict), keyed
+ * by everything but the camera (geometry, materials, textures with their
+ * texels, lights, background, flags): a dict that differs only in its camera
+ * moves the kept scene's camera instead of uploading the scene again */
 static std::mutex g_scene_mu;
 static crt_hip_scene *g_scene = nullptr;
 static std::string g_scene_key;
+static long long g_creates = 0, g_camera_moves = 0, g_reuses = 0;
+
+template <class T>
+static void key_put(std::string &k, const T *p, size_t n) {
+    const uint64_t nb = (uint64_t)(n * sizeof(T));
+    k.append(reinterpret_cast<const char *>(&nb), sizeof nb);
+    if (p && n) k.append(reinterpret_cast<const char *>(p), n * sizeof(T));
+}
+
+/* The scene without its camera, as bytes. */
+static std::string scene_key(const crt_scene_desc *d, const char *root, size_t rn) {
+    std::string k(root, rn);
+    k.push_back('\0');
+    key_put(k, &d->background_color, 1);
+    const int32_t flags[4] = {d->bucket_size, d->gi_on, d->reflections_on, d->refractions_on};
+    key_put(k, flags, 4);
+    key_put(k, &d->mesh_count, 1);
+    for (int32_t i = 0; i < d->mesh_count; ++i) {
+        const crt_mesh_desc &m = d->meshes[i];
+        key_put(k, m.positions, (size_t)m.vertex_count * 3);
+        key_put(k, m.uvs, m.uvs ? (size_t)m.vertex_count * 3 : 0);
+        key_put(k, m.indices, (size_t)m.index_count);
+        key_put(k, &m.material_index, 1);
+    }
+    key_put(k, d->materials, (size_t)d->material_count);
+    key_put(k, d->lights, (size_t)d->light_count);
+    key_put(k, &d->texture_count, 1);
+    for (int32_t i = 0; i < d->texture_count; ++i) {
+        const crt_texture_desc &t = d->textures[i];
+        const float f[7] = {t.color0.x, t.color0.y, t.color0.z, t.color1.x, t.color1.y, t.color1.z, t.scalar};
+        const int32_t ti[3] = {t.type, t.bitmap_width, t.bitmap_height};
+        key_put(k, ti, 3);
+        key_put(k, f, 7);
+        /* bitmap textures are read from disk by every parse (as the reference
+         * reloads them every call): their decoded texels are part of the key,
+         * so an edited texture file never reuses the kept device scene */
+        if (t.type == CRT_TEXTURE_BITMAP && t.bitmap_rgb)
+            key_put(k, t.bitmap_rgb, (size_t)t.bitmap_width * t.bitmap_height * 3);
+    }
+    return k;
+}
+
+static bool same_camera(const crt_hip_scene *sc, const crt_camera_desc &c) {
+    crt_camera_desc cur;
+    float fov = 0.f;
+    if (crt_hip_scene_camera(sc, &cur, &fov) != CRT_OK) return false;
+    const float want = c.fov_degrees * 3.14159265358979323846f / 180.0f;   /* crt_camera.h:20 */
+    return cur.location.x == c.location.x && cur.location.y == c.location.y && cur.location.z == c.location.z &&
+           std::memcmp(cur.rotation, c.rotation, sizeof cur.rotation) == 0 && cur.width == c.width &&
+           cur.height == c.height && fov == want;
+}
 
 static PyStructSequence_Field settings_fields[] = {
     {(char *)"max_ray_depth", (char *)"Maximum recursion depth for rays"},
@@ -82,9 +137,6 @@ static PyObject *render_scene_from_dict(PyObject *, PyObject *args) {
         Py_DECREF(text);
         return nullptr;
     }
-    std::string key(root, (size_t)rn);
-    key.push_back('\0');
-    key.append(utf8, (size_t)n);
     crt_scene_file *sf = nullptr;
     const int prc = crt_scene_file_parse(utf8, (size_t)n, root, &sf);
     Py_DECREF(text);
@@ -99,37 +151,33 @@ static PyObject *render_scene_from_dict(PyObject *, PyObject *args) {
     }
     const crt_scene_desc *desc = crt_scene_file_desc(sf);
     const int W = desc->camera.width, H = desc->camera.height;
-    /* bitmap textures are read from disk by every parse (as the reference
-     * reloads them every call): their decoded texels are part of the key, so an
-     * edited texture file never reuses the kept device scene */
-    for (int32_t i = 0; i < desc->texture_count; ++i) {
-        const crt_texture_desc &t = desc->textures[i];
-        if (t.type != CRT_TEXTURE_BITMAP || !t.bitmap_rgb) continue;
-        uint64_t hsh = 1469598103934665603ull;   /* FNV-1a over the texel bytes */
-        const unsigned char *b = reinterpret_cast<const unsigned char *>(t.bitmap_rgb);
-        const size_t nb = (size_t)t.bitmap_width * t.bitmap_height * 3 * sizeof(float);
-        for (size_t k = 0; k < nb; ++k) hsh = (hsh ^ b[k]) * 1099511628211ull;
-        key.push_back('\0');
-        key.append(std::to_string(i) + ":" + std::to_string(t.bitmap_width) + "x" + std::to_string(t.bitmap_height) +
-                   ":" + std::to_string(hsh));
-    }
     std::vector<float> img((size_t)W * H * 3);
     int rc;
     std::string err;
     Py_BEGIN_ALLOW_THREADS
     {
         /* the device scene of the last dict is kept (a Blender session
-         * re-renders the same scene with other settings): same JSON text and
-         * asset root -> no new upload, and its measured tile plan stays */
+         * re-renders the same scene with other settings, or with the camera
+         * moved from frame to frame): the same scene without its camera and
+         * the same asset root -> no new upload, the camera moved in place, and
+         * the measured tile plan stays */
+        const std::string key = scene_key(desc, root, (size_t)rn);
         std::lock_guard<std::mutex> lock(g_scene_mu);
         if (!g_scene || g_scene_key != key) {
             crt_hip_scene_destroy(g_scene);
             g_scene = nullptr;
             g_scene_key.clear();
             rc = crt_hip_scene_create_auto(desc, &st, CRT_SCENE_TREE_AUTO, &g_scene);   /* GPUs the frame pays for */
-            if (rc == CRT_OK) g_scene_key = key;
+            if (rc == CRT_OK) {
+                g_scene_key = key;
+                ++g_creates;
+            }
+        } else if (!same_camera(g_scene, desc->camera)) {
+            rc = crt_hip_scene_set_camera(g_scene, &desc->camera);
+            ++g_camera_moves;
         } else {
             rc = CRT_OK;
+            ++g_reuses;
         }
         if (rc == CRT_OK) rc = crt_hip_render(g_scene, &st, img.data(), nullptr);
         if (rc != CRT_OK) {
@@ -160,9 +208,19 @@ static PyObject *render_scene_from_dict(PyObject *, PyObject *args) {
     return list;
 }
 
+/* Diagnostics (not in the reference module): how render_scene_from_dict
+ * treated the calls so far — new device scenes, camera moves of the kept one,
+ * reuses as they were. */
+static PyObject *device_scene_stats(PyObject *, PyObject *) {
+    std::lock_guard<std::mutex> lock(g_scene_mu);
+    return Py_BuildValue("{sLsLsL}", "creates", g_creates, "camera_moves", g_camera_moves, "reuses", g_reuses);
+}
+
 static PyMethodDef methods[] = {
     {"render_scene_from_dict", (PyCFunction)render_scene_from_dict, METH_VARARGS,
      "render_scene_from_dict(scene_dict, asset_root, settings) -> list of (r, g, b, a), bottom row first"},
+    {"_device_scene_stats", (PyCFunction)device_scene_stats, METH_NOARGS,
+     "diagnostics: {creates, camera_moves, reuses} of render_scene_from_dict's kept device scene"},
     {nullptr, nullptr, 0, nullptr}};
 
 static PyModuleDef module_def = {PyModuleDef_HEAD_INIT, "_crt", nullptr, -1, methods};

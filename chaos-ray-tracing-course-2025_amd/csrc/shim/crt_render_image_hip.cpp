@@ -38,7 +38,6 @@
 #include "core/crt_renderer.h"
 #include "core/crt_scene.h"
 #include "crt_hip.h"
-#include "crt_scene_lru.h"
 
 namespace {
 
@@ -170,68 +169,6 @@ void flatten(const crt::Scene &s, Flat &f) {
     d.light_count = (int32_t)f.lights.size();
 }
 
-template <class T>
-bool same_vec(const std::vector<T> &a, const std::vector<T> &b) {
-    return a.size() == b.size() && (a.empty() || std::memcmp(a.data(), b.data(), a.size() * sizeof(T)) == 0);
-}
-
-/* Byte-equality of two flattened scenes, including the arrays the
- * descriptions point to outside the Flat (vertices, bitmap texels). */
-bool same_scene(const Flat &a, const std::vector<float> &a_vertices, const std::vector<std::vector<float>> &a_texels,
-                const Flat &b) {
-    crt_tree_scene_desc x = a.desc, y = b.desc;
-    for (crt_tree_scene_desc *d : {&x, &y}) {
-        d->vertices = nullptr;
-        d->node_bounds = nullptr;
-        d->node_children = nullptr;
-        d->leaf_offsets = nullptr;
-        d->leaf_triangles = nullptr;
-        d->materials = nullptr;
-        d->textures = nullptr;
-        d->lights = nullptr;
-    }
-    if (std::memcmp(&x, &y, sizeof x) != 0) return false;
-    if (!same_vec(a.bounds, b.bounds) || !same_vec(a.children, b.children) || !same_vec(a.offsets, b.offsets))
-        return false;
-    if (a.tris.size() != b.tris.size() ||
-        (!a.tris.empty() && std::memcmp(a.tris.data(), b.tris.data(), a.tris.size() * sizeof(crt_tree_triangle)) != 0))
-        return false;
-    if (a.materials.size() != b.materials.size() || a.lights.size() != b.lights.size() ||
-        a.textures.size() != b.textures.size())
-        return false;
-    if (!a.materials.empty() &&
-        std::memcmp(a.materials.data(), b.materials.data(), a.materials.size() * sizeof(crt_material_desc)) != 0)
-        return false;
-    if (!a.lights.empty() && std::memcmp(a.lights.data(), b.lights.data(), a.lights.size() * sizeof(crt_light_desc)) != 0)
-        return false;
-    if ((size_t)b.desc.vertex_count * 9 != a_vertices.size() ||
-        (!a_vertices.empty() && std::memcmp(a_vertices.data(), b.desc.vertices, a_vertices.size() * sizeof(float)) != 0))
-        return false;
-    for (size_t i = 0; i < a.textures.size(); ++i) {
-        crt_texture_desc p = a.textures[i], q = b.textures[i];
-        p.bitmap_rgb = q.bitmap_rgb = nullptr;
-        if (std::memcmp(&p, &q, sizeof p) != 0) return false;
-        const size_t nt = (size_t)q.bitmap_width * q.bitmap_height * 3;
-        if (b.textures[i].type == CRT_TEXTURE_BITMAP &&
-            (a_texels[i].size() != nt || (nt && std::memcmp(a_texels[i].data(), b.textures[i].bitmap_rgb, nt * 4) != 0)))
-            return false;
-    }
-    return true;
-}
-
-struct Cached {
-    Flat flat;
-    std::vector<float> vertices;                /* copies of the pointed-to arrays */
-    std::vector<std::vector<float>> texels;
-    crt_hip_scene *scene = nullptr;
-    ~Cached() { crt_hip_scene_destroy(scene); }
-};
-
-/* the two most recently rendered scenes (crt_scene_lru.h): a changed Scene
- * replaces the older entry, whose device memory is freed */
-std::mutex g_mu;
-crt_shim::SceneLru<Cached> g_cache(2);
-
 [[noreturn]] void fail(const char *what) {
     throw std::runtime_error(std::string("crt_hip ") + what + ": " + crt_hip_last_error());
 }
@@ -242,35 +179,13 @@ namespace crt {
 
 Image render_image(const Scene &scene, const RendererSettings &settings) {
     Image result{scene.camera.resolution_x(), scene.camera.resolution_y()};
-    std::lock_guard<std::mutex> lock(g_mu);
-    std::unique_ptr<Flat> now(new Flat());
-    flatten(scene, *now);
-    Cached *c = g_cache.find([&](const Cached &e) { return same_scene(e.flat, e.vertices, e.texels, *now); });
-    if (!c) {
-        std::unique_ptr<Cached> fresh(new Cached());
-        /* as many GPUs as the frame pays for (crt_hip_scene_from_tree_auto;
-         * CRT_HIP_GPUS=N sets the count), as render_image spans every hardware
-         * thread (crt_renderer.cpp:176-196); CRT_HIP_DEVICE=K pins one device */
-        const crt_renderer_settings st0{settings.max_ray_depth, settings.diffuse_reflection_ray_count,
-                                        settings.shadow_bias, settings.reflection_bias,
-                                        settings.diffuse_reflection_bias, settings.refraction_bias};
-        const char *dev = std::getenv("CRT_HIP_DEVICE");
-        const int urc = dev ? crt_hip_scene_from_tree(&now->desc, std::atoi(dev), &fresh->scene)
-                            : crt_hip_scene_from_tree_auto(&now->desc, &st0, &fresh->scene);
-        if (urc != CRT_OK) fail("scene upload");
-        const float *vp = now->desc.vertices;
-        fresh->vertices.assign(vp, vp + 9 * now->desc.vertex_count);
-        for (const crt_texture_desc &t : now->textures)
-            fresh->texels.emplace_back(t.bitmap_rgb, t.bitmap_rgb + (t.type == CRT_TEXTURE_BITMAP && t.bitmap_rgb
-                                                                         ? (size_t)t.bitmap_width * t.bitmap_height * 3
-                                                                         : 0));
-        fresh->flat = std::move(*now);
-        c = g_cache.insert(std::move(fresh));
-    }
+    Flat flat;
+    flatten(scene, flat);
     const crt_renderer_settings st{settings.max_ray_depth, settings.diffuse_reflection_ray_count, settings.shadow_bias,
                                    settings.reflection_bias, settings.diffuse_reflection_bias, settings.refraction_bias};
-    if (crt_hip_render(c->scene, &st, reinterpret_cast<float *>(result.buffer.data()), nullptr) != CRT_OK)
-        fail("render");
+    /* the device-scene cache and the render: csrc/shim/crt_shim_core.cpp */
+    if (crt_hip_render_image_tree(&flat.desc, &st, reinterpret_cast<float *>(result.buffer.data())) != CRT_OK)
+        fail("render_image");
     return result;
 }
 

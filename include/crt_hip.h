@@ -145,6 +145,14 @@ typedef struct crt_scene_info {
     int32_t wf_sets;           /* wavefront frame buffer sets holding buffers (1 for a caller that waits for
                                 * each frame; up to 12 for frames issued back to back) */
     int32_t pad0;
+    int64_t camera_moves;      /* crt_hip_scene_set_camera calls that changed the camera */
+    int64_t view_rebuilds;     /* ... of them that rebuilt the view's plans / buffers (new resolution, camera
+                                * bins built or dropped for the new camera) with the device drained */
+    int64_t records_written;   /* device scene records written (one per camera, plus table pointers) */
+    int32_t multi_probe;       /* handles over >= 2 distinct GPUs: 1 the probe frame matched, -1 it differed and
+                                * -2 it failed (the handle then renders on one GPU), 0 not run */
+    int32_t pad1;
+    double  multi_probe_ms;    /* wall time of that probe (two 64x36 frames and two view rebuilds) */
 } crt_scene_info;
 
 typedef struct crt_render_stats {
@@ -270,6 +278,23 @@ int  crt_hip_scene_from_tree(const crt_tree_scene_desc *desc, int device, crt_hi
 /* Host-only part of the same (tree flatten; no GPU). */
 int  crt_host_scene_from_tree(const crt_tree_scene_desc *desc, crt_host_scene **out);
 
+/* crt::render_image (crt_renderer.h:27) for the reference's built Scene, as
+ * the shim (csrc/shim/crt_render_image_hip.cpp) calls it once it has read
+ * the Scene's fields into a crt_tree_scene_desc: the device scenes of the two
+ * most recently rendered scenes stay cached by content (vertices, tree,
+ * materials, textures with their texels, lights, flags); a scene equal to a
+ * cached one but for its camera moves that scene's camera
+ * (crt_hip_scene_set_camera_rad) instead of uploading it again; then the
+ * blocking render into rgb_out (W*H*3 fp32, top row first).  A new scene is
+ * created over crt_auto_gpus_tree GPUs (CRT_HIP_DEVICE=K: device K alone).
+ * Thread-safe (one render at a time).  _stats: calls that created a device
+ * scene, moved a cached scene's camera, reused one as it was; _reset drops
+ * the cache. */
+int  crt_hip_render_image_tree(const crt_tree_scene_desc *desc, const crt_renderer_settings *settings,
+                               float *rgb_out);
+int  crt_hip_render_image_tree_stats(int64_t *creates, int64_t *camera_moves, int64_t *reuses);
+void crt_hip_render_image_tree_reset(void);
+
 /* The scene's tree in the reference's preorder numbering, as
  * crt_host_scene_tree (sizes from crt_hip_scene_info). */
 int  crt_hip_scene_tree(const crt_hip_scene *scene, float *bounds, int32_t *children, int64_t *leaf_offsets,
@@ -313,10 +338,38 @@ int  crt_hip_scene_create_auto(const crt_scene_desc *desc, const crt_renderer_se
                                crt_hip_scene **out);
 int  crt_hip_scene_from_tree_auto(const crt_tree_scene_desc *desc, const crt_renderer_settings *settings,
                                   crt_hip_scene **out);
+/* The multi-GPU probe's decision (run by the create of a handle over >= 2
+ * distinct devices, crt_scene_info.multi_probe): 0 keep the replicas, 1 the
+ * replicas' probe frame differs from device 0's, 2 a probe render failed
+ * (render_status != 0) — both fall back to one GPU.  No GPU needed. */
+int  crt_multi_probe_verdict(const float *multi, const float *single, int64_t n, int render_status);
 /* Replica devices (devices may be NULL); returns the replica count. */
 int  crt_hip_scene_devices(const crt_hip_scene *scene, int32_t *devices, int32_t cap);
 /* Kernel ms of each replica's shard in the last render (blocks until done). */
 int  crt_hip_last_replica_ms(crt_hip_scene *scene, double *ms, int32_t cap);
+
+/* ---- moving the camera ------------------------------------------------
+ * The reference renders whatever camera its Scene holds on every call
+ * (render_image, crt_renderer.cpp:157-199; the Blender add-on hands a new
+ * scene dict per frame, bl_crt_engine.py:12-31).  A device scene keeps its
+ * geometry, trees, BVH, textures and lights and takes a new camera here: the
+ * camera's per-frame constants (float(W)/H, std::tan(fov * 0.5f),
+ * crt_camera.cpp:23,26-27) are recomputed on the host with the reference's
+ * libm, frames already issued keep the camera they were issued with (each
+ * frame reads its own device scene record and its own binning camera), and
+ * the next frames take the new one — no upload, no host wait.  A new
+ * resolution, or a camera for which the camera bins must be built or dropped
+ * (the bins need the camera inside the hull margins' origin bound), rebuilds
+ * the view's tile plan and buffers with the device drained
+ * (crt_scene_info.view_rebuilds).  Every replica of a multi-GPU handle takes
+ * the camera.  set_camera converts fov_degrees as the scene loader does
+ * (crt_camera.h:20: deg * pi / 180 in float); _rad takes the reference
+ * Camera's stored m_fov_radians (crt_tree_scene_desc). */
+int  crt_hip_scene_set_camera(crt_hip_scene *scene, const crt_camera_desc *camera);
+int  crt_hip_scene_set_camera_rad(crt_hip_scene *scene, const crt_vec3 *location, const float *rotation,
+                                  float fov_radians, int32_t width, int32_t height);
+/* The current camera (either pointer may be NULL; fov_degrees = fov_radians * 180 / pi). */
+int  crt_hip_scene_camera(const crt_hip_scene *scene, crt_camera_desc *camera, float *fov_radians);
 
 /* Blocking drop-in for render_image: rgb_out is caller-allocated W*H*3 fp32,
  * row-major, top row first, unclamped (crt_image.h:11-27). */

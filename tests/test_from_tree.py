@@ -105,6 +105,46 @@ def test_render_image_shim(tmp_path):
         assert np.array_equal(bits(got), bits(want)), name
 
 
+@pytest.mark.gpu
+def test_render_image_tree_core(oracle):
+    """The shim's body (csrc/shim/crt_shim_core.cpp, in lib/libcrt_hip.so):
+    crt::render_image on the reference's built Scenes (tests/golden/reftree_*)
+    renders the oracle's bits; the same Scene again reuses its cached device
+    scene; the Scene with only its camera moved moves the cached scene's
+    camera (no new device scene) and renders the moved camera's bits; two
+    other scenes fill the two-entry cache and evict the first."""
+    from crt_amd import native as N
+    from crt_amd.camera import orbit_poses
+    lib = N.lib()
+    lib.crt_hip_render_image_tree_reset()
+    name = "14-01-acceleration-tree__scene1"
+    st = N.RendererSettings.default()
+    sc, ts = tree_scene(name, 240, 135)
+    want = bits(oracle.OracleScene(sc).render(st))
+    s0 = N.render_image_tree_stats()
+    assert np.array_equal(bits(N.render_image_tree(ts, st)), want)
+    assert np.array_equal(bits(N.render_image_tree(ts, st)), want)
+    s1 = N.render_image_tree_stats()
+    assert s1["creates"] - s0["creates"] == 1 and s1["reuses"] - s0["reuses"] == 1
+    fov = np.float32(np.float32(sc.desc().camera.fov_degrees) * np.float32(np.pi)) / np.float32(180.0)
+    for loc, rot in orbit_poses(sc.a, 5)[1:]:
+        sc.set_camera(location=loc, rotation=rot)
+        ts.set_camera(location=loc, rotation=rot, fov_radians=fov)
+        assert np.array_equal(bits(N.render_image_tree(ts, st)), bits(oracle.OracleScene(sc).render(st)))
+    ts.set_resolution(200, 160)
+    sc.set_resolution(200, 160)
+    assert np.array_equal(bits(N.render_image_tree(ts, st)), bits(oracle.OracleScene(sc).render(st)))
+    s2 = N.render_image_tree_stats()
+    assert s2["creates"] == s1["creates"] and s2["camera_moves"] - s1["camera_moves"] == 5
+    for other in [n for n in SCENES if n != name][:2]:
+        sc2, ts2 = tree_scene(other, 160, 90)
+        st2 = N.RendererSettings.default(**({"max_ray_depth": 8} if "refractive" in other else {}))
+        assert np.array_equal(bits(N.render_image_tree(ts2, st2)), bits(oracle.OracleScene(sc2).render(st2)))
+    assert np.array_equal(bits(N.render_image_tree(ts, st)), bits(oracle.OracleScene(sc).render(st)))
+    assert N.render_image_tree_stats()["creates"] - s2["creates"] == 3   # the first scene was evicted
+    lib.crt_hip_render_image_tree_reset()
+
+
 def test_render_image_shim_builds_against_reference_headers():
     """The shim compiles against the reference's crt_renderer.h / crt_scene.h
     and links with its TUs (oracle/Makefile `shim`, run by build())."""
@@ -117,4 +157,4 @@ def test_render_image_shim_builds_against_reference_headers():
     import subprocess
     syms = subprocess.run(["nm", "-DC", str(path)], capture_output=True, text=True, check=True).stdout
     assert "crt::render_image(crt::Scene const&, crt::RendererSettings const&)" in syms
-    assert "crt_hip_scene_from_tree" in syms and "shim_check_render" in syms
+    assert "crt_hip_render_image_tree" in syms and "shim_check_render" in syms

@@ -61,3 +61,18 @@ def test_tree_desc_policy(N, monkeypatch):
     assert N.lib().crt_auto_gpus_tree(ts.tree_desc_ptr(), C.byref(s), 8) == 8
     _, ts2 = tree_scene("14-01-acceleration-tree__scene1", 1920, 1080)
     assert N.lib().crt_auto_gpus_tree(ts2.tree_desc_ptr(), C.byref(s), 8) == 1
+
+
+def test_multi_probe_verdict(N):
+    """The multi-GPU probe's decision (crt_multi.hip, run by the create of a
+    handle over >= 2 distinct devices): identical probe frames keep the
+    replicas; one differing bit or a failed probe render falls back to one GPU."""
+    import numpy as np
+    a = np.random.default_rng(1).random(64 * 36 * 3).astype(np.float32)
+    b = a.copy()
+    f = N.lib().crt_multi_probe_verdict
+    assert f(a.ctypes.data, b.ctypes.data, a.size, 0) == 0
+    b.view(np.uint32)[1234] ^= 1
+    assert f(a.ctypes.data, b.ctypes.data, a.size, 0) == 1
+    assert f(a.ctypes.data, a.ctypes.data, a.size, -4) == 2
+    assert f(a.ctypes.data, a.ctypes.data, 0, 0) == 0

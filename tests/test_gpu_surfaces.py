@@ -115,3 +115,38 @@ def test_crt_module_reloads_an_edited_bitmap(tmp_path):
     fresh = native.HipScene(native.SceneFile(text=json.dumps(doc), asset_root=str(tmp_path))).render(st)
     assert not np.array_equal(bits(np.ascontiguousarray(a)), bits(np.ascontiguousarray(c)))
     assert np.array_equal(bits(np.ascontiguousarray(c)), bits(fresh))
+
+
+def test_crt_module_moves_camera_without_upload(oracle):
+    """A Blender-style session: the same scene dict with the camera moved on
+    every call (bl_crt_engine.py:12-31 builds a new dict per frame).  _crt keys
+    its kept device scene on the scene without its camera, so a camera-only
+    change moves the kept scene's camera (crt_hip_scene_set_camera) instead of
+    creating and uploading the scene again; every frame equals the oracle's
+    render of the same dict, for 8 poses and a second resolution."""
+    if str(PKG) not in sys.path:
+        sys.path.insert(0, str(PKG))
+    import _crt
+    from crt_amd import native
+    from crt_amd.camera import orbit_poses
+    name = "14-01-acceleration-tree__scene1"
+    st = native.RendererSettings.default()
+    settings = _crt.RendererSettings((st.max_ray_depth, st.diffuse_reflection_ray_count, st.shadow_bias,
+                                      st.reflection_bias, st.diffuse_reflection_bias, st.refraction_bias))
+    ps = orbit_poses(scene_npz(name).a, 8)
+    frames = [(loc, rot, 320, 180) for loc, rot in ps] + [(ps[3][0], ps[3][1], 256, 256)]
+    before = None
+    for k, (loc, rot, w, h) in enumerate(frames):
+        sc, doc = _doc(name, w, h)
+        sc.set_camera(location=loc, rotation=rot)
+        doc["camera"]["position"] = [float(x) for x in loc]
+        doc["camera"]["matrix"] = [float(x) for x in rot]
+        px = _crt.render_scene_from_dict(doc, str(GOLDEN), settings)
+        got = np.ascontiguousarray(np.array([p[:3] for p in px], np.float32).reshape(h, w, 3)[::-1])
+        assert np.array_equal(bits(got), bits(oracle.OracleScene(sc).render(st))), f"frame {k}"
+        stats = _crt._device_scene_stats()
+        if before is None:
+            before = stats
+        else:   # no new device scene: the camera moved in place
+            assert stats["creates"] == before["creates"], (k, stats, before)
+    assert stats["camera_moves"] - before["camera_moves"] == len(frames) - 1
