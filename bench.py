@@ -541,6 +541,7 @@ def main():
     # before its render kernel; their device time alone, and the same frame
     # with the bins off (every camera ray through the BVH walk, no binning)
     bins = None
+    one_last = None
     if mode == "single" and not a.shadows:
         b_ms = gpu.bins_ms(50)
         if b_ms > 0.0:
@@ -567,6 +568,7 @@ def main():
                 torch.cuda.synchronize()
                 ser.append(e0.elapsed_time(e1))
             one_ms = statistics.median(ser)
+            one_last = frame.clone() if a.check else None   # for the check below
             bins = {"rebuilt_every_frame": True, "list_sets": 3, "bins_ms": round(b_ms, 5),
                     "frame_ms_one_at_a_time": round(one_ms, 5),
                     "frame_ms_bins_off": round(off_ms, 5),
@@ -638,8 +640,8 @@ def main():
         else:
             wb = want.view(np.uint32)
             results = {"timed": np.array_equal(timed_last.view(H, W, 3).cpu().numpy().view(np.uint32), wb)}
-            if bins:
-                results["one_at_a_time"] = np.array_equal(frame.view(H, W, 3).cpu().numpy().view(np.uint32), wb)
+            if one_last is not None:
+                results["one_at_a_time"] = np.array_equal(one_last.view(H, W, 3).cpu().numpy().view(np.uint32), wb)
         same = all(results.values())
         check = "bit-identical" if same else "DIFFERS"
         verdicts = ", ".join(f"{k} frame " + ("bit-identical" if v else "DIFFERS") for k, v in results.items())

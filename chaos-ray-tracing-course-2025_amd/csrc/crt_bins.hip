@@ -978,6 +978,7 @@ int bins_view(crt_hip_scene *sc) {
         HIP_TRY(hipEventCreateWithFlags(&b.rdone[i], CRT_PIPE_EV_FLAGS));
         HIP_TRY(hipEventRecord(b.rdone[i], sc->stream));
         HIP_TRY(hipEventRecord(b.bdone[i], sc->stream));
+        b.rdone_s[i] = b.bdone_s[i] = sc->stream;
     }
     /* k_bins_sort's grid: a wave per long list (at least kBinShards waves),
      * then the listed cells (every cell when some hull is everywhere),
@@ -1086,8 +1087,11 @@ int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *p
      * on an event already reached on the same stream costs nothing */
     const bool overlap = hipEventQuery(b.rdone[prev]) == hipErrorNotReady;
     const hipStream_t bs = overlap ? b.stream : s;
-    HIP_TRY(hipStreamWaitEvent(bs, b.rdone[par], 0));
-    HIP_TRY(hipStreamWaitEvent(bs, b.bdone[prev], 0));
+    auto after = [&](hipEvent_t e, hipStream_t es) -> hipError_t {   /* (implied on its own stream, or done) */
+        return es == bs || hipEventQuery(e) == hipSuccess ? hipSuccess : hipStreamWaitEvent(bs, e, 0);
+    };
+    HIP_TRY(after(b.rdone[par], b.rdone_s[par]));
+    HIP_TRY(after(b.bdone[prev], b.bdone_s[prev]));
     int rc = launch_project(sc, bs, par, plan.bp.phdr);
     if (rc != CRT_OK) return rc;
     BinsPlan bp = plan.bp;
@@ -1101,6 +1105,7 @@ int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *p
                        b.off + (size_t)par * b.ncell, b.len + (size_t)par * b.ncell, b.tx, b.ncell, bp);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(b.bdone[par], bs));
+    b.bdone_s[par] = bs;
     if (overlap) HIP_TRY(hipStreamWaitEvent(s, b.bdone[par], 0));
     if (par_out) *par_out = par;
 #ifdef CRT_BINS_STAMPS

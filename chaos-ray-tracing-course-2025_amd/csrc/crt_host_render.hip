@@ -418,10 +418,13 @@ int ensure_gi_tables(crt_hip_scene *sc) {
 /* Device copy of sc->ds for the render kernels.  When the host record
  * changed (a new camera, the first GI frame's tables) the next slot of a ring
  * of kRecRing records takes it, written on `stream` by a one-thread kernel
- * (the record travels as its by-value argument: no host sync, no staging),
- * after the frames that last read that slot (rec_use); frames issued before
- * keep reading their own slot.  Work on another stream that reads the record
- * waits for rec_up of its slot (wait_device_record). */
+ * (the record travels as its by-value argument: no host sync, no staging);
+ * frames issued before keep reading their own slot.  Ordering costs nothing
+ * on one stream: a slot is rewritten after its last frame when both were
+ * issued on the same stream, and read after its write by frames on the
+ * writing stream.  Only across streams an event is recorded — on the stream
+ * of the slot's last frame, or of its write, at the time another stream needs
+ * it (later on that stream than strictly needed, never earlier). */
 int sync_device_record(crt_hip_scene *sc, const DeviceScene **out, hipStream_t stream) {
     if (!sc->d_ring) {
         void *p = nullptr;
@@ -434,13 +437,21 @@ int sync_device_record(crt_hip_scene *sc, const DeviceScene **out, hipStream_t s
         }
     }
     if (sc->ring_cur < 0 || std::memcmp(&sc->ds_uploaded, &sc->ds, sizeof(DeviceScene)) != 0) {
+        if (sc->ring_cur >= 0) sc->rec_use_stream[sc->ring_cur] = sc->rec_last_stream;
+        sc->rec_last_stream = nullptr;
         const int j = (sc->ring_cur + 1) % kRecRing;
-        if (sc->rec_used[j]) HIP_TRY(hipStreamWaitEvent(stream, sc->rec_use[j], 0));
+        /* slot j's last frame: implied on this stream, else an event behind it */
+        if (sc->rec_use_stream[j] && sc->rec_use_stream[j] != stream) {
+            HIP_TRY(hipEventRecord(sc->rec_use[j], sc->rec_use_stream[j]));
+            HIP_TRY(hipStreamWaitEvent(stream, sc->rec_use[j], 0));
+        }
+        sc->rec_use_stream[j] = nullptr;
         hipLaunchKernelGGL(k_put_record, dim3(1), dim3(64), 0, stream, sc->d_ring + j, sc->ds);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(sc->rec_up[j], stream));
         sc->ring_cur = j;
         sc->rec_up_stream = stream;
+        sc->rec_up_done = false;
+        sc->rec_up_recorded = false;
         sc->d_ds = sc->d_ring + j;
         std::memcpy(&sc->ds_uploaded, &sc->ds, sizeof(DeviceScene));
         ++sc->records_written;
@@ -455,20 +466,24 @@ int sync_device_record(crt_hip_scene *sc, const DeviceScene **out, hipStream_t s
 /* `stream` will read the current record: after its write (nothing to wait
  * for on the stream that wrote it, or once the write is done). */
 int wait_device_record(crt_hip_scene *sc, hipStream_t stream) {
-    if (sc->ring_cur < 0 || stream == sc->rec_up_stream) return CRT_OK;
+    if (sc->ring_cur < 0 || sc->rec_up_done || stream == sc->rec_up_stream) return CRT_OK;
+    if (!sc->rec_up_recorded) {
+        HIP_TRY(hipEventRecord(sc->rec_up[sc->ring_cur], sc->rec_up_stream));
+        sc->rec_up_recorded = true;
+    }
     if (hipEventQuery(sc->rec_up[sc->ring_cur]) == hipSuccess) {
-        sc->rec_up_stream = nullptr;   /* written: every stream may read it */
+        sc->rec_up_done = true;   /* written: every stream may read it */
         return CRT_OK;
     }
     HIP_TRY(hipStreamWaitEvent(stream, sc->rec_up[sc->ring_cur], 0));
     return CRT_OK;
 }
 
-/* The frame issued on `stream` is the current record's last reader so far. */
+/* The frame issued on `stream` is the current record's last reader so far
+ * (frames of one record on several streams: the API asks callers to order
+ * them, include/crt_hip.h crt_hip_render_device). */
 int used_device_record(crt_hip_scene *sc, hipStream_t stream) {
-    if (sc->ring_cur < 0) return CRT_OK;
-    HIP_TRY(hipEventRecord(sc->rec_use[sc->ring_cur], stream));
-    sc->rec_used[sc->ring_cur] = true;
+    sc->rec_last_stream = stream;
     return CRT_OK;
 }
 
@@ -1056,7 +1071,8 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         if (count) CRT_LAUNCH_B(true); else CRT_LAUNCH_B(false);
 #undef CRT_LAUNCH_B
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(sc->bins.rdone[par], stream));   /* this parity's lists are free again */
+        HIP_TRY(hipEventRecord(sc->bins.rdone[par], stream));   /* this set's lists are free again */
+        sc->bins.rdone_s[par] = stream;
     } else if (!full) {
         switch (trav) {
         case 7: if (count) CRT_LAUNCH_T(false, 0, 7, true); else CRT_LAUNCH_T(false, 0, 7, false); break;

@@ -16,11 +16,28 @@ namespace crt_amd {
  * BinsPlan): a quarter of a heavy cell, a medium, light or bvh cell of this
  * frame's work lists (with the cell's list: off, len), or a rest tile (len
  * -2: the wave reads its cell's list).  The list's count and the entry are
- * loaded together.  rep: the slot's rep-th entry (entries gcap apart).
- * Returns 0: nothing to do (an unused list slot, or no further entry), 1: the
- * tile, 2: a fill wave (off: its index). */
-__device__ __forceinline__ int bins_tile(const BinsPlan &bp, const Tile *__restrict__ tiles, int wave, int rep,
-                                         Tile &tl, int &off, int &len) {
+ * loaded together.  Returns 0: nothing to do (an unused list slot), 1: the
+ * tile, 2: a fill wave (off: its index).  *next: the slot's further entries
+ * (a frame whose camera lists more cells of the kind than the grid has
+ * slots: the entries gcap apart; next->n = 0 for none). */
+struct BinsNext {
+    const BinsWork *work;   /* the slot's list */
+    int i, n, step, q;      /* this entry, the list's length, entries between the slot's, quarter (-1: whole) */
+};
+
+__device__ __forceinline__ void bins_quarter(Tile &tl, int q, int quad) {
+    const int xx = (q & 1) * 4, yy = (q >> 1) * 4;
+    tl.x += xx;
+    tl.y += yy;
+    tl.w = max(0, min(4, tl.w - xx));
+    tl.h = max(0, min(4, tl.h - yy));
+    tl.out_base += (int64_t)yy * tl.out_stride + xx;
+    tl.prio = quad ? 3 : 1;
+}
+
+__device__ __forceinline__ int bins_tile(const BinsPlan &bp, const Tile *__restrict__ tiles, int wave, Tile &tl,
+                                         int &off, int &len, BinsNext &next) {
+    next.n = 0;
     int kind = 0, slot = wave >> 2, q = wave & 3;
     if (wave >= 4 * kBinShards * bp.gcap[0]) {
         slot = wave - 4 * kBinShards * bp.gcap[0];
@@ -31,7 +48,6 @@ __device__ __forceinline__ int bins_tile(const BinsPlan &bp, const Tile *__restr
             ++kind;
         }
         if (kind == kBinKinds) {
-            if (rep > 0) return 0;
             if (slot >= bp.nrest) {
                 off = slot - bp.nrest;
                 return 2;
@@ -41,24 +57,20 @@ __device__ __forceinline__ int bins_tile(const BinsPlan &bp, const Tile *__restr
             return 1;
         }
     }
-    const int sh = slot % kBinShards, i = slot / kBinShards + rep * bp.gcap[kind];
-    const int n = load_scalar(bp.phdr, bins_phdr_at(bp.par, kind, sh));
-    if (i >= bp.ecap) return 0;
-    const BinsWork w = bp.work[bp.wbase[kind] + sh * bp.ecap + i];
+    const int sh = slot % kBinShards, i = slot / kBinShards;
+    const int n = min(load_scalar(bp.phdr, bins_phdr_at(bp.par, kind, sh)), bp.ecap);
+    const BinsWork *work = bp.work + bp.wbase[kind] + sh * bp.ecap;
+    const BinsWork w = work[i];
     if (i >= n) return 0;
+    next.work = work;
+    next.i = i;
+    next.n = n;
+    next.step = bp.gcap[kind];
+    next.q = q;
     tl = w.t;
     off = w.off;
     len = w.len;
-    if (q >= 0) {
-        const int xx = (q & 1) * 4, yy = (q >> 1) * 4;
-        if (xx >= tl.w || yy >= tl.h) return 0;
-        tl.x += xx;
-        tl.y += yy;
-        tl.w = min(4, tl.w - xx);
-        tl.h = min(4, tl.h - yy);
-        tl.out_base += (int64_t)yy * tl.out_stride + xx;
-        tl.prio = bp.quad ? 3 : 1;
-    }
+    if (q >= 0) bins_quarter(tl, q, bp.quad);   /* (a quarter outside a partial cell: w or h 0, no pixel) */
     return 1;
 }
 
@@ -118,8 +130,8 @@ template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW>
 __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSettings &st, Tile tl, int bin_beg,
                                             int bin_len, float *__restrict__ out,
                                             unsigned long long *__restrict__ counters,
-                                            unsigned long long *__restrict__ stamps, const BinsPlan &bp, int wave,
-                                            int lane) {
+                                            unsigned long long *__restrict__ stamps, int bpar, int bncell,
+                                            int wave, int lane) {
     /* the heaviest tiles set the frame length (their walks are long chains of
      * dependent loads): they get issue priority over the light waves that
      * share their SIMD (s_setprio; scheduling only, results unchanged) */
@@ -176,7 +188,7 @@ __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSetting
         const int tx0 = uniform_i(tl.x), ty0 = uniform_i(tl.y), tw = uniform_i(tl.w), th = uniform_i(tl.h);
         const int cell = (ty0 >> 3) * s.bin_tx + (tx0 >> 3);
         const bool one = (tx0 & 7) + tw <= 8 && (ty0 & 7) + th <= 8;
-        const int pc = bp.par * bp.ncell + cell;   /* this frame's set of the per-cell lists */
+        const int pc = bpar * bncell + cell;   /* this frame's set of the per-cell lists */
         const int len = uniform_i(bin_len != -2 ? bin_len : one ? load_scalar(s.bin_len, pc) : -1);
         if (len >= 0) {   /* -1: not inside one cell, or the cell's list is over the cap: the BVH walk below */
             const int beg = uniform_i(bin_len != -2 ? bin_beg : load_scalar(s.bin_off, pc)), end = beg + len;
@@ -329,21 +341,31 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
     /* diagnostic build only (stamps != nullptr): wave start / end in s_memrealtime ticks (100 MHz) */
     if (stamps && lane == 0) stamps[2 * wave] = __builtin_amdgcn_s_memrealtime();
     if constexpr (TRAV == 15 && !FULL && !SHADOW) {
-        /* camera bins: the wave's work-list slot, and the entries a grid's
+        /* camera bins: the wave's work-list slot, then the entries a grid's
          * capacity further on when this frame's list outgrew the grid (the
          * camera moved since the sizing pass) */
-        for (int rep = 0;; ++rep) {
-            Tile tl;
-            int bin_beg = 0, bin_len = -2;   /* the cell's list from the work list (-2: read it in render_tile) */
-            const int r = bins_tile(bp, tiles, wave, rep, tl, bin_beg, bin_len);
-            if (r == 2) bins_fill(s, bp, tiles, bin_beg, out, COUNT ? counters : nullptr);
-            if (r != 1) return;
-            render_tile<FULL, MAXF, TRAV, SEC, COUNT, SHADOW>(s, st, tl, bin_beg, bin_len, out, counters, stamps, bp,
-                                                              wave, lane);
+        Tile tl;
+        int bin_beg = 0, bin_len = -2;   /* the cell's list from the work list (-2: read it in render_tile) */
+        BinsNext nx;
+        const int r = bins_tile(bp, tiles, wave, tl, bin_beg, bin_len, nx);
+        if (r == 2) bins_fill(s, bp, tiles, bin_beg, out, COUNT ? counters : nullptr);
+        if (r != 1) return;
+        const int bpar = bp.par, bncell = bp.ncell, quad = bp.quad;
+        for (;;) {
+            if (tl.w > 0 && tl.h > 0)   /* (a quarter outside a partial cell has no pixel) */
+                render_tile<FULL, MAXF, TRAV, SEC, COUNT, SHADOW>(s, st, tl, bin_beg, bin_len, out, counters, stamps,
+                                                                  bpar, bncell, wave, lane);
+            nx.i += nx.step;
+            if (nx.i >= nx.n) return;
+            const BinsWork w = nx.work[nx.i];
+            tl = w.t;
+            bin_beg = w.off;
+            bin_len = w.len;
+            if (nx.q >= 0) bins_quarter(tl, nx.q, quad);
         }
     } else {
-        render_tile<FULL, MAXF, TRAV, SEC, COUNT, SHADOW>(s, st, tiles[wave], 0, -2, out, counters, stamps, bp, wave,
-                                                          lane);
+        render_tile<FULL, MAXF, TRAV, SEC, COUNT, SHADOW>(s, st, tiles[wave], 0, -2, out, counters, stamps, bp.par,
+                                                          bp.ncell, wave, lane);
     }
 }
 

@@ -82,6 +82,7 @@ struct BinsDev {
      * set p's render done with them */
     hipStream_t stream = nullptr;
     hipEvent_t bdone[crt_amd::kBinSets] = {}, rdone[crt_amd::kBinSets] = {};
+    hipStream_t bdone_s[crt_amd::kBinSets] = {}, rdone_s[crt_amd::kBinSets] = {};   /* where each was last recorded */
 };
 
 
@@ -176,10 +177,13 @@ struct crt_hip_scene {
     DeviceScene *d_ds = nullptr;     /* the current record: a slot of d_ring (sync_device_record) */
     DeviceScene *d_ring = nullptr;
     int ring_cur = -1;
-    hipStream_t rec_up_stream = nullptr;   /* where the current record was written (null: done) */
+    hipStream_t rec_up_stream = nullptr;   /* where the current record was written */
+    bool rec_up_done = false;              /* ... and the write is done */
+    bool rec_up_recorded = false;          /* rec_up of the current slot recorded (a reader on another stream) */
+    hipStream_t rec_last_stream = nullptr;  /* where the last frame that read the current record was issued */
     hipEvent_t rec_up[kRecRing] = {};    /* slot written */
     hipEvent_t rec_use[kRecRing] = {};   /* the last frame that read the slot is done */
-    bool rec_used[kRecRing] = {};
+    hipStream_t rec_use_stream[kRecRing] = {};   /* where each slot's last frame was issued (null: none) */
     int64_t records_written = 0;
     crt_wave_counts wave_counts{};   /* from the last crt_hip_count_work */
     std::vector<void *> allocs;
