@@ -537,46 +537,68 @@ def main():
     # measurements after this one write into the same buffers)
     timed_last = (frame8 if (mode == "tiles" and u8) else frame).clone() if (a.check and rank == 0) else None
 
-    # camera bins (crt_bins.hip): every frame above rebuilds them on the device
-    # before its render kernel; their device time alone, and the same frame
-    # with the bins off (every camera ray through the BVH walk, no binning)
+    # camera bins (crt_bins.hip): the frames above keep one camera, so the
+    # first binning's lists serve them all (option "bins_reuse", a frame whose
+    # camera and plan are the last binning's); beside them the same frames
+    # binning every one (bins_reuse 0: the next frames' binnings overlap frame
+    # k's render) and with the bins off (every camera ray through the BVH
+    # walk), each back to back and one at a time
     bins = None
     one_last = None
     if mode == "single" and not a.shadows:
         b_ms = gpu.bins_ms(50)
         if b_ms > 0.0:
-            gpu.set_option("bins", 0)
-            for _ in range(a.warmup):
-                step(mode)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(a.steps):
-                step(mode)
-            torch.cuda.synchronize()
-            off_ms = (time.perf_counter() - t0) / a.steps * 1e3
-            gpu.set_option("bins", 1)
-            # one frame at a time (a host sync after each): no overlap with the
-            # next frame's binning — the single-frame latency, and the render
-            # kernel's own time (= that frame - the binning) for the roofline
-            ser = []
-            for _ in range(max(10, a.steps // 2)):
+            def back_to_back():
+                for _ in range(a.warmup):
+                    step(mode)
                 torch.cuda.synchronize()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                gpu.render_device(settings, frame.data_ptr(), sptr)
-                e1.record(stream)
+                t0 = time.perf_counter()
+                for _ in range(a.steps):
+                    step(mode)
                 torch.cuda.synchronize()
-                ser.append(e0.elapsed_time(e1))
-            one_ms = statistics.median(ser)
+                return (time.perf_counter() - t0) / a.steps * 1e3
+
+            def one_at_a_time():
+                # a host sync after each frame: the single-frame latency (HIP
+                # events around the frame's launches on its stream)
+                ser = []
+                for _ in range(max(10, a.steps // 2)):
+                    torch.cuda.synchronize()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    gpu.render_device(settings, frame.data_ptr(), sptr)
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    ser.append(e0.elapsed_time(e1))
+                return statistics.median(ser)
+
+            one_ms = one_at_a_time()
             one_last = frame.clone() if a.check else None   # for the check below
-            bins = {"rebuilt_every_frame": True, "list_sets": 3, "bins_ms": round(b_ms, 5),
+            i0 = gpu.info()
+            gpu.set_option("bins_reuse", 0)
+            rebin_ms = back_to_back()
+            rebin_one_ms = one_at_a_time()
+            gpu.set_option("bins_reuse", 1)
+            i1 = gpu.info()
+            gpu.set_option("bins", 0)
+            off_ms = back_to_back()
+            off_one_ms = one_at_a_time()
+            gpu.set_option("bins", 1)
+            bins = {"lists_reused": True, "list_sets": 3, "bins_ms": round(b_ms, 5),
                     "frame_ms_one_at_a_time": round(one_ms, 5),
-                    "frame_ms_bins_off": round(off_ms, 5),
-                    "value_bins_off": round(rays_per_frame / (off_ms * 1e-3) / 1e6, 3),
-                    "note": "frame = device binning (k_bins_project [+ k_bins_pairs] + k_bins_sort) + render; frames "
-                            "back to back (ms_per_step): the next frames' binnings overlap frame k's render (3 "
-                            "sets of lists, crt_kernel_common.h kBinSets); frame_ms_one_at_a_time: a host sync after every frame; bins_ms = the "
-                            "binning alone (HIP events, 50 frames); bins off = the BVH walk for every camera ray"}
+                    "rebinned_every_frame": {"ms_per_step": round(rebin_ms, 5),
+                                             "value": round(rays_per_frame / (rebin_ms * 1e-3) / 1e6, 3),
+                                             "frame_ms_one_at_a_time": round(rebin_one_ms, 5),
+                                             "binnings": i1["bins_binnings"] - i0["bins_binnings"]},
+                    "bins_off": {"ms_per_step": round(off_ms, 5),
+                                 "value": round(rays_per_frame / (off_ms * 1e-3) / 1e6, 3),
+                                 "frame_ms_one_at_a_time": round(off_one_ms, 5)},
+                    "note": "ms_per_step frames keep the scene's camera: the first frame bins (k_bins_project [+ "
+                            "k_bins_pairs] + k_bins_sort), the rest render its lists again (option bins_reuse; a "
+                            "camera move bins again, see camera_orbit); rebinned_every_frame = bins_reuse 0, the "
+                            "next frames' binnings overlapping frame k's render (3 sets of lists, "
+                            "crt_kernel_common.h kBinSets); one_at_a_time = a host sync after every frame; bins_ms = "
+                            "the binning alone (HIP events, 50 binnings); bins_off = the BVH walk for every camera ray"}
 
     # moving camera: a new pose before every frame, frames back to back
     # (the binning of each frame runs with its own pose; frames in flight keep
@@ -615,10 +637,12 @@ def main():
         orbit = {"poses": len(cams), "frames": a.steps, "ms_per_step": round(o_ms, 5),
                  "value": round(npx / (o_ms * 1e-3) / 1e6, 3), "unit": "Mrays/s (camera rays: one per pixel)",
                  "vs_fixed_camera": round(o_ms / (elapsed / a.steps * 1e3), 4),
+                 "vs_rebinned": (round(o_ms / bins["rebinned_every_frame"]["ms_per_step"], 4) if bins else None),
                  "view_rebuilds": gpu.info()["view_rebuilds"] - moves0, "check": o_check,
                  "note": "crt_hip_scene_set_camera before every frame (yaw 20 deg sin, pitch 6 deg cos around the "
-                         "scene's centre), frames issued back to back into HBM; the camera bins are rebuilt for "
-                         "every pose inside its frame"}
+                         "scene's centre), frames issued back to back into HBM; every frame bins its own pose "
+                         "(vs_fixed_camera: against ms_per_step, whose frames reuse one binning; "
+                         "vs_rebinned: against camera_bins.rebinned_every_frame)"}
         if o_check == "DIFFERS":
             print("check: orbit frame DIFFERS from the blocking render of its pose", flush=True)
             raise SystemExit(1)
@@ -683,11 +707,11 @@ def main():
     pmc = load_pmc(a.pmc_json, a.config, W, H)
     # the dominant kernel is the render; a camera-bins frame also runs the
     # binning launches before it (their time measured alone above)
-    render_ms = bins["frame_ms_one_at_a_time"] - bins["bins_ms"] if bins else kern_ms
+    render_ms = bins["frame_ms_one_at_a_time"] if bins else kern_ms
     roof = roofline_block(render_ms, counts, waves, npx, pmc, build_id, shard_frac)
     if bins:
-        roof["kernel_ms_basis"] = ("render kernel = one frame at a time (HIP events) - binning (HIP events, measured "
-                                   f"alone): {bins['frame_ms_one_at_a_time']:.5f} - {bins['bins_ms']:.5f} ms")
+        roof["kernel_ms_basis"] = ("render kernel = a frame that renders the last binning's lists, one at a time "
+                                   f"(HIP events around its launch, median): {bins['frame_ms_one_at_a_time']:.5f} ms")
 
     out = None
     if rank == 0:

@@ -132,7 +132,8 @@ class SceneInfo(C.Structure):
                 ("bins_ms", C.c_double), ("upload_ms", C.c_double), ("create_ms", C.c_double),
                 ("wf_sets", C.c_int32), ("pad0", C.c_int32), ("camera_moves", C.c_int64),
                 ("view_rebuilds", C.c_int64), ("records_written", C.c_int64), ("multi_probe", C.c_int32),
-                ("pad1", C.c_int32), ("multi_probe_ms", C.c_double)]
+                ("pad1", C.c_int32), ("multi_probe_ms", C.c_double), ("bins_binnings", C.c_int64),
+                ("bins_reuses", C.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -385,6 +385,8 @@ int crt_hip_scene_info(const crt_hip_scene *sc, crt_scene_info *out) {
     out->camera_moves = sc->camera_moves;
     out->view_rebuilds = sc->view_rebuilds;
     out->records_written = sc->records_written;
+    out->bins_binnings = sc->bins.binnings;
+    out->bins_reuses = sc->bins.reuses;
     return CRT_OK;
 }
 
@@ -752,9 +754,13 @@ static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
     } else if (k == "rec_machine") {
         sc->rec_machine = value != 0;
         sc->calib_walk = -1;
-    } else if (k == "bins" || k == "bins_split" || k == "bins_quad") {   /* camera bins: the full-frame plan depends on them */
+    } else if (k == "bins_reuse") {   /* no plan depends on it */
+        sc->bins_reuse = value != 0;
+        return CRT_OK;
+    } else if (k == "bins" || k == "bins_split" || k == "bins_quad" || k == "bins_slack") {   /* camera bins: the full-frame plan depends on them */
         if (k == "bins_split" && value < 1) return set_error(CRT_E_INVALID, "bins_split must be >= 1");
-        int &field = k == "bins" ? sc->bins_on : k == "bins_quad" ? sc->bins_quad : sc->bins_split;
+        if (k == "bins_slack" && (value < 0 || value > 1000)) return set_error(CRT_E_INVALID, "bins_slack must be 0..1000");
+        int &field = k == "bins" ? sc->bins_on : k == "bins_quad" ? sc->bins_quad : k == "bins_slack" ? sc->bins_slack : sc->bins_split;
         const int v = k == "bins" || k == "bins_quad" ? (value != 0) : (int)value;
         if (v != field) {
             HIP_TRY(hipDeviceSynchronize());

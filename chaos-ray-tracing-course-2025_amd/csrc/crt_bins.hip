@@ -108,6 +108,9 @@ namespace {
 #define CRT_BINS_CNT_STRIDE 16   /* int32 between two cells' counters (atomics on one line serialise) */
 #endif
 constexpr int kCntStride = CRT_BINS_CNT_STRIDE;
+#ifndef CRT_PAIRS_PER_BLOCK
+#define CRT_PAIRS_PER_BLOCK 512
+#endif
 constexpr int kProjTris = 32;     /* triangles per k_bins_project block: 8 lanes each (one hull corner per lane) */
 
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
@@ -793,6 +796,8 @@ void bins_free_view(crt_hip_scene *sc) {
     b.every = b.nonempty = b.bigl = nullptr;
     b.hdr = nullptr;
     b.frame = 0;
+    b.last = -1;
+    b.binned_plan = nullptr;
     b.caps = BinsCaps{};
     b.recs = nullptr;
     b.rec_cap = 0;
@@ -930,10 +935,11 @@ int bins_view(crt_hip_scene *sc) {
     HIP_TRY(hipMemsetAsync(b.hdr, 0, kBinSets * sizeof(BinsHdr), sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
     b.frame = 0;
+    b.last = -1;
     b.count.assign((size_t)b.ncell, 0);
     int64_t queued = 0;   /* pairs past the first kExpand of their group */
     for (const int32_t g : gsum) queued += std::max(0, g - kExpand);
-    b.pair_blocks = queued ? (int)std::max<int64_t>(8, std::min<int64_t>(2048, (queued + 511) / 512)) : 0;
+    b.pair_blocks = queued ? (int)std::max<int64_t>(8, std::min<int64_t>(2048, (queued + CRT_PAIRS_PER_BLOCK - 1) / CRT_PAIRS_PER_BLOCK)) : 0;
     int64_t total = 0, shard_rec[kBinShards] = {0}, shard_listed[kBinShards] = {0}, shard_long[kBinShards] = {0};
     for (int c = 0; c < b.ncell; ++c) {
         const int64_t n = (int64_t)cnt[(size_t)c * kCntStride] + n_every;
@@ -1031,12 +1037,14 @@ int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
         if (!inside[(size_t)k] || cell_tile[(size_t)(t.y >> 3) * b.tx + (t.x >> 3)] == -2) rest.push_back(k);
     }
     /* the lists hold every cell of a shard (a moved camera may list any cell
-     * of any kind); the grid takes the sizing pass's counts, at least one
-     * slot per shard and kind */
+     * of any kind); the grid takes the sizing pass's counts plus bins_slack %
+     * (a moved camera's extra cells of a kind: slots beyond take several
+     * entries), at least one slot per shard and kind */
     bp.ecap = b.cap_shard;
     int64_t slots = 0;
     for (int q = 0; q < kBinKinds; ++q) {
-        bp.gcap[q] = std::max(1, *std::max_element(per[q], per[q] + kBinShards));
+        const int64_t most = *std::max_element(per[q], per[q] + kBinShards);
+        bp.gcap[q] = (int32_t)std::min<int64_t>(b.cap_shard, std::max<int64_t>(1, most + (most * sc->bins_slack + 99) / 100));
         bp.wbase[q] = (int32_t)slots;
         slots += (int64_t)kBinShards * bp.ecap;
     }
@@ -1070,9 +1078,20 @@ int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
  * back (same set) is done with the set and after the previous binning — and
  * `s` waits for it: the next frames' binnings overlap frame k's render.
  * Otherwise (one frame at a time) `s` takes the binning itself, after the
- * same two events. */
-int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *par_out) {
+ * same two events.  A frame with the camera and plan of the last binning
+ * (bins_reuse, not `force`) takes that binning's set as it is: `s` only
+ * waits for the binning if it ran elsewhere. */
+int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *par_out, bool force) {
     BinsDev &b = sc->bins;
+    if (!force && sc->bins_reuse && b.last >= 0 && b.binned_plan == plan.bp.work && plan.bp.work &&
+        std::memcmp(&b.binned, &b.cam, sizeof b.cam) == 0) {
+        const int par = b.last;
+        if (b.bdone_s[par] != s && hipEventQuery(b.bdone[par]) != hipSuccess)
+            HIP_TRY(hipStreamWaitEvent(s, b.bdone[par], 0));
+        ++b.reuses;
+        if (par_out) *par_out = par;
+        return CRT_OK;
+    }
     const int par = (int)(b.frame++ % kBinSets);
     const int prev = (par + kBinSets - 1) % kBinSets;
     {
@@ -1107,6 +1126,10 @@ int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *p
     HIP_TRY(hipEventRecord(b.bdone[par], bs));
     b.bdone_s[par] = bs;
     if (overlap) HIP_TRY(hipStreamWaitEvent(s, b.bdone[par], 0));
+    b.last = par;
+    b.binned = b.cam;
+    b.binned_plan = plan.bp.work;
+    ++b.binnings;
     if (par_out) *par_out = par;
 #ifdef CRT_BINS_STAMPS
     if (const char *fn = std::getenv("CRT_BINS_STAMPS_FILE")) {
@@ -1151,7 +1174,7 @@ int64_t crt_hip_camera_bins(crt_hip_scene *sc, int32_t *len_out, void *recs_out,
     }
     HIP_TRY(hipStreamSynchronize(sc->stream));
     ShardPlan none;   /* no tile plan: every cell's list */
-    int rc = bins_enqueue(sc, none, sc->stream, nullptr);
+    int rc = bins_enqueue(sc, none, sc->stream, nullptr, true);
     if (rc != CRT_OK) return rc;
     if ((rc = bins_dbg_arm(sc, none)) != CRT_OK) return rc;   /* diagnostic builds: this frame's violations */
     const int par = (int)((b.frame - 1) % kBinSets);   /* the set that frame used */
@@ -1183,10 +1206,10 @@ int crt_hip_bins_time(crt_hip_scene *sc, int32_t frames, double *ms) {
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
     int rc = CRT_OK;
-    for (int w = 0; w < 3 && rc == CRT_OK; ++w) rc = bins_enqueue(sc, sc->full, sc->stream, nullptr);   /* warm */
+    for (int w = 0; w < 3 && rc == CRT_OK; ++w) rc = bins_enqueue(sc, sc->full, sc->stream, nullptr, true);   /* warm */
     hipError_t e = rc == CRT_OK ? hipEventRecord(e0, sc->stream) : hipSuccess;
     for (int f = 0; f < frames && rc == CRT_OK && e == hipSuccess; ++f)
-        rc = bins_enqueue(sc, sc->full, sc->stream, nullptr);
+        rc = bins_enqueue(sc, sc->full, sc->stream, nullptr, true);
     if (rc == CRT_OK && e == hipSuccess) e = hipEventRecord(e1, sc->stream);
     if (rc == CRT_OK && e == hipSuccess) e = hipEventSynchronize(e1);
     float f = 0.f;

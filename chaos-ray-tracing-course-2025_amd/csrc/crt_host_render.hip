@@ -340,6 +340,7 @@ void free_plans(crt_hip_scene *sc) {
     wf_graphs_clear(sc->wf);
     sc->full = ShardPlan{};
     sc->shard_plans.clear();
+    sc->bins.last = -1;   /* the work lists were the freed plans' */
     sc->compact_plans.clear();
 }
 
@@ -1071,8 +1072,14 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         if (count) CRT_LAUNCH_B(true); else CRT_LAUNCH_B(false);
 #undef CRT_LAUNCH_B
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(sc->bins.rdone[par], stream));   /* this set's lists are free again */
-        sc->bins.rdone_s[par] = stream;
+        /* this set's lists are free again — after every render that read
+         * them: a set taken again (bins_reuse) by a frame on another stream
+         * chains the earlier reader's event into this one */
+        BinsDev &b = sc->bins;
+        if (b.rdone_s[par] != stream && hipEventQuery(b.rdone[par]) != hipSuccess)
+            HIP_TRY(hipStreamWaitEvent(stream, b.rdone[par], 0));
+        HIP_TRY(hipEventRecord(b.rdone[par], stream));
+        b.rdone_s[par] = stream;
     } else if (!full) {
         switch (trav) {
         case 7: if (count) CRT_LAUNCH_T(false, 0, 7, true); else CRT_LAUNCH_T(false, 0, 7, false); break;

@@ -66,6 +66,13 @@ struct BinsDev {
     int long_waves = 0;                   /* k_bins_sort waves for the long lists */
     crt_amd::BinsHdr *hdr = nullptr;      /* kBinSets sets: frames take them in turn */
     uint64_t frame = 0;                   /* frames binned (set = frame % kBinSets) */
+    /* the last binning: its set, camera and plan (the work lists it wrote).
+     * A frame with the same camera and plan renders that set again instead of
+     * binning (the lists are a function of the camera: option "bins_reuse") */
+    int last = -1;
+    crt_amd::BinCamera binned{};
+    const void *binned_plan = nullptr;
+    int64_t binnings = 0, reuses = 0;
     crt_amd::BinsCaps caps{};             /* per shard: its region of recs */
     crt_amd::CamCand *recs = nullptr;     /* the lists, kBinSets sets (rec_cap each) */
     int32_t rec_cap = 0;
@@ -248,6 +255,8 @@ struct crt_hip_scene {
                                     * caller sets calibrate / calib_k_milli / calib_min) */
     int calib_deferred_walk = -1;  /* walk whose first frame skipped the calibration */
     int bins_on = 1;               /* camera frames take the camera bins where built (walk 15; option "bins") */
+    int bins_slack = 100;          /* camera-bins grid slots per kind: the sizing pass's count + this % (option "bins_slack") */
+    int bins_reuse = 1;            /* a frame whose camera the last binning used renders its lists (option "bins_reuse") */
     int bins_split = 48;           /* cells with this many candidates run as four 4x4 waves (option "bins_split") */
     int bins_quad = 1;             /* those waves walk with four lanes per pixel (option "bins_quad") */
     void *probe_buf = nullptr;     /* calibration probes: tile list + costs (probe_tiles) */
@@ -312,7 +321,7 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs);
 int bins_view(crt_hip_scene *sc);
 void bins_free_view(crt_hip_scene *sc);
 int bins_plan(crt_hip_scene *sc, ShardPlan &plan);
-int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *par_out);
+int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *par_out, bool force = false);
 void bins_free(crt_hip_scene *sc);
 /* crt_multi.hip: the frame over every replica of a multi-GPU scene into d_rgb
  * (on the scene's device) on `stream`; *overflow: some replica's recorded

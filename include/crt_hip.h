@@ -153,6 +153,8 @@ typedef struct crt_scene_info {
                                 * -2 it failed (the handle then renders on one GPU), 0 not run */
     int32_t pad1;
     double  multi_probe_ms;    /* wall time of that probe (two 64x36 frames and two view rebuilds) */
+    int64_t bins_binnings;     /* camera-bins binnings run (frames, plus the test hooks') */
+    int64_t bins_reuses;       /* frames that rendered the last binning's lists (same camera; option "bins_reuse") */
 } crt_scene_info;
 
 typedef struct crt_render_stats {
@@ -498,6 +500,12 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  *                four 4x4-pixel waves
  *   "bins_quad"  0/1 (default 1): those waves walk the list with four lanes
  *                per pixel
+ *   "bins_slack" 0..1000 (default 100): the grid's waves per kind of cell are
+ *                the sizing pass's count plus this percentage (room for a
+ *                moved camera; cells beyond take a wave's further entries)
+ *   "bins_reuse" 0/1 (default 1): a frame whose camera and plan are the last
+ *                binning's renders that binning's lists (no binning); 0 bins
+ *                every frame (crt_scene_info.bins_binnings / bins_reuses)
  *   "secondary"  walk of secondary rays: 0 = by frame (default: 14 where the
  *                scene has a BVH), 4 = cooperative walk in the reference's
  *                order, 10 = pruned cooperative, 14 = BVH + proof

@@ -143,36 +143,79 @@ def test_bins_frames_pipelined_bit_exact(N, oracle, devbuf):
     assert np.array_equal(bits(g.render(st)), want)
 
 
-def test_bins_frames_pipelined_full_size_every_frame(N, oracle, devbuf):
+@pytest.mark.parametrize("reuse", [1, 0])
+def test_bins_frames_pipelined_full_size_every_frame(N, oracle, devbuf, reuse):
     """The bench's own C2 mode at the benched size: 1920x1080 frames issued back
-    to back with no host wait (the next frames' binnings overlap frame k's
-    render, kBinSets sets of lists in turn), each into a buffer of its own, and
-    every one of the 24 frames compared with the oracle's frame."""
+    to back with no host wait, each into a buffer of its own, and every one of
+    the 24 frames compared with the oracle's frame.  reuse 1 (the default): the
+    camera does not move, so the frames render the first binning's lists;
+    reuse 0: every frame bins (the next frames' binnings overlap frame k's
+    render, kBinSets sets of lists in turn)."""
     sc = scene_npz("14-01-acceleration-tree__scene1")
     st = N.RendererSettings.default()
     want = bits(oracle.OracleScene(sc).render(st))
-    g = N.HipScene(sc)
+    g = N.HipScene(sc, bins_reuse=reuse)
     nb = 1920 * 1080 * 3 * 4
     d = [devbuf.alloc(nb) for _ in range(24)]
     for k in range(24):
         g.render_device(st, d[k])
     bad = [k for k in range(24) if not np.array_equal(bits(devbuf.download(d[k], (1080, 1920, 3), np.float32)), want)]
     assert not bad, f"frames {bad} differ from the oracle"
+    info = g.info()
+    if reuse:
+        assert info["bins_reuses"] >= 23, info
+    else:
+        assert info["bins_reuses"] == 0 and info["bins_binnings"] >= 24, info
 
 
-def test_bins_frames_on_alternating_streams(N, oracle, devbuf):
+@pytest.mark.parametrize("reuse", [1, 0])
+def test_bins_frames_on_alternating_streams(N, oracle, devbuf, reuse):
     """Frames issued on two caller streams in turn, no host wait: a binning
     waits for the render kBinSets frames back and for the previous binning
     whichever stream they ran on (crt_bins.hip bins_enqueue), so the shared
-    binning scratch is never rewritten under a render.  30 frames, each into a
-    buffer of its own, every one equal to the oracle."""
+    binning scratch is never rewritten under a render; frames that take the
+    last binning's lists again (reuse 1) chain their set's render events
+    across the streams.  30 frames, each into a buffer of its own, every one
+    equal to the oracle."""
     sc = scene_npz("14-01-acceleration-tree__scene1").set_resolution(960, 540)
     st = N.RendererSettings.default()
     want = bits(oracle.OracleScene(sc).render(st))
-    g = N.HipScene(sc)
+    g = N.HipScene(sc, bins_reuse=reuse)
     streams = [devbuf.stream(), devbuf.stream()]
     d = [devbuf.alloc(960 * 540 * 3 * 4) for _ in range(30)]
     for k in range(30):
         g.render_device(st, d[k], streams[k % 2])
     bad = [k for k in range(30) if not np.array_equal(bits(devbuf.download(d[k], (540, 960, 3), np.float32)), want)]
     assert not bad, f"frames {bad} differ from the oracle"
+
+
+def test_bins_reuse_across_camera_moves_and_streams(N, oracle, devbuf):
+    """Two poses, three frames each in turn, issued on two caller streams with
+    no host wait: a pose's first frame bins (a new set), the next two render
+    those lists again; a binning after reused frames waits for every render of
+    the set it clears, whichever stream.  24 frames, each against the oracle's
+    frame for its pose."""
+    from crt_amd.camera import orbit_poses
+    name = "14-01-acceleration-tree__scene1"
+    w, h = 960, 540
+    base = scene_npz(name).set_resolution(w, h)
+    st = N.RendererSettings.default()
+    ps = orbit_poses(scene_npz(name).a, 4)[:2]
+    fov = float(scene_npz(name).a["cam_fov"][0])
+    wants = [bits(oracle.OracleScene(base.set_camera(location=l, rotation=r, fov_degrees=fov)).render(st))
+             for l, r in ps]
+    g = N.HipScene(base)
+    streams = [devbuf.stream(), devbuf.stream()]
+    d = [devbuf.alloc(w * h * 3 * 4) for _ in range(24)]
+    pose = []
+    for k in range(24):
+        i = (k // 3) % 2
+        if k % 3 == 0:
+            g.set_camera(*ps[i], fov_degrees=fov)
+        pose.append(i)
+        g.render_device(st, d[k], streams[k % 2])
+    bad = [k for k in range(24)
+           if not np.array_equal(bits(devbuf.download(d[k], (h, w, 3), np.float32)), wants[pose[k]])]
+    assert not bad, f"frames {bad} differ from the oracle"
+    info = g.info()
+    assert info["bins_binnings"] >= 8 and info["bins_reuses"] >= 16, info
