@@ -133,7 +133,7 @@ class SceneInfo(C.Structure):
                 ("wf_sets", C.c_int32), ("pad0", C.c_int32), ("camera_moves", C.c_int64),
                 ("view_rebuilds", C.c_int64), ("records_written", C.c_int64), ("multi_probe", C.c_int32),
                 ("pad1", C.c_int32), ("multi_probe_ms", C.c_double), ("bins_binnings", C.c_int64),
-                ("bins_reuses", C.c_int64)]
+                ("bins_reuses", C.c_int64), ("bvh_on_device", C.c_int32), ("bvh_depth", C.c_int32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -201,6 +201,7 @@ EXPORTS = [
     ("crt_hip_render_image_tree_reset", None, []),
     ("crt_host_scene_from_tree", C.c_int, [C.POINTER(TreeSceneDesc), C.POINTER(_P)]),
     ("crt_hip_scene_tree", C.c_int, [_P, _P, _P, _P, _P]),
+    ("crt_hip_scene_bvh", C.c_int64, [_P, _P, _P]),
     ("crt_hip_scene_upload", C.c_int, [_P, C.c_int, C.POINTER(_P)]),
     ("crt_hip_scene_info", C.c_int, [_P, C.POINTER(SceneInfo)]),
     ("crt_hip_scene_destroy", None, [_P]),
@@ -607,6 +608,22 @@ class HipScene:
         _check(lib().crt_hip_scene_tree(self._h, b.ctypes.data, c.ctypes.data, o.ctypes.data, t.ctypes.data))
         return b, c, o, t[:m]
 
+    def bvh(self):
+        """The secondary-ray BVH (crt_hip_scene_bvh): (nodes, tri_ids) with
+        nodes an (8, N + 1) structured array of BNode records, or None."""
+        n = lib().crt_hip_scene_bvh(self._h, None, None)
+        if n < 0:
+            _check(int(n))
+        if n == 0:
+            return None
+        dt = np.dtype([("lo_x", "<f4"), ("hi_x", "<f4"), ("lo_y", "<f4"), ("hi_y", "<f4"), ("lo_z", "<f4"),
+                       ("hi_z", "<f4"), ("skip", "<i4"), ("leaf", "<i4")])
+        nodes = np.zeros((8, n + 1), dt)
+        ids = np.zeros(self.info()["triangle_count"], np.int32)
+        r = lib().crt_hip_scene_bvh(self._h, nodes.ctypes.data, ids.ctypes.data)
+        if r < 0:
+            _check(int(r))
+        return nodes, ids
     def render(self, settings: RendererSettings | None = None, with_stats: bool = False):
         """Blocking render_image: returns float32 [H, W, 3], top row first."""
         st = settings or RendererSettings.default()

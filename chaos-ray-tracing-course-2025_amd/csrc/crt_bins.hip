@@ -955,7 +955,7 @@ int bins_view(crt_hip_scene *sc) {
     }
     bool over = false;   /* some cell over the cap: it walks the BVH */
     for (int c = 0; c < b.ncell; ++c) over = over || b.count[(size_t)c] < 0;
-    if (n_every > kBinMaxEverywhere || total > kBinMeanCap * b.ncell || total >= INT32_MAX / 4 ||
+    if (n_every > kBinMaxEverywhere || total > sc->bins_mean_cap * b.ncell || total >= INT32_MAX / 4 ||
         (over && !sc->ds.bnodes)) {
         bins_free_view(sc);   /* the scene walks the BVH (or the kd tree) */
         return CRT_OK;

@@ -122,6 +122,8 @@ inline float fov_degrees_to_radians(float deg) { return deg * 3.1415926535897932
 /* The secondary-ray BVH over hs's triangles (crt_bvh_build.cpp); needs the
  * mesh prep and prune_G. */
 int build_bvh(HostScene &hs);
+/* scenes above this many triangles get the device-built BVH (crt_lbvh.hip) */
+constexpr size_t kHostBvhMax = (size_t)1 << 18;
 
 /* The topology records of the flattened tree hs.nodes (crt_layout.h KTopo)
  * for crt_bvh.h verify_topo (crt_bvh_build.cpp); none (verify_kd then) if a

@@ -397,10 +397,11 @@ int flatten_tree(const std::vector<BuildNode> &bn, HostScene &hs) {
     return CRT_OK;
 }
 
-/* The BVH (crt_bvh.h): built when the scene makes scattered rays (GI with a
- * diffuse material, reflective or refractive materials), and for any scene
- * small enough that the host build costs little (camera rays may take it,
- * option "traversal" 14). */
+/* The BVH (crt_bvh.h): built on the host when the scene makes scattered rays
+ * (GI with a diffuse material, reflective or refractive materials), and for
+ * any scene small enough that the host build costs little (camera rays may
+ * take it, option "traversal" 14); above kHostBvhMax triangles the upload
+ * builds it on the device instead (crt_lbvh.hip). */
 int maybe_build_bvh_(HostScene &hs);
 double ms_since(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -412,7 +413,8 @@ int maybe_build_bvh(HostScene &hs) {
     return rc;
 }
 int maybe_build_bvh_(HostScene &hs) {
-    bool need = hs.tri_attr.size() <= ((size_t)1 << 18);
+    if (hs.tri_attr.size() > kHostBvhMax) return hs.nodes.empty() ? CRT_OK : build_proof_tables(hs);
+    bool need = true;
     for (const DMaterial &m : hs.materials)
         need = need || m.type == CRT_MATERIAL_REFLECTIVE || m.type == CRT_MATERIAL_REFRACTIVE ||
                (hs.gi_on && m.type == CRT_MATERIAL_DIFFUSE);

@@ -138,7 +138,7 @@ typedef struct crt_scene_info {
     double  tree_build_ms;     /* wall time of the tree build (host: build + flatten into the device layout) */
     /* scene-create cost (wall ms; host scenes: the host parts only) */
     double  prep_ms;           /* host preparation in all: mesh prep, host tree build, BVH */
-    double  bvh_ms;            /* the secondary-ray BVH and proof tables (host) */
+    double  bvh_ms;            /* the secondary-ray BVH and proof tables (host; + the device build, bvh_on_device) */
     double  bins_ms;           /* camera-bins setup: templates, buffers, the sizing pass (device) */
     double  upload_ms;         /* upload to every device (incl. device tree build and bins setup) */
     double  create_ms;         /* the whole crt_hip_scene_create* call */
@@ -155,6 +155,9 @@ typedef struct crt_scene_info {
     double  multi_probe_ms;    /* wall time of that probe (two 64x36 frames and two view rebuilds) */
     int64_t bins_binnings;     /* camera-bins binnings run (frames, plus the test hooks') */
     int64_t bins_reuses;       /* frames that rendered the last binning's lists (same camera; option "bins_reuse") */
+    int32_t bvh_on_device;     /* 1: the BVH was built on the device (crt_lbvh.hip, > 2^18 triangles; its
+                                * time is in bvh_ms) */
+    int32_t bvh_depth;         /* ... its deepest node (root 0), 0 for the host build */
 } crt_scene_info;
 
 typedef struct crt_render_stats {
@@ -301,6 +304,12 @@ void crt_hip_render_image_tree_reset(void);
  * crt_host_scene_tree (sizes from crt_hip_scene_info). */
 int  crt_hip_scene_tree(const crt_hip_scene *scene, float *bounds, int32_t *children, int64_t *leaf_offsets,
                         int32_t *leaf_tris);
+/* The secondary-ray BVH (crt_bvh.h; test hook): its node count N (returned;
+ * 0 without a BVH) and, when the pointers are non-null, the 8 octant orders
+ * of N + 1 32-B records each (crt_layout.h BNode: 6 floats lo_x hi_x lo_y hi_y
+ * lo_z hi_z, skip, leaf = first * 16 + count) and the triangle id of every
+ * leaf position (id | back_face_culling << 31; triangle_count entries). */
+int64_t crt_hip_scene_bvh(const crt_hip_scene *scene, void *nodes_out, int32_t *tri_ids_out);
 /* Copy a prepared scene into HBM of `device` (the host scene may be destroyed after). */
 int  crt_hip_scene_upload(const crt_host_scene *hs, int device, crt_hip_scene **out);
 int  crt_hip_scene_info(const crt_hip_scene *scene, crt_scene_info *out);

@@ -100,13 +100,15 @@ def c5_1m():
 @pytest.mark.parametrize("w,h", [(64, 36), (160, 90)])
 def test_c5_1m_triangles(N, oracle, c5_1m, w, h):
     """C5's 1M-triangle mesh (880,933 nodes, device-built tree) rendered
-    through the pruned walks, bit for bit against the oracle."""
+    through the device-built BVH (crt_lbvh.hip) and the proof on the
+    device-built tree, bit for bit against the oracle."""
     sc = c5_1m
     sc.desc().camera.width, sc.desc().camera.height = w, h
     st = N.RendererSettings.default()
     gpu = N.HipScene(sc)
     info = gpu.info()
     assert info["tree_on_device"] == 1 and info["node_count"] == 880_933
+    assert info["bvh_on_device"] == 1
     got = gpu.render(st)
     want = oracle.OracleScene(sc).render(st)
     rmse, nbad = compare(got, want)
