@@ -789,6 +789,21 @@ static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
     } else if (k == "rec_machine") {
         sc->rec_machine = value != 0;
         sc->calib_walk = -1;
+    } else if (k == "wf_rpw_lane") {
+        if (value < 1 || value > 64) return set_error(CRT_E_INVALID, "wf_rpw_lane must be 1..64");
+        HIP_TRY(hipDeviceSynchronize());
+        sc->wf_rpw_lane = (int)value;
+        wf_graphs_clear(sc->wf);
+        sc->wf.recs.clear();
+        return CRT_OK;
+    } else if (k == "wf_window") {
+        if (sc->wf_window != (value != 0)) {
+            HIP_TRY(hipDeviceSynchronize());
+            sc->wf_window = value != 0;
+            wf_graphs_clear(sc->wf);   /* graphs hold the level kernels */
+            sc->wf.recs.clear();
+        }
+        return CRT_OK;
     } else if (k == "bins_reuse") {   /* no plan depends on it */
         sc->bins_reuse = value != 0;
         return CRT_OK;

@@ -42,8 +42,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
     } else {
         const int ray0 = (gid >> 6) * lv.rpw;
         if (ray0 >= lv.n) return;          /* whole wave past the queue */
-        const int ray = ray0 + lane;
-        has = lane < lv.rpw && ray < lv.n;
+        /* TRAV 16: a ray per group of four lanes (the BVH window walk) */
+        const int ray = ray0 + (TRAV == 16 ? lane >> 2 : lane);
+        has = (TRAV == 16 ? (lane >> 2) : lane) < lv.rpw && ray < lv.n;
         if (has) {
             const WRay r = lv.in[ray];
             o = vec(r.ox, r.oy, r.oz);
@@ -53,11 +54,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         }
     }
     LaneCounts cnt = {};
-    constexpr bool kCoop = kIsCoop<TRAV>;
+    constexpr bool kCoop = TRAV != 16 && kIsCoop<TRAV>;
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
     int slot;
-    slot = trace<TRAV, COUNT>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has, o, d, t, cnt);
+    if constexpr (TRAV == 16) {   /* four lanes walk the group's ray; the first shades it */
+        slot = trace_bvh_window<COUNT, 4>(s, lane & 3, has, o, d, t, cnt);
+        has = has && (lane & 3) == 0;
+    } else {
+        slot = trace<TRAV, COUNT>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has, o, d, t, cnt);
+    }
 
     WNode node = {wFinal, -1, -1, 0, 0.f, 0.f, 0.f, 0.f};
     Vec col = vec(0.f, 0.f, 0.f);

@@ -256,6 +256,8 @@ struct crt_hip_scene {
     int calib_deferred_walk = -1;  /* walk whose first frame skipped the calibration */
     int bins_on = 1;               /* camera frames take the camera bins where built (walk 15; option "bins") */
     int64_t bins_mean_cap = crt_amd::kBinMeanCap;   /* candidates per cell on average, at most (env CRT_BINS_MEAN_CAP) */
+    int wf_rpw_lane = 64;          /* rays per wave of levels >= 1 on the per-lane BVH walk (option "wf_rpw_lane") */
+    int wf_window = 0;             /* wavefront levels >= 1: the BVH window walk, four lanes a ray (option "wf_window") */
     int bvh_device = 1;            /* build the BVH on the device above kHostBvhMax triangles (env CRT_BVH_DEVICE=0: not) */
     int bins_slack = 100;          /* camera-bins grid slots per kind: the sizing pass's count + this % (option "bins_slack") */
     int bins_reuse = 1;            /* a frame whose camera the last binning used renders its lists (option "bins_reuse") */

@@ -43,12 +43,15 @@ def compare(got, want):
     return rmse, nbad
 
 
-def test_c3_full_frame(N, oracle):
-    """C3 at its own size: 1920x1080, max_ray_depth 8 (wavefront levels)."""
+@pytest.mark.parametrize("window", [0, 1], ids=["lane-walk", "window-walk"])
+def test_c3_full_frame(N, oracle, window):
+    """C3 at its own size: 1920x1080, max_ray_depth 8 (wavefront levels; levels
+    >= 1 through the per-lane BVH walk, or the window walk of four lanes a ray,
+    option wf_window)."""
     h = HASHES["C3"]
     sc = scene_npz(h["scene"])
     st = N.RendererSettings.default(**h["settings"])
-    gpu = N.HipScene(sc)
+    gpu = N.HipScene(sc, wf_window=window)
     got = gpu.render(st)
     assert got.shape == (1080, 1920, 3)
     want = oracle.OracleScene(sc).render(st)
