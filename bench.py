@@ -92,6 +92,8 @@ def parse(argv=None):
     p.add_argument("--height", type=int, default=None, help="override the config's image height")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample, all cores (wall s)")
     p.add_argument("--cpu-single-seconds", type=float, default=6.0, help="bounded single-core CPU sample (wall s)")
+    p.add_argument("--no-cpu-full", action="store_true",
+                   help="skip the CPU baseline's full-size frame (configs whose sample is a reduced size: C4, C5)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (render + D2H) timing")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo stages "
@@ -121,7 +123,7 @@ def parse(argv=None):
                    help="bracket every k-th render of the timed region with HIP events (kernel time sample; "
                         "an event pair between two renders costs ~7 us of a ~165 us C2 step)")
     p.add_argument("--pmc-json", default=None,
-                   help="PMC record of the render kernel (profiles/r04/pmc_<config>.json by default); used for "
+                   help="PMC record of the render kernel (profiles/r05/pmc_<config>.json by default); used for "
                         "the issue roofline and measured HBM traffic when its build id equals the library's")
     p.add_argument("--selftest-launch", action="store_true",
                    help="launcher plumbing only: ranks join the process group and report; no GPU work")
@@ -175,6 +177,11 @@ def cpu_worker(spec: dict) -> dict:
     st = RendererSettings.default(**cfg["settings"])
     orc = pyoracle.OracleScene(scene).set_shadows(bool(spec.get("shadows")))
     wc = WorkCounts()
+    if spec.get("once"):   # one timed frame (a full-size frame of minutes), its rays counted in it
+        s = time.perf_counter()
+        orc.render(st, nthreads=spec["threads"], counts=wc)
+        el = time.perf_counter() - s
+        return {"rays_per_frame": int(wc.traversals), "frames": 1, "best_s": el, "median_s": el, "wall_s": el}
     orc.render(st, nthreads=spec["threads"], counts=wc)      # warm-up frame, and the frame's ray count
     rays = int(wc.traversals)
     times = []
@@ -213,12 +220,14 @@ def cpu_info() -> dict:
 
 
 def cpu_baseline(config: str, w: int, h: int, seconds: float, single_seconds: float, size_note: str,
-                 shadows: bool = False) -> dict:
+                 shadows: bool = False, full: tuple | None = None) -> dict:
     """Legs: hardware_concurrency() threads (the affinity mask, as
     crt_renderer.cpp:178 would spawn), threads = the cgroup CPU quota when it
     is smaller (what the box actually grants: `value` is the better of the
     two, `cores` its thread count, `effective_cpus` the quota), and one
-    pinned core."""
+    pinned core.  full = (W, H): the sample is a reduced size; one frame at
+    the benched size on the quota's threads is timed too (`full_size`, with
+    its per-ray rate against the sample's)."""
     info = cpu_info()
     affinity = info["affinity_cpus"]
     quota = info["cgroup_cpu_quota"]
@@ -233,6 +242,15 @@ def cpu_baseline(config: str, w: int, h: int, seconds: float, single_seconds: fl
     rays = legs[affinity]["rays_per_frame"]
     best_n = min(legs, key=lambda n: legs[n]["median_s"])
     multi = legs[best_n]
+    full_leg = None
+    if full:
+        f = run_cpu_worker({"config": config, "w": full[0], "h": full[1], "threads": best_n, "pin": None,
+                            "seconds": 0, "min_frames": 1, "shadows": shadows, "once": True})
+        fv = f["rays_per_frame"] / f["median_s"] / 1e6
+        full_leg = {"w": full[0], "h": full[1], "threads": best_n, "frames": 1, "rays": f["rays_per_frame"],
+                    "frame_ms": round(f["median_s"] * 1e3, 1), "value": round(fv, 3), "unit": "Mrays/s",
+                    "per_ray_vs_sample": round(fv / (rays / multi["median_s"] / 1e6), 4),
+                    "note": "one whole frame at the benched size (no warm-up frame), the same oracle and threads"}
     return {
         "value": round(rays / multi["median_s"] / 1e6, 3), "unit": "Mrays/s", "cores": best_n, "kind": "port",
         "effective_cpus": effective, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
@@ -245,6 +263,7 @@ def cpu_baseline(config: str, w: int, h: int, seconds: float, single_seconds: fl
                         "frame_ms_median": round(single["median_s"] * 1e3, 3), "frames": single["frames"],
                         "pinned_cpu": pin},
         "cpu_model": info["model"],
+        "full_size": full_leg,
         "sample": f"{multi['frames']} whole frames{size_note} of the same workload, oracle/crt_oracle.cpp "
                   f"render_image (24-px bucket queue, g++ -O3, no FMA) in a child process on {info['model']}: "
                   f"{best_n} threads (legs: {', '.join(f'{n} threads' for n in sorted(legs))}; the affinity mask "
@@ -344,7 +363,7 @@ def roofline_block(kernel_ms: float, counts: dict, waves: dict, npx: int, pmc: d
 
 
 def load_pmc(path: str | None, config: str, w: int, h: int) -> dict | None:
-    p = Path(path) if path else ROOT / "profiles" / "r04" / f"pmc_{config}.json"
+    p = Path(path) if path else ROOT / "profiles" / "r05" / f"pmc_{config}.json"
     try:
         d = json.loads(p.read_text())
     except (OSError, ValueError):
@@ -719,7 +738,8 @@ def main():
         if world == 1 and not a.no_cpu_baseline:
             cw, ch = cfg["cpu_size"] if (W, H) == cfg["size"] else (W, H)
             note = "" if (cw, ch) == (W, H) else f" at {cw}x{ch} (same scene and settings; Mrays/s is per-ray work)"
-            cpu = cpu_baseline(a.config, cw, ch, a.cpu_seconds, a.cpu_single_seconds, note, a.shadows)
+            cpu = cpu_baseline(a.config, cw, ch, a.cpu_seconds, a.cpu_single_seconds, note, a.shadows,
+                               full=(W, H) if (cw, ch) != (W, H) and not a.no_cpu_full else None)
         parallel = {"single": "single-gpu", "tiles": f"bucket-shard{world}+{'rccl' if dist_backend == 'nccl' else dist_backend}"
                     f"-gather-{a.shards}-{a.payload}", "frames": f"frame-parallel{world}"}[mode]
         out = {

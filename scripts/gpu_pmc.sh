@@ -1,7 +1,7 @@
 #!/bin/bash
 # Kernel trace + PMC passes (one counter group per pass, MI355X_MICROARCH.md)
 # of one config's render kernel -> gpurun_out/<TAG>/pmc_<CFG>.json (bench.py
-# reads profiles/r04/pmc_<CFG>.json when its build id equals the library's).
+# reads profiles/r05/pmc_<CFG>.json when its build id equals the library's).
 #   TAG=x CFG=c4 KERNEL=k_render_refill SIZE="3840 2160" LAST=2 CMD="scripts/render_loop.py ..." bash scripts/gpu_pmc.sh
 set -u
 cd "$(dirname "$0")/.."
