@@ -1083,6 +1083,11 @@ int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
  * waits for the binning if it ran elsewhere. */
 int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *par_out, bool force) {
     BinsDev &b = sc->bins;
+    static const bool trace = std::getenv("CRT_BINS_TRACE") != nullptr;   /* diagnostics: each decision on stderr */
+    if (trace)
+        std::fprintf(stderr, "bins_enqueue plan=%p work=%p waves=%d last=%d binned=%p frame=%llu force=%d cam_same=%d\n",
+                     (const void *)&plan, (const void *)plan.bp.work, plan.waves, b.last, b.binned_plan,
+                     (unsigned long long)b.frame, (int)force, (int)(std::memcmp(&b.binned, &b.cam, sizeof b.cam) == 0));
     if (!force && sc->bins_reuse && b.last >= 0 && b.binned_plan == plan.bp.work && plan.bp.work &&
         std::memcmp(&b.binned, &b.cam, sizeof b.cam) == 0) {
         const int par = b.last;
@@ -1125,6 +1130,48 @@ int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *p
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(b.bdone[par], bs));
     b.bdone_s[par] = bs;
+#ifdef CRT_BINS_CHECK
+    {   /* diagnostic builds: this binning's violations before its render runs,
+         * and the render's inputs read back and checked on the host */
+        const int rc1 = bins_dbg_arm(sc, plan);
+        if (rc1 != CRT_OK) return rc1;
+        if (plan.bp.work) {
+            const BinsPlan &q = plan.bp;
+            std::vector<int32_t> ph((size_t)kBinsPhdrInts), ln((size_t)b.ncell), of((size_t)b.ncell);
+            std::vector<BinsWork> wk((size_t)q.wslots);
+            HIP_TRY(hipMemcpy(ph.data(), q.phdr, ph.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(wk.data(), q.work + (size_t)par * q.wslots, wk.size() * sizeof(BinsWork),
+                              hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(ln.data(), b.len + (size_t)par * b.ncell, ln.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(of.data(), b.off + (size_t)par * b.ncell, of.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+            int bad = 0;
+            const int64_t rtot = (int64_t)kBinSets * b.rec_cap;
+            for (int k2 = 0; k2 < kBinKinds; ++k2)
+                for (int s3 = 0; s3 < kBinShards; ++s3) {
+                    const int n = std::min(ph[(size_t)bins_phdr_at(par, k2, s3)], q.ecap);
+                    for (int i = 0; i < n; ++i) {
+                        const BinsWork &w = wk[(size_t)q.wbase[k2] + (size_t)s3 * q.ecap + i];
+                        bool ok = w.cell >= 0 && w.cell < b.ncell && w.len >= -1 && w.len <= kBinCellCap &&
+                                  (w.len < 0 || (w.off >= 0 && (int64_t)w.off + w.len <= rtot));
+                        bool found = false;
+                        for (const Tile &t : plan.tiles)
+                            if (std::memcmp(&t, &w.t, sizeof t) == 0) found = true;
+                        if ((!ok || !found) && bad++ < 8)
+                            std::fprintf(stderr, "bins check: kind %d shard %d entry %d cell %d off %d len %d tile (%d %d %d %d) %s\n",
+                                         k2, s3, i, w.cell, w.off, w.len, w.t.x, w.t.y, w.t.w, w.t.h,
+                                         found ? "" : "NOT A PLAN TILE");
+                    }
+                }
+            for (int c = 0; c < b.ncell; ++c)
+                if (ln[(size_t)c] > 0 && (of[(size_t)c] < 0 || (int64_t)of[(size_t)c] + ln[(size_t)c] > rtot) && bad++ < 16)
+                    std::fprintf(stderr, "bins check: cell %d off %d len %d\n", c, of[(size_t)c], ln[(size_t)c]);
+            std::fprintf(stderr, "bins check: plan %p set %d: %d bad\n", (const void *)&plan, par, bad);
+            if (bad) return set_error(CRT_E_STATE, "bins check: bad render inputs");
+            if (const char *e = std::getenv("CRT_BINS_NORENDER"))   /* from this binning on: no render */
+                if ((long long)b.frame - 1 >= std::atoll(e)) return set_error(CRT_E_STATE, "bins check: render skipped");
+        }
+    }
+#endif
     if (overlap) HIP_TRY(hipStreamWaitEvent(s, b.bdone[par], 0));
     b.last = par;
     b.binned = b.cam;

@@ -341,6 +341,7 @@ void free_plans(crt_hip_scene *sc) {
     sc->full = ShardPlan{};
     sc->shard_plans.clear();
     sc->bins.last = -1;   /* the work lists were the freed plans' */
+    if (std::getenv("CRT_BINS_TRACE")) std::fprintf(stderr, "free_plans\n");
     sc->compact_plans.clear();
 }
 
@@ -1069,6 +1070,10 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         BinsPlan bp = plan.bp;
         bp.par = par;
         bp.work += (size_t)par * bp.wslots;   /* this frame's set of the work lists */
+        static const bool trace = std::getenv("CRT_BINS_TRACE") != nullptr;   /* diagnostics on stderr */
+        if (trace)
+            std::fprintf(stderr, "launch bins plan=%p ntiles=%d waves=%d par=%d out=%p stream=%p\n", (const void *)&plan,
+                         plan.ntiles, plan.waves, par, (void *)d_out, (void *)stream);
         const unsigned bb = (unsigned)((plan.waves + 3) / 4);
 #define CRT_LAUNCH_B(COUNT)                                                                                 \
     hipLaunchKernelGGL((k_render_tiles<false, 0, 15, 15, COUNT>), dim3(bb), dim3(256), 0, stream, d_scene, ds, \

@@ -37,7 +37,13 @@ __device__ __forceinline__ void bins_quarter(Tile &tl, int q, int quad) {
 
 __device__ __forceinline__ int bins_tile(const BinsPlan &bp, const Tile *__restrict__ tiles, int wave, Tile &tl,
                                          int &off, int &len, BinsNext &next) {
+    /* no further entry unless a list slot below sets them (a rest tile's
+     * continuation must end the kernel's loop: i + step >= n) */
+    next.work = nullptr;
+    next.i = 0;
     next.n = 0;
+    next.step = 1;
+    next.q = -1;
     int kind = 0, slot = wave >> 2, q = wave & 3;
     if (wave >= 4 * kBinShards * bp.gcap[0]) {
         slot = wave - 4 * kBinShards * bp.gcap[0];
