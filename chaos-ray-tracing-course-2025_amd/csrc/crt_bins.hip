@@ -196,11 +196,12 @@ constexpr int kMaxGroups = 8192;   /* 2^18 triangles (bins are built up to the B
 __device__ void bins_pairs(const BinItem *__restrict__ items, const int32_t *__restrict__ tpref,
                            const int32_t *__restrict__ gsum, const int32_t *__restrict__ rem, int nt, int tx,
                            int32_t *__restrict__ cnt, uint64_t *__restrict__ keys, int32_t *__restrict__ nonempty,
-                           int32_t *__restrict__ bigl, int cap_shard, BinsHdr *__restrict__ hdr, int bid, int nblk) {
+                           int32_t *__restrict__ bigl, int cap_shard, BinsHdr *__restrict__ hdr, int bid, int nblk,
+                           int qmax) {
     __shared__ int32_t gp[kMaxGroups + 1];
     __shared__ int32_t part[256];
     const int tid = (int)threadIdx.x;
-    const int nq = min(hdr->nrem.v, kMaxGroups);   /* k_bins_project queues no more (the rest scatter themselves) */
+    const int nq = min(hdr->nrem.v, qmax);   /* k_bins_project queues no more (the rest scatter themselves) */
     /* exclusive prefix of the queued groups' remaining counts: each thread sums a run, then the runs are scanned */
     const int per = (nq + 255) / 256, g0 = tid * per, g1 = min(nq, g0 + per);
     int run = 0;
@@ -389,7 +390,7 @@ __global__ __launch_bounds__(256) void k_bins_project(const CamCand *__restrict_
         int qd = 0;
         if (G > kExpand && queue) {
             const int k = atomicAdd(&hdr->nrem.v, 1);
-            if (k < kMaxGroups) {
+            if (k < queue) {   /* (queue: the groups k_bins_pairs takes, <= kMaxGroups) */
                 rem[BCK(k, BDBG(nt), 38)] = (int)blockIdx.x;
                 qd = 1;
             }
@@ -559,9 +560,9 @@ __global__ __launch_bounds__(256) void k_bins_pairs(const BinItem *__restrict__ 
                                                     int nt, int tx, int32_t *__restrict__ cnt,
                                                     uint64_t *__restrict__ keys, int32_t *__restrict__ nonempty,
                                                     int32_t *__restrict__ bigl, int cap_shard, BinsHdr *__restrict__ hdr2,
-                                                    int par) {
+                                                    int par, int qmax) {
     bins_pairs(items, tpref, gsum, rem, nt, tx, cnt, keys, nonempty, bigl, cap_shard, hdr2 + par, (int)blockIdx.x,
-               (int)gridDim.x);
+               (int)gridDim.x, qmax);
 }
 
 /* A cell into its work list (BinsPlan): one lane. */
@@ -836,12 +837,12 @@ int launch_project(crt_hip_scene *sc, hipStream_t s, int par, int32_t *phdr) {
     hipLaunchKernelGGL(k_bins_project, dim3((unsigned)groups), dim3(256), 0, s, b.tpl, b.nt, b.cam, b.items, b.tpref,
                        b.gsum, b.every, b.hdr, par, phdr, b.len + (size_t)par * b.ncell, b.ncell, b.tx, b.cnt, b.keys,
                        b.nonempty, b.bigl,
-                       b.cap_shard, b.rem, b.pair_blocks > 0 ? 1 : 0);
+                       b.cap_shard, b.rem, b.pair_blocks > 0 ? b.qmax : 0);
     HIP_TRY(hipGetLastError());
     if (b.pair_blocks > 0) {
         hipLaunchKernelGGL(k_bins_pairs, dim3((unsigned)b.pair_blocks), dim3(256), 0, s, b.items, b.tpref, b.gsum,
                            b.rem, b.nt, b.tx, b.cnt + (size_t)par * b.ncell * kCntStride, b.keys, b.nonempty, b.bigl,
-                           b.cap_shard, b.hdr, par);
+                           b.cap_shard, b.hdr, par, b.qmax);
         HIP_TRY(hipGetLastError());
     }
     return CRT_OK;
@@ -883,6 +884,8 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
     /* per triangle, kept for every view: the records' static parts and the
      * projection's scratch */
     b.nt = (int)hs.tri_attr.size();
+    b.qmax = kMaxGroups;   /* tests lower it (CRT_BINS_QMAX): the groups past it scatter their own pairs */
+    if (const char *e = std::getenv("CRT_BINS_QMAX")) b.qmax = std::max(1, std::min(kMaxGroups, std::atoi(e)));
     std::vector<CamCand> tpl;
     bin_templates(hs, tpl);
     int rc;

@@ -20,6 +20,7 @@
  */
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <limits>
 #include <vector>
 
@@ -391,7 +392,9 @@ int build_camera_bins(const HostScene &hs, std::vector<CamCand> &bins, std::vect
         if (cnt[(size_t)c] > kBinCellCap) ov[(size_t)c] = 1;   /* this cell's pixels walk the BVH */
         else total += cnt[(size_t)c];
     }
-    if (total > kBinMeanCap * ncell || total >= (int64_t)std::numeric_limits<int32_t>::max()) return CRT_OK;
+    int64_t mean_cap = kBinMeanCap;   /* the device's cap (crt_api.hip: env CRT_BINS_MEAN_CAP) */
+    if (const char *e = std::getenv("CRT_BINS_MEAN_CAP")) mean_cap = std::max<int64_t>(1, std::atoll(e));
+    if (total > mean_cap * ncell || total >= (int64_t)std::numeric_limits<int32_t>::max()) return CRT_OK;
     off.assign((size_t)ncell + 1, 0);
     for (int64_t c = 0; c < ncell; ++c) off[(size_t)c + 1] = off[(size_t)c] + (ov[(size_t)c] ? 0 : (int32_t)cnt[(size_t)c]);
     bins.resize((size_t)total);

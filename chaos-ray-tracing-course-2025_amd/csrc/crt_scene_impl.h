@@ -57,6 +57,7 @@ struct BinsDev {
     int32_t *gsum = nullptr;              /* per group: pairs */
     int32_t *rem = nullptr;               /* groups queued for k_bins_pairs */
     int pair_blocks = 0;                  /* k_bins_pairs grid (0: not launched; the sizing pass queued none) */
+    int qmax = 8192;                      /* groups k_bins_pairs takes (kMaxGroups; env CRT_BINS_QMAX lowers it) */
     int32_t *cnt = nullptr;               /* per cell: candidates; kBinSets sets (a frame zeroes the next one's) */
     uint64_t *keys = nullptr;             /* per cell: kBinCellCap sort keys (dmin bits << 32 | triangle id) */
     int32_t *every = nullptr;             /* everywhere triangles */
