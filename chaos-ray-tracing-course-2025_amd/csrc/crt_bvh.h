@@ -41,7 +41,13 @@
 #define CRT_PROOF_TOPO 1     /* 0: the proof descends the 32-B nodes (verify_kd) even where KTopo exists */
 #endif
 #ifndef CRT_BVH_PREFETCH
-#define CRT_BVH_PREFETCH 1
+#define CRT_BVH_PREFETCH 1   /* walk_bvh: 0 none, 1 both successor nodes, 2 + the node's first triangle, 3 + its second */
+#endif
+#ifndef CRT_WALK_HOOK
+#define CRT_WALK_HOOK()        /* diagnostic builds: after step 1 (crt_render_wf.hip CRT_WF_STAMPS) */
+#endif
+#ifndef CRT_FALLBACK_HOOK
+#define CRT_FALLBACK_HOOK()    /* diagnostic builds: when step 3 runs */
 #endif
 #ifndef CRT_PROOF_TOPO2
 #define CRT_PROOF_TOPO2 1    /* 0: the proof's descent loads one KTopo a level even where KTopo2 exists */
@@ -78,7 +84,7 @@ CRT_HD bool bnode_alive(const BNode &n, const PruneRay &p, float lim) {
 /* Step 1: closest reference hit over all triangles.  Returns the triangle id
  * (-1: no triangle is hit), its t, and tie = another triangle hits at the
  * same t (each triangle is in the BVH once, so an equal t is another one). */
-template <bool COUNT, bool PF = (CRT_BVH_PREFETCH != 0)>
+template <bool COUNT, int PF = CRT_BVH_PREFETCH>
 CRT_HD int walk_bvh(const BNode *nodes, int n, const DTriGeo *geo, const int32_t *tid, Vec o, Vec d,
                     const PruneRay &pr, float &best_t, bool &tie, WalkCounts &c) {
     int best = -1;
@@ -90,31 +96,54 @@ CRT_HD int walk_bvh(const BNode *nodes, int n, const DTriGeo *geo, const int32_t
      * tested: the walk is a chain of dependent loads, and each step's test
      * then overlaps the next step's load (every order ends with a zero
      * record, so i + 1 <= n and skip <= n are always in bounds).  Pays on
-     * scattered rays (C3); the coherent camera rays of C2 walk without it. */
+     * scattered rays (C3); the coherent camera rays of C2 walk without it.
+     * PF 2: the node's first triangle too (an interior node's leaf field is 0:
+     * triangle 0, a valid address), so an alive leaf costs no extra load. */
     BNode cur, n1, n2;
-    if constexpr (PF) cur = CRT_LDG(nodes, 0);
+    DTriGeo g0, g1;
+    int32_t id0 = 0, id1 = 0;
+    if constexpr (PF > 0) cur = CRT_LDG(nodes, 0);
     while (i < n) {
         BNode nd;
-        if constexpr (PF) {
+        if constexpr (PF > 0) {
             nd = cur;
             n1 = CRT_LDG(nodes, i + 1);
             n2 = CRT_LDG(nodes, nd.skip);
+            if constexpr (PF > 1) {
+                g0 = CRT_LDG(geo, nd.leaf >> 4);
+                id0 = CRT_LDG(tid, nd.leaf >> 4);
+            }
+            if constexpr (PF > 2) {   /* and its second (a one-triangle leaf: the next leaf's first, in bounds) */
+                const int f1 = (nd.leaf >> 4) + ((nd.leaf & 15) > 1 ? 1 : 0);
+                g1 = CRT_LDG(geo, f1);
+                id1 = CRT_LDG(tid, f1);
+            }
         } else {
             nd = CRT_LDG(nodes, i);
         }
         if (COUNT) ++c.nodes;
         if (!bnode_alive(nd, pr, lim)) {
             i = nd.skip;
-            if constexpr (PF) cur = n2;
+            if constexpr (PF > 0) cur = n2;
             continue;
         }
         ++i;                                   /* interior: first child; leaf: next in preorder */
-        if constexpr (PF) cur = n1;
+        if constexpr (PF > 0) cur = n1;
         const int cnt = nd.leaf & 15;
         const int first = nd.leaf >> 4;
         for (int k = 0; k < cnt; ++k) {
-            const DTriGeo g = CRT_LDG(geo, first + k);
-            const int32_t id = CRT_LDG(tid, first + k);
+            DTriGeo g;
+            int32_t id;
+            if (PF > 1 && k == 0) {
+                g = g0;
+                id = id0;
+            } else if (PF > 2 && k == 1) {
+                g = g1;
+                id = id1;
+            } else {
+                g = CRT_LDG(geo, first + k);
+                id = CRT_LDG(tid, first + k);
+            }
             const uint8_t cull = (uint8_t)((uint32_t)id >> 31);
             float t;
             if (COUNT) ++c.tris;
@@ -563,6 +592,7 @@ CRT_HD int resolve_closest(const DNode *nodes, const PNode *pnodes, int n, const
         }
     }
     if (fb) *fb = true;
+    CRT_FALLBACK_HOOK();
     return walk_pruned<COUNT>(pnode_order(pnodes, n, ray_octant(d)), n, slots, slot_cull, o, d, rr, pr, best_t, c);
 }
 
@@ -570,7 +600,7 @@ CRT_HD int resolve_closest(const DNode *nodes, const PNode *pnodes, int n, const
  * numbering, -1: miss) by steps 1-3.  fb (optional) is set when step 3 ran.
  * Rays with a NaN component miss every cell (each face test reads a NaN
  * coordinate), so they are answered without a walk. */
-template <bool COUNT, bool PF = (CRT_BVH_PREFETCH != 0)>
+template <bool COUNT, int PF = CRT_BVH_PREFETCH>
 CRT_HD int trace_bvh_exact(const BNode *bnodes, int bn, const DTriGeo *btri, const int32_t *btri_id,
                            const DNode *nodes, const PNode *pnodes, int n, const DTriGeo *slots,
                            const uint8_t *slot_cull, const int32_t *slot_tri, const KTopo *ktopo,
@@ -585,6 +615,7 @@ CRT_HD int trace_bvh_exact(const BNode *bnodes, int bn, const DTriGeo *btri, con
     bool tie = false;
     float t = 0.0f;
     const int tri = walk_bvh<COUNT, PF>(bnode_order(bnodes, bn, oct), bn, btri, btri_id, o, d, pr, t, tie, c);
+    CRT_WALK_HOOK();
     return resolve_closest<COUNT>(nodes, pnodes, n, slots, slot_cull, slot_tri, ktopo, planes_ok, o, d, pr, tri, t, tie,
                                   best_t, c, fb, ktopo2);
 }

@@ -741,6 +741,9 @@ int wf_streams(WfBuffers &wb, hipStream_t stream) {
  * back 1.20 ms with 2 sets/2 streams, 1.07 with 4/4, 0.93 with 8/8, 0.89
  * with 12/12, 0.90 with 16/16; sets sharing streams were slower
  * (profiles/r04/ab_wf_sets.txt). */
+#ifdef CRT_WF_STAMPS
+int wf_stamps_dump(const char *fn, int levels);
+#endif
 int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_settings *st, const ShardPlan &plan,
                      float *d_out, hipStream_t stream, bool count, const DeviceScene *d_scene, int sec, int primary) {
     WfBuffers &wb = sc->wf;
@@ -850,6 +853,12 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
             HIP_TRY(hipEventRecord(w.flag_ev, stream));
             w.flag_pending = true;
         }
+#ifdef CRT_WF_STAMPS
+        if (const char *fn = std::getenv("CRT_WF_STAMPS_FILE")) {
+            HIP_TRY(hipStreamSynchronize(stream));
+            if (wf_stamps_dump(fn, kMaxLevels) != 0) return CRT_E_HIP;
+        }
+#endif
         return CRT_OK;
     };
     /* a recorded-size frame's levels are a fixed launch sequence: replayed

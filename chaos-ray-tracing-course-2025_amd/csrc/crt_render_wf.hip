@@ -6,10 +6,96 @@
  * LLVM scheduling strategy (Makefile WF_SCHED).
  */
 #define CRT_KERNEL_TU 1
+/* the wavefront levels' BVH walk also loads each node's first triangle with
+ * its successors (crt_bvh.h walk_bvh PF 2): an alive leaf then costs no load
+ * round of its own (C3 lone frame 1.84 -> 1.77 ms; both triangles, PF 3: 1.81) */
+#ifndef CRT_BVH_PREFETCH
+#define CRT_BVH_PREFETCH 2
+#endif
+#ifdef CRT_WF_STAMPS
+/* diagnostic builds only: per level and wave, s_memrealtime (100 MHz) at the
+ * wave's start, once its BVH walk is done (crt_bvh.h CRT_WALK_HOOK), once its
+ * trace is done (proof and fallbacks) and at its end, and how many of its
+ * lanes ran the fallback walk (CRT_FALLBACK_HOOK) */
+#include <hip/hip_runtime.h>
+namespace crt_amd {
+__device__ __forceinline__ unsigned long long *wf_phase_lds() {
+    __shared__ unsigned long long p[4][2];
+    return &p[threadIdx.x >> 6][0];
+}
+}  // namespace crt_amd
+#if defined(__HIP_DEVICE_COMPILE__)
+#define CRT_WALK_HOOK()                                                                                  \
+    do {                                                                                                 \
+        if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1)                              \
+            crt_amd::wf_phase_lds()[0] = __builtin_amdgcn_s_memrealtime();                                \
+    } while (0)
+#define CRT_FALLBACK_HOOK() atomicAdd(&crt_amd::wf_phase_lds()[1], 1ull)
+#endif
+#endif
 #include "crt_kernels.h"
 #include "crt_shade.h"
+#ifdef CRT_WF_STAMPS
+#include <cstdio>
+#include <vector>
+#endif
 
 namespace crt_amd {
+
+#ifdef CRT_WF_STAMPS
+/* per level and wave: start, walk done, trace done, end, fallback lanes;
+ * COUNT frames: the sum and the max over its lanes of node + triangle tests */
+constexpr int kWfStampWaves = 65536;
+__device__ unsigned long long g_wf_stamps[16][kWfStampWaves][7];
+int wf_stamps_dump(const char *fn, int levels) {
+    std::vector<unsigned long long> h((size_t)16 * kWfStampWaves * 7);
+    if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_wf_stamps), h.size() * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    FILE *f = std::fopen(fn, "w");
+    if (!f) return -1;
+    for (int L = 0; L < levels && L < 16; ++L)
+        for (int w = 0; w < kWfStampWaves; ++w) {
+            const unsigned long long *e = &h[((size_t)L * kWfStampWaves + w) * 7];
+            if (e[0])
+                std::fprintf(f, "%d %d %llu %llu %llu %llu %llu %llu %llu\n", L, w, e[0], e[1], e[2], e[3], e[4], e[5], e[6]);
+        }
+    std::fclose(f);
+    std::fill(h.begin(), h.end(), 0ull);   /* the next frame's stamps start clean */
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_wf_stamps), h.data(), h.size() * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#define WF_SLOT g_wf_stamps[LEVEL0 ? 0 : min(lv.depth, 15)][gid >> 6]
+/* k: 0 start, 1 walk done (from LDS), 2 trace done, 3 end (+ the fallback count) */
+#define WF_STAMP(k)                                                                                      \
+    do {                                                                                                 \
+        if (k == 0 && lane == 0) {                                                                       \
+            wf_phase_lds()[0] = 0;                                                                       \
+            wf_phase_lds()[1] = 0;                                                                       \
+        }                                                                                                \
+        if (lane == 0 && (gid >> 6) < kWfStampWaves) {                                                   \
+            if (k == 2) WF_SLOT[1] = wf_phase_lds()[0];                                                  \
+            if (k == 3) WF_SLOT[4] = wf_phase_lds()[1];                                                  \
+            WF_SLOT[k == 0 ? 0 : k] = __builtin_amdgcn_s_memrealtime();                                  \
+        }                                                                                                \
+    } while (0)
+/* COUNT frames: the wave's sum and max of node + triangle tests per lane */
+#define WF_STEPS()                                                                                       \
+    do {                                                                                                 \
+        if (COUNT) {                                                                                     \
+            unsigned st_sum = cnt.nodes + cnt.tris, st_max = st_sum;                                     \
+            for (int m = 1; m < 64; m <<= 1) {                                                           \
+                st_sum += (unsigned)__shfl_xor((int)st_sum, m);                                          \
+                st_max = max(st_max, (unsigned)__shfl_xor((int)st_max, m));                              \
+            }                                                                                            \
+            if (lane == 0 && (gid >> 6) < kWfStampWaves) {                                               \
+                WF_SLOT[5] = st_sum;                                                                     \
+                WF_SLOT[6] = st_max;                                                                     \
+            }                                                                                            \
+        }                                                                                                \
+    } while (0)
+#else
+#define WF_STAMP(k)
+#define WF_STEPS()
+#endif
 
 template <int TRAV, bool LEVEL0, bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CRT_WF0_WAVES : CRT_WF_WAVES))) void k_wf_level(const DeviceScene *__restrict__ scene, DSettings st,
@@ -27,6 +113,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
     }
     const int gid = (int)(blk * blockDim.x + threadIdx.x);
     const int lane = (int)(threadIdx.x & 63);
+    WF_STAMP(0);
     bool has;
     Vec o = vec(0.f, 0.f, 0.f), d = vec(0.f, 0.f, 1.f);
     int id = gid, depth = 0;
@@ -64,6 +151,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
     } else {
         slot = trace<TRAV, COUNT>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has, o, d, t, cnt);
     }
+    WF_STAMP(2);
 
     WNode node = {wFinal, -1, -1, 0, 0.f, 0.f, 0.f, 0.f};
     Vec col = vec(0.f, 0.f, 0.f);
@@ -157,6 +245,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         lv.nodes[id] = node;
         if (node.kind == wFinal) lv.cols[id] = DVec4{col.x, col.y, col.z, 0.f};
     }
+    WF_STEPS();
+    WF_STAMP(3);
     if (COUNT) {
         atomicAdd(&counters[0], (unsigned long long)cnt.traversals);
         atomicAdd(&counters[1], (unsigned long long)cnt.nodes);

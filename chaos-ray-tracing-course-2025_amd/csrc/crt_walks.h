@@ -803,7 +803,7 @@ __device__ __forceinline__ int trace_lane_pruned(const DeviceScene &s, bool acti
 /* Per-lane BVH walk with its proof on the reference's tree (crt_bvh.h):
  * scattered rays (GI bounces, reflections, refractions) of the frame-stack,
  * refill and wavefront kernels when the scene has its BVH. */
-template <bool COUNT, bool PF = (CRT_BVH_PREFETCH != 0)>
+template <bool COUNT, int PF = CRT_BVH_PREFETCH>
 __device__ __forceinline__ int trace_lane_bvh(const DeviceScene &s, bool active, Vec o, Vec d, float &best_t,
                                               LaneCounts &c) {
     best_t = 0.0f;
@@ -1214,7 +1214,7 @@ __device__ int trace_bins_lanes(const DeviceScene &s, CamCand *stage, int beg, i
 template <int TRAV>
 constexpr bool kIsCoop = TRAV == 4 || TRAV == 10;
 
-template <int TRAV, bool COUNT, bool PF = (CRT_BVH_PREFETCH != 0)>
+template <int TRAV, bool COUNT, int PF = CRT_BVH_PREFETCH>
 __device__ __forceinline__ int trace(const DeviceScene &s, CoopLds *L, bool active, Vec o, Vec d, float &best_t,
                                      LaneCounts &c) {
     static_assert(TRAV == 4 || TRAV == 7 || TRAV == 8 || TRAV == 10 || TRAV == 12 || TRAV == 13 || TRAV == 14,

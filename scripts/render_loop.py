@@ -72,7 +72,9 @@ def main():
         for name, g in scenes:
             out[name]["work"] = g.count_work(st)
             out[name]["wave"] = g.wave_counts()
-    print(json.dumps({"scene": a.scene, "size": [a.width, a.height], "depth": a.depth, "kernel": out}))
+    import hashlib
+    print(json.dumps({"scene": a.scene, "size": [a.width, a.height], "depth": a.depth, "kernel": out,
+                      "image_sha1": hashlib.sha1(ref.tobytes()).hexdigest()[:16]}))
 
 
 if __name__ == "__main__":
