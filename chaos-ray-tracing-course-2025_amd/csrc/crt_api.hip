@@ -794,14 +794,22 @@ static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
         HIP_TRY(hipDeviceSynchronize());
         sc->wf_rpw_lane = (int)value;
         wf_graphs_clear(sc->wf);
-        sc->wf.recs.clear();
+        { sc->wf.recs.clear(); ++sc->wf.epoch; }
+        return CRT_OK;
+    } else if (k == "wf_dynamic" || k == "wf_dyn_ids" || k == "wf_dyn_waves") {   /* device-sized frames (render_wavefront) */
+        if (k == "wf_dyn_ids" && (value < 1 || value > 64)) return set_error(CRT_E_INVALID, "wf_dyn_ids must be 1..64");
+        if (k == "wf_dyn_waves" && (value < 64 || value > (1 << 20)))
+            return set_error(CRT_E_INVALID, "wf_dyn_waves must be 64..2^20");
+        HIP_TRY(hipDeviceSynchronize());
+        (k == "wf_dynamic" ? sc->wf_dynamic : k == "wf_dyn_ids" ? sc->wf_dyn_ids : sc->wf_dyn_waves) =
+            k == "wf_dynamic" ? (value != 0) : (int)value;
         return CRT_OK;
     } else if (k == "wf_window") {
         if (sc->wf_window != (value != 0)) {
             HIP_TRY(hipDeviceSynchronize());
             sc->wf_window = value != 0;
             wf_graphs_clear(sc->wf);   /* graphs hold the level kernels */
-            sc->wf.recs.clear();
+            { sc->wf.recs.clear(); ++sc->wf.epoch; }
         }
         return CRT_OK;
     } else if (k == "bins_reuse") {   /* no plan depends on it */
@@ -835,7 +843,7 @@ static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
     } else if (k == "wf_replay") {
         if (value < 0 || value > 2) return set_error(CRT_E_INVALID, "wf_replay must be 0, 1 or 2");
         sc->wf_replay = value;
-        sc->wf.recs.clear();
+        { sc->wf.recs.clear(); ++sc->wf.epoch; }
         wf_graphs_clear(sc->wf);
     } else if (k == "wf_rpw") {
         if (value < 1 || value > 64) return set_error(CRT_E_INVALID, "wf_rpw must be 1..64");
@@ -952,6 +960,7 @@ int set_camera_one(crt_hip_scene *sc, const DCamera &c, float fov_radians, bool 
         wf_graphs_clear(sc->wf);
         sc->wf.recs.clear();
     }
+    ++sc->wf.epoch;   /* nor may a device-sized frame of the old camera record its sizes (wf_harvest) */
     return CRT_OK;
 }
 

@@ -336,7 +336,7 @@ int calibrate_plan(crt_hip_scene *sc, const DeviceScene *d_scene, int walk, hipS
 void free_plans(crt_hip_scene *sc) {
     for (void *p : sc->plan_allocs) (void)hipFree(p);
     sc->plan_allocs.clear();
-    sc->wf.recs.clear();   /* keyed by the tile lists' device pointers */
+    { sc->wf.recs.clear(); ++sc->wf.epoch; }   /* keyed by the tile lists' device pointers */
     wf_graphs_clear(sc->wf);
     sc->full = ShardPlan{};
     sc->shard_plans.clear();
@@ -447,6 +447,12 @@ int sync_device_record(crt_hip_scene *sc, const DeviceScene **out, hipStream_t s
             HIP_TRY(hipEventRecord(sc->rec_use[j], sc->rec_use_stream[j]));
             HIP_TRY(hipStreamWaitEvent(stream, sc->rec_use[j], 0));
         }
+        /* ... and wavefront levels that read it on their sets' streams */
+        for (WfSet &w : sc->wf.set)
+            if (w.rec_slot == j) {
+                if (w.done_ev) HIP_TRY(hipStreamWaitEvent(stream, w.done_ev, 0));
+                w.rec_slot = -1;
+            }
         sc->rec_use_stream[j] = nullptr;
         hipLaunchKernelGGL(k_put_record, dim3(1), dim3(64), 0, stream, sc->d_ring + j, sc->ds);
         HIP_TRY(hipGetLastError());
@@ -485,7 +491,8 @@ int wait_device_record(crt_hip_scene *sc, hipStream_t stream) {
  * (frames of one record on several streams: the API asks callers to order
  * them, include/crt_hip.h crt_hip_render_device). */
 int used_device_record(crt_hip_scene *sc, hipStream_t stream) {
-    sc->rec_last_stream = stream;
+    if (!sc->rec_read_by_set) sc->rec_last_stream = stream;
+    sc->rec_read_by_set = false;
     return CRT_OK;
 }
 
@@ -666,7 +673,8 @@ void wf_free(WfBuffers &wb) {
         for (void *p : {(void *)w.nodes, (void *)w.cols, (void *)w.q[0], (void *)w.q[1], (void *)w.counts, (void *)w.d_flag})
             if (p) (void)hipFree(p);
         if (w.h_flag) (void)hipHostFree(w.h_flag);
-        for (hipEvent_t e : {w.flag_ev, w.free_ev, w.done_ev})
+        if (w.h_counts) (void)hipHostFree(w.h_counts);
+        for (hipEvent_t e : {w.flag_ev, w.free_ev, w.done_ev, w.counts_ev})
             if (e) (void)hipEventDestroy(e);
     }
     for (hipStream_t st : wb.streams)
@@ -699,6 +707,8 @@ bool wf_overflowed(WfBuffers &wb, bool wait) {
         w.flag_pending = false;
     }
     wb.recs.clear();
+    ++wb.epoch;
+    wb.force_readback = true;   /* the next frame reads its sizes back (a device-sized frame may have overflowed) */
     wf_graphs_clear(wb);
     return true;
 }
@@ -741,6 +751,33 @@ int wf_streams(WfBuffers &wb, hipStream_t stream) {
  * back 1.20 ms with 2 sets/2 streams, 1.07 with 4/4, 0.93 with 8/8, 0.89
  * with 12/12, 0.90 with 16/16; sets sharing streams were slower
  * (profiles/r04/ab_wf_sets.txt). */
+/* Record the level sizes of device-sized frames whose copies have landed
+ * (WfSet::counts_*): for their tile list and settings, unless a record was
+ * dropped since the frame was issued (camera moved, plans freed, overflow)
+ * or a level outgrew its queue. */
+void wf_harvest(WfBuffers &wb) {
+    for (WfSet &w : wb.set) {
+        if (!w.counts_pending || hipEventQuery(w.counts_ev) != hipSuccess) continue;
+        w.counts_pending = false;
+        if (w.counts_epoch != wb.epoch || wb.recs.count(w.counts_tiles)) continue;
+        std::vector<int32_t> sizes;
+        bool ok = true;
+        for (int L = 1; L < w.counts_levels; ++L) {
+            const int32_t n = w.h_counts[L - 1];
+            if (n == 0) break;
+            ok = ok && n > 0 && n <= w.counts_qcap;
+            sizes.push_back(n);
+        }
+        if (!ok) continue;
+        WfBuffers::Rec &r = wb.recs[w.counts_tiles];
+        if (wb.shrink_records)
+            for (int32_t &n : sizes) n = n > 1 ? n - 1 : n;
+        r.sizes.swap(sizes);
+        r.st = w.counts_st;
+        r.ntiles = w.counts_ntiles;
+    }
+}
+
 #ifdef CRT_WF_STAMPS
 int wf_stamps_dump(const char *fn, int levels);
 #endif
@@ -757,9 +794,21 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         return set_error(CRT_E_STATE, "a wavefront level outgrew its recorded size in the previous frame; "
                                          "that frame is wrong (sizes are now read back again)");
     const int64_t n0 = (int64_t)plan.ntiles * 64;
+    wb.shrink_records = sc->wf_replay == 2;
+    wf_harvest(wb);
     const auto rit = wb.recs.find((const void *)plan.d_tiles);
     const bool replay = !count && sc->wf_replay && rit != wb.recs.end() && rit->second.ntiles == plan.ntiles &&
                         std::memcmp(&rit->second.st, st, sizeof *st) == 0;
+    /* no recorded sizes (a new camera, tile list or settings): device-sized
+     * levels instead of read-backs — queues of 2 x n0 rays, wf_dyn_ids x n0
+     * ray ids, each level's size read by its kernels from the counts the
+     * levels before wrote; the same overflow flag as recorded-size frames.
+     * Its level sizes are copied back behind it and recorded (wf_harvest)
+     * if no record was dropped meanwhile, so the next frames replay. */
+    const bool dyn_ok = sc->wf_replay && sc->wf_dynamic && ds.max_ray_depth + 2 <= (uint32_t)kWfDynMaxLevels;
+    const bool dyn = !replay && !count && dyn_ok && !wb.force_readback;
+    const bool async_frame = replay || dyn;
+    const int64_t dyn_q = std::max<int64_t>(2 * n0, 4096), dyn_ids = std::max<int64_t>(1, sc->wf_dyn_ids) * n0;
     /* sets in use: as many as CRT_WF_SET_BUDGET holds of this frame size
      * (rays x (node + colour) + two queues), 2 <= sets <= kWfSets; each set
      * waits for its own previous frame, so the count may change between frames */
@@ -768,11 +817,20 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         if (rc0 != CRT_OK) return rc0;
     }
     int si = 0;
-    if (replay) {
+    if (async_frame) {
         int64_t tot = n0, mx = 1;
-        for (int32_t n : rit->second.sizes) {
-            tot += n;
-            mx = std::max<int64_t>(mx, n);
+        if (replay) {
+            for (int32_t n : rit->second.sizes) {
+                tot += n;
+                mx = std::max<int64_t>(mx, n);
+            }
+            if (dyn_ok) {
+                tot = std::max(tot, dyn_ids);
+                mx = std::max(mx, dyn_q);
+            }
+        } else {
+            tot = dyn_ids;
+            mx = dyn_q;
         }
         const int64_t set_bytes = tot * (int64_t)(sizeof(WNode) + sizeof(DVec4)) + 2 * mx * (int64_t)sizeof(WRay);
         const int64_t fit = CRT_WF_SET_BUDGET / std::max<int64_t>(set_bytes, 1);
@@ -793,9 +851,16 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
     WfSet &w = wb.set[si];
     /* where the levels run: a recorded-size frame on its set's stream, after
      * the set's previous frame; a frame with read-backs on the caller's */
-    const hipStream_t ls = replay ? wb.streams[si % kWfStreams] : stream;
+    const hipStream_t ls = async_frame ? wb.streams[si % kWfStreams] : stream;
     HIP_TRY(hipStreamWaitEvent(ls, w.free_ev, 0));
-    if (replay) {   /* the scene record this frame reads was written on another stream */
+    if (!d_scene) {   /* the scene record: written on ls if it changed, else waited for there */
+        const int rc0 = sync_device_record(sc, &d_scene, ls);
+        if (rc0 != CRT_OK) return rc0;
+        if (async_frame) {   /* its readers: this set's levels (done_ev), not the caller's stream */
+            w.rec_slot = sc->ring_cur;
+            sc->rec_read_by_set = true;
+        }
+    } else if (async_frame) {   /* the scene record this frame reads was written on another stream */
         const int rc0 = wait_device_record(sc, ls);
         if (rc0 != CRT_OK) return rc0;
     }
@@ -832,24 +897,48 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         }
         qneed = std::max<int64_t>(mx, 1);
         ids = tot;
+        if (dyn_ok) {   /* sized for device-sized frames too: a camera move then grows no set (a hipFree syncs the device) */
+            qneed = std::max(qneed, dyn_q);
+            ids = std::max(ids, dyn_ids);
+        }
+    } else if (dyn) {
+        qneed = dyn_q;
+        ids = dyn_ids;
     }
     if ((rc = wf_grow_ids(wb, si, ids, 0, ls)) != CRT_OK) return rc;
     if ((rc = wf_grow_queue(wb, si, 0, qneed)) != CRT_OK) return rc;
-    if (replay && (rc = wf_grow_queue(wb, si, 1, qneed)) != CRT_OK) return rc;
+    if (async_frame && (rc = wf_grow_queue(wb, si, 1, qneed)) != CRT_OK) return rc;
+    if (dyn && !w.h_counts) {
+        void *p = nullptr;
+        HIP_TRY(hipHostMalloc(&p, kWfDynMaxLevels * sizeof(int32_t), hipHostMallocDefault));
+        w.h_counts = static_cast<int32_t *>(p);
+        HIP_TRY(hipEventCreateWithFlags(&w.counts_ev, hipEventDisableTiming));
+    }
     /* the pixels on the caller's stream once the levels are done; the set is
      * free again after them */
     auto finish = [&]() -> int {
-        if (replay) {
+        if (dyn) {   /* the level sizes, to record once they land (wf_harvest) */
+            HIP_TRY(hipMemcpyAsync(w.h_counts, w.counts, (size_t)kMaxLevels * sizeof(int32_t), hipMemcpyDeviceToHost, ls));
+            HIP_TRY(hipEventRecord(w.counts_ev, ls));
+            w.counts_pending = true;
+            w.counts_tiles = (const void *)plan.d_tiles;
+            w.counts_st = *st;
+            w.counts_ntiles = plan.ntiles;
+            w.counts_levels = kMaxLevels;
+            w.counts_epoch = wb.epoch;
+            w.counts_qcap = dyn_q;
+        }
+        if (async_frame) {
             HIP_TRY(hipEventRecord(w.done_ev, ls));
             HIP_TRY(hipStreamWaitEvent(stream, w.done_ev, 0));
         }
         hipLaunchKernelGGL(k_wf_pixels, dim3((unsigned)((plan.ntiles + 3) / 4)), dim3(256), 0, stream, w.nodes, w.cols,
                            plan.d_tiles, plan.ntiles, d_out);
         HIP_TRY(hipGetLastError());
-        if (replay)   /* the device flag is sticky: a later frame's copy cannot hide an earlier overflow */
+        if (async_frame)   /* the device flag is sticky: a later frame's copy cannot hide an earlier overflow */
             HIP_TRY(hipMemcpyAsync(w.h_flag, w.d_flag, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipEventRecord(w.free_ev, stream));
-        if (replay) {
+        if (async_frame) {
             HIP_TRY(hipEventRecord(w.flag_ev, stream));
             w.flag_pending = true;
         }
@@ -880,7 +969,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
     HIP_TRY(hipMemsetAsync(w.counts, 0, kMaxLevels * sizeof(int32_t), ls));
     unsigned long long *cnt = sc->d_counters;
     WLevel lv{nullptr, 0, 0, w.q[0], w.counts, (int32_t)n0, w.nodes, w.cols, 64,
-              replay ? (rec.empty() ? 0 : rec[0]) : cap_of(w.qcap[0]), w.d_flag};
+              replay ? (rec.empty() ? 0 : rec[0]) : cap_of(w.qcap[0]), w.d_flag, nullptr, (int32_t)n0, cap_of(w.cap)};
     const int blocks0 = (plan.ntiles + 3) / 4;
 #define CRT_WF0(T, COUNT)                                                                                   \
     hipLaunchKernelGGL((k_wf_level<T, true, COUNT>), dim3(blocks0), dim3(256), 0, ls, d_scene, ds,          \
@@ -900,6 +989,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
     int64_t base = n0;
     int cur = 0;
     const int rpw = std::min(64, std::max(1, sc->wf_rays_per_wave));   /* coop walks: idle lanes take donated pieces */
+    const int32_t dyn_cap = cap_of(std::min(w.qcap[0], w.qcap[1]));   /* device-sized levels: either queue holds this many */
     for (int L = 1; L < kMaxLevels; ++L) {
         int32_t n = 0;
         int32_t out_cap = 0;
@@ -907,6 +997,10 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
             if (L - 1 >= (int)rec.size()) break;
             n = rec[L - 1];
             out_cap = L < (int)rec.size() ? rec[L] : 0;
+        } else if (dyn) {   /* levels 1..max_ray_depth may hold rays (deeper children are never queued) */
+            if (L > (int)ds.max_ray_depth) break;
+            n = dyn_cap;
+            out_cap = dyn_cap;
         } else {
             HIP_TRY(hipMemcpyAsync(&n, w.counts + (L - 1), sizeof n, hipMemcpyDeviceToHost, ls));
             HIP_TRY(hipStreamSynchronize(ls));
@@ -924,9 +1018,12 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         /* sec 16: the BVH window walk, four lanes a ray (wf_window) */
         const int rpw_l = sec == 16 ? 16 : sec == 14 ? sc->wf_rpw_lane : std::min(rpw, std::max(8, (int)((n + 4095) / 4096)));
         WLevel l{w.q[cur], n, L, w.q[cur ^ 1], w.counts + L, (int32_t)(base + n), w.nodes, w.cols, rpw_l, out_cap,
-                 w.d_flag};
-        const int64_t waves = ((int64_t)n + rpw_l - 1) / rpw_l;
-        const int blocks = (int)((waves + 3) / 4);
+                 w.d_flag, dyn ? w.counts : nullptr, (int32_t)n0, cap_of(w.cap)};
+        /* device-sized: a fixed grid whose waves stride over the level */
+        const int64_t waves = dyn ? std::min<int64_t>(((int64_t)n + rpw_l - 1) / rpw_l, std::max(64, sc->wf_dyn_waves))
+                                  : ((int64_t)n + rpw_l - 1) / rpw_l;
+        const int blocks = dyn ? (int)(((waves + 3) / 4 + 7) & ~7ll)   /* (device-sized: a multiple of the 8 XCDs) */
+                               : (int)((waves + 3) / 4);
 #define CRT_WF(SEC, COUNT)                                                                                  \
     hipLaunchKernelGGL((k_wf_level<SEC, false, COUNT>), dim3(blocks), dim3(256), 0, ls, d_scene, ds,         \
                        plan.d_tiles, plan.ntiles, l, cnt)
@@ -941,13 +1038,18 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         }
 #undef CRT_WF
         HIP_TRY(hipGetLastError());
-        levels.emplace_back(base, n);
+        levels.emplace_back(dyn ? L : base, n);
         base += n;
         cur ^= 1;
     }
-    for (auto it = levels.rbegin(); it != levels.rend(); ++it)
-        hipLaunchKernelGGL(k_wf_compose, dim3((unsigned)((it->second + 255) / 256)), dim3(256), 0, ls, w.nodes,
-                           w.cols, (int32_t)it->first, (int32_t)it->second);
+    for (auto it = levels.rbegin(); it != levels.rend(); ++it) {
+        if (dyn)   /* (first = the level) */
+            hipLaunchKernelGGL(k_wf_compose_dyn, dim3(1024), dim3(256), 0, ls, w.nodes, w.cols, w.counts,
+                               (int32_t)it->first, (int32_t)n0, dyn_cap, cap_of(w.cap));
+        else
+            hipLaunchKernelGGL(k_wf_compose, dim3((unsigned)((it->second + 255) / 256)), dim3(256), 0, ls, w.nodes,
+                               w.cols, (int32_t)it->first, (int32_t)it->second);
+    }
     HIP_TRY(hipGetLastError());
     return CRT_OK;
     };
@@ -970,9 +1072,10 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         return rc;
     }
     if ((rc = finish()) != CRT_OK) return rc;
-    if (!replay && !count && sc->wf_replay) {
+    if (!replay && !dyn && !count && sc->wf_replay) {
+        wb.force_readback = false;
         WfBuffers::Rec &r = wb.recs[(const void *)plan.d_tiles];
-        if (sc->wf_replay == 2)
+        if (wb.shrink_records)
             for (int32_t &n : sizes) n = n > 1 ? n - 1 : n;
         r.sizes.swap(sizes);
         r.st = *st;
@@ -1001,7 +1104,12 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
      * ring's lazy slot-reuse event then orders the binning after the
      * previous render — 0.0675 -> 0.0736 ms) */
     const bool bins_frame = !full && !sc->shadows && bins_active(sc) && plan.bp.cell_tile;   /* (the branch below) */
-    {
+    /* a wavefront frame writes a changed record on the stream its levels run
+     * on (render_wavefront): on the caller's stream it would wait for the
+     * previous frame's pixels, and frames with a new camera each could not
+     * run side by side */
+    const bool wf_frame = !sc->shadows && full && !gi && sc->wavefront && !stamps && !rec_machine_on(sc, st);
+    if (!wf_frame) {
         const int rc = sync_device_record(sc, &d_scene, stream);
         if (rc != CRT_OK) return rc;
     }
@@ -1059,7 +1167,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     }
     /* recursion without GI (C3): the per-lane state machine (rec_machine), or level by level (wavefront) */
     const bool rec_machine = full && !gi && rec_machine_on(sc, st) && !stamps;
-    if (full && !gi && sc->wavefront && !stamps && !rec_machine)
+    if (wf_frame)
         return render_wavefront(sc, ds, st, plan, d_out, stream, count, d_scene,
                                 sec == 14 && sc->wf_window ? 16 : sec, camera_walk(sc, sc->traversal));
     /* frame-stack kernel: one walk for every ray */

@@ -77,6 +77,12 @@ struct WLevel {
     int32_t rpw;             /* levels >= 1: rays per wave (lanes rpw..63 start idle and take donated pieces) */
     int32_t out_cap;         /* children this level may queue (recorded level sizes: exactly the next level) */
     int32_t *overflow;       /* set when a level queued more children than out_cap (none written) */
+    /* device-sized frames: the levels' counts (level L's size is dyn[L - 1],
+     * its first ray id n0 + dyn[0] + ... + dyn[L - 2]); n is then the queue's
+     * capacity and the waves stride over the level; nullptr: n rays, one pass */
+    const int32_t *dyn;
+    int32_t n0;              /* camera rays (level 0's ids) */
+    int32_t id_cap;          /* ray ids the node / colour arrays hold */
 };
 
 template <class T>
@@ -102,6 +108,9 @@ template <int TRAV, bool LEVEL0, bool COUNT>
 __global__ void k_wf_level(const DeviceScene *__restrict__ scene, DSettings st, const Tile *__restrict__ tiles,
                            int ntiles, WLevel lv, unsigned long long *__restrict__ counters);
 __global__ void k_wf_compose(const WNode *__restrict__ nodes, DVec4 *__restrict__ cols, int32_t begin, int32_t n);
+__global__ void k_wf_compose_dyn(const WNode *__restrict__ nodes, DVec4 *__restrict__ cols,
+                                 const int32_t *__restrict__ counts, int32_t level, int32_t n0, int32_t qcap,
+                                 int32_t id_cap);
 __global__ void k_wf_pixels(const WNode *__restrict__ nodes, const DVec4 *__restrict__ cols,
                             const Tile *__restrict__ tiles, int ntiles, float *__restrict__ out);
 __global__ void k_trace_rays(DeviceScene s, const float *__restrict__ rays, int64_t n, crt_hit *__restrict__ hits,

@@ -114,6 +114,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
     const int gid = (int)(blk * blockDim.x + threadIdx.x);
     const int lane = (int)(threadIdx.x & 63);
     WF_STAMP(0);
+    /* this level's size and its children's first id: given, or (device-sized
+     * frames) from the counts the levels before wrote */
+    int n = lv.n, out_base = lv.out_base;
+    if (!LEVEL0 && lv.dyn) {
+        int64_t b = lv.n0;
+        for (int k = 0; k < lv.depth; ++k) b += lv.dyn[k];
+        n = min(lv.dyn[lv.depth - 1], lv.n);
+        out_base = b < (int64_t)INT32_MAX ? (int)b : INT32_MAX;
+    }
+    constexpr bool kCoop = TRAV != 16 && kIsCoop<TRAV>;
+    __shared__ CoopLds coop[kCoop ? 4 : 1];
+    /* the level's waves: one pass over the grid, or (device-sized levels, a
+     * fixed grid) each XCD strides over its own eighth of the level, as the
+     * remap above gives each XCD a contiguous range */
+    int wv = gid >> 6, wv_end = 0x7fffffff, wv_step = 0;
+    if (!LEVEL0 && lv.dyn) {
+        const int nw = (n + lv.rpw - 1) / lv.rpw, chunk = (nw + 7) >> 3, xcd = (int)blockIdx.x & 7;
+        wv = xcd * chunk + ((int)blockIdx.x >> 3) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
+        wv_end = min(nw, (xcd + 1) * chunk);
+        wv_step = ((int)gridDim.x >> 3) * (int)(blockDim.x >> 6);
+    }
+    for (;; wv += wv_step) {   /* one pass unless the level is device-sized */
+    if (wv >= wv_end) return;
     bool has;
     Vec o = vec(0.f, 0.f, 0.f), d = vec(0.f, 0.f, 1.f);
     int id = gid, depth = 0;
@@ -127,11 +150,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         has = lx < tl.w && ly < tl.h;
         if (has) camera_ray(s.cam, tl.x + lx, tl.y + ly, o, d);
     } else {
-        const int ray0 = (gid >> 6) * lv.rpw;
-        if (ray0 >= lv.n) return;          /* whole wave past the queue */
+        const int ray0 = wv * lv.rpw;
+        if (ray0 >= n) return;             /* whole wave past the queue */
         /* TRAV 16: a ray per group of four lanes (the BVH window walk) */
         const int ray = ray0 + (TRAV == 16 ? lane >> 2 : lane);
-        has = (TRAV == 16 ? (lane >> 2) : lane) < lv.rpw && ray < lv.n;
+        has = (TRAV == 16 ? (lane >> 2) : lane) < lv.rpw && ray < n;
         if (has) {
             const WRay r = lv.in[ray];
             o = vec(r.ox, r.oy, r.oz);
@@ -141,8 +164,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         }
     }
     LaneCounts cnt = {};
-    constexpr bool kCoop = TRAV != 16 && kIsCoop<TRAV>;
-    __shared__ CoopLds coop[kCoop ? 4 : 1];
     float t;
     int slot;
     if constexpr (TRAV == 16) {   /* four lanes walk the group's ray; the first shades it */
@@ -223,10 +244,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         int base = 0;
         if (lane == __ffsll((long long)(b1 | b2)) - 1) {
             base = atomicAdd(lv.out_count, total);
-            if (base + total > lv.out_cap) atomicOr(lv.overflow, 1);
+            if (base + total > lv.out_cap || (int64_t)out_base + base + total > lv.id_cap) atomicOr(lv.overflow, 1);
         }
         base = __shfl(base, __ffsll((long long)(b1 | b2)) - 1);
-        if (base + total > lv.out_cap) nch = 0;   /* never past the queue (the frame is then reported, not used) */
+        /* never past the queue or the ids (the frame is then reported, not used) */
+        if (base + total > lv.out_cap || (int64_t)out_base + base + total > lv.id_cap) nch = 0;
         /* a lane's children side by side */
         const int k0 = base + __popcll(b1 & lt) + __popcll(b2 & lt);
         const int k1 = k0 + 1;
@@ -235,7 +257,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
             WRay r;
             r.ox = co[c].x; r.oy = co[c].y; r.oz = co[c].z;
             r.dx = cd[c].x; r.dy = cd[c].y; r.dz = cd[c].z;
-            r.id = lv.out_base + k;
+            r.id = out_base + k;
             r.depth = depth + 1;
             lv.out[k] = r;
             if (c == 0) node.c0 = r.id; else node.c1 = r.id;
@@ -258,6 +280,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
             atomicMax(&counters[6], (unsigned long long)cnt.wave_nodes);
             atomicAdd(&counters[7], 1ull);
         }
+    }
+    if (LEVEL0 || !lv.dyn) break;
     }
 }
 
@@ -282,6 +306,24 @@ __global__ __launch_bounds__(256) void k_wf_compose(const WNode *__restrict__ no
     if (nd.kind == wFinal) return;
     const Vec c = wf_compose(nd, cols, vec(0.f, 0.f, 0.f));
     cols[id] = DVec4{c.x, c.y, c.z, 0.f};
+}
+
+/* k_wf_compose for a device-sized frame: level `level`'s first id and size
+ * from the counts (clamped to the queue and id capacities the level wrote) */
+__global__ __launch_bounds__(256) void k_wf_compose_dyn(const WNode *__restrict__ nodes, DVec4 *__restrict__ cols,
+                                                        const int32_t *__restrict__ counts, int32_t level, int32_t n0,
+                                                        int32_t qcap, int32_t id_cap) {
+    int64_t b = n0;
+    for (int k = 0; k < level - 1; ++k) b += counts[k];
+    const int64_t nq = min(counts[level - 1], qcap), nid = (int64_t)id_cap - b;
+    const int64_t n = nq < nid ? nq : nid;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t id = b + k;
+        const WNode nd = nodes[id];
+        if (nd.kind == wFinal) continue;
+        const Vec c = wf_compose(nd, cols, vec(0.f, 0.f, 0.f));
+        cols[id] = DVec4{c.x, c.y, c.z, 0.f};
+    }
 }
 
 /* level 0: compose the camera rays and write the pixels */

@@ -116,6 +116,18 @@ struct WfSet {
     hipEvent_t free_ev = nullptr;     /* the set's last frame has written its pixels */
     uint64_t seq = 0;                 /* WfBuffers::frame of the set's last frame */
     hipEvent_t done_ev = nullptr;     /* the set's levels of the current frame are done */
+    /* a device-sized frame's level sizes, copied back behind it to record them
+     * (WfBuffers::Rec) once they land, if the camera has not moved since */
+    int32_t *h_counts = nullptr;      /* pinned, kWfDynMaxLevels */
+    hipEvent_t counts_ev = nullptr;
+    bool counts_pending = false;
+    const void *counts_tiles = nullptr;
+    crt_renderer_settings counts_st{};
+    int counts_ntiles = 0;
+    int counts_levels = 0;
+    int64_t counts_qcap = 0;
+    int rec_slot = -1;                /* the device record ring slot the set's last frame read (its levels, on the set's stream) */
+    uint64_t counts_epoch = 0;
 };
 
 #ifndef CRT_WF_SETS
@@ -145,6 +157,10 @@ struct WfBuffers {
         int ntiles = 0;
     };
     std::map<const void *, Rec> recs;   /* by tile list (device pointer; cleared when plans are freed) */
+    bool force_readback = false;        /* after an overflow: the next frame reads its sizes back */
+    bool shrink_records = false;        /* option wf_replay 2 (tests): sizes recorded minus one */
+    uint64_t epoch = 0;                 /* bumped whenever recs are dropped (a device-sized frame's sizes
+                                         * are recorded only if no drop happened since it was issued) */
     /* recorded-size frames captured as HIP graphs, by everything their
      * launches bake in (cleared whenever a buffer, tile list or record changes) */
     struct Graph {
@@ -164,6 +180,8 @@ constexpr int kRecRing = 16;
 
 /* Deepest recursion the wavefront path accepts (levels are launched one by one). */
 constexpr int kWfMaxDepth = 4096;
+/* device-sized wavefront frames (render_wavefront): up to this max_ray_depth + 2 levels */
+constexpr int kWfDynMaxLevels = 66;
 
 struct crt_hip_scene {
     int device = 0;
@@ -189,6 +207,8 @@ struct crt_hip_scene {
     bool rec_up_done = false;              /* ... and the write is done */
     bool rec_up_recorded = false;          /* rec_up of the current slot recorded (a reader on another stream) */
     hipStream_t rec_last_stream = nullptr;  /* where the last frame that read the current record was issued */
+    bool rec_read_by_set = false;          /* the frame just issued read it on a wavefront set's stream
+                                            * (WfSet::rec_slot + done_ev cover it, not rec_last_stream) */
     hipEvent_t rec_up[kRecRing] = {};    /* slot written */
     hipEvent_t rec_use[kRecRing] = {};   /* the last frame that read the slot is done */
     hipStream_t rec_use_stream[kRecRing] = {};   /* where each slot's last frame was issued (null: none) */
@@ -258,6 +278,9 @@ struct crt_hip_scene {
     int bins_on = 1;               /* camera frames take the camera bins where built (walk 15; option "bins") */
     int64_t bins_mean_cap = crt_amd::kBinMeanCap;   /* candidates per cell on average, at most (env CRT_BINS_MEAN_CAP) */
     int wf_rpw_lane = 64;          /* rays per wave of levels >= 1 on the per-lane BVH walk (option "wf_rpw_lane") */
+    int wf_dynamic = 1;            /* wavefront frames without recorded sizes: device-sized levels, no read-back (option "wf_dynamic") */
+    int wf_dyn_ids = 4;            /* ... their ray-id capacity, x camera rays (option "wf_dyn_ids") */
+    int wf_dyn_waves = 8192;       /* ... the waves of each level's grid, at most (option "wf_dyn_waves") */
     int wf_window = 0;             /* wavefront levels >= 1: the BVH window walk, four lanes a ray (option "wf_window") */
     int bvh_device = 1;            /* build the BVH on the device above kHostBvhMax triangles (env CRT_BVH_DEVICE=0: not) */
     int bins_slack = 100;          /* camera-bins grid slots per kind: the sizing pass's count + this % (option "bins_slack") */

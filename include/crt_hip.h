@@ -541,6 +541,14 @@ int  crt_hip_wave_counts(crt_hip_scene *scene, crt_wave_counts *out);
  *                back | 2: tests only, recorded sizes minus one (overflow path)
  *   "wf_graph"   0/1 (default 1): such frames run as a HIP graph captured on
  *                their first replay (per tile list, settings, output, stream)
+ *   "wf_dynamic" 1 (default): a wavefront frame with no recorded sizes (a new
+ *                camera, tile list or settings) sizes its levels on the device
+ *                — no read-back; queues of 2 x the camera rays, "wf_dyn_ids"
+ *                (default 4) x the camera rays of ray ids, grids of at most
+ *                "wf_dyn_waves" (default 8192) waves striding over a level —
+ *                and its sizes are recorded behind it; a level past those
+ *                capacities is reported like a recorded-size overflow and the
+ *                next frame reads its sizes back | 0: read-backs
  *   "trace_walk" 0 = reference order, 1 = pruned per-ray walk, 2 = BVH + proof
  *                (crt_hip_trace_batch)
  *   "events"     0/1 (default 1): start/stop events around every render

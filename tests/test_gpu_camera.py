@@ -117,6 +117,44 @@ def test_camera_poses_c3_wavefront(N, oracle, devbuf):
     assert not bad, f"device frames {bad} differ"
 
 
+def test_c3_device_sized_frames(N, oracle, devbuf):
+    """Wavefront frames with no recorded level sizes (every frame after a
+    camera move) size their levels on the device instead of reading them back
+    (option wf_dynamic): 8 poses issued back to back as device frames run
+    side by side on the buffer sets and each equals the oracle's render of
+    its pose; a blocking frame of the last pose records its sizes, and the
+    frame after it replays them.  A device-sized frame whose levels outgrow
+    their capacities (wf_dyn_ids 1: no room for any child's id) is rendered
+    again with read-backs by crt_hip_render and reported by the next device
+    frame's call."""
+    name = "11-01-refractive__scene8"
+    st = N.RendererSettings.default(max_ray_depth=8)
+    size = (240, 135)
+    ps = poses(name, 8, yaw_amp=18.0)
+    wants = [bits(oracle.OracleScene(posed(name, loc, rot, None, size)).render(st)) for loc, rot in ps]
+    g = N.HipScene(scene_npz(name).set_resolution(*size))
+    d = [devbuf.alloc(size[0] * size[1] * 12) for _ in ps]
+    for k, (loc, rot) in enumerate(ps):
+        g.set_camera(loc, rot)
+        g.render_device(st, d[k])
+    bad = [k for k in range(len(ps))
+           if not np.array_equal(bits(devbuf.download(d[k], (size[1], size[0], 3), np.float32)), wants[k])]
+    assert not bad, f"device-sized frames {bad} differ"
+    for _ in range(3):   # device-sized (its sizes recorded behind it), then recorded-size frames
+        assert np.array_equal(bits(g.render(st)), wants[-1])
+    assert g.info()["wf_sets"] >= 2
+    h = N.HipScene(scene_npz(name).set_resolution(*size), wf_dyn_ids=1)
+    h.set_camera(*ps[2])
+    assert np.array_equal(bits(h.render(st)), wants[2])   # overflowed, rendered again with read-backs
+    h = N.HipScene(scene_npz(name).set_resolution(*size), wf_dyn_ids=1)   # (h's read-back frame grew its ids)
+    h.set_camera(*ps[3])
+    h.render_device(st, d[0])                              # overflows: reported on the next call
+    devbuf.sync()
+    with pytest.raises(N.CrtError):
+        h.render_device(st, d[1])
+    assert np.array_equal(bits(h.render(st)), wants[3])   # read-back frame
+
+
 def test_camera_poses_gi(N, oracle):
     """C4's GI scene at 96x96: new poses through the GI state machine."""
     name = "15-01-conclusion__scene2"
