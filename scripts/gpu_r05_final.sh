@@ -33,7 +33,7 @@ if [[ $STEPS == *pmc* ]]; then
 fi
 if [[ $STEPS == *bench* ]]; then
   run bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5
-  run bench_c3 600 python bench.py --config c3 --steps 20 --warmup 3
+  run bench_c3 600 python bench.py --config c3 --steps 100 --warmup 10
   run bench_c4 1100 python bench.py --config c4 --steps 8 --warmup 2
   run bench_c5 900 python bench.py --config c5 --steps 10 --warmup 2
 fi
