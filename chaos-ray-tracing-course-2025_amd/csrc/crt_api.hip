@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -26,73 +27,7 @@
 
 namespace {
 
-/* Persistent host threads for the host half of a staged copy (a per-call
- * thread start would cost more than the copy chunk it serves). */
-class CopyPool {
-public:
-    explicit CopyPool(int n) {
-        for (int i = 0; i < n; ++i) th_.emplace_back([this]() { loop(); });
-    }
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto &t : th_) t.join();
-    }
-    /* f(0 .. n-1) over the pool and the calling thread; returns when all ran.
-     * One job at a time: concurrent callers (renders of different scenes on
-     * different host threads) queue on run_mu_, so a job's counters are never
-     * reset while its workers still run it. */
-    void run(int n, const std::function<void(int)> &f) {
-        std::lock_guard<std::mutex> one(run_mu_);
-        std::unique_lock<std::mutex> l(mu_);
-        job_ = &f;
-        n_ = n;
-        next_ = 0;
-        done_ = 0;
-        cv_.notify_all();
-        while (next_ < n_) {
-            const int i = next_++;
-            l.unlock();
-            f(i);
-            l.lock();
-            ++done_;
-        }
-        done_cv_.wait(l, [&]() { return done_ == n_; });
-        job_ = nullptr;
-    }
-
-private:
-    void loop() {
-        std::unique_lock<std::mutex> l(mu_);
-        for (;;) {
-            cv_.wait(l, [&]() { return stop_ || (job_ && next_ < n_); });
-            if (stop_) return;
-            const int i = next_++;
-            const std::function<void(int)> *f = job_;
-            l.unlock();
-            (*f)(i);
-            l.lock();
-            if (++done_ == n_) done_cv_.notify_all();
-        }
-    }
-    std::mutex run_mu_;
-    std::mutex mu_;
-    std::condition_variable cv_, done_cv_;
-    std::vector<std::thread> th_;
-    const std::function<void(int)> *job_ = nullptr;
-    int n_ = 0, next_ = 0, done_ = 0;
-    bool stop_ = false;
-};
-
 constexpr int kStageChunks = 8;
-
-CopyPool &copy_pool() {
-    static CopyPool pool((int)std::max(1u, std::min(7u, std::thread::hardware_concurrency())));
-    return pool;
-}
 
 bool host_pinned(const void *p) {
     hipPointerAttribute_t a;
@@ -103,14 +38,22 @@ bool host_pinned(const void *p) {
     return a.type == hipMemoryTypeHost;
 }
 
-/* The scene's image d_out into host memory, queued behind the frame on the
- * scene's stream.  Pinned (or registered) memory: one DMA.  Pageable memory:
- * the runtime would first page-lock the caller's buffer (~10 ms for a
- * 1920x1080 image the first time, profiles/r03/cold), so the image goes
- * through the scene's pinned staging copy in chunks instead, each chunk
- * copied on to the caller's buffer by a pool thread as soon as its DMA is
- * done. */
-int image_to_host(crt_hip_scene *sc, float *dst, size_t nfl) {
+/* hipEventQuery until the event is reached (the copy's host threads poll:
+ * a blocking wait may sleep past a ~10 us chunk). */
+hipError_t spin_event(hipEvent_t e) {
+    for (;;) {
+        const hipError_t r = hipEventQuery(e);
+        if (r != hipErrorNotReady) return r;
+        for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+    }
+}
+
+/* The whole image through the pinned staging copy in chunks, each chunk copied
+ * on to the caller's buffer by a pool thread as soon as its DMA is done (the
+ * runtime would first page-lock a pageable caller buffer: ~10 ms for a
+ * 1920x1080 image the first time, profiles/r03/cold).  Pinned caller memory:
+ * one DMA. */
+int image_to_host_full(crt_hip_scene *sc, float *dst, size_t nfl) {
     const size_t bytes = nfl * sizeof(float);
     if (!sc->h_stage || host_pinned(dst)) {
         HIP_TRY(hipMemcpyAsync(dst, sc->d_out, bytes, hipMemcpyDeviceToHost, sc->stream));
@@ -125,15 +68,141 @@ int image_to_host(crt_hip_scene *sc, float *dst, size_t nfl) {
                                len, hipMemcpyDeviceToHost, sc->stream));
         HIP_TRY(hipEventRecord(sc->stage_ev[(size_t)nc], sc->stream));
     }
-    std::vector<hipError_t> err((size_t)nc, hipSuccess);
-    copy_pool().run(nc, [&](int i) {
-        const size_t off = (size_t)i * step, len = std::min(step, bytes - off);
-        err[(size_t)i] = hipEventSynchronize(sc->stage_ev[(size_t)i]);
-        if (err[(size_t)i] == hipSuccess)
-            std::memcpy(reinterpret_cast<char *>(dst) + off, reinterpret_cast<const char *>(sc->h_stage) + off, len);
-    });
-    for (hipError_t e : err)
-        if (e != hipSuccess) return set_error(CRT_E_HIP, std::string("image copy: ") + hipGetErrorString(e));
+    struct Job {
+        crt_hip_scene *sc;
+        float *dst;
+        size_t bytes, step;
+        hipError_t err[kStageChunks];
+    } job{sc, dst, bytes, step, {}};
+    HostPool::get().run(nc, [](void *a, int i) {
+        Job &j = *static_cast<Job *>(a);
+        const size_t off = (size_t)i * j.step, len = std::min(j.step, j.bytes - off);
+        j.err[i] = spin_event(j.sc->stage_ev[(size_t)i]);
+        if (j.err[i] == hipSuccess)
+            std::memcpy(reinterpret_cast<char *>(j.dst) + off, reinterpret_cast<const char *>(j.sc->h_stage) + off, len);
+    }, &job);
+    for (int i = 0; i < nc; ++i)
+        if (job.err[i] != hipSuccess) return set_error(CRT_E_HIP, std::string("image copy: ") + hipGetErrorString(job.err[i]));
+    return CRT_OK;
+}
+
+/* The compact copy's row records for the scene's frame height. */
+int ensure_copy_rows(crt_hip_scene *sc) {
+    const int H = sc->info.height;
+    if (sc->h_rows && sc->copy_h == H) return CRT_OK;
+    HIP_TRY(hipStreamSynchronize(sc->stream));
+    if (sc->h_rows) (void)hipHostFree(sc->h_rows);
+    sc->h_rows = nullptr;
+    sc->copy_h = 0;
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&sc->h_rows), (size_t)H * sizeof(HostRow), hipHostMallocDefault));
+    std::memset(sc->h_rows, 0, (size_t)H * sizeof(HostRow));
+    sc->copy_gen = 0;   /* no row carries a copy number above 0 */
+    if (!sc->copy_ev) HIP_TRY(hipEventCreateWithFlags(&sc->copy_ev, hipEventDisableTiming));
+    sc->copy_h = H;
+    return CRT_OK;
+}
+
+/* Device address of pinned (or registered) host memory, or null. */
+void *device_view(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
+}
+
+/* The compact copy of the frame in d_out into host memory, queued behind the
+ * frame on the scene's stream.  k_rows_to_host (one block a row) finds each
+ * row's span of non-background pixels, publishes it in the row's pinned
+ * record and writes the span straight into host memory: into the caller's
+ * image when it is pinned, else into the pinned staging image.  Meanwhile
+ * the host (HostPool, one band of rows a thread) writes the background
+ * outside each span as soon as the span is published, and (staging) copies
+ * each span on once its pixels are published.  Every pixel outside a row's
+ * span has the background's bits (k_rows_to_host compares bits), so the
+ * caller's image equals d_out bit for bit.  ~1/7 of C2's frame crosses PCIe. */
+int image_to_host(crt_hip_scene *sc, float *dst, size_t nfl) {
+    const int W = sc->info.width, H = sc->info.height;
+    if (!sc->compact_copy || !sc->h_stage || sc->grid_empty || W <= 0 || H <= 0 || (size_t)W * H * 3 != nfl)
+        return image_to_host_full(sc, dst, nfl);
+    int rc = ensure_copy_rows(sc);
+    if (rc != CRT_OK) return rc;
+    float *dst_dev = static_cast<float *>(device_view(dst));
+    float *target = dst_dev;
+    if (!target && !(target = static_cast<float *>(device_view(sc->h_stage))))
+        return image_to_host_full(sc, dst, nfl);
+    HostRow *rows_dev = static_cast<HostRow *>(device_view(sc->h_rows));
+    if (!rows_dev) return image_to_host_full(sc, dst, nfl);
+    const uint32_t gen = ++sc->copy_gen;
+    Rgb<uint32_t> bgb;
+    std::memcpy(bgb.c, sc->ds.background, sizeof bgb.c);
+    hipLaunchKernelGGL(k_rows_to_host, dim3((unsigned)H), dim3(256), 0, sc->stream, sc->d_out, W, bgb, target, rows_dev,
+                       gen);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(sc->copy_ev, sc->stream));
+    HostPool &pool = HostPool::get();
+    const int nb = std::min(pool.threads(), H);
+    struct Job {
+        crt_hip_scene *sc;
+        float *dst;
+        bool staged;
+        int W, H, nb;
+        uint32_t gen;
+        float bg[3];
+        std::atomic<int> err{0};   /* a hipError_t of the copy kernel's event, or -1: a row never came */
+    } job;
+    job.sc = sc;
+    job.dst = dst;
+    job.staged = dst_dev == nullptr;
+    job.W = W;
+    job.H = H;
+    job.nb = nb;
+    job.gen = gen;
+    std::memcpy(job.bg, sc->ds.background, sizeof job.bg);
+    pool.run(nb, [](void *a, int b) {
+        Job &j = *static_cast<Job *>(a);
+        const int r0 = (int)((int64_t)j.H * b / j.nb), r1 = (int)((int64_t)j.H * (b + 1) / j.nb);
+        const int64_t row = 3 * (int64_t)j.W;
+        HostRow *R = j.sc->h_rows;
+        /* the row's mark reaches gen; polls hipEventQuery now and then, so a
+         * kernel that faulted (or any copy error) ends the wait */
+        auto wait_mark = [&](const uint32_t *mark) -> bool {
+            for (int polls = 0;; ++polls) {
+                if (__atomic_load_n(mark, __ATOMIC_ACQUIRE) == j.gen) return true;
+                if (j.err.load(std::memory_order_relaxed)) return false;
+                if ((polls & 1023) == 1023) {
+                    const hipError_t e = hipEventQuery(j.sc->copy_ev);
+                    if (e != hipErrorNotReady) {
+                        if (__atomic_load_n(mark, __ATOMIC_ACQUIRE) == j.gen) return true;
+                        int z = 0;
+                        j.err.compare_exchange_strong(z, e != hipSuccess ? (int)e : -1);
+                        return false;
+                    }
+                }
+                __builtin_ia32_pause();
+            }
+        };
+        for (int y = r0; y < r1; ++y) {   /* the background, row by row as the spans are published */
+            if (!wait_mark(&R[y].span_gen)) return;
+            float *d = j.dst + y * row;
+            const int x0 = R[y].x0, x1 = R[y].x1;
+            fill_background(d, x0, j.bg);
+            fill_background(d + 3 * (int64_t)x1, j.W - x1, j.bg);
+        }
+        for (int y = r0; y < r1; ++y) {   /* the spans' pixels */
+            if (!wait_mark(&R[y].px_gen)) return;
+            if (j.staged && R[y].x1 > R[y].x0)
+                std::memcpy(j.dst + y * row + 3 * (int64_t)R[y].x0, j.sc->h_stage + y * row + 3 * (int64_t)R[y].x0,
+                            (size_t)(R[y].x1 - R[y].x0) * 3 * sizeof(float));
+        }
+        store_fence();
+    }, &job);
+    const int err = job.err.load();
+    const hipError_t e = hipEventSynchronize(sc->copy_ev);
+    if (err > 0 || e != hipSuccess)
+        return set_error(CRT_E_HIP, std::string("image copy: ") + hipGetErrorString(err > 0 ? (hipError_t)err : e));
+    if (err < 0) return set_error(CRT_E_HIP, "image copy: a row's copy was never published");
     return CRT_OK;
 }
 
@@ -340,7 +409,7 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
             HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&sc->h_stage), bytes, hipHostMallocDefault));
             sc->stage_ev.assign(kStageChunks, nullptr);
             for (auto &e : sc->stage_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            (void)copy_pool();
+            (void)HostPool::get();
             /* the first DMA into a fresh pinned buffer, and the stream's first
              * asynchronous copy, pay one-time setup (~7 ms: profiles/r03/cold) */
             HIP_TRY(hipMemcpyAsync(sc->h_stage, sc->d_out, bytes, hipMemcpyDeviceToHost, sc->stream));
@@ -434,6 +503,8 @@ void crt_hip_scene_destroy(crt_hip_scene *sc) {
     for (void *p : sc->plan_allocs) (void)hipFree(p);
     bins_free(sc);
     if (sc->d_out) (void)hipFree(sc->d_out);
+    if (sc->h_rows) (void)hipHostFree(sc->h_rows);
+    if (sc->copy_ev) (void)hipEventDestroy(sc->copy_ev);
     if (sc->gi_frames) (void)hipFree(sc->gi_frames);
     wf_free(sc->wf);
     for (auto &kv : sc->unpack_plans) (void)hipFree(kv.second.first);
@@ -811,6 +882,9 @@ static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
             wf_graphs_clear(sc->wf);   /* graphs hold the level kernels */
             { sc->wf.recs.clear(); ++sc->wf.epoch; }
         }
+        return CRT_OK;
+    } else if (k == "compact_copy") {   /* crt_hip_render's image copy: 1 compact (default), 0 the whole image */
+        sc->compact_copy = value != 0;
         return CRT_OK;
     } else if (k == "bins_reuse") {   /* no plan depends on it */
         sc->bins_reuse = value != 0;

@@ -175,4 +175,27 @@ std::vector<DBucket> shard_buckets(int32_t width, int32_t height, int32_t bucket
 std::vector<DBucket> shard_live_tiles(int32_t width, int32_t height, int32_t bucket_size, int shard, int shard_count,
                                       const uint8_t *live, int64_t *packed_pixels, std::vector<DBucket> *dead);
 
+/* Host half of the compact image copy (crt_host_copy.cpp, crt_api.hip
+ * image_to_host).  fill_background: n pixels of the colour bg from dst on;
+ * store_fence() orders a thread's stores before a handover to another. */
+void fill_background(float *dst, int64_t n, const float bg[3]);
+void store_fence();
+
+/* Persistent host threads that run the bands of a host-side image copy with
+ * the calling thread: task i of n runs on thread i mod (workers + 1), the
+ * caller taking i = 0, T, 2T...  Workers spin for a while after each job (a
+ * frame's copy follows the previous one closely) and then sleep. */
+class HostPool {
+public:
+    static HostPool &get();
+    int threads() const;                                    /* workers + the caller */
+    void run(int n, void (*fn)(void *, int), void *arg);   /* returns when all n tasks ran */
+    ~HostPool();
+
+private:
+    explicit HostPool(int workers);
+    struct Impl;
+    Impl *impl_;
+};
+
 }  // namespace crt_amd

@@ -221,6 +221,15 @@ struct crt_hip_scene {
      * staging image and one event per chunk of the copy */
     float *h_stage = nullptr;
     std::vector<hipEvent_t> stage_ev;
+    /* the compact image copy (crt_api.hip image_to_host): per row of the
+     * frame its span of non-background pixels and its progress (k_rows_to_host
+     * writes them into pinned memory), the frames copied so far (each copy's
+     * number marks its rows), the copy kernel's end */
+    crt_amd::HostRow *h_rows = nullptr;
+    int32_t copy_h = 0;
+    uint32_t copy_gen = 0;
+    hipEvent_t copy_ev = nullptr;
+    int compact_copy = 1;          /* option "compact_copy": 0 copies the whole image */
     ShardPlan full;
     std::map<std::pair<int, int>, ShardPlan> shard_plans;
     std::map<int, std::pair<UnpackBucket *, int>> unpack_plans;
