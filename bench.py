@@ -103,9 +103,11 @@ def parse(argv=None):
                         "with a blocking 1-GPU render (on by default)")
     p.add_argument("--check", dest="check", action="store_true", help=argparse.SUPPRESS)   # the default; old scripts
     p.set_defaults(check=True)
-    p.add_argument("--mode", choices=["tiles", "frames"], default="tiles",
-                   help="N>1: tiles = one frame sharded over the GPUs + RCCL gather (strong scaling, default); "
-                        "frames = each GPU renders whole frames (weak scaling)")
+    p.add_argument("--mode", choices=["auto", "tiles", "frames"], default="auto",
+                   help="N>1: tiles = one frame sharded over the GPUs + RCCL gather (strong scaling); frames = each "
+                        "GPU renders whole frames (weak scaling); auto (default) = frames when the library's GPU-count "
+                        "policy gives the frame one GPU (its one-GPU estimate is under 2 ms: C2, C3), else tiles "
+                        "(C4, C5); the other mode is measured as `secondary`")
     p.add_argument("--payload", choices=["f32", "u8"], default="f32",
                    help="tiles mode: gather fp32 RGB (the render_image image) or write_ppm's 8-bit components")
     p.add_argument("--shards", choices=["compact", "full"], default="compact",
@@ -128,6 +130,7 @@ def parse(argv=None):
     p.add_argument("--selftest-launch", action="store_true",
                    help="launcher plumbing only: ranks join the process group and report; no GPU work")
     p.add_argument("--cpu-worker", default=None, help=argparse.SUPPRESS)
+    p.add_argument("--shim-worker", default=None, help=argparse.SUPPRESS)
     return p.parse_args(argv)
 
 
@@ -304,6 +307,65 @@ def cold_cli(cfg: dict, w: int, h: int, settings) -> dict | None:
             "command": "bin/crt_renderer scene.crtscene out.ppm --gpus 1 (fresh process)"}
 
 
+REFTREES = {"c2": "14-01-acceleration-tree__scene1", "c3": "11-01-refractive__scene8", "c4": "15-01-conclusion__scene2"}
+
+
+def shim_worker(spec: dict) -> dict:
+    """The reference's main.cpp timed region with the crt::render_image shim
+    linked (csrc/shim/crt_render_image_hip.cpp -> crt_hip_render_image_tree,
+    csrc/shim/crt_shim_core.cpp), in a process that has not touched the GPU:
+    the Scene the reference built (its vertex array and acceleration tree as
+    its own compiled TUs produced them, tests/golden/reftree_*.npz) handed
+    over as render_image hands it.  first = the first call (it creates the
+    device scene: HIP start-up, upload, BVH, bins, inside the reference's
+    timer); repeat = the median of the calls after it (the cached device scene,
+    its content compared with the caller's while the frame renders)."""
+    import ctypes as C
+    import numpy as np
+    from crt_amd import native as N
+    cfg = CONFIGS[spec["config"]]
+    name = REFTREES[spec["config"]]
+    z = np.load(ROOT / "tests" / "golden" / f"reftree_{name}.npz")
+    sc = make_scene(cfg, spec["w"], spec["h"])
+    ts = N.TreeScene(sc, z["vertices"], z["bounds"], z["children"], z["leaf_offsets"], z["leaf_triangles"])
+    st = N.RendererSettings.default(**cfg["settings"])
+    L = N.lib()
+    first_out = np.zeros((spec["h"], spec["w"], 3), np.float32)   # render_image's Image (crt_image.h:15-19)
+    t0 = time.perf_counter()
+    rc = L.crt_hip_render_image_tree(ts.tree_desc_ptr(), C.byref(st), first_out.ctypes.data)
+    first = (time.perf_counter() - t0) * 1e3
+    if rc != 0:
+        return {"error": N.last_error()}
+    out = np.zeros_like(first_out)
+    ts_ms = []
+    for _ in range(spec["frames"]):
+        t0 = time.perf_counter()
+        L.crt_hip_render_image_tree(ts.tree_desc_ptr(), C.byref(st), out.ctypes.data)
+        ts_ms.append((time.perf_counter() - t0) * 1e3)
+    same = bool(np.array_equal(out.view(np.uint32), first_out.view(np.uint32)))
+    stats = N.render_image_tree_stats()
+    return {"first_call_ms": round(first, 3), "repeat_ms": round(statistics.median(ts_ms), 4),
+            "repeat_ms_min": round(min(ts_ms), 4), "repeats": len(ts_ms), "repeat_equals_first": same,
+            "creates": stats["creates"], "reuses": stats["reuses"]}
+
+
+def shim_timing(config: str, w: int, h: int, frames: int = 30) -> dict | None:
+    if config not in REFTREES:
+        return None
+    try:
+        out = subprocess.run([sys.executable, str(Path(__file__).resolve()), "--shim-worker",
+                              json.dumps({"config": config, "w": w, "h": h, "frames": frames})],
+                             capture_output=True, text=True, timeout=300)
+        d = json.loads(out.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError) as e:
+        return {"error": str(e)[-300:]}
+    d["scene"] = f"tests/golden/reftree_{REFTREES[config]}.npz (the reference's built Scene) at {w}x{h}"
+    d["note"] = ("crt_hip_render_image_tree (the shim's body) in a fresh process; the reference's timer "
+                 "(main.cpp:37-43) also holds render_image's zero-filled Image (crt_image.h:15-19) and the shim's "
+                 "flatten of the Scene, both host work outside this call")
+    return d
+
+
 # --------------------------------------------------------------------------
 #  roofline
 # --------------------------------------------------------------------------
@@ -377,6 +439,14 @@ def load_pmc(path: str | None, config: str, w: int, h: int) -> dict | None:
 # --------------------------------------------------------------------------
 #  ranks
 # --------------------------------------------------------------------------
+def policy_gpus(scene, settings, visible: int) -> int:
+    """crt_auto_gpus: the GPUs the library's policy gives this frame out of
+    `visible`; reads the scene description only (no GPU)."""
+    import ctypes as C
+    from crt_amd import native as N
+    return int(N.lib().crt_auto_gpus(N._desc_ptr(scene), C.byref(settings), int(visible)))
+
+
 def selftest_launch(a) -> None:
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -390,8 +460,13 @@ def selftest_launch(a) -> None:
     else:
         ok = True
     if int(os.environ.get("RANK", "0")) == 0:
+        from crt_amd import native as N
+        from crt_amd.distributed import select_mode
+        cfg = CONFIGS[a.config]
+        st = N.RendererSettings.default(**cfg["settings"])
+        mode = select_mode(a.mode, policy_gpus(make_scene(cfg, *cfg["size"]), st, max(world, a.gpus)))
         print(json.dumps({"selftest": "launch", "n_gpus": world, "requested": a.gpus, "all_reduce_ok": ok,
-                          "scaling": "strong" if a.mode == "tiles" else "weak"}), flush=True)
+                          "mode": mode, "scaling": "strong" if mode == "tiles" else "weak"}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -401,6 +476,9 @@ def main():
     a = parse(argv)
     if a.cpu_worker is not None:
         print(json.dumps(cpu_worker(json.loads(a.cpu_worker))), flush=True)
+        return 0
+    if a.shim_worker is not None:
+        print(json.dumps(shim_worker(json.loads(a.shim_worker))), flush=True)
         return 0
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(a.gpus, argv)
@@ -412,7 +490,7 @@ def main():
     import torch  # import before libcrt_hip so both share torch's HIP runtime
     import torch.distributed as dist
     from crt_amd import native as N
-    from crt_amd.distributed import FramePipeline
+    from crt_amd.distributed import FrameParallel, FramePipeline, select_mode
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -506,7 +584,8 @@ def main():
             up = gpu.unpack_compact if compact else gpu.unpack_shards
             up(world, src.data_ptr(), frame.data_ptr(), sptr)
 
-    mode = a.mode if world > 1 else "single"
+    mode = select_mode(a.mode, policy_gpus(scene, settings, world)) if world > 1 else "single"
+    other = {"tiles": "frames", "frames": "tiles"}.get(mode)
     if world > 1:
         dt = torch.uint8 if u8 else torch.float32
         shard_u8 = torch.empty(stride, dtype=torch.uint8, device="cuda")
@@ -517,11 +596,13 @@ def main():
         pipe = FramePipeline(rank, world, stride, lambda n: torch.empty(n, dtype=dt, device=dev), render_shard,
                              unpack, dist)
 
+    fpar = FrameParallel(rank, world, lambda k: timed(lambda: gpu.render_device(settings, frame.data_ptr(), sptr)))
+
     def step(m):
         if m == "tiles":
             pipe.step()
         else:
-            timed(lambda: gpu.render_device(settings, frame.data_ptr(), sptr))
+            fpar.step()
 
     def drain(m):
         if m == "tiles":
@@ -707,28 +788,38 @@ def main():
     mrays = rays_per_frame * frames_per_step * a.steps / elapsed / 1e6
 
     secondary = None
-    if world > 1 and mode == "tiles" and not a.no_secondary:
-        el2, km2 = measure("frames", a.steps)
-        secondary = {"mode": "frames", "scaling": "weak", "value": round(rays_per_frame * world * a.steps / el2 / 1e6, 3),
+    if world > 1 and not a.no_secondary:
+        el2, km2 = measure(other, a.steps)
+        fps2 = world if other == "frames" else 1
+        secondary = {"mode": other, "scaling": "weak" if other == "frames" else "strong",
+                     "value": round(rays_per_frame * fps2 * a.steps / el2 / 1e6, 3),
                      "unit": "Mrays/s", "ms_per_step": round(el2 / a.steps * 1e3, 5), "kernel_ms": round(km2, 5),
-                     "frames_per_step": world}
+                     "frames_per_step": fps2}
 
     # end-to-end frame time of the reference's call: render_image returns a
     # host image (crt_image.h:11-27), the CLI times the whole call (main.cpp:37-43)
-    e2e = None
+    e2e = e2e_page = None
     if world == 1 and not a.no_e2e:
         host = torch.empty(npx * 3, dtype=torch.float32, pin_memory=True)
-        for _ in range(3):
-            gpu.render_host(settings, host.data_ptr())
-        ts = []
-        for _ in range(max(5, min(a.steps, 50))):
-            s = time.perf_counter()
-            gpu.render_host(settings, host.data_ptr())
-            ts.append(time.perf_counter() - s)
-        e2e = statistics.median(ts) * 1e3
-    cold = None
+        page = np.zeros(npx * 3, np.float32)
+
+        def e2e_of(ptr):
+            for _ in range(3):
+                gpu.render_host(settings, ptr)
+            ts = []
+            for _ in range(max(5, min(a.steps, 50))):
+                s = time.perf_counter()
+                gpu.render_host(settings, ptr)
+                ts.append(time.perf_counter() - s)
+            return statistics.median(ts) * 1e3
+
+        e2e = e2e_of(host.data_ptr())
+        e2e_page = e2e_of(page.ctypes.data)
+    cold = shim = None
     if world == 1 and rank == 0 and not a.no_e2e:
         cold = cold_cli(cfg, W, H, settings)
+        if not a.shadows:
+            shim = shim_timing(a.config, W, H)
 
     shard_frac = 1.0 / world if mode == "tiles" else 1.0
     pmc = load_pmc(a.pmc_json, a.config, W, H)
@@ -779,9 +870,14 @@ def main():
                        "frames_per_step": frames_per_step,
                        "frame_ms": round(ms_per_step, 5), "kernel_ms": round(kern_ms, 5),
                        "e2e_ms": round(e2e, 4) if e2e is not None else None,
-                       "e2e_note": ("crt_hip_render into a pinned host buffer: render + D2H of the fp32 image, "
-                                    "the reference's render_image call (main.cpp:37-43)") if e2e is not None else None,
+                       "e2e_pageable_ms": round(e2e_page, 4) if e2e_page is not None else None,
+                       "e2e_note": ("crt_hip_render into a pinned (e2e_ms) / pageable (e2e_pageable_ms) host buffer, "
+                                    "median of blocking calls: the render and the fp32 image in host memory, the "
+                                    "reference's render_image call (main.cpp:37-43); the image copy is compact "
+                                    "(crt_api.hip image_to_host: each row's non-background span over PCIe, the "
+                                    "background written by host threads)") if e2e is not None else None,
                        "cold_cli": cold,
+                       "shim": shim,
                        "check": check, "build_id": build_id,
                        "camera_bins": bins,
                        "camera_orbit": orbit,

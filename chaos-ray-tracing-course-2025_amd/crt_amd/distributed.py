@@ -27,6 +27,44 @@ import numpy as np
 from .native import shard_compact_plan, shard_plan
 
 
+def select_mode(requested: str, policy_gpus: int) -> str:
+    """The N-GPU mode of bench.py.  requested: "auto" | "tiles" |
+    "frames"; policy_gpus: crt_auto_gpus of the frame for the N visible GPUs
+    (the GPUs one frame pays for: 1 when its one-GPU estimate is under 2 ms).
+    A frame that does not pay for a second GPU cannot strong-scale (C2: 1.08x,
+    C3: 1.13x at 8 shards), so "auto" renders whole frames per GPU (weak
+    scaling); frames that do (C4, C5) are sharded as tiles (strong scaling)."""
+    if requested not in ("auto", "tiles", "frames"):
+        raise ValueError(f"mode {requested!r}")
+    if requested != "auto":
+        return requested
+    return "frames" if policy_gpus <= 1 else "tiles"
+
+
+class FrameParallel:
+    """Whole frames per rank (frames mode): step s renders frame
+    s * world + rank on this rank, with no collective on the data path.
+    `render(frame_index)` renders one frame (and returns an optional digest
+    of it, kept with its index); `collect(dist)` hands every rank's
+    (frame, digest) pairs to every rank, so rank 0 can account for each frame
+    of the run exactly once."""
+
+    def __init__(self, rank: int, world: int, render: Callable[[int], object]):
+        self.rank, self.world, self.render = rank, world, render
+        self.steps = 0
+        self.done: list = []
+
+    def step(self) -> None:
+        k = self.steps * self.world + self.rank
+        self.done.append((k, self.render(k)))
+        self.steps += 1
+
+    def collect(self, dist) -> list:
+        out = [None] * self.world
+        dist.all_gather_object(out, self.done)
+        return sorted(x for part in out for x in part)
+
+
 class FrameSharder:
     """Buffers + steps of one sharded frame for `rank` of `world`."""
 

@@ -14,7 +14,9 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <future>
 #include <thread>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -92,12 +94,16 @@ int ensure_copy_rows(crt_hip_scene *sc) {
     if (sc->h_rows && sc->copy_h == H) return CRT_OK;
     HIP_TRY(hipStreamSynchronize(sc->stream));
     if (sc->h_rows) (void)hipHostFree(sc->h_rows);
+    if (sc->d_row_spans) (void)hipFree(sc->d_row_spans);
     sc->h_rows = nullptr;
+    sc->d_row_spans = nullptr;
     sc->copy_h = 0;
     HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&sc->h_rows), (size_t)H * sizeof(HostRow), hipHostMallocDefault));
-    std::memset(sc->h_rows, 0, (size_t)H * sizeof(HostRow));
-    sc->copy_gen = 0;   /* no row carries a copy number above 0 */
+    HIP_TRY(hipMalloc(&sc->d_row_spans, (size_t)H * sizeof(int2)));
+    if (!sc->spans_ev) HIP_TRY(hipEventCreateWithFlags(&sc->spans_ev, hipEventDisableTiming));
     if (!sc->copy_ev) HIP_TRY(hipEventCreateWithFlags(&sc->copy_ev, hipEventDisableTiming));
+    for (hipEvent_t &e : sc->copy_band_ev)
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     sc->copy_h = H;
     return CRT_OK;
 }
@@ -112,34 +118,64 @@ void *device_view(const void *p) {
     return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
 }
 
+/* A check for the copy's host threads to run while the frame renders
+ * (render_checked): fn(arg, i, n) for i < n; any false sets `failed`. */
+struct HostCheck {
+    bool (*fn)(void *, int, int) = nullptr;
+    void *arg = nullptr;
+    std::atomic<bool> failed{false};
+};
+
+int image_to_host_full_checked(crt_hip_scene *sc, float *dst, size_t nfl, HostCheck *check) {
+    if (check && check->fn) {   /* the check on the pool while the frame renders, then the copy */
+        HostPool &pool = HostPool::get();
+        pool.run(pool.threads(), [](void *a, int i) {
+            HostCheck &c = *static_cast<HostCheck *>(a);
+            if (!c.fn(c.arg, i, HostPool::get().threads())) c.failed = true;
+        }, check);
+    }
+    return image_to_host_full(sc, dst, nfl);
+}
+
 /* The compact copy of the frame in d_out into host memory, queued behind the
- * frame on the scene's stream.  k_rows_to_host (one block a row) finds each
- * row's span of non-background pixels, publishes it in the row's pinned
- * record and writes the span straight into host memory: into the caller's
- * image when it is pinned, else into the pinned staging image.  Meanwhile
- * the host (HostPool, one band of rows a thread) writes the background
- * outside each span as soon as the span is published, and (staging) copies
- * each span on once its pixels are published.  Every pixel outside a row's
- * span has the background's bits (k_rows_to_host compares bits), so the
- * caller's image equals d_out bit for bit.  ~1/7 of C2's frame crosses PCIe. */
-int image_to_host(crt_hip_scene *sc, float *dst, size_t nfl) {
+ * frame on the scene's stream.  k_row_spans finds each row's span of
+ * non-background pixels (into pinned row records); k_rows_to_host writes the
+ * spans straight into host memory: into the caller's image when it is pinned,
+ * else into the pinned staging image.  Meanwhile the host (HostPool, one band
+ * of rows a thread) writes the background outside each span as soon as the
+ * spans are known, and (staging) copies each span on once the spans are in
+ * host memory.  Every pixel outside a row's span has the background's bits
+ * (k_row_spans compares bits), so the caller's image equals d_out bit for
+ * bit.  ~1/7 of C2's frame crosses PCIe. */
+int image_to_host(crt_hip_scene *sc, float *dst, size_t nfl, HostCheck *check = nullptr) {
     const int W = sc->info.width, H = sc->info.height;
     if (!sc->compact_copy || !sc->h_stage || sc->grid_empty || W <= 0 || H <= 0 || (size_t)W * H * 3 != nfl)
-        return image_to_host_full(sc, dst, nfl);
+        return image_to_host_full_checked(sc, dst, nfl, check);
     int rc = ensure_copy_rows(sc);
     if (rc != CRT_OK) return rc;
     float *dst_dev = static_cast<float *>(device_view(dst));
     float *target = dst_dev;
     if (!target && !(target = static_cast<float *>(device_view(sc->h_stage))))
-        return image_to_host_full(sc, dst, nfl);
+        return image_to_host_full_checked(sc, dst, nfl, check);
     HostRow *rows_dev = static_cast<HostRow *>(device_view(sc->h_rows));
-    if (!rows_dev) return image_to_host_full(sc, dst, nfl);
-    const uint32_t gen = ++sc->copy_gen;
+    if (!rows_dev) return image_to_host_full_checked(sc, dst, nfl, check);
     Rgb<uint32_t> bgb;
     std::memcpy(bgb.c, sc->ds.background, sizeof bgb.c);
-    hipLaunchKernelGGL(k_rows_to_host, dim3((unsigned)H), dim3(256), 0, sc->stream, sc->d_out, W, bgb, target, rows_dev,
-                       gen);
+    hipLaunchKernelGGL(k_row_spans, dim3((unsigned)H), dim3(256), 0, sc->stream, sc->d_out, W, bgb, sc->d_row_spans,
+                       rows_dev);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(sc->spans_ev, sc->stream));
+    /* into the staging image in bands of rows, so the host copies a band on
+     * while the next ones cross PCIe; into the caller's pinned image at once */
+    const bool staged = dst_dev == nullptr;
+    const int G = staged ? std::min(4, H) : 1;
+    for (int g = 0; g < G; ++g) {
+        const int y0 = (int)((int64_t)H * g / G), y1 = (int)((int64_t)H * (g + 1) / G);
+        hipLaunchKernelGGL(k_rows_to_host, dim3((unsigned)(y1 - y0)), dim3(256), 0, sc->stream, sc->d_out, W, H, y0,
+                           sc->d_row_spans, target);
+        HIP_TRY(hipGetLastError());
+        if (g + 1 < G) HIP_TRY(hipEventRecord(sc->copy_band_ev[g], sc->stream));
+    }
     HIP_TRY(hipEventRecord(sc->copy_ev, sc->stream));
     HostPool &pool = HostPool::get();
     const int nb = std::min(pool.threads(), H);
@@ -147,62 +183,62 @@ int image_to_host(crt_hip_scene *sc, float *dst, size_t nfl) {
         crt_hip_scene *sc;
         float *dst;
         bool staged;
-        int W, H, nb;
-        uint32_t gen;
+        int W, H, nb, G;
         float bg[3];
-        std::atomic<int> err{0};   /* a hipError_t of the copy kernel's event, or -1: a row never came */
+        HostCheck *check;
+        std::atomic<int> err{0};   /* a hipError_t of a copy kernel's event */
     } job;
+    job.check = check && check->fn ? check : nullptr;
     job.sc = sc;
     job.dst = dst;
-    job.staged = dst_dev == nullptr;
+    job.staged = staged;
+    job.G = G;
     job.W = W;
     job.H = H;
     job.nb = nb;
-    job.gen = gen;
     std::memcpy(job.bg, sc->ds.background, sizeof job.bg);
     pool.run(nb, [](void *a, int b) {
         Job &j = *static_cast<Job *>(a);
         const int r0 = (int)((int64_t)j.H * b / j.nb), r1 = (int)((int64_t)j.H * (b + 1) / j.nb);
         const int64_t row = 3 * (int64_t)j.W;
-        HostRow *R = j.sc->h_rows;
-        /* the row's mark reaches gen; polls hipEventQuery now and then, so a
-         * kernel that faulted (or any copy error) ends the wait */
-        auto wait_mark = [&](const uint32_t *mark) -> bool {
-            for (int polls = 0;; ++polls) {
-                if (__atomic_load_n(mark, __ATOMIC_ACQUIRE) == j.gen) return true;
-                if (j.err.load(std::memory_order_relaxed)) return false;
-                if ((polls & 1023) == 1023) {
-                    const hipError_t e = hipEventQuery(j.sc->copy_ev);
-                    if (e != hipErrorNotReady) {
-                        if (__atomic_load_n(mark, __ATOMIC_ACQUIRE) == j.gen) return true;
-                        int z = 0;
-                        j.err.compare_exchange_strong(z, e != hipSuccess ? (int)e : -1);
-                        return false;
-                    }
+        const HostRow *R = j.sc->h_rows;
+        if (j.check && !j.check->fn(j.check->arg, b, j.nb)) j.check->failed = true;   /* while the GPU renders */
+        auto wait = [&](hipEvent_t ev) -> bool {   /* poll: a blocking wait may sleep past the copy */
+            for (;;) {
+                const hipError_t e = hipEventQuery(ev);
+                if (e == hipSuccess) return true;
+                if (e != hipErrorNotReady) {
+                    int z = 0;
+                    j.err.compare_exchange_strong(z, (int)e);
+                    return false;
                 }
-                __builtin_ia32_pause();
+                if (j.err.load(std::memory_order_relaxed)) return false;
+                for (int i = 0; i < 64; ++i) __builtin_ia32_pause();
             }
         };
-        for (int y = r0; y < r1; ++y) {   /* the background, row by row as the spans are published */
-            if (!wait_mark(&R[y].span_gen)) return;
+        if (!wait(j.sc->spans_ev)) return;
+        for (int y = r0; y < r1; ++y) {   /* the background, while the spans cross PCIe */
             float *d = j.dst + y * row;
             const int x0 = R[y].x0, x1 = R[y].x1;
             fill_background(d, x0, j.bg);
             fill_background(d + 3 * (int64_t)x1, j.W - x1, j.bg);
         }
-        for (int y = r0; y < r1; ++y) {   /* the spans' pixels */
-            if (!wait_mark(&R[y].px_gen)) return;
-            if (j.staged && R[y].x1 > R[y].x0)
-                std::memcpy(j.dst + y * row + 3 * (int64_t)R[y].x0, j.sc->h_stage + y * row + 3 * (int64_t)R[y].x0,
-                            (size_t)(R[y].x1 - R[y].x0) * 3 * sizeof(float));
+        if (j.staged) {
+            /* the launches (bands of rows) that hold rows r0 .. r1 - 1 */
+            for (int g = 0; g < j.G; ++g) {
+                const int y0 = (int)((int64_t)j.H * g / j.G), y1 = (int)((int64_t)j.H * (g + 1) / j.G);
+                if (y1 > r0 && y0 < r1 && !wait(g + 1 < j.G ? j.sc->copy_band_ev[g] : j.sc->copy_ev)) return;
+            }
+            for (int y = r0; y < r1; ++y)
+                if (R[y].x1 > R[y].x0)
+                    std::memcpy(j.dst + y * row + 3 * (int64_t)R[y].x0, j.sc->h_stage + y * row + 3 * (int64_t)R[y].x0,
+                                (size_t)(R[y].x1 - R[y].x0) * 3 * sizeof(float));
         }
         store_fence();
     }, &job);
     const int err = job.err.load();
-    const hipError_t e = hipEventSynchronize(sc->copy_ev);
-    if (err > 0 || e != hipSuccess)
-        return set_error(CRT_E_HIP, std::string("image copy: ") + hipGetErrorString(err > 0 ? (hipError_t)err : e));
-    if (err < 0) return set_error(CRT_E_HIP, "image copy: a row's copy was never published");
+    const hipError_t e = err ? (hipError_t)err : spin_event(sc->copy_ev);
+    if (e != hipSuccess) return set_error(CRT_E_HIP, std::string("image copy: ") + hipGetErrorString(e));
     return CRT_OK;
 }
 
@@ -210,16 +246,68 @@ int image_to_host(crt_hip_scene *sc, float *dst, size_t nfl) {
 
 namespace crt_amd {
 
+int UploadBatch::flush(crt_hip_scene *sc) {
+    if (items_.empty()) return CRT_OK;
+    void *p = nullptr;
+    HIP_TRY(hipMalloc(&p, host_.size()));
+    sc->allocs.push_back(p);
+    HIP_TRY(hipMemcpy(p, host_.data(), host_.size(), hipMemcpyHostToDevice));
+    for (const Item &it : items_) *it.dst = static_cast<const char *>(p) + it.off;
+    sc->info.device_bytes += (int64_t)host_.size();
+    items_.clear();
+    host_.clear();
+    return CRT_OK;
+}
+
 /* A prepared host scene into HBM of `device`.  primary = false: a further
  * replica of a multi-GPU handle (crt_multi.hip), which renders into the
  * gather buffers only — no output image, no pinned staging image. */
+/* CRT_CREATE_TRACE builds (A/B): each step of scene_upload timed on stderr */
+#ifdef CRT_CREATE_TRACE
+#define CRT_CREATE_STAMP(what)                                                                                  \
+    do {                                                                                                       \
+        const auto t_ = std::chrono::steady_clock::now();                                                      \
+        std::fprintf(stderr, "create %-10s %8.3f ms\n", what,                                                  \
+                     std::chrono::duration<double, std::milli>(t_ - t_stamp).count());                         \
+        t_stamp = t_;                                                                                          \
+    } while (0)
+#else
+#define CRT_CREATE_STAMP(what) ((void)0)
+#endif
+
 int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **out) {
     *out = nullptr;
     const auto t_up = std::chrono::steady_clock::now();
+#ifdef CRT_CREATE_TRACE
+    auto t_stamp = t_up;
+#endif
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return set_error(CRT_E_INVALID, "no such HIP device");
     HIP_TRY(hipSetDevice(device));
+    /* the pinned staging image (copies into pageable memory, image_to_host):
+     * page-locking 25 MB takes ~4 ms, so it runs beside the rest of the upload */
+    const size_t out_bytes = (size_t)hs.width * hs.height * 3 * sizeof(float);
+    const bool want_stage = primary && out_bytes > 0;
+    std::future<std::pair<hipError_t, float *>> stage_f;
+    if (want_stage)
+        stage_f = std::async(std::launch::async, [device, out_bytes]() {
+            float *p = nullptr;
+            hipError_t e = hipSetDevice(device);
+            if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&p), out_bytes, hipHostMallocDefault);
+            return std::make_pair(e, p);
+        });
+    /* joined on every return path: a staging image not taken by the scene (an
+     * error, an empty bucket grid) is freed here */
+    struct StageJoin {
+        std::future<std::pair<hipError_t, float *>> *f;
+        ~StageJoin() {
+            if (f->valid()) {
+                const auto r = f->get();
+                if (r.second) (void)hipHostFree(r.second);
+            }
+        }
+    } stage_join{&stage_f};
     std::unique_ptr<crt_hip_scene> sc(new crt_hip_scene());
     sc->device = device;
 #ifdef CRT_AB_OPTIONS
@@ -263,11 +351,12 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
     start_host_tables(gi_tables, pow5_table);   /* background, overlapping the upload below */
     DeviceScene &ds = sc->ds;
     int rc;
+    UploadBatch ub;   /* every host array of the scene: one allocation, one copy */
     ds.prune_origin_max = hs.prune_origin_max;
     if (hs.tree_on_host) {
-        if ((rc = upload(sc.get(), hs.nodes, &ds.nodes)) != CRT_OK) return rc;
+        ub.add(hs.nodes, &ds.nodes);
         ds.node_count = (int32_t)hs.nodes.size();
-        if ((rc = upload(sc.get(), hs.pnodes, &ds.pnodes)) != CRT_OK) return rc;
+        ub.add(hs.pnodes, &ds.pnodes);
         auto ok = [](float x) {
             const float m = std::fabs(x);
             return x == 0.0f || (m >= 0x1p-40f && m <= 0x1p62f);
@@ -277,13 +366,13 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
             if (!(ok(n.lo_x) && ok(n.lo_y) && ok(n.lo_z) && ok(n.hi_x) && ok(n.hi_y) && ok(n.hi_z) &&
                   n.lo_x <= n.hi_x && n.lo_y <= n.hi_y && n.lo_z <= n.hi_z))   /* ordered: crt_device.h in_slab */
                 ds.planes_ok = 0;
-        if ((rc = upload(sc.get(), hs.slots, &ds.slots)) != CRT_OK) return rc;
-        if ((rc = upload(sc.get(), hs.slot_tri, &ds.slot_tri)) != CRT_OK) return rc;
-        if ((rc = upload(sc.get(), hs.slot_cull, &ds.slot_cull)) != CRT_OK) return rc;
+        ub.add(hs.slots, &ds.slots);
+        ub.add(hs.slot_tri, &ds.slot_tri);
+        ub.add(hs.slot_cull, &ds.slot_cull);
         std::vector<uint32_t> bits((hs.slot_cull.size() + 31) / 32 + 1, 0u);
         for (size_t k = 0; k < hs.slot_cull.size(); ++k)
             if (hs.slot_cull[k]) bits[k >> 5] |= 1u << (k & 31);
-        if ((rc = upload(sc.get(), bits, &ds.slot_cull_bits)) != CRT_OK) return rc;
+        ub.add(bits, &ds.slot_cull_bits);
         sc->ref_bounds = hs.ref_bounds;
         sc->ref_children = hs.ref_children;
         sc->ref_leaf_off = hs.ref_leaf_off;
@@ -318,12 +407,12 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
                                  m * (int64_t)(sizeof(DTriGeo) + 4 + 1) + (m / 32 + 1) * 4;
     }
     if (hs.bnode_count > 0) {   /* secondary-ray BVH (crt_bvh.h) */
-        if ((rc = upload(sc.get(), hs.bnodes, &ds.bnodes)) != CRT_OK) return rc;
-        if ((rc = upload(sc.get(), hs.btri, &ds.btri)) != CRT_OK) return rc;
-        if ((rc = upload(sc.get(), hs.btri_id, &ds.btri_id)) != CRT_OK) return rc;
+        ub.add(hs.bnodes, &ds.bnodes);
+        ub.add(hs.btri, &ds.btri);
+        ub.add(hs.btri_id, &ds.btri_id);
         ds.bnode_count = hs.bnode_count;
-        if ((rc = upload(sc.get(), hs.ktopo, &ds.ktopo)) != CRT_OK) return rc;
-        if ((rc = upload(sc.get(), hs.ktopo2, &ds.ktopo2)) != CRT_OK) return rc;
+        ub.add(hs.ktopo, &ds.ktopo);
+        ub.add(hs.ktopo2, &ds.ktopo2);
     } else if (hs.tri_attr.size() > kHostBvhMax && sc->bvh_device) {   /* too large for the host build: on the device */
         DeviceBvh db;
         rc = build_bvh_device(hs, nullptr, db);
@@ -333,8 +422,8 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
         ds.btri = db.btri;
         ds.btri_id = db.btri_id;
         ds.bnode_count = db.node_count;
-        if ((rc = upload(sc.get(), hs.ktopo, &ds.ktopo)) != CRT_OK) return rc;   /* host-built trees only */
-        if ((rc = upload(sc.get(), hs.ktopo2, &ds.ktopo2)) != CRT_OK) return rc;
+        ub.add(hs.ktopo, &ds.ktopo);   /* host-built trees only */
+        ub.add(hs.ktopo2, &ds.ktopo2);
         sc->info.bvh_on_device = 1;
         sc->info.bvh_depth = db.max_depth;
         sc->info.bvh_ms += db.build_ms;
@@ -349,13 +438,15 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
      * one: C5's camera rays take the pruned kd packet walk faster (4.49 against
      * 4.80 ms at 4K); that BVH serves the scattered rays */
     if (ds.bnodes && !sc->info.bvh_on_device) sc->traversal = 14;
-    if ((rc = upload(sc.get(), hs.tri_attr, &ds.tri_attr)) != CRT_OK) return rc;
-    if ((rc = upload(sc.get(), hs.vnormal, &ds.vnormal)) != CRT_OK) return rc;
-    if ((rc = upload(sc.get(), hs.vuv, &ds.vuv)) != CRT_OK) return rc;
-    if ((rc = upload(sc.get(), hs.materials, &ds.materials)) != CRT_OK) return rc;
-    if ((rc = upload(sc.get(), hs.textures, &ds.textures)) != CRT_OK) return rc;
-    if ((rc = upload(sc.get(), hs.texels, &ds.texels)) != CRT_OK) return rc;
-    if ((rc = upload(sc.get(), hs.lights, &ds.lights)) != CRT_OK) return rc;
+    ub.add(hs.tri_attr, &ds.tri_attr);
+    ub.add(hs.vnormal, &ds.vnormal);
+    ub.add(hs.vuv, &ds.vuv);
+    ub.add(hs.materials, &ds.materials);
+    ub.add(hs.textures, &ds.textures);
+    ub.add(hs.texels, &ds.texels);
+    ub.add(hs.lights, &ds.lights);
+    if ((rc = ub.flush(sc.get())) != CRT_OK) return rc;
+    CRT_CREATE_STAMP("flush");
     ds.light_count = (int32_t)hs.lights.size();
     std::memcpy(ds.background, hs.background, sizeof ds.background);
     ds.gi_on = hs.gi_on;
@@ -363,9 +454,11 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
     ds.refractions_on = hs.refractions_on;
 
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
+    CRT_CREATE_STAMP("stream");
     if (sc->has_secondary && !(hs.gi_on && sc->has_diffuse))   /* the wavefront path's frame sets (render_wavefront) */
         if ((rc = wf_streams(sc->wf, sc->stream)) != CRT_OK) return rc;
     warm_code_objects(sc->device, sc->stream);
+    CRT_CREATE_STAMP("warm");
     /* camera bins (crt_bins.hip), rebuilt on the device by every camera frame
      * of scenes whose camera rays the tile kernels trace without recursion
      * (no reflective / refractive material, no GI with a diffuse one); on a
@@ -373,6 +466,7 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
      * over the cap (those cells walk the BVH) */
     if (!sc->has_secondary && !(hs.gi_on && sc->has_diffuse)) {
         if ((rc = bins_setup(sc.get(), hs)) != CRT_OK) return rc;
+        CRT_CREATE_STAMP("bins");
         if (ds.bins) sc->traversal = 14;   /* bins off: the BVH walk, or the kd walk without a BVH */
     }
     HIP_TRY(hipEventCreate(&sc->ev_start));
@@ -390,6 +484,7 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
     const std::vector<DBucket> all = shard_buckets(hs.width, hs.height, hs.bucket_size, 0, 1, &px);
     sc->grid_empty = all.empty();
     if ((rc = make_tile_plan(sc.get(), all, true, sc->full)) != CRT_OK) return rc;
+    CRT_CREATE_STAMP("plan");
     /* one-time costs of a first render that belong to the upload, like the
      * runtime's own initialisation (profiles/r03/cold): the device record, the
      * output image of crt_hip_render, and the runtime's staging for copies into
@@ -398,6 +493,7 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
      * process-lifetime precompute of the host libm's values, kept out of the
      * first frame (main.cpp:37-43 times that frame) */
     if (gi_tables && (rc = ensure_gi_tables(sc.get())) != CRT_OK) return rc;
+    CRT_CREATE_STAMP("tables");
     if (pow5_table && (rc = ensure_pow5_table(sc.get())) != CRT_OK) return rc;
     {
         const DeviceScene *d = nullptr;
@@ -405,8 +501,16 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
         if (!sc->grid_empty && primary) {
             const size_t bytes = (size_t)hs.width * hs.height * 3 * sizeof(float);
             HIP_TRY(hipMalloc(&sc->d_out, bytes));
-            /* the staging image of copies into pageable memory (image_to_host) */
-            HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&sc->h_stage), bytes, hipHostMallocDefault));
+            CRT_CREATE_STAMP("d_out");
+            /* the staging image of copies into pageable memory (image_to_host), allocated beside the upload */
+            if (want_stage) {
+                const auto r = stage_f.get();
+                if (r.first != hipSuccess) return set_error(CRT_E_HIP, std::string("staging image: ") + hipGetErrorString(r.first));
+                sc->h_stage = r.second;
+            } else {
+                HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&sc->h_stage), bytes, hipHostMallocDefault));
+            }
+            CRT_CREATE_STAMP("h_stage");
             sc->stage_ev.assign(kStageChunks, nullptr);
             for (auto &e : sc->stage_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             (void)HostPool::get();
@@ -414,12 +518,15 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
              * asynchronous copy, pay one-time setup (~7 ms: profiles/r03/cold) */
             HIP_TRY(hipMemcpyAsync(sc->h_stage, sc->d_out, bytes, hipMemcpyDeviceToHost, sc->stream));
             HIP_TRY(hipStreamSynchronize(sc->stream));
+            if ((rc = ensure_copy_rows(sc.get())) != CRT_OK) return rc;   /* the compact copy's row records */
+            CRT_CREATE_STAMP("first_dma");
         }
         unsigned long long probe[16];
         HIP_TRY(hipMemcpy(probe, sc->d_counters, sizeof probe, hipMemcpyDeviceToHost));
     }
     sc->info.bins_ms = sc->bins.setup_ms;
     sc->info.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_up).count();
+    CRT_CREATE_STAMP("end");
     *out = sc.release();
     return CRT_OK;
 }
@@ -504,7 +611,11 @@ void crt_hip_scene_destroy(crt_hip_scene *sc) {
     bins_free(sc);
     if (sc->d_out) (void)hipFree(sc->d_out);
     if (sc->h_rows) (void)hipHostFree(sc->h_rows);
+    if (sc->d_row_spans) (void)hipFree(sc->d_row_spans);
+    if (sc->spans_ev) (void)hipEventDestroy(sc->spans_ev);
     if (sc->copy_ev) (void)hipEventDestroy(sc->copy_ev);
+    for (hipEvent_t e : sc->copy_band_ev)
+        if (e) (void)hipEventDestroy(e);
     if (sc->gi_frames) (void)hipFree(sc->gi_frames);
     wf_free(sc->wf);
     for (auto &kv : sc->unpack_plans) (void)hipFree(kv.second.first);
@@ -539,7 +650,13 @@ int crt_hip_render_device(crt_hip_scene *sc, const crt_renderer_settings *st, fl
 }
 
 
-int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rgb_out, crt_render_stats *stats) {
+}  // extern "C"
+
+namespace crt_amd {
+
+int render_checked(crt_hip_scene *sc, const crt_renderer_settings *st, float *rgb_out, crt_render_stats *stats,
+                   bool (*check)(void *, int, int), void *check_arg, bool *mismatch) {
+    if (mismatch) *mismatch = false;
     if (!sc || !rgb_out) return set_error(CRT_E_INVALID, "null argument");
     int rc = check_settings(st);
     if (rc != CRT_OK) return rc;
@@ -553,8 +670,16 @@ int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rg
     };
     rc = frame();
     if (rc != CRT_OK) return rc;
-    if ((rc = image_to_host(sc, rgb_out, nfl)) != CRT_OK) return rc;
-    if (multi ? multi_overflowed(sc) : wf_overflowed(sc->wf, true)) {   /* recorded level sizes did not hold: render again with read-backs */
+    HostCheck hc;
+    hc.fn = check;
+    hc.arg = check_arg;
+    if ((rc = image_to_host(sc, rgb_out, nfl, check ? &hc : nullptr)) != CRT_OK) return rc;
+    const bool overflow = multi ? multi_overflowed(sc) : wf_overflowed(sc->wf, true);
+    if (check && hc.failed) {   /* the caller's scene is not this one: the frame is for nobody */
+        if (mismatch) *mismatch = true;
+        return CRT_OK;
+    }
+    if (overflow) {   /* recorded level sizes did not hold: render again with read-backs */
         if ((rc = frame()) != CRT_OK) return rc;
         if ((rc = image_to_host(sc, rgb_out, nfl)) != CRT_OK) return rc;
     }
@@ -574,6 +699,15 @@ int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rg
         stats->height = sc->info.height;
     }
     return CRT_OK;
+}
+
+
+}  // namespace crt_amd
+
+extern "C" {
+
+int crt_hip_render(crt_hip_scene *sc, const crt_renderer_settings *st, float *rgb_out, crt_render_stats *stats) {
+    return render_checked(sc, st, rgb_out, stats, nullptr, nullptr, nullptr);
 }
 
 int crt_hip_plan_info(const crt_hip_scene *sc, crt_plan_info *out) {

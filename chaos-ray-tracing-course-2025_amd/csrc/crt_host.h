@@ -181,6 +181,13 @@ std::vector<DBucket> shard_live_tiles(int32_t width, int32_t height, int32_t buc
 void fill_background(float *dst, int64_t n, const float bg[3]);
 void store_fence();
 
+/* crt_hip_render with a check that the image copy's host threads run while
+ * the frame renders (crt_shim_core.cpp: the cached scene's content against
+ * the caller's Scene): check(arg, i, n) for i < n; if any returns false,
+ * *mismatch is set and the image in rgb_out is not to be used. */
+int render_checked(crt_hip_scene *sc, const crt_renderer_settings *st, float *rgb_out, crt_render_stats *stats,
+                   bool (*check)(void *, int, int), void *check_arg, bool *mismatch);
+
 /* Persistent host threads that run the bands of a host-side image copy with
  * the calling thread: task i of n runs on thread i mod (workers + 1), the
  * caller taking i = 0, T, 2T...  Workers spin for a while after each job (a

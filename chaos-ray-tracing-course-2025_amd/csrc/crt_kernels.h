@@ -90,11 +90,9 @@ struct Rgb { T c[3]; };
 
 /* One image row of the compact image copy (crt_api.hip image_to_host), in
  * pinned host memory: its pixels [x0, x1) hold every pixel whose bits differ
- * from the background's (x0 = x1: none); span_gen = the frame's copy number
- * once x0, x1 are written, px_gen once the row's span has reached host memory. */
+ * from the background's (x0 = x1: none). */
 struct HostRow {
     int32_t x0, x1;
-    uint32_t span_gen, px_gen;
 };
 
 /* ---- declarations (definitions: the kernel TUs) ---- */
@@ -130,8 +128,10 @@ __global__ void k_unpack(const UnpackBucket *__restrict__ buckets, const T *__re
 __global__ void k_live_pixels(const DeviceScene *__restrict__ scene, uint8_t *__restrict__ live);
 __global__ void k_put_record(DeviceScene *__restrict__ dst, DeviceScene v);
 __global__ void k_quantize(const float *__restrict__ src, uint8_t *__restrict__ dst, int64_t n, float maxf, int maxi);
-__global__ void k_rows_to_host(const float *__restrict__ img, int width, Rgb<uint32_t> bg, float *__restrict__ host,
-                               HostRow *__restrict__ rows, uint32_t gen);
+__global__ void k_row_spans(const float *__restrict__ img, int width, Rgb<uint32_t> bg, int2 *__restrict__ spans,
+                            HostRow *__restrict__ rows);
+__global__ void k_rows_to_host(const float *__restrict__ img, int width, int height, int y0,
+                               const int2 *__restrict__ spans, float *__restrict__ host);
 __global__ void k_warm_render();
 __global__ void k_warm_gi();
 __global__ void k_warm_wf();

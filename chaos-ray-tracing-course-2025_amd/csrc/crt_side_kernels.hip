@@ -119,16 +119,14 @@ __global__ __launch_bounds__(256) void k_quantize(const float *__restrict__ src,
     }
 }
 
-/* The compact image copy (crt_api.hip image_to_host), one block a row: the
- * row's first and last pixel whose bits differ from the background's (so
- * every pixel outside [x0, x1) is the background bit for bit, for every
- * renderer, NaN included), published to the host at once (rows[y], then
- * span_gen), and then the span itself written straight into host memory
- * (`host`: the caller's pinned image or the pinned staging image, same
- * layout) and published (px_gen).  Only the spans cross PCIe; the host
- * writes the background while they do. */
-__global__ __launch_bounds__(256) void k_rows_to_host(const float *__restrict__ img, int width, Rgb<uint32_t> bg,
-                                                      float *__restrict__ host, HostRow *__restrict__ rows, uint32_t gen) {
+/* The compact image copy (crt_api.hip image_to_host), first kernel, one block
+ * a row: the row's first and last pixel whose bits differ from the
+ * background's, so every pixel outside [x0, x1) is the background bit for
+ * bit, for every renderer (NaN included).  The span goes to the device list
+ * (k_rows_to_host reads it) and to the row's pinned host record (the host
+ * writes the background outside it once this kernel's end is signalled). */
+__global__ __launch_bounds__(256) void k_row_spans(const float *__restrict__ img, int width, Rgb<uint32_t> bg,
+                                                   int2 *__restrict__ spans, HostRow *__restrict__ rows) {
     __shared__ int lo, hi;
     if (threadIdx.x == 0) {
         lo = width;
@@ -170,36 +168,39 @@ __global__ __launch_bounds__(256) void k_rows_to_host(const float *__restrict__ 
         atomicMax(&hi, myhi);
     }
     __syncthreads();
-    const int x0 = hi < 0 ? 0 : lo, x1 = hi < 0 ? 0 : hi + 1;
     if (threadIdx.x == 0) {
+        const int x0 = hi < 0 ? 0 : lo, x1 = hi < 0 ? 0 : hi + 1;
+        spans[y] = make_int2(x0, x1);
         rows[y].x0 = x0;
         rows[y].x1 = x1;
-        __hip_atomic_store(&rows[y].span_gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    if (x1 > x0) {
-        /* host[i] = img[i] over the span, widened to whole 16-B words of host
-         * memory (PCIe carries 16-B stores far better than 4-B ones).  Any
-         * float the widening adds gets its own correct value, which is also the
-         * value the host writes there if it writes it at all (the background,
-         * outside a span), so the order of the two writers does not matter. */
-        const int64_t total = n * (int64_t)gridDim.x;
-        const int64_t mis = (int64_t)((reinterpret_cast<uintptr_t>(host) >> 2) & 3);
-        int64_t a = (int64_t)y * n + 3 * (int64_t)x0, b = (int64_t)y * n + 3 * (int64_t)x1;
-        if ((reinterpret_cast<uintptr_t>(host) & 3) == 0 && mis == 0) {   /* both 16-B aligned at a multiple of 4 */
-            a &= ~(int64_t)3;
-            b = min((b + 3) & ~(int64_t)3, total);
-            const int64_t q1 = b >> 2;
-            const float4 *s4 = reinterpret_cast<const float4 *>(img);
-            float4 *d4 = reinterpret_cast<float4 *>(host);
-            for (int64_t q = (a >> 2) + threadIdx.x; q < q1; q += blockDim.x) d4[q] = s4[q];
-            for (int64_t i = (q1 << 2) + threadIdx.x; i < b; i += blockDim.x) host[i] = img[i];
-        } else {
-            for (int64_t i = a + threadIdx.x; i < b; i += blockDim.x) host[i] = img[i];
-        }
+}
+
+/* ... second kernel, one block a row: the row's span written straight into
+ * host memory (`host`: the caller's pinned image or the pinned staging image,
+ * same layout), widened to whole 16-B words of host memory (PCIe carries
+ * 16-B stores far better than 4-B ones).  Any float the widening adds gets
+ * its own correct value — the one the host writes there too if it writes it
+ * at all (the background, outside a span) — so the order of the two writers
+ * does not matter.  Only the spans cross PCIe. */
+__global__ __launch_bounds__(256) void k_rows_to_host(const float *__restrict__ img, int width, int height, int y0,
+                                                      const int2 *__restrict__ spans, float *__restrict__ host) {
+    const int y = y0 + (int)blockIdx.x;   /* a launch takes a band of rows from y0 */
+    const int2 sp = spans[y];
+    if (sp.y <= sp.x) return;
+    const int64_t n = 3 * (int64_t)width, total = n * (int64_t)height;
+    int64_t a = (int64_t)y * n + 3 * (int64_t)sp.x, b = (int64_t)y * n + 3 * (int64_t)sp.y;
+    if ((reinterpret_cast<uintptr_t>(host) & 15) == 0) {   /* host and img both 16-B aligned at multiples of 4 floats */
+        a &= ~(int64_t)3;
+        b = min((b + 3) & ~(int64_t)3, total);
+        const int64_t q1 = b >> 2;
+        const float4 *s4 = reinterpret_cast<const float4 *>(img);
+        float4 *d4 = reinterpret_cast<float4 *>(host);
+        for (int64_t q = (a >> 2) + threadIdx.x; q < q1; q += blockDim.x) d4[q] = s4[q];
+        for (int64_t i = (q1 << 2) + threadIdx.x; i < b; i += blockDim.x) host[i] = img[i];
+    } else {
+        for (int64_t i = a + threadIdx.x; i < b; i += blockDim.x) host[i] = img[i];
     }
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(&rows[y].px_gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template __global__ void k_unpack<float>(const UnpackBucket *__restrict__, const float *__restrict__,

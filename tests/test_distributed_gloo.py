@@ -219,3 +219,103 @@ def test_compact_plan_covers_live_pixels():
             full = shard_compact_plan(W, H, b, s, world, None)          # no mask: every tile of the buckets
             assert int((full[:, 2] * full[:, 3]).sum()) == int((shard_plan(W, H, b, s, world)[:, 2:4].prod(1)).sum())
         assert (cover <= 1).all() and (cover[mask == 1] == 1).all()
+
+
+def test_mode_rule_by_policy():
+    """bench.py --gpus N picks whole frames per GPU when the library's policy
+    gives the frame one GPU (C2, C3: a one-GPU frame under 2 ms cannot
+    strong-scale) and sharded tiles when it gives it more (C4, C5)."""
+    import ctypes as C
+    from conftest import scene_npz
+    from crt_amd import native as N
+    from crt_amd.distributed import select_mode
+    from crt_amd.synthetic import c5_scene
+    os.environ.pop("CRT_HIP_GPUS", None)
+    cases = [(scene_npz("14-01-acceleration-tree__scene1").set_resolution(1920, 1080), {}, "frames"),
+             (scene_npz("11-01-refractive__scene8").set_resolution(1920, 1080), {"max_ray_depth": 8}, "frames"),
+             (scene_npz("15-01-conclusion__scene2").set_resolution(3840, 2160), {}, "tiles"),
+             (c5_scene(1_000_000), {}, "tiles")]
+    for sc, over, want in cases:
+        st = N.RendererSettings.default(**over)
+        pol = N.lib().crt_auto_gpus(N._desc_ptr(sc), C.byref(st), 8)
+        assert select_mode("auto", pol) == want
+        assert select_mode("tiles", pol) == "tiles" and select_mode("frames", pol) == "frames"
+    with pytest.raises(ValueError):
+        select_mode("rows", 1)
+
+
+def _frames_worker(rank, world, port, W, H, steps, out_path):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path.insert(0, str(root / "chaos-ray-tracing-course-2025_amd"))
+    sys.path.insert(0, str(root))
+    import hashlib
+    import torch.distributed as dist
+    from crt_amd.camera import orbit_poses
+    from crt_amd.distributed import FrameParallel
+    from crt_amd.native import RendererSettings
+    from crt_amd.scene_npz import load_npz
+    from oracle import pyoracle
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    path = root / "tests/golden/scenes/14-01-acceleration-tree__scene1.npz"
+    poses = orbit_poses(load_npz(path).a, steps * world)
+    st = RendererSettings.default()
+
+    def render(k):   # frame k: the k-th pose of an orbit, rendered whole on this rank
+        sc = load_npz(path).set_resolution(W, H).set_camera(location=poses[k][0], rotation=poses[k][1])
+        img = pyoracle.OracleScene(sc).render(st)
+        return hashlib.sha256(img.tobytes()).hexdigest()
+
+    fp = FrameParallel(rank, world, render)
+    for _ in range(steps):
+        fp.step()
+    got = fp.collect(dist)
+    if rank == 0:
+        import json
+        Path(out_path).write_text(json.dumps(got))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_frames_mode_accounts_every_frame(tmp_path, oracle):
+    """Frames mode at world 2 (bench.py's default for C2 / C3 at N > 1):
+    step s renders frame s * world + rank; every frame of the run is rendered
+    exactly once, by its rank, and equals the frame rendered alone."""
+    import hashlib
+    import json
+    import torch.multiprocessing as mp
+    from crt_amd.camera import orbit_poses
+    from crt_amd.native import RendererSettings
+    from conftest import scene_npz
+    W, H, steps, world = 96, 54, 3, 2
+    out = tmp_path / "frames.json"
+    mp.spawn(_frames_worker, args=(world, free_port(), W, H, steps, str(out)), nprocs=world, join=True)
+    got = json.loads(out.read_text())
+    assert [k for k, _ in got] == list(range(steps * world))
+    poses = orbit_poses(scene_npz("14-01-acceleration-tree__scene1").a, steps * world)
+    for k, digest in got:
+        sc = scene_npz("14-01-acceleration-tree__scene1").set_resolution(W, H).set_camera(
+            location=poses[k][0], rotation=poses[k][1])
+        img = oracle.OracleScene(sc).render(RendererSettings.default())
+        assert hashlib.sha256(img.tobytes()).hexdigest() == digest, f"frame {k}"
+
+
+@pytest.mark.parametrize("config,mode", [("c2", "frames"), ("c4", "tiles")])
+def test_bench_launcher_picks_mode(config, mode):
+    """bench.py --gpus 2 without torchrun's environment starts two rank
+    processes itself (python -m torch.distributed.run) and reports the mode
+    its rule picks (--selftest-launch: ranks join a gloo group, no GPU work)."""
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "CRT_HIP_GPUS")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--selftest-launch", "--config", config],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["all_reduce_ok"] and d["mode"] == mode
+    assert d["scaling"] == ("weak" if mode == "frames" else "strong")

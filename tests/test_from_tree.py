@@ -145,6 +145,51 @@ def test_render_image_tree_core(oracle):
     lib.crt_hip_render_image_tree_reset()
 
 
+@pytest.mark.gpu
+def test_render_image_tree_same_shape_other_content():
+    """A Scene with the cached one's shape (counts, materials, lights) but other
+    content in one of its large arrays: the cached scene is rendered while the
+    arrays are compared on the copy's host threads (crt_shim_core.cpp
+    slice_same); the difference must be found in any slice (first and last
+    float of the vertices, a leaf triangle's normal in the middle, a node
+    bound) and the new content rendered from a new device scene."""
+    from crt_amd import native as N
+    lib = N.lib()
+    lib.crt_hip_render_image_tree_reset()
+    name = "14-01-acceleration-tree__scene1"
+    st = N.RendererSettings.default()
+    z = np.load(GOLDEN / f"reftree_{name}.npz")
+    sc = scene_npz(name).set_resolution(320, 180)
+
+    def ts_of(vertices=None, bounds=None, tris=None):
+        return N.TreeScene(sc, z["vertices"] if vertices is None else vertices, z["bounds"] if bounds is None else bounds,
+                           z["children"], z["leaf_offsets"], z["leaf_triangles"] if tris is None else tris)
+
+    base = ts_of()
+    N.render_image_tree(base, st)
+    v0 = z["vertices"].copy().reshape(-1)
+    v0[0] = np.float32(v0[0] + 0.5)                   # first slice: vertex 0's x
+    v1 = z["vertices"].copy().reshape(-1)
+    v1[-3 - 2] = np.float32(-v1[-3 - 2])              # last slice: a vertex normal component
+    tr = z["leaf_triangles"].copy()
+    raw = tr.view(np.uint8).reshape(len(tr), -1)
+    mid = len(tr) // 2
+    fn = raw[mid, 12:16].view(np.float32)
+    fn[0] = np.float32(-fn[0])                        # a face normal in the middle
+    b = z["bounds"].copy()
+    b.reshape(-1)[-1] = np.float32(b.reshape(-1)[-1] + 1.0)
+    for k, ts in enumerate([ts_of(vertices=v0), ts_of(vertices=v1), ts_of(tris=tr), ts_of(bounds=b)]):
+        s0 = N.render_image_tree_stats()
+        got = N.render_image_tree(ts, st)
+        s1 = N.render_image_tree_stats()
+        assert s1["creates"] - s0["creates"] == 1, f"case {k}: the changed content was not found"
+        want = N.HipScene(ts).render(st)
+        assert np.array_equal(bits(got), bits(want)), f"case {k}"
+        assert np.array_equal(bits(N.render_image_tree(ts, st)), bits(want)), f"case {k} repeat"
+        assert N.render_image_tree_stats()["reuses"] - s1["reuses"] == 1
+    lib.crt_hip_render_image_tree_reset()
+
+
 def test_render_image_shim_builds_against_reference_headers():
     """The shim compiles against the reference's crt_renderer.h / crt_scene.h
     and links with its TUs (oracle/Makefile `shim`, run by build())."""
