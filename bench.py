@@ -16,8 +16,12 @@ is reported beside it as config.e2e_ms.
 
 N>1: one process per GPU.  Without torchrun's environment, `--gpus N` starts
 the N rank processes itself (python -m torch.distributed.run, before this
-process touches the GPU) and exits with their status.  Default mode `tiles`
-(strong scaling, the north_star's image-tile sharding): the reference's bucket
+process touches the GPU) and exits with their status.  The mode (`--mode
+auto`, crt_amd.distributed.select_mode): a frame the library's GPU-count
+policy keeps on one GPU (its one-GPU estimate under 2 ms: C2, C3) cannot
+strong-scale, so every rank renders whole frames (`frames`, weak scaling);
+longer frames (C4, C5) take `tiles` (strong scaling, the north_star's
+image-tile sharding); the other mode is measured as `secondary`.  Tiles: the reference's bucket
 grid (crt_renderer.cpp:160-174) is dealt bucket k -> rank k mod N, each rank
 renders its buckets packed, the packed shards are gathered to rank 0 over RCCL
 (torch.distributed "nccl") and unpacked there, one frame per step; frame k's
@@ -27,9 +31,11 @@ pixel whose camera ray passes the reference's root-cell test — every other
 pixel is a miss, i.e. the background, written by the unpack on rank 0
 (lossless; 28% of C2's tiles are live).  `--payload u8` gathers write_ppm's
 8-bit components instead (device quantise-and-pack, crt_image_ppm.cpp:9-23;
-4x fewer bytes again, the PPM the CLI writes).  The
-frame-parallel mode (`frames`, weak scaling: every rank renders whole frames)
-is reported as a secondary field.
+4x fewer bytes again, the PPM the CLI writes).
+
+N=1, C2: `secondary` is BASELINE C2's "primary + shadow rays" leg — the
+course's earlier renderer (option "shadows"), on which the reference's only
+published number was taken — with its own roofline.
 
 Also reported: the roofline of the render kernel (see roofline_block) and the
 CPU baseline (oracle/crt_oracle.cpp, the from-scratch restatement of the
@@ -425,7 +431,7 @@ def roofline_block(kernel_ms: float, counts: dict, waves: dict, npx: int, pmc: d
 
 
 def load_pmc(path: str | None, config: str, w: int, h: int) -> dict | None:
-    p = Path(path) if path else ROOT / "profiles" / "r05" / f"pmc_{config}.json"
+    p = Path(path) if path else ROOT / "profiles" / "r06" / f"pmc_{config}.json"
     try:
         d = json.loads(p.read_text())
     except (OSError, ValueError):
@@ -795,6 +801,55 @@ def main():
                      "value": round(rays_per_frame * fps2 * a.steps / el2 / 1e6, 3),
                      "unit": "Mrays/s", "ms_per_step": round(el2 / a.steps * 1e3, 5), "kernel_ms": round(km2, 5),
                      "frames_per_step": fps2}
+
+    # BASELINE C2's "primary + shadow rays": the course's earlier renderer (the
+    # reference's published 0.066962 s was taken at tag 14-01, which traced
+    # shadow rays; at HEAD the loop is dead code, crt_renderer.cpp:29-44),
+    # option "shadows" on the same scene: frames back to back and one at a
+    # time, its rays counted, its last frame checked against a blocking render
+    # (pinned to the oracle by tests/test_png_pins.py), its own roofline
+    if world == 1 and not a.shadows and a.config == "c2" and secondary is None:
+        gs = N.HipScene(scene, device=local, events=0, shadows=1, calibrate=1)
+        cs = gs.count_work(settings)
+        ws = gs.wave_counts()
+        for _ in range(a.warmup):
+            gs.render_device(settings, frame.data_ptr(), sptr)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            gs.render_device(settings, frame.data_ptr(), sptr)
+        torch.cuda.synchronize()
+        s_ms = (time.perf_counter() - t0) / a.steps * 1e3
+        s_last = frame.clone()
+        ser = []
+        for _ in range(max(10, a.steps // 2)):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            gs.render_device(settings, frame.data_ptr(), sptr)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ser.append(e0.elapsed_time(e1))
+        s_one = statistics.median(ser)
+        s_check = "bit-identical" if np.array_equal(s_last.view(H, W, 3).cpu().numpy().view(np.uint32),
+                                                    gs.render(settings).view(np.uint32)) else "DIFFERS"
+        s_roof = roofline_block(s_one, cs, ws, npx, load_pmc(None, "c2s", W, H), build_id, 1.0)
+        s_roof["kernel_ms_basis"] = f"one frame at a time (HIP events around its launches, median): {s_one:.5f} ms"
+        secondary = {"mode": "shadow_rays", "metric": "Mrays/sec + frame ms, 1920x1080 scene 14-01 (primary + shadow "
+                                                      "rays)",
+                     "value": round(cs["traversals"] / (s_ms * 1e-3) / 1e6, 3), "unit": "Mrays/s",
+                     "ms_per_step": round(s_ms, 5), "frame_ms_one_at_a_time": round(s_one, 5),
+                     "rays_per_frame": cs["traversals"], "node_tests_per_frame": cs["node_tests"],
+                     "triangle_tests_per_frame": cs["triangle_tests"], "check": s_check, "roofline": s_roof,
+                     "vs_reference_published_s": round(0.066962 / (s_ms * 1e-3), 1),
+                     "note": "the course's earlier renderer (option shadows; the reference's published KD-tree time, "
+                             "0.066962 s at src/README.md:11, was taken at tag 14-01, which traced shadow rays): camera "
+                             "bins for the camera rays, one shadow ray per (diffuse hit, light) through the BVH to "
+                             "its first hit within the light (crt_bvh.h occluded_bvh); not HEAD parity"}
+        del gs
+        if s_check == "DIFFERS":
+            print("check: shadow-ray frame DIFFERS from the blocking render", flush=True)
+            raise SystemExit(1)
 
     # end-to-end frame time of the reference's call: render_image returns a
     # host image (crt_image.h:11-27), the CLI times the whole call (main.cpp:37-43)

@@ -140,6 +140,8 @@ class SceneInfo(C.Structure):
 
 
 TREE_AUTO, TREE_HOST, TREE_DEVICE = 0, 1, 2   # crt_hip_scene_create_ex flags
+# further create flag bits (include/crt_hip.h)
+SCENE_NO_DEVICE_BVH, SCENE_PROBE_OFF, SCENE_PROBE_FORCE, SCENE_PROBE_TEST_MISMATCH = 1 << 4, 1 << 5, 1 << 6, 1 << 7
 
 
 class RenderStats(C.Structure):
@@ -512,13 +514,15 @@ class PlanInfo(C.Structure):
 
 
 class HipScene:
-    def __init__(self, src, device: int = 0, tree_build: str = "auto", devices=None, **options):
+    def __init__(self, src, device: int = 0, tree_build: str = "auto", devices=None, create_flags: int = 0,
+                 **options):
         """tree_build: "auto" | "host" | "device" — where the acceleration tree is
         built (crt_hip_scene_create_ex; both builds give identical bits).
         devices: a list of HIP devices (repeats allowed) — the scene replicated
-        on each, frames split over them (crt_hip_scene_create_on)."""
+        on each, frames split over them (crt_hip_scene_create_on).
+        create_flags: further SCENE_* flag bits of the create call."""
         h = C.c_void_p()
-        flag = {"auto": TREE_AUTO, "host": TREE_HOST, "device": TREE_DEVICE}[tree_build]
+        flag = {"auto": TREE_AUTO, "host": TREE_HOST, "device": TREE_DEVICE}[tree_build] | int(create_flags)
         if devices is not None:
             devs = np.ascontiguousarray(devices, np.int32)
             if hasattr(src, "tree_desc_ptr"):

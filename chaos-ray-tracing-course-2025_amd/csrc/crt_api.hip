@@ -325,9 +325,9 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
         sc->calib_k = (float)std::atof(e);
         if (sc->calibrate) sc->calibrate = 2;
     }
-#endif
-    if (const char *e = std::getenv("CRT_BVH_DEVICE")) sc->bvh_device = std::atoi(e) != 0;   /* 0: no device BVH */
     if (const char *e = std::getenv("CRT_BINS_MEAN_CAP")) sc->bins_mean_cap = std::max<int64_t>(1, std::atoll(e));
+#endif
+    sc->bvh_device = hs.device_bvh;   /* create flag CRT_SCENE_NO_DEVICE_BVH: none */
     if (hs.tree_on_host) sc->tile_work = tile_work_estimate(hs, (hs.width + 7) / 8, (hs.height + 7) / 8);
     {
         hipDeviceProp_t prop;
@@ -1019,6 +1019,10 @@ static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
         return CRT_OK;
     } else if (k == "compact_copy") {   /* crt_hip_render's image copy: 1 compact (default), 0 the whole image */
         sc->compact_copy = value != 0;
+        return CRT_OK;
+    } else if (k == "bins_qmax") {   /* test hook: groups k_bins_pairs takes (a kernel argument of the binning) */
+        if (value < 1) return set_error(CRT_E_INVALID, "bins_qmax must be >= 1");
+        sc->bins.qmax = std::min((int)value, 8192);   /* kMaxGroups (crt_bins.hip) */
         return CRT_OK;
     } else if (k == "bins_reuse") {   /* no plan depends on it */
         sc->bins_reuse = value != 0;

@@ -166,7 +166,7 @@ __device__ __forceinline__ void bins_scatter(const int (&cell)[U], const uint64_
         slot[u] = cell[u] >= 0 ? atomicAdd(&cnt[(size_t)BCK(cell[u], BDBG(ncell), 7) * kCntStride], 1) : kBinCellCap;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        if (cell[u] < 0) continue;
+        if (cell[u] < 0 || !keys) continue;   /* (no keys: the create's counting pass, bins_view) */
         if (slot[u] < kBinCellCap)
             keys[BCK((size_t)cell[u] * kBinCellCap + slot[u], (int64_t)BDBG(ncell) * kBinCellCap, 8)] = key[u];
         if (slot[u] == 0) {
@@ -884,8 +884,7 @@ int bins_setup(crt_hip_scene *sc, const HostScene &hs) {
     /* per triangle, kept for every view: the records' static parts and the
      * projection's scratch */
     b.nt = (int)hs.tri_attr.size();
-    b.qmax = kMaxGroups;   /* tests lower it (CRT_BINS_QMAX): the groups past it scatter their own pairs */
-    if (const char *e = std::getenv("CRT_BINS_QMAX")) b.qmax = std::max(1, std::min(kMaxGroups, std::atoi(e)));
+    b.qmax = kMaxGroups;   /* tests lower it (option "bins_qmax"): the groups past it scatter their own pairs */
     std::vector<CamCand> tpl;
     bin_templates(hs, tpl);
     int rc;
@@ -915,16 +914,17 @@ int bins_view(crt_hip_scene *sc) {
     b.ncell = cam.tx * cam.ty;
     b.cap_shard = (b.ncell + kBinShards - 1) / kBinShards;
     int rc;
-    b.pair_blocks = 256;   /* the sizing pass's grid; resized from its queued pairs below */
+    b.pair_blocks = 0;   /* the sizing pass: every group counts its own pairs */
     if ((rc = bins_alloc(sc, &b.cnt, (size_t)kBinSets * b.ncell * kCntStride, true)) != CRT_OK) return rc;   /* per set */
-    if ((rc = bins_alloc(sc, &b.keys, (size_t)b.ncell * kBinCellCap)) != CRT_OK) return rc;   /* 64-bit keys */
     if ((rc = bins_alloc(sc, &b.every, (size_t)kBinMaxEverywhere)) != CRT_OK) return rc;
-    if ((rc = bins_alloc(sc, &b.nonempty, (size_t)kBinShards * b.cap_shard)) != CRT_OK) return rc;
-    if ((rc = bins_alloc(sc, &b.bigl, (size_t)kBinShards * b.cap_shard)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.hdr, kBinSets, true)) != CRT_OK) return rc;
     if ((rc = bins_alloc(sc, &b.off, (size_t)kBinSets * b.ncell, true)) != CRT_OK) return rc;   /* per set */
     if ((rc = bins_alloc(sc, &b.len, (size_t)kBinSets * b.ncell, true)) != CRT_OK) return rc;
-    /* sizing pass: counts per cell of this camera */
+    /* sizing pass: counts per cell of this camera (the projection without
+     * keys: nothing is scattered, and a view the counts reject never
+     * allocates its ~0.5 GB of 4K keys — C5: 80 ms of a create) */
+    b.keys = nullptr;
+    b.nonempty = b.bigl = nullptr;
     if ((rc = bins_dbg_arm(sc, ShardPlan{})) != CRT_OK) return rc;
     if ((rc = launch_project(sc, sc->stream, 0, nullptr)) != CRT_OK) return rc;
     std::vector<int32_t> cnt((size_t)b.ncell * kCntStride), gsum((size_t)((b.nt + kProjTris - 1) / kProjTris));
@@ -963,6 +963,9 @@ int bins_view(crt_hip_scene *sc) {
         bins_free_view(sc);   /* the scene walks the BVH (or the kd tree) */
         return CRT_OK;
     }
+    if ((rc = bins_alloc(sc, &b.keys, (size_t)b.ncell * kBinCellCap)) != CRT_OK) return rc;   /* 64-bit keys */
+    if ((rc = bins_alloc(sc, &b.nonempty, (size_t)kBinShards * b.cap_shard)) != CRT_OK) return rc;
+    if ((rc = bins_alloc(sc, &b.bigl, (size_t)kBinShards * b.cap_shard)) != CRT_OK) return rc;
     /* each shard's records in a region of its own, sized from the pass with
      * room for a camera that moves (crt_hip_scene_set_camera): a cell whose
      * list does not fit walks the BVH */
@@ -1086,8 +1089,11 @@ int bins_plan(crt_hip_scene *sc, ShardPlan &plan) {
  * waits for the binning if it ran elsewhere. */
 int bins_enqueue(crt_hip_scene *sc, const ShardPlan &plan, hipStream_t s, int *par_out, bool force) {
     BinsDev &b = sc->bins;
-    static const bool trace = std::getenv("CRT_BINS_TRACE") != nullptr;   /* diagnostics: each decision on stderr */
-    if (trace)
+#ifdef CRT_BINS_TRACE   /* diagnostic builds (BINS_FLAGS=-DCRT_BINS_TRACE): each decision on stderr */
+    if (true)
+#else
+    if (false)
+#endif
         std::fprintf(stderr, "bins_enqueue plan=%p work=%p waves=%d last=%d binned=%p frame=%llu force=%d cam_same=%d\n",
                      (const void *)&plan, (const void *)plan.bp.work, plan.waves, b.last, b.binned_plan,
                      (unsigned long long)b.frame, (int)force, (int)(std::memcmp(&b.binned, &b.cam, sizeof b.cam) == 0));

@@ -620,6 +620,56 @@ CRT_HD int trace_bvh_exact(const BNode *bnodes, int bn, const DTriGeo *btri, con
                                   best_t, c, fb, ktopo2);
 }
 
+/* Shadow rays (option "shadows", the course's earlier renderer,
+ * crt_renderer.cpp:90-92): whether the reference's closest hit of the ray
+ * lies within the light, !(t * t > r2).  Any hit with !(fl(t * t) > r2)
+ * decides it — the closest hit is no farther and rounding is monotone — so
+ * the BVH walk stops at the first such hit whose triangle the reference
+ * reaches (step 2's proof towards that hit's point), instead of walking to
+ * the closest.  With lim = sqrt(r2) (1 + 2^-20) the walk drops every box that
+ * cannot hold such a hit (fl(t * t) <= r2 implies t <= sqrt(r2) (1 + 2^-24)),
+ * and a ray with no such hit among all triangles has none among the copies the
+ * reference reaches.  Returns 1 (occluded), 0 (lit) or -1: the hit found
+ * failed the proof (a cell edge) and the exact walk decides. */
+template <bool COUNT>
+CRT_HD int occluded_bvh(const BNode *bnodes, int bn, const DTriGeo *btri, const int32_t *btri_id, const DNode *nodes,
+                        const int32_t *slot_tri, const KTopo *ktopo, const KTopo2 *ktopo2, float prune_origin_max,
+                        bool planes_ok, Vec o, Vec d, float r2, WalkCounts &c) {
+    if (isnan(o.x) || isnan(o.y) || isnan(o.z) || isnan(d.x) || isnan(d.y) || isnan(d.z)) return 0;   /* misses every cell */
+    const BNode *ord = bnode_order(bnodes, bn, ray_octant(d));
+    const PruneRay pr = make_prune_ray(o, d, prune_origin_max);
+    const float lim = sqrtf(r2) * (1.0f + 0x1p-20f);
+    int i = 0;
+    while (i < bn) {
+        const BNode nd = CRT_LDG(ord, i);
+        if (COUNT) ++c.nodes;
+        if (!bnode_alive(nd, pr, lim)) {
+            i = nd.skip;
+            continue;
+        }
+        ++i;
+        const int cnt = nd.leaf & 15, first = nd.leaf >> 4;
+        for (int k = 0; k < cnt; ++k) {
+            const DTriGeo g = CRT_LDG(btri, first + k);
+            const int32_t id = CRT_LDG(btri_id, first + k);
+            const uint8_t cull = (uint8_t)((uint32_t)id >> 31);
+            float t;
+            if (COUNT) ++c.tris;
+            if (tri_hit(o, d, g, &cull, t) && !(t * t > r2)) {
+                const RayRcp rr = make_ray_rcp(o, d, planes_ok);
+                const Vec p = vadd(o, vscale(d, t));
+                const int tri = id & 0x7fffffff;
+                const int slot = CRT_PROOF_TOPO && ktopo
+                                     ? verify_topo<COUNT>(ktopo, nodes, slot_tri, tri, o, d, rr, p, c,
+                                                          CRT_PROOF_TOPO2 ? ktopo2 : nullptr)
+                                     : verify_kd<COUNT>(nodes, slot_tri, tri, o, d, rr, p, c);
+                return slot >= 0 ? 1 : -1;
+            }
+        }
+    }
+    return 0;
+}
+
 /* The same answer for a camera ray of cell [beg, end) through the camera bins. */
 template <bool COUNT>
 CRT_HD int trace_bins_exact(const CamCand *cands, int beg, int end, int bit, const DNode *nodes, const PNode *pnodes, int n,

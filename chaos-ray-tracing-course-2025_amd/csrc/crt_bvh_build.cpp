@@ -22,6 +22,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <limits>
+#include <thread>
 #include <vector>
 
 #include "crt_bins.h"
@@ -338,13 +339,27 @@ bool bin_camera_of(const DCamera &c, float prune_origin_max, BinCamera &cam) {
     return true;
 }
 
+void bin_templates_range(const HostScene &hs, std::vector<CamCand> &tpl, int32_t t0, int32_t t1);
+
 /* Per triangle: its hull box (crt_device.h triangle_hull, rounded outwards),
  * id | culling << 31 and geometry as the BVH's triangle arrays hold them; the
  * per-frame fields (dmin, mask, rest) zero. */
 void bin_templates(const HostScene &hs, std::vector<CamCand> &tpl) {
     const int32_t nt = (int32_t)hs.tri_attr.size();
     tpl.assign((size_t)nt, CamCand{});
-    for (int32_t t = 0; t < nt; ++t) {
+    /* independent per triangle: large scenes (C5: 1 M triangles, ~50 ms of
+     * f64 hulls) on several threads */
+    const int nth = nt < 65536 ? 1 : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> pool;
+    for (int k = 1; k < nth; ++k)
+        pool.emplace_back([&, k]() { bin_templates_range(hs, tpl, (int32_t)((int64_t)nt * k / nth),
+                                                         (int32_t)((int64_t)nt * (k + 1) / nth)); });
+    bin_templates_range(hs, tpl, 0, (int32_t)((int64_t)nt / nth));
+    for (auto &th : pool) th.join();
+}
+
+void bin_templates_range(const HostScene &hs, std::vector<CamCand> &tpl, int32_t t0, int32_t t1) {
+    for (int32_t t = t0; t < t1; ++t) {
         const DTriAttr &at = hs.tri_attr[t];
         const float *v[3] = {&hs.vpos[3 * (size_t)at.i0], &hs.vpos[3 * (size_t)at.i1], &hs.vpos[3 * (size_t)at.i2]};
         const HullD hd = triangle_hull(v[0], v[1], v[2], &hs.face_normal[3 * (size_t)t], hs.prune_G);
@@ -392,8 +407,10 @@ int build_camera_bins(const HostScene &hs, std::vector<CamCand> &bins, std::vect
         if (cnt[(size_t)c] > kBinCellCap) ov[(size_t)c] = 1;   /* this cell's pixels walk the BVH */
         else total += cnt[(size_t)c];
     }
-    int64_t mean_cap = kBinMeanCap;   /* the device's cap (crt_api.hip: env CRT_BINS_MEAN_CAP) */
+    int64_t mean_cap = kBinMeanCap;   /* the device's cap (crt_api.hip; A/B builds: env CRT_BINS_MEAN_CAP) */
+#ifdef CRT_AB_OPTIONS
     if (const char *e = std::getenv("CRT_BINS_MEAN_CAP")) mean_cap = std::max<int64_t>(1, std::atoll(e));
+#endif
     if (total > mean_cap * ncell || total >= (int64_t)std::numeric_limits<int32_t>::max()) return CRT_OK;
     off.assign((size_t)ncell + 1, 0);
     for (int64_t c = 0; c < ncell; ++c) off[(size_t)c + 1] = off[(size_t)c] + (ov[(size_t)c] ? 0 : (int32_t)cnt[(size_t)c]);

@@ -94,6 +94,8 @@ struct HostScene {
      * prepare_scene skipped the tree (built on the device, crt_tree_build.h) */
     float root_box[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     bool tree_on_host = true;
+    bool device_bvh = true;             /* scenes above kHostBvhMax triangles: BVH built on the device
+                                         * (create flag CRT_SCENE_NO_DEVICE_BVH: none) */
 
     /* shading */
     std::vector<DMaterial> materials;

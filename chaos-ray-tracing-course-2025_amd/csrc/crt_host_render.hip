@@ -32,13 +32,19 @@ std::vector<float> g_gi_host;
 
 constexpr int64_t kGiN = int64_t(1) << 23;
 
-/* Host threads for the table builds: the process's CPU quota (OMP_NUM_THREADS
- * when set, as on the GPU boxes), at most 64. */
+/* Host threads for the table builds: the process's CPU quota (the cgroup's
+ * cpu.max, as on the GPU boxes: 16 CPUs of 256), else the hardware threads,
+ * at most 64. */
 unsigned table_threads() {
     unsigned n = std::thread::hardware_concurrency();
-    if (const char *e = std::getenv("OMP_NUM_THREADS")) {
-        const long v = std::strtol(e, nullptr, 10);
-        if (v > 0) n = (unsigned)v;
+    if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long long per = 0;
+        if (std::fscanf(f, "%31s %lld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0) {
+            const long long quota = std::atoll(q);
+            if (quota > 0) n = std::min(n, (unsigned)std::max(1ll, quota / per));
+        }
+        std::fclose(f);
     }
     return std::max(1u, std::min(64u, n));
 }
@@ -341,7 +347,9 @@ void free_plans(crt_hip_scene *sc) {
     sc->full = ShardPlan{};
     sc->shard_plans.clear();
     sc->bins.last = -1;   /* the work lists were the freed plans' */
-    if (std::getenv("CRT_BINS_TRACE")) std::fprintf(stderr, "free_plans\n");
+#ifdef CRT_BINS_TRACE   /* diagnostic builds: the binning's decisions on stderr */
+    std::fprintf(stderr, "free_plans\n");
+#endif
     sc->compact_plans.clear();
 }
 
@@ -1103,7 +1111,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
      * event the render waits for, measured slower for orbit frames: the
      * ring's lazy slot-reuse event then orders the binning after the
      * previous render — 0.0675 -> 0.0736 ms) */
-    const bool bins_frame = !full && !sc->shadows && bins_active(sc) && plan.bp.cell_tile;   /* (the branch below) */
+    const bool bins_frame = !full && bins_active(sc) && plan.bp.cell_tile;   /* (the branch below) */
     /* a wavefront frame writes a changed record on the stream its levels run
      * on (render_wavefront): on the caller's stream it would wait for the
      * previous frame's pixels, and frames with a new camera each could not
@@ -1125,9 +1133,10 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     int sec = sc->secondary;
     if (sec == 14 && !sc->ds.bnodes) sec = 10;   /* no BVH (device-built tree) */
     if (sec == 0) sec = !pruned ? 4 : sc->ds.bnodes ? 14 : gi ? 4 : 10;
-    if (sc->shadows) {
+    if (sc->shadows && !bins_frame) {
         /* shadow-ray frames (option "shadows"): frame-stack kernel, pruned
-         * cooperative walk for every traced ray, per-lane shadow walks */
+         * cooperative walk for every traced ray, per-lane shadow walks (any
+         * hit through the BVH where the scene has one, crt_bvh.h occluded_bvh) */
         if (stamps) return set_error(CRT_E_UNSUPPORTED, "wave profiles of shadow-ray frames are not supported");
         const uint64_t nf = (uint64_t)st->max_ray_depth + 1;
         const int nb = (plan.ntiles + 3) / 4;
@@ -1138,7 +1147,9 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
 #define CRT_LAUNCH_SH(TR, COUNT)                                                                            \
     hipLaunchKernelGGL((k_render_tiles<false, 0, TR, TR, COUNT, true>), dim3(nb), dim3(256), 0, stream, d_scene, ds, \
                        plan.d_tiles, plan.ntiles, d_out, cn, nullptr, BinsPlan{})
-            if (tr == 13) {
+            if (tr == 14) {
+                if (count) CRT_LAUNCH_SH(14, true); else CRT_LAUNCH_SH(14, false);
+            } else if (tr == 13) {
                 if (count) CRT_LAUNCH_SH(13, true); else CRT_LAUNCH_SH(13, false);
             } else if (tr == 12) {
                 if (count) CRT_LAUNCH_SH(12, true); else CRT_LAUNCH_SH(12, false);
@@ -1193,15 +1204,19 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         BinsPlan bp = plan.bp;
         bp.par = par;
         bp.work += (size_t)par * bp.wslots;   /* this frame's set of the work lists */
-        static const bool trace = std::getenv("CRT_BINS_TRACE") != nullptr;   /* diagnostics on stderr */
-        if (trace)
-            std::fprintf(stderr, "launch bins plan=%p ntiles=%d waves=%d par=%d out=%p stream=%p\n", (const void *)&plan,
-                         plan.ntiles, plan.waves, par, (void *)d_out, (void *)stream);
+#ifdef CRT_BINS_TRACE   /* diagnostic builds: the binning's decisions on stderr */
+        std::fprintf(stderr, "launch bins plan=%p ntiles=%d waves=%d par=%d out=%p stream=%p\n", (const void *)&plan,
+                     plan.ntiles, plan.waves, par, (void *)d_out, (void *)stream);
+#endif
         const unsigned bb = (unsigned)((plan.waves + 3) / 4);
-#define CRT_LAUNCH_B(COUNT)                                                                                 \
-    hipLaunchKernelGGL((k_render_tiles<false, 0, 15, 15, COUNT>), dim3(bb), dim3(256), 0, stream, d_scene, ds, \
+#define CRT_LAUNCH_B(COUNT, SH)                                                                             \
+    hipLaunchKernelGGL((k_render_tiles<false, 0, 15, 15, COUNT, SH>), dim3(bb), dim3(256), 0, stream, d_scene, ds, \
                        plan.d_tiles, plan.waves, d_out, cnt, stamps, bp)
-        if (count) CRT_LAUNCH_B(true); else CRT_LAUNCH_B(false);
+        if (sc->shadows) {   /* the course's earlier renderer: shadow rays per lane (crt_shade.h shadow_occluded) */
+            if (count) CRT_LAUNCH_B(true, true); else CRT_LAUNCH_B(false, true);
+        } else {
+            if (count) CRT_LAUNCH_B(true, false); else CRT_LAUNCH_B(false, false);
+        }
 #undef CRT_LAUNCH_B
         HIP_TRY(hipGetLastError());
         /* this set's lists are free again — after every render that read

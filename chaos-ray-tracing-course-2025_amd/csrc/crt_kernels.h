@@ -146,6 +146,8 @@ __global__ void k_warm_bins();
     X(false, 0, 14, 14, true, false) X(false, 0, 15, 15, false, false) X(false, 0, 15, 15, true, false)   \
     X(false, 0, 8, 8, false, true) X(false, 0, 8, 8, true, true) X(false, 0, 12, 12, false, true)          \
     X(false, 0, 12, 12, true, true) X(false, 0, 13, 13, false, true) X(false, 0, 13, 13, true, true)       \
+    X(false, 0, 14, 14, false, true) X(false, 0, 14, 14, true, true) X(false, 0, 15, 15, false, true)      \
+    X(false, 0, 15, 15, true, true)                                                                         \
     X(true, 4, 4, 4, false, false) X(true, 4, 4, 4, true, false) X(true, 16, 4, 4, false, false)           \
     X(true, 16, 4, 4, true, false) X(true, 64, 4, 4, false, false) X(true, 64, 4, 4, true, false)          \
     X(true, 4, 10, 10, false, false) X(true, 4, 10, 10, true, false) X(true, 16, 10, 10, false, false)     \

@@ -84,8 +84,8 @@ int multi_probe(crt_hip_scene *sc) {
     }
     std::string why = rc != CRT_OK ? std::string(crt_hip_last_error()) : std::string();
     if (rc == CRT_OK) {
-        if (const char *e = std::getenv("CRT_MULTI_PROBE_INJECT"))
-            if (std::atoi(e) == 1 && !multi.empty()) reinterpret_cast<uint32_t *>(multi.data())[0] ^= 1u;
+        if ((sc->create_flags & CRT_SCENE_PROBE_TEST_MISMATCH) && !multi.empty())   /* test hook: a differing bit */
+            reinterpret_cast<uint32_t *>(multi.data())[0] ^= 1u;
     }
     const int verdict = probe_verdict(multi.data(), single.data(), (int64_t)multi.size(), rc);
     /* back to the scene's own camera, then drop the replicas if the probe failed */
@@ -110,7 +110,7 @@ int multi_probe(crt_hip_scene *sc) {
 }
 
 /* One prepared host scene uploaded to every listed device. */
-int upload_on(const HostScene &hs, const int32_t *devices, int32_t count, crt_hip_scene **out) {
+int upload_on(const HostScene &hs, const int32_t *devices, int32_t count, crt_hip_scene **out, int flags = 0) {
     *out = nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     if (!devices || count < 1) return set_error(CRT_E_INVALID, "no devices");
@@ -118,6 +118,7 @@ int upload_on(const HostScene &hs, const int32_t *devices, int32_t count, crt_hi
     int rc = scene_upload(hs, devices[0], true, &first);
     if (rc != CRT_OK) return rc;
     std::unique_ptr<crt_hip_scene, void (*)(crt_hip_scene *)> sc(first, crt_hip_scene_destroy);
+    sc->create_flags = flags;
     for (int32_t i = 1; i < count; ++i) {
         crt_hip_scene *r = nullptr;
         if ((rc = scene_upload(hs, devices[i], false, &r)) != CRT_OK) return rc;
@@ -131,8 +132,7 @@ int upload_on(const HostScene &hs, const int32_t *devices, int32_t count, crt_hi
         HIP_TRY(hipEventCreateWithFlags(&sc->mg_done, hipEventDisableTiming));   /* "gather unpacked" */
         bool distinct = false;
         for (int32_t i = 1; i < count; ++i) distinct = distinct || devices[i] != devices[0];
-        const char *e = std::getenv("CRT_MULTI_PROBE");
-        const bool force = e && std::strcmp(e, "force") == 0, off = e && std::strcmp(e, "0") == 0;
+        const bool force = (flags & CRT_SCENE_PROBE_FORCE) != 0, off = (flags & CRT_SCENE_PROBE_OFF) != 0;
         if (!off && (distinct || force) && !sc->grid_empty) {
             const int rc2 = multi_probe(sc.get());
             if (rc2 != CRT_OK) return rc2;
@@ -165,12 +165,14 @@ int mask_devices(uint64_t mask, std::vector<int32_t> &devs) {
 
 int tree_mode(const crt_scene_desc *desc, int flags) {
     int mode = flags & 3;
-    if (mode == CRT_SCENE_TREE_AUTO) {
+#ifdef CRT_AB_OPTIONS
+    if (mode == CRT_SCENE_TREE_AUTO) {   /* A/B builds: the build site from the environment */
         if (const char *e = std::getenv("CRT_TREE_BUILD")) {
             if (std::strcmp(e, "host") == 0) mode = CRT_SCENE_TREE_HOST;
             if (std::strcmp(e, "device") == 0) mode = CRT_SCENE_TREE_DEVICE;
         }
     }
+#endif
     if (mode == CRT_SCENE_TREE_AUTO) {
         int64_t nt = 0;
         for (int i = 0; i < desc->mesh_count && desc->meshes; ++i) nt += desc->meshes[i].index_count / 3;
@@ -355,7 +357,8 @@ int crt_hip_scene_create_on(const crt_scene_desc *desc, const int32_t *devices, 
     std::unique_ptr<HostScene> hs(new HostScene());
     int rc = prepare_scene(desc, *hs, mode == CRT_SCENE_TREE_HOST);
     if (rc != CRT_OK) return rc;
-    if ((rc = upload_on(*hs, devices, count, out)) != CRT_OK) return rc;
+    hs->device_bvh = (flags & CRT_SCENE_NO_DEVICE_BVH) == 0;
+    if ((rc = upload_on(*hs, devices, count, out, flags)) != CRT_OK) return rc;
     (*out)->info.create_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return CRT_OK;
 }

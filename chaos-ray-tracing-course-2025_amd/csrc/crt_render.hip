@@ -160,7 +160,7 @@ __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSetting
             Vec c;
             if constexpr (SHADOW) c = shade_hit_shadowed<COUNT>(s, st, act && sl == 0, o, d, slot, t, cw);   /* wave-wide */
             if (act && sl == 0) {
-                if constexpr (!SHADOW) c = shade_primary(s, st, o, d, slot, t);
+                if constexpr (!SHADOW) c = shade_primary(s, st, o, d, slot, t);   /* (SHADOW: wave-wide above) */
                 float *pxo = out + 3 * (tl.out_base + (int64_t)py * tl.out_stride + px);
                 pxo[0] = c.x;
                 pxo[1] = c.y;
@@ -189,7 +189,7 @@ __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSetting
             return;
         }
     }
-    if constexpr (TRAV == 15 && !FULL && !SHADOW) {
+    if constexpr (TRAV == 15 && !FULL) {
         /* a tile inside one 8x8 camera-bins cell: the cell's candidate list */
         const int tx0 = uniform_i(tl.x), ty0 = uniform_i(tl.y), tw = uniform_i(tl.w), th = uniform_i(tl.h);
         const int cell = (ty0 >> 3) * s.bin_tx + (tx0 >> 3);
@@ -210,8 +210,10 @@ __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSetting
                 const int bit = 8 * ((ty0 & 7) + ly) + (tx0 & 7) + lx;
                 CamCand *stw = stage + (threadIdx.x >> 6) * kBinChunk;
                 const int slot = trace_bins_lanes<COUNT, 4>(s, stw, beg, end, bit, sl, act, o, d, t, cw);
+                Vec c;
+                if constexpr (SHADOW) c = shade_hit_shadowed<COUNT>(s, st, act && sl == 0, o, d, slot, t, cw);   /* wave-wide */
                 if (act && sl == 0) {
-                    const Vec c = shade_primary(s, st, o, d, slot, t);
+                    if constexpr (!SHADOW) c = shade_primary(s, st, o, d, slot, t);
                     float *pxo = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
                     pxo[0] = c.x;
                     pxo[1] = c.y;
@@ -236,8 +238,10 @@ __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSetting
             const int bit = 8 * ((ty0 & 7) + ly) + (tx0 & 7) + lx;
             const int slot = trace_bins_wave<COUNT>(s, stage + (threadIdx.x >> 6) * kBinChunk, beg, end, bit, act, o,
                                                     d, t, cw, stamps ? &stamps[2 * wave] : nullptr);
+            Vec c;
+            if constexpr (SHADOW) c = shade_hit_shadowed<COUNT>(s, st, act, o, d, slot, t, cw);   /* wave-wide */
             if (act) {
-                const Vec c = shade_primary(s, st, o, d, slot, t);
+                if constexpr (!SHADOW) c = shade_primary(s, st, o, d, slot, t);
                 float *pxo = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
                 pxo[0] = c.x;
                 pxo[1] = c.y;
@@ -255,7 +259,7 @@ __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSetting
         }
     }
 #if CRT_BVH_WINDOW
-    if constexpr ((TRAV == 14 || TRAV == 15) && !FULL && !SHADOW) {
+    if constexpr ((TRAV == 14 || TRAV == 15) && !FULL) {
         /* tiles of <= 16 rays (the measured plan's splits of heavy tiles):
          * each ray walked by a group of 64/R lanes (crt_walks.h trace_bvh_window) */
         const int tw = uniform_i(tl.w), th = uniform_i(tl.h);
@@ -271,8 +275,10 @@ __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSetting
             float t;
             const int slot = K == 16 ? trace_bvh_window<COUNT, 16>(s, sl, act, o, d, t, cw)
                                      : trace_bvh_window<COUNT, 4>(s, sl, act, o, d, t, cw);
+            Vec c;
+            if constexpr (SHADOW) c = shade_hit_shadowed<COUNT>(s, st, act && sl == 0, o, d, slot, t, cw);   /* wave-wide */
             if (act && sl == 0) {
-                const Vec c = shade_primary(s, st, o, d, slot, t);
+                if constexpr (!SHADOW) c = shade_primary(s, st, o, d, slot, t);
                 float *pxo = out + 3 * (tl.out_base + (int64_t)py * tl.out_stride + px);
                 pxo[0] = c.x;
                 pxo[1] = c.y;
@@ -301,8 +307,8 @@ __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSetting
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     Vec c;
     if constexpr (SHADOW && !FULL)
-        c = shade_shadowed<TRAV, COUNT>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt,
-                                        &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px);
+        c = shade_shadowed<(TRAV == 15 ? 14 : TRAV), COUNT>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0),
+                                                            cnt, &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px);
     else
         c = shade_pixel<FULL, MAXF, (TRAV == 15 ? 14 : TRAV), (SEC == 15 ? 14 : SEC), COUNT, SHADOW>(
             s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt, &coop[kCoop ? (threadIdx.x >> 6) : 0],
@@ -346,7 +352,7 @@ __global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT
     const DeviceScene &s = *scene;
     /* diagnostic build only (stamps != nullptr): wave start / end in s_memrealtime ticks (100 MHz) */
     if (stamps && lane == 0) stamps[2 * wave] = __builtin_amdgcn_s_memrealtime();
-    if constexpr (TRAV == 15 && !FULL && !SHADOW) {
+    if constexpr (TRAV == 15 && !FULL) {
         /* camera bins: the wave's work-list slot, then the entries a grid's
          * capacity further on when this frame's list outgrew the grid (the
          * camera moved since the sizing pass) */

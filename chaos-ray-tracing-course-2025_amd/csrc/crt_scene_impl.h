@@ -58,7 +58,7 @@ struct BinsDev {
     int32_t *gsum = nullptr;              /* per group: pairs */
     int32_t *rem = nullptr;               /* groups queued for k_bins_pairs */
     int pair_blocks = 0;                  /* k_bins_pairs grid (0: not launched; the sizing pass queued none) */
-    int qmax = 8192;                      /* groups k_bins_pairs takes (kMaxGroups; env CRT_BINS_QMAX lowers it) */
+    int qmax = 8192;                      /* groups k_bins_pairs takes (kMaxGroups; option "bins_qmax" lowers it) */
     int32_t *cnt = nullptr;               /* per cell: candidates; kBinSets sets (a frame zeroes the next one's) */
     uint64_t *keys = nullptr;             /* per cell: kBinCellCap sort keys (dmin bits << 32 | triangle id) */
     int32_t *every = nullptr;             /* everywhere triangles */
@@ -292,7 +292,9 @@ struct crt_hip_scene {
     int wf_dyn_ids = 4;            /* ... their ray-id capacity, x camera rays (option "wf_dyn_ids") */
     int wf_dyn_waves = 8192;       /* ... the waves of each level's grid, at most (option "wf_dyn_waves") */
     int wf_window = 0;             /* wavefront levels >= 1: the BVH window walk, four lanes a ray (option "wf_window") */
-    int bvh_device = 1;            /* build the BVH on the device above kHostBvhMax triangles (env CRT_BVH_DEVICE=0: not) */
+    int bvh_device = 1;            /* build the BVH on the device above kHostBvhMax triangles (create flag
+                                    * CRT_SCENE_NO_DEVICE_BVH: not) */
+    int create_flags = 0;          /* the create's CRT_SCENE_* flags (crt_multi.hip: the probe's test hook) */
     int bins_slack = 100;          /* camera-bins grid slots per kind: the sizing pass's count + this % (option "bins_slack") */
     int bins_reuse = 1;            /* a frame whose camera the last binning used renders its lists (option "bins_reuse") */
     int bins_split = 48;           /* cells with this many candidates run as four 4x4 waves (option "bins_split") */

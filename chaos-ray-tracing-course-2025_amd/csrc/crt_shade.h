@@ -35,10 +35,26 @@ __device__ __forceinline__ void make_hit(const DeviceScene &s, Vec o, Vec d, flo
  * unchanged shadow ray every time (tests/test_shadows.py).  Per-lane pruned
  * walk (called from divergent shading code), closest hit as the reference. */
 template <bool COUNT>
-__device__ __forceinline__ bool shadow_occluded(const DeviceScene &s, Vec o, Vec d, float r2, LaneCounts &c) {
+__device__ __forceinline__ bool shadow_occluded_kd(const DeviceScene &s, Vec o, Vec d, float r2, LaneCounts &c) {
     float t;
     const int best = trace_lane_pruned<COUNT>(s, true, o, d, t, c);
     return best >= 0 && !(t * t > r2);
+}
+
+template <bool COUNT>
+__device__ __forceinline__ bool shadow_occluded(const DeviceScene &s, Vec o, Vec d, float r2, LaneCounts &c) {
+    if (s.bnodes) {   /* any hit within the light through the BVH, proved on the reference's tree (crt_bvh.h) */
+        WalkCounts wc = {0u, 0u};
+        const int r = occluded_bvh<COUNT>(s.bnodes, s.bnode_count, s.btri, s.btri_id, s.nodes, s.slot_tri, s.ktopo,
+                                          s.ktopo2, s.prune_origin_max, s.planes_ok != 0, o, d, r2, wc);
+        if (COUNT) {
+            c.nodes += wc.nodes;
+            c.tris += wc.tris;
+            if (r >= 0) ++c.traversals;
+        }
+        if (r >= 0) return r == 1;
+    }
+    return shadow_occluded_kd<COUNT>(s, o, d, r2, c);
 }
 
 /* Diffuse direct term + normalisation (crt_renderer.cpp:81-99).  SHADOW: the
@@ -108,13 +124,15 @@ __device__ __forceinline__ float fresnel_of(const DeviceScene &s, float dot) {
 /* shade_ray of a camera ray whose closest hit is known, for frames without
  * recursion (FULL=false: diffuse / constant materials, GI off) — the same
  * operations as shade_pixel<false>. */
-__device__ __forceinline__ Vec shade_primary(const DeviceScene &s, const DSettings &st, Vec o, Vec d, int slot, float t) {
+template <bool SHADOW = false, bool COUNT = false>
+__device__ __forceinline__ Vec shade_primary(const DeviceScene &s, const DSettings &st, Vec o, Vec d, int slot, float t,
+                                             LaneCounts *c = nullptr) {
     if (slot < 0) return vec(s.background[0], s.background[1], s.background[2]);
     HitRec h;
     make_hit(s, o, d, t, slot, h);
     const DMaterial m = s.materials[h.mat];
     const Vec alb = sample_texture(s.textures[m.tex], s.texels, h.uv, h.bu, h.bv);
-    if (m.type == CRT_MATERIAL_DIFFUSE) return diffuse_finish(s, st, vec(0.f, 0.f, 0.f), h.p, h.n, alb);
+    if (m.type == CRT_MATERIAL_DIFFUSE) return diffuse_finish<SHADOW, COUNT>(s, st, vec(0.f, 0.f, 0.f), h.p, h.n, alb, c);
     return alb;
 }
 
@@ -329,8 +347,13 @@ __device__ Vec shade_hit_shadowed(const DeviceScene &s, const DSettings &st, boo
         const float cos_law = (0.0f < dn) ? dn : 0.0f;
         const float area = 4 * kPi * r2;
         bool lit = true;
-        if (__ballot(diffuse) != 0ull)
+        if (s.bnodes) {   /* the wave's shadow rays through the BVH (any hit within the light) */
+            const Vec so = vadd(h.p, vscale(h.n, st.shadow_bias));
+            const int r = occluded_bvh_wave<COUNT>(s, diffuse, so, ld, r2, cnt);
+            if (r != 0) lit = r == 1 ? false : !shadow_occluded_kd<COUNT>(s, so, ld, r2, cnt);
+        } else if (__ballot(diffuse) != 0ull) {
             lit = !shadow_occluded_packet<COUNT>(s, diffuse, vadd(h.p, vscale(h.n, st.shadow_bias)), ld, r2, cnt);
+        }
         if (diffuse && lit) acc = vadd(acc, vscale(vdiv(vscale(alb, Lt.intensity), area), cos_law));
     }
     if (diffuse) col = vdiv(acc, (float)(st.diffuse_reflection_ray_count + 1));

@@ -611,6 +611,91 @@ __device__ __forceinline__ int trace_packet_pruned_t(const DeviceScene &s, bool 
     return best;
 }
 
+/* A wave's shadow rays towards one light through the BVH (option "shadows";
+ * crt_bvh.h occluded_bvh for one ray): the wave walks the union of its lanes'
+ * alive boxes in one preorder — wave-uniform node index, scalar node and
+ * triangle loads, branches on ballots — each lane testing the triangles of
+ * the leaves its own ray reaches, and a lane leaves at its first hit within
+ * the light; then every such hit is proved at once (the reference reaches
+ * that triangle: the proof on the reference tree).  The walk order (the lanes' majority octant) changes nothing but
+ * the time: every alive box is visited until a lane is settled.  Returns the
+ * lane's verdict: 1 occluded, 0 lit, -1 undecided (its hit failed the proof:
+ * the caller's exact walk decides). */
+template <bool COUNT>
+__device__ int occluded_bvh_wave(const DeviceScene &s, bool active, Vec o, Vec d, float r2, LaneCounts &c) {
+    bool live = active && !(isnan(o.x) || isnan(o.y) || isnan(o.z) || isnan(d.x) || isnan(d.y) || isnan(d.z));
+    int res = 0;
+    int ptri = -1;      /* the lane's first hit within the light: triangle, t */
+    float pt = 0.0f;
+    const int na = __popcll(__ballot(live));
+    if (na == 0) {
+        if (COUNT && active) ++c.traversals;
+        return 0;
+    }
+    int oct = 0;
+    if (2 * __popcll(__ballot(live && d.x < 0.0f)) > na) oct |= 1;
+    if (2 * __popcll(__ballot(live && d.y < 0.0f)) > na) oct |= 2;
+    if (2 * __popcll(__ballot(live && d.z < 0.0f)) > na) oct |= 4;
+    const int bn = s.bnode_count;
+    const BNode *ord = bnode_order(s.bnodes, bn, uniform_i(oct));
+    const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
+    const float lim = sqrtf(r2) * (1.0f + 0x1p-20f);
+    int i = 0;
+    BNode cur = load_scalar(ord, 0);
+    while (i < bn) {
+        if (__ballot(live) == 0ull) break;   /* every lane settled */
+        /* both successors in flight before the test (every order ends with a zero record: i + 1 <= bn) */
+        const BNode n1 = load_scalar(ord, i + 1);
+        const BNode n2 = load_scalar(ord, cur.skip);
+        const bool alive = live && bnode_alive(cur, pr, lim);
+        if (COUNT) {
+            ++c.wave_nodes;
+            if (alive) ++c.nodes;
+        }
+        if (__ballot(alive) == 0ull) {
+            i = cur.skip;
+            cur = n2;
+            continue;
+        }
+        const int cnt = cur.leaf & 15, first = cur.leaf >> 4;
+        for (int k = 0; k < cnt; ++k) {
+            const DTriGeo g = load_scalar(s.btri, first + k);
+            const int32_t id = load_scalar(s.btri_id, first + k);
+            const uint8_t cull = (uint8_t)((uint32_t)id >> 31);
+            float t = 0.0f;
+            if (COUNT) {
+                ++c.wave_tris;
+                if (alive && live) ++c.tris;
+            }
+            if (alive && live && tri_hit(o, d, g, &cull, t) && !(t * t > r2)) {
+                ptri = id & 0x7fffffff;   /* settled: its proof runs after the walk, with the wave's other ones */
+                pt = t;
+                live = false;
+            }
+        }
+        i = i + 1;
+        cur = n1;
+    }
+    /* the proofs of every settled lane at once (one descent each, side by
+     * side, instead of one whenever a lane settles) */
+    if (ptri >= 0) {
+        const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
+        const Vec p = vadd(o, vscale(d, pt));
+        WalkCounts wc = {0u, 0u};
+        const int slot = CRT_PROOF_TOPO && s.ktopo
+                             ? verify_topo<COUNT>(s.ktopo, s.nodes, s.slot_tri, ptri, o, d, rr, p, wc,
+                                                  CRT_PROOF_TOPO2 ? s.ktopo2 : nullptr)
+                             : verify_kd<COUNT>(s.nodes, s.slot_tri, ptri, o, d, rr, p, wc);
+        if (COUNT) {
+            c.nodes += wc.nodes;
+            c.tris += wc.tris;
+        }
+        res = slot >= 0 ? 1 : -1;
+    }
+    if (COUNT && active && res >= 0) ++c.traversals;
+    return res;
+}
+
 /* FAST (walk 12, picked by the host): every camera ray of the frame is in the
  * hoisted-division window (camera_rays_fast), so the out-of-line exact box
  * path is not compiled in — 77 instead of 82 VGPRs, 6 waves/SIMD. */

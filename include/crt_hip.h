@@ -230,6 +230,11 @@ int  crt_hip_scene_create(const crt_scene_desc *desc, int device, crt_hip_scene 
 #define CRT_SCENE_TREE_HOST   1
 #define CRT_SCENE_TREE_DEVICE 2
 #define CRT_SCENE_DEVICE_BUILD_MIN 65536
+/* further flag bits of the create calls that take flags (_ex, _on, _mask, _auto) */
+#define CRT_SCENE_NO_DEVICE_BVH        (1 << 4)   /* no device-built BVH above 2^18 triangles (kd walks for every ray) */
+#define CRT_SCENE_PROBE_OFF            (1 << 5)   /* multi-device creates: no probe frame */
+#define CRT_SCENE_PROBE_FORCE          (1 << 6)   /* ... the probe even over repeated devices */
+#define CRT_SCENE_PROBE_TEST_MISMATCH  (1 << 7)   /* test hook: the probe's sharded image gets a differing bit */
 int  crt_hip_scene_create_ex(const crt_scene_desc *desc, int device, int flags, crt_hip_scene **out);
 
 /* ---- device scene from the reference's already-built crt::Scene -------

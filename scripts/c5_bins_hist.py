@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Diagnostic: C5's camera-bins list lengths per 8x8 cell at 4K (mean cap
-raised by CRT_BINS_MEAN_CAP): how many cells are over the cell cap (they walk
+raised by CRT_BINS_MEAN_CAP, read by CRT_AB_OPTIONS builds only: run with
+CRT_PKG=abtest/<variant built with HOST_AB_FLAGS=-DCRT_AB_OPTIONS>): how many cells are over the cell cap (they walk
 the BVH) and the length distribution of the rest."""
 import os
 import sys

@@ -31,6 +31,8 @@ def main():
     p.add_argument("--gi", type=int, default=4, help="diffuse_reflection_ray_count")
     p.add_argument("--ab", default=None, help="ENVVAR=v1,v2,... — build one scene per value")
     p.add_argument("--opt", default=None, help="OPTION=v1,v2,... — one scene per crt_hip_scene_set_option value")
+    p.add_argument("--set", action="append", default=[], metavar="OPTION=V",
+                   help="crt_hip_scene_set_option on every scene (repeatable), e.g. --set shadows=1")
     p.add_argument("--counts", action="store_true", help="print per-ray and per-wave work counts per variant")
     p.add_argument("--synthetic", type=int, default=0, help="C5: synthetic mesh of N triangles instead of --scene")
     a = p.parse_args()
@@ -57,6 +59,10 @@ def main():
         if kv:
             os.environ[kv[0]] = kv[1]
         scenes.append((name, N.HipScene(sc)))
+    for kv in a.set:
+        k, v = kv.split("=", 1)
+        for _, g in scenes:
+            g.set_option(k, int(v))
     times = {name: [] for name, _ in scenes}
     ref = None
     for _ in range(a.frames):

@@ -55,9 +55,9 @@ CASES = [("14-01-acceleration-tree__scene1", None), ("14-01-acceleration-tree__s
          ("13-01-optimizations__scene0", (640, 360))]
 
 
-def _compare(N, sc):
+def _compare(N, sc, **opts):
     hl, hr = N.HostScene(sc).camera_bins()
-    g = N.HipScene(sc)
+    g = N.HipScene(sc, **opts)
     dl, dr = g.camera_bins()
     assert len(hr) > 0, "the host built no bins"
     assert len(dr) > 0, "the device built no bins"
@@ -93,14 +93,13 @@ def test_device_bins_queued_groups(N, oracle, size):
 
 
 @pytest.mark.parametrize("qmax", [1, 2])
-def test_device_bins_groups_past_the_queue(N, oracle, monkeypatch, qmax):
+def test_device_bins_groups_past_the_queue(N, oracle, qmax):
     """More queued groups than k_bins_pairs takes: the queue's capacity
     (kMaxGroups = 8192, 2^18 triangles) lowered to qmax for the test
-    (CRT_BINS_QMAX).  Five large triangles 32 apart each make their group
+    (option "bins_qmax").  Five large triangles 32 apart each make their group
     queue its pairs past kExpand; the groups past qmax scatter their own pairs,
     kExpand a round.  The lists equal the host checker's record for record and
     the frame the oracle's."""
-    monkeypatch.setenv("CRT_BINS_QMAX", str(qmax))
     rng = np.random.default_rng(17)
     n = 160
     c = rng.uniform([-2.0, -1.0, -6.0], [2.0, 1.0, -3.0], (n, 3)).astype(np.float32)
@@ -109,9 +108,9 @@ def test_device_bins_groups_past_the_queue(N, oracle, monkeypatch, qmax):
         z = -8.0 - k
         v[32 * k] = np.array([[-12 + 2 * k, -9, z], [12, -9 + k, z - 1], [0, 9, z + 0.5]], np.float32)
     sc = N.SyntheticScene(v.reshape(-1, 3), np.arange(3 * n, dtype=np.int32), width=640, height=360, fov_degrees=80.0)
-    _compare(N, sc)
+    _compare(N, sc, bins_qmax=qmax)
     st = N.RendererSettings.default()
-    assert np.array_equal(bits(N.HipScene(sc).render(st)), bits(oracle.OracleScene(sc).render(st)))
+    assert np.array_equal(bits(N.HipScene(sc, bins_qmax=qmax).render(st)), bits(oracle.OracleScene(sc).render(st)))
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])

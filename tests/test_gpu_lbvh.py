@@ -95,13 +95,11 @@ def test_lbvh_scattered_rays_equal_reference_walk(N, c5_small):
     assert int(got["hit"].sum()) > n // 4
 
 
-def test_lbvh_off_keeps_kd_walk(N, c5_small, monkeypatch):
-    """CRT_BVH_DEVICE=0: no device BVH (the pruned kd walks, as before); the
-    frame is the same bits either way."""
-    monkeypatch.setenv("CRT_BVH_DEVICE", "0")
-    g0 = N.HipScene(c5_small)
+def test_lbvh_off_keeps_kd_walk(N, c5_small):
+    """Create flag CRT_SCENE_NO_DEVICE_BVH: no device BVH (the pruned kd walks,
+    as before); the frame is the same bits either way."""
+    g0 = N.HipScene(c5_small, create_flags=N.SCENE_NO_DEVICE_BVH)
     assert g0.info()["bvh_on_device"] == 0 and g0.bvh() is None
-    monkeypatch.delenv("CRT_BVH_DEVICE")
     st = N.RendererSettings.default()
     a = g0.render(st)
     b = N.HipScene(c5_small).render(st)

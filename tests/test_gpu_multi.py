@@ -116,17 +116,16 @@ def test_concurrent_renders_into_pageable_memory(N):
 
 
 @pytest.mark.parametrize("inject", [0, 1])
-def test_multi_probe_keeps_or_drops_replicas(N, oracle, monkeypatch, inject):
+def test_multi_probe_keeps_or_drops_replicas(N, oracle, inject):
     """The create's multi-GPU probe (forced over repeated devices here: the
     box has one GPU): a 64x36 frame through the replicas against device 0
     alone.  Matching bits keep the replicas; an injected differing bit drops
     them (crt_scene_info.multi_probe -1, the reason in crt_hip_last_error())
     and the handle renders on one GPU — the same image either way."""
-    monkeypatch.setenv("CRT_MULTI_PROBE", "force")
-    monkeypatch.setenv("CRT_MULTI_PROBE_INJECT", str(inject))
     sc = scene_npz("14-01-acceleration-tree__scene1").set_resolution(320, 180)
     st = N.RendererSettings.default()
-    g = N.HipScene(sc, devices=[0, 0, 0])
+    g = N.HipScene(sc, devices=[0, 0, 0],
+                   create_flags=N.SCENE_PROBE_FORCE | (N.SCENE_PROBE_TEST_MISMATCH if inject else 0))
     info = g.info()
     assert info["multi_probe"] == (-1 if inject else 1), info["multi_probe"]
     assert len(g.devices()) == (1 if inject else 3)

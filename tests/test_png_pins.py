@@ -117,6 +117,28 @@ def test_gpu_shadow_rays_match_oracle(oracle, name, w, h, over):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("opts", [{}, {"bins": 0}, {"traversal": 8}, {"bins_reuse": 0}])
+def test_gpu_shadow_walks_agree(oracle, opts):
+    """Shadow rays through every camera walk: camera bins (the default), the
+    BVH walk (bins off), the kd packet walk; each frame's shadow rays go
+    through the BVH to their first hit within the light (crt_bvh.h
+    occluded_bvh) — all equal to the oracle's closest-hit shadow test, frame
+    after frame, and at three camera poses (bins rebuilt per pose)."""
+    from crt_amd import native as N
+    from crt_amd.camera import orbit_poses
+    name = "14-01-acceleration-tree__scene1"
+    st = N.RendererSettings.default()
+    gpu = N.HipScene(scene_npz(name).set_resolution(640, 360), shadows=1, **opts)
+    for k, (loc, rot) in enumerate(orbit_poses(scene_npz(name).a, 3, yaw_amp=25.0)):
+        sc = scene_npz(name).set_resolution(640, 360).set_camera(location=loc, rotation=rot)
+        want = bits(oracle.OracleScene(sc).set_shadows(True).render(st))
+        gpu.set_camera(location=loc, rotation=rot)
+        for f in range(2):
+            got = bits(gpu.render(st))
+            assert int((got != want).sum()) == 0, f"pose {k} frame {f} {opts}"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("shards", [3, 8])
 def test_gpu_shadow_shards_reassemble(devbuf, shards):
     """Shadow-ray frames sharded by the reference's bucket grid (compact shards,
