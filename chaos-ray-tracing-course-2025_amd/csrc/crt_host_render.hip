@@ -456,10 +456,10 @@ int sync_device_record(crt_hip_scene *sc, const DeviceScene **out, hipStream_t s
             HIP_TRY(hipStreamWaitEvent(stream, sc->rec_use[j], 0));
         }
         /* ... and wavefront levels that read it on their sets' streams */
-        for (WfSet &w : sc->wf.set)
-            if (w.rec_slot == j) {
+        for (WfSet &w : sc->wf.set)   /* (a set's done_ev is its latest frame's: it covers the set's earlier ones) */
+            if ((w.rec_slots >> j) & 1u) {
                 if (w.done_ev) HIP_TRY(hipStreamWaitEvent(stream, w.done_ev, 0));
-                w.rec_slot = -1;
+                w.rec_slots &= ~(1u << j);
             }
         sc->rec_use_stream[j] = nullptr;
         hipLaunchKernelGGL(k_put_record, dim3(1), dim3(64), 0, stream, sc->d_ring + j, sc->ds);
@@ -768,15 +768,18 @@ void wf_harvest(WfBuffers &wb) {
         if (!w.counts_pending || hipEventQuery(w.counts_ev) != hipSuccess) continue;
         w.counts_pending = false;
         if (w.counts_epoch != wb.epoch || wb.recs.count(w.counts_tiles)) continue;
+        if (w.h_counts[kWfDynMaxLevels] != 0) continue;   /* the frame overflowed: its counts are not its rays */
         std::vector<int32_t> sizes;
         bool ok = true;
+        int64_t ids = 0;
         for (int L = 1; L < w.counts_levels; ++L) {
             const int32_t n = w.h_counts[L - 1];
             if (n == 0) break;
             ok = ok && n > 0 && n <= w.counts_qcap;
+            ids += n;
             sizes.push_back(n);
         }
-        if (!ok) continue;
+        if (!ok || ids > w.counts_idcap) continue;
         WfBuffers::Rec &r = wb.recs[w.counts_tiles];
         if (wb.shrink_records)
             for (int32_t &n : sizes) n = n > 1 ? n - 1 : n;
@@ -865,7 +868,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
         const int rc0 = sync_device_record(sc, &d_scene, ls);
         if (rc0 != CRT_OK) return rc0;
         if (async_frame) {   /* its readers: this set's levels (done_ev), not the caller's stream */
-            w.rec_slot = sc->ring_cur;
+            w.rec_slots |= 1u << sc->ring_cur;
             sc->rec_read_by_set = true;
         }
     } else if (async_frame) {   /* the scene record this frame reads was written on another stream */
@@ -918,7 +921,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
     if (async_frame && (rc = wf_grow_queue(wb, si, 1, qneed)) != CRT_OK) return rc;
     if (dyn && !w.h_counts) {
         void *p = nullptr;
-        HIP_TRY(hipHostMalloc(&p, kWfDynMaxLevels * sizeof(int32_t), hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(&p, (kWfDynMaxLevels + 1) * sizeof(int32_t), hipHostMallocDefault));   /* + the overflow flag */
         w.h_counts = static_cast<int32_t *>(p);
         HIP_TRY(hipEventCreateWithFlags(&w.counts_ev, hipEventDisableTiming));
     }
@@ -927,6 +930,9 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
     auto finish = [&]() -> int {
         if (dyn) {   /* the level sizes, to record once they land (wf_harvest) */
             HIP_TRY(hipMemcpyAsync(w.h_counts, w.counts, (size_t)kMaxLevels * sizeof(int32_t), hipMemcpyDeviceToHost, ls));
+            /* the set's overflow flag beside them, on the same stream: sizes of a
+             * frame that overflowed (a queue or the ray ids) are not recorded */
+            HIP_TRY(hipMemcpyAsync(w.h_counts + kWfDynMaxLevels, w.d_flag, sizeof(int32_t), hipMemcpyDeviceToHost, ls));
             HIP_TRY(hipEventRecord(w.counts_ev, ls));
             w.counts_pending = true;
             w.counts_tiles = (const void *)plan.d_tiles;
@@ -935,6 +941,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
             w.counts_levels = kMaxLevels;
             w.counts_epoch = wb.epoch;
             w.counts_qcap = dyn_q;
+            w.counts_idcap = (int64_t)w.cap - (int64_t)n0;   /* ray ids past the camera rays */
         }
         if (async_frame) {
             HIP_TRY(hipEventRecord(w.done_ev, ls));

@@ -161,6 +161,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
             d = vec(r.dx, r.dy, r.dz);
             id = r.id;
             depth = r.depth;
+            has = (uint32_t)r.id < (uint32_t)lv.id_cap;   /* a skipped slot of an overflowing wave (id -1) */
         }
     }
     LaneCounts cnt = {};
@@ -247,11 +248,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
             if (base + total > lv.out_cap || (int64_t)out_base + base + total > lv.id_cap) atomicOr(lv.overflow, 1);
         }
         base = __shfl(base, __ffsll((long long)(b1 | b2)) - 1);
-        /* never past the queue or the ids (the frame is then reported, not used) */
-        if (base + total > lv.out_cap || (int64_t)out_base + base + total > lv.id_cap) nch = 0;
         /* a lane's children side by side */
         const int k0 = base + __popcll(b1 & lt) + __popcll(b2 & lt);
         const int k1 = k0 + 1;
+        /* never past the queue or the ids (the frame is then reported, not
+         * used): the wave's reserved slots that exist are still filled — a
+         * ray the next level skips (id -1) and, under each reserved id, a
+         * final black activation — so a device-sized level, which takes every
+         * reserved slot, reads no stale ray and the compose no stale node */
+        if (base + total > lv.out_cap || (int64_t)out_base + base + total > lv.id_cap) {
+            for (int c = 0; c < nch; ++c) {
+                const int k = c == 0 ? k0 : k1;
+                if (k < lv.out_cap) {
+                    WRay r = {};
+                    r.id = -1;
+                    lv.out[k] = r;
+                }
+                if ((int64_t)out_base + k < lv.id_cap) {
+                    WNode z = {};
+                    z.kind = wFinal;
+                    z.c0 = z.c1 = -1;
+                    lv.nodes[out_base + k] = z;
+                    lv.cols[out_base + k] = DVec4{0.f, 0.f, 0.f, 0.f};
+                }
+            }
+            nch = 0;
+        }
         for (int c = 0; c < nch; ++c) {
             const int k = c == 0 ? k0 : k1;
             WRay r;

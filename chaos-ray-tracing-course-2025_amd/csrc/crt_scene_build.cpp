@@ -397,11 +397,11 @@ int flatten_tree(const std::vector<BuildNode> &bn, HostScene &hs) {
     return CRT_OK;
 }
 
-/* The BVH (crt_bvh.h): built on the host when the scene makes scattered rays
- * (GI with a diffuse material, reflective or refractive materials), and for
- * any scene small enough that the host build costs little (camera rays may
- * take it, option "traversal" 14); above kHostBvhMax triangles the upload
- * builds it on the device instead (crt_lbvh.hip). */
+/* The BVH (crt_bvh.h): built on the host for every scene up to kHostBvhMax
+ * triangles (camera rays take it too: walks 14 / 15).  Above that the host
+ * never builds it (C5's 1 M triangles: 3.9 s); the upload builds it on the
+ * device instead (crt_lbvh.hip), or, with create flag CRT_SCENE_NO_DEVICE_BVH,
+ * there is none and every ray takes the exact kd walks. */
 int maybe_build_bvh_(HostScene &hs);
 double ms_since(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -414,11 +414,6 @@ int maybe_build_bvh(HostScene &hs) {
 }
 int maybe_build_bvh_(HostScene &hs) {
     if (hs.tri_attr.size() > kHostBvhMax) return hs.nodes.empty() ? CRT_OK : build_proof_tables(hs);
-    bool need = true;
-    for (const DMaterial &m : hs.materials)
-        need = need || m.type == CRT_MATERIAL_REFLECTIVE || m.type == CRT_MATERIAL_REFRACTIVE ||
-               (hs.gi_on && m.type == CRT_MATERIAL_DIFFUSE);
-    if (!need) return CRT_OK;
     const int rc = build_bvh(hs);
     if (rc != CRT_OK || hs.nodes.empty()) return rc;   /* device-built tree: the proof descends it (verify_kd) */
     return build_proof_tables(hs);

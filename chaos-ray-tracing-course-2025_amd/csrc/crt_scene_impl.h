@@ -127,7 +127,9 @@ struct WfSet {
     int counts_ntiles = 0;
     int counts_levels = 0;
     int64_t counts_qcap = 0;
-    int rec_slot = -1;                /* the device record ring slot the set's last frame read (its levels, on the set's stream) */
+    int64_t counts_idcap = 0;         /* ray ids the frame's levels could take */
+    uint32_t rec_slots = 0;           /* device record ring slots the set's frames read (their levels, on the set's
+                                       * stream) since that slot was last reused */
     uint64_t counts_epoch = 0;
 };
 
@@ -178,6 +180,7 @@ struct WfBuffers {
 
 /* Device scene records in flight (crt_host_render.hip sync_device_record). */
 constexpr int kRecRing = 16;
+static_assert(kRecRing <= 32, "WfSet::rec_slots is a 32-bit mask of ring slots");
 
 /* Deepest recursion the wavefront path accepts (levels are launched one by one). */
 constexpr int kWfMaxDepth = 4096;
@@ -209,7 +212,7 @@ struct crt_hip_scene {
     bool rec_up_recorded = false;          /* rec_up of the current slot recorded (a reader on another stream) */
     hipStream_t rec_last_stream = nullptr;  /* where the last frame that read the current record was issued */
     bool rec_read_by_set = false;          /* the frame just issued read it on a wavefront set's stream
-                                            * (WfSet::rec_slot + done_ev cover it, not rec_last_stream) */
+                                            * (WfSet::rec_slots + done_ev cover it, not rec_last_stream) */
     hipEvent_t rec_up[kRecRing] = {};    /* slot written */
     hipEvent_t rec_use[kRecRing] = {};   /* the last frame that read the slot is done */
     hipStream_t rec_use_stream[kRecRing] = {};   /* where each slot's last frame was issued (null: none) */

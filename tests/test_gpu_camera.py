@@ -155,6 +155,60 @@ def test_c3_device_sized_frames(N, oracle, devbuf):
     assert np.array_equal(bits(h.render(st)), wants[3])   # read-back frame
 
 
+def test_c3_overflow_over_stale_queues(N, oracle, devbuf):
+    """An overflowing device-sized frame (wf_dyn_ids 2: the ids run out a few
+    levels down) over queues and nodes full of another pose's rays: the
+    overflowing waves fill their reserved slots with rays the next level skips
+    and final black activations, so no level reads a stale ray (no fault); the
+    frame is reported and every frame rendered afterwards is exact."""
+    name = "11-01-refractive__scene8"
+    st = N.RendererSettings.default(max_ray_depth=8)
+    size = (240, 135)
+    ps = poses(name, 4, yaw_amp=25.0)
+    g = N.HipScene(scene_npz(name).set_resolution(*size))
+    d = [devbuf.alloc(size[0] * size[1] * 12) for _ in range(3)]
+    for loc, rot in ps[:2]:   # queues, nodes and colours hold these poses' rays
+        g.set_camera(loc, rot)
+        g.render_device(st, d[0])
+        g.render_device(st, d[1])
+    devbuf.sync()
+    g.set_option("wf_dyn_ids", 2)
+    g.set_camera(*ps[2])
+    g.render_device(st, d[2])
+    devbuf.sync()
+    try:
+        g.render_device(st, d[2])   # reports the previous frame's overflow (if its ids ran out)
+    except N.CrtError:
+        pass
+    devbuf.sync()
+    want = bits(oracle.OracleScene(posed(name, *ps[2], None, size)).render(st))
+    assert np.array_equal(bits(g.render(st)), want)
+    g.set_option("wf_dyn_ids", 4)
+    g.set_camera(*ps[3])
+    assert np.array_equal(bits(g.render(st)), bits(oracle.OracleScene(posed(name, *ps[3], None, size)).render(st)))
+
+
+def test_c3_moving_camera_three_streams(N, oracle, devbuf):
+    """Frames with a new pose each, issued back to back on three caller streams
+    in turn (the device scene record ring: a slot is rewritten only after every
+    wavefront set that read it is done, WfSet::rec_slots), each equal to the
+    oracle's render of its pose."""
+    name = "11-01-refractive__scene8"
+    st = N.RendererSettings.default(max_ray_depth=8)
+    size = (200, 112)
+    ps = poses(name, 24, yaw_amp=20.0)
+    g = N.HipScene(scene_npz(name).set_resolution(*size))
+    streams = [devbuf.stream() for _ in range(3)]
+    d = [devbuf.alloc(size[0] * size[1] * 12) for _ in ps]
+    for k, (loc, rot) in enumerate(ps):
+        g.set_camera(loc, rot)
+        g.render_device(st, d[k], streams[k % 3])
+    devbuf.sync()
+    for k in (0, 5, 11, 17, 23):
+        want = bits(oracle.OracleScene(posed(name, *ps[k], None, size)).render(st))
+        assert np.array_equal(bits(devbuf.download(d[k], (size[1], size[0], 3), np.float32)), want), f"pose {k}"
+
+
 def test_camera_poses_gi(N, oracle):
     """C4's GI scene at 96x96: new poses through the GI state machine."""
     name = "15-01-conclusion__scene2"
