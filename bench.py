@@ -122,6 +122,8 @@ def parse(argv=None):
     p.add_argument("--shadows", action="store_true",
                    help="trace the shadow rays (option \"shadows\": the course's earlier renderer, dead code at HEAD; "
                         "a separate report, never the HEAD-parity headline): rays = camera + shadow rays")
+    p.add_argument("--set", action="append", default=[], metavar="OPTION=V",
+                   help="A/B runs: crt_hip_scene_set_option on the benched scene (repeatable)")
     p.add_argument("--no-secondary", action="store_true", help="N>1: skip the secondary frames-mode measurement")
     p.add_argument("--camera-orbit", type=int, default=60, metavar="POSES",
                    help="N=1: also time frames with a new camera pose every frame (crt_hip_scene_set_camera; the pose "
@@ -527,6 +529,9 @@ def main():
     # default to the fixed threshold, see cold_cli below)
     t_create = time.perf_counter()
     gpu = N.HipScene(scene, device=local, events=0, shadows=int(a.shadows), calibrate=1)
+    for kv in a.set:   # A/B runs: options of the benched scene (crt_hip_scene_set_option)
+        k, v = kv.split("=", 1)
+        gpu.set_option(k, int(v))
     create_wall_ms = (time.perf_counter() - t_create) * 1e3
     build_id = N.build_id()
     # the same scene created again in this warm process (no runtime / code

@@ -994,12 +994,8 @@ static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
     } else if (k == "rec_machine") {
         sc->rec_machine = value != 0;
         sc->calib_walk = -1;
-    } else if (k == "wf_rpw_lane") {
-        if (value < 1 || value > 64) return set_error(CRT_E_INVALID, "wf_rpw_lane must be 1..64");
-        HIP_TRY(hipDeviceSynchronize());
-        sc->wf_rpw_lane = (int)value;
-        wf_graphs_clear(sc->wf);
-        { sc->wf.recs.clear(); ++sc->wf.epoch; }
+    } else if (k == "wf_record") {   /* the next frames' choice between recorded sizes and device-sized levels */
+        sc->wf_record = value != 0;
         return CRT_OK;
     } else if (k == "wf_dynamic" || k == "wf_dyn_ids" || k == "wf_dyn_waves") {   /* device-sized frames (render_wavefront) */
         if (k == "wf_dyn_ids" && (value < 1 || value > 64)) return set_error(CRT_E_INVALID, "wf_dyn_ids must be 1..64");
@@ -1008,14 +1004,6 @@ static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
         HIP_TRY(hipDeviceSynchronize());
         (k == "wf_dynamic" ? sc->wf_dynamic : k == "wf_dyn_ids" ? sc->wf_dyn_ids : sc->wf_dyn_waves) =
             k == "wf_dynamic" ? (value != 0) : (int)value;
-        return CRT_OK;
-    } else if (k == "wf_window") {
-        if (sc->wf_window != (value != 0)) {
-            HIP_TRY(hipDeviceSynchronize());
-            sc->wf_window = value != 0;
-            wf_graphs_clear(sc->wf);   /* graphs hold the level kernels */
-            { sc->wf.recs.clear(); ++sc->wf.epoch; }
-        }
         return CRT_OK;
     } else if (k == "compact_copy") {   /* crt_hip_render's image copy: 1 compact (default), 0 the whole image */
         sc->compact_copy = value != 0;

@@ -808,8 +808,8 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
     wb.shrink_records = sc->wf_replay == 2;
     wf_harvest(wb);
     const auto rit = wb.recs.find((const void *)plan.d_tiles);
-    const bool replay = !count && sc->wf_replay && rit != wb.recs.end() && rit->second.ntiles == plan.ntiles &&
-                        std::memcmp(&rit->second.st, st, sizeof *st) == 0;
+    const bool replay = !count && sc->wf_replay && sc->wf_record && rit != wb.recs.end() &&
+                        rit->second.ntiles == plan.ntiles && std::memcmp(&rit->second.st, st, sizeof *st) == 0;
     /* no recorded sizes (a new camera, tile list or settings): device-sized
      * levels instead of read-backs — queues of 2 x n0 rays, wf_dyn_ids x n0
      * ray ids, each level's size read by its kernels from the counts the
@@ -1030,8 +1030,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
          * the level has fewer rays than ~4096 waves' worth, at least 8, at most
          * the wf_rpw cap — a level's time is its slowest waves'
          * (C3 3.60 -> 3.33 ms, profiles/r02/ab_c3_rpw) */
-        /* sec 16: the BVH window walk, four lanes a ray (wf_window) */
-        const int rpw_l = sec == 16 ? 16 : sec == 14 ? sc->wf_rpw_lane : std::min(rpw, std::max(8, (int)((n + 4095) / 4096)));
+        const int rpw_l = sec == 14 ? 64 : std::min(rpw, std::max(8, (int)((n + 4095) / 4096)));
         WLevel l{w.q[cur], n, L, w.q[cur ^ 1], w.counts + L, (int32_t)(base + n), w.nodes, w.cols, rpw_l, out_cap,
                  w.d_flag, dyn ? w.counts : nullptr, (int32_t)n0, cap_of(w.cap)};
         /* device-sized: a fixed grid whose waves stride over the level */
@@ -1042,9 +1041,7 @@ int render_wavefront(crt_hip_scene *sc, const DSettings &ds, const crt_renderer_
 #define CRT_WF(SEC, COUNT)                                                                                  \
     hipLaunchKernelGGL((k_wf_level<SEC, false, COUNT>), dim3(blocks), dim3(256), 0, ls, d_scene, ds,         \
                        plan.d_tiles, plan.ntiles, l, cnt)
-        if (sec == 16) {
-            if (count) CRT_WF(16, true); else CRT_WF(16, false);
-        } else if (sec == 14) {
+        if (sec == 14) {
             if (count) CRT_WF(14, true); else CRT_WF(14, false);
         } else if (sec == 10) {
             if (count) CRT_WF(10, true); else CRT_WF(10, false);
@@ -1187,7 +1184,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     const bool rec_machine = full && !gi && rec_machine_on(sc, st) && !stamps;
     if (wf_frame)
         return render_wavefront(sc, ds, st, plan, d_out, stream, count, d_scene,
-                                sec == 14 && sc->wf_window ? 16 : sec, camera_walk(sc, sc->traversal));
+                                sec, camera_walk(sc, sc->traversal));
     /* frame-stack kernel: one walk for every ray */
     int trav = full ? sec : camera_walk(sc, sc->traversal);
     if (trav == 13 && !plan.has_small) trav = 12;   /* no split tiles: the leaner packet-only kernel */

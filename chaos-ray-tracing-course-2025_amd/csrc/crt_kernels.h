@@ -169,7 +169,7 @@ __global__ void k_warm_bins();
     uint32_t *__restrict__);
 #define CRT_WF_INSTANCES(X) X(4, false, false) X(4, false, true) X(10, false, false) X(10, false, true)        \
     X(14, false, false) X(14, false, true) X(7, true, false) X(7, true, true) X(8, true, false) X(8, true, true) \
-    X(12, true, false) X(12, true, true) X(14, true, false) X(14, true, true) X(16, false, false) X(16, false, true)
+    X(12, true, false) X(12, true, true) X(14, true, false) X(14, true, true)
 #define CRT_WF_SIG(T, L0, C) void k_wf_level<T, L0, C>(const DeviceScene *__restrict__, DSettings, \
     const Tile *__restrict__, int, WLevel, unsigned long long *__restrict__);
 

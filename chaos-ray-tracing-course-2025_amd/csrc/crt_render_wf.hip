@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
         n = min(lv.dyn[lv.depth - 1], lv.n);
         out_base = b < (int64_t)INT32_MAX ? (int)b : INT32_MAX;
     }
-    constexpr bool kCoop = TRAV != 16 && kIsCoop<TRAV>;
+    constexpr bool kCoop = kIsCoop<TRAV>;
     __shared__ CoopLds coop[kCoop ? 4 : 1];
     /* the level's waves: one pass over the grid, or (device-sized levels, a
      * fixed grid) each XCD strides over its own eighth of the level, as the
@@ -152,9 +152,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
     } else {
         const int ray0 = wv * lv.rpw;
         if (ray0 >= n) return;             /* whole wave past the queue */
-        /* TRAV 16: a ray per group of four lanes (the BVH window walk) */
-        const int ray = ray0 + (TRAV == 16 ? lane >> 2 : lane);
-        has = (TRAV == 16 ? (lane >> 2) : lane) < lv.rpw && ray < n;
+        const int ray = ray0 + lane;
+        has = lane < lv.rpw && ray < n;
         if (has) {
             const WRay r = lv.in[ray];
             o = vec(r.ox, r.oy, r.oz);
@@ -167,12 +166,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVEL0 ? CR
     LaneCounts cnt = {};
     float t;
     int slot;
-    if constexpr (TRAV == 16) {   /* four lanes walk the group's ray; the first shades it */
-        slot = trace_bvh_window<COUNT, 4>(s, lane & 3, has, o, d, t, cnt);
-        has = has && (lane & 3) == 0;
-    } else {
-        slot = trace<TRAV, COUNT>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has, o, d, t, cnt);
-    }
+    slot = trace<TRAV, COUNT>(s, &coop[kCoop ? (threadIdx.x >> 6) : 0], has, o, d, t, cnt);
     WF_STAMP(2);
 
     WNode node = {wFinal, -1, -1, 0, 0.f, 0.f, 0.f, 0.f};

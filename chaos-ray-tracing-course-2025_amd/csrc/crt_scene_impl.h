@@ -290,11 +290,11 @@ struct crt_hip_scene {
     int calib_deferred_walk = -1;  /* walk whose first frame skipped the calibration */
     int bins_on = 1;               /* camera frames take the camera bins where built (walk 15; option "bins") */
     int64_t bins_mean_cap = crt_amd::kBinMeanCap;   /* candidates per cell on average, at most (env CRT_BINS_MEAN_CAP) */
-    int wf_rpw_lane = 64;          /* rays per wave of levels >= 1 on the per-lane BVH walk (option "wf_rpw_lane") */
     int wf_dynamic = 1;            /* wavefront frames without recorded sizes: device-sized levels, no read-back (option "wf_dynamic") */
+    int wf_record = 1;             /* frames replay recorded level sizes (HIP graphs) when they have them; 0: every
+                                    * frame device-sized (option "wf_record") */
     int wf_dyn_ids = 4;            /* ... their ray-id capacity, x camera rays (option "wf_dyn_ids") */
     int wf_dyn_waves = 8192;       /* ... the waves of each level's grid, at most (option "wf_dyn_waves") */
-    int wf_window = 0;             /* wavefront levels >= 1: the BVH window walk, four lanes a ray (option "wf_window") */
     int bvh_device = 1;            /* build the BVH on the device above kHostBvhMax triangles (create flag
                                     * CRT_SCENE_NO_DEVICE_BVH: not) */
     int create_flags = 0;          /* the create's CRT_SCENE_* flags (crt_multi.hip: the probe's test hook) */

@@ -43,15 +43,13 @@ def compare(got, want):
     return rmse, nbad
 
 
-@pytest.mark.parametrize("window", [0, 1], ids=["lane-walk", "window-walk"])
-def test_c3_full_frame(N, oracle, window):
+def test_c3_full_frame(N, oracle):
     """C3 at its own size: 1920x1080, max_ray_depth 8 (wavefront levels; levels
-    >= 1 through the per-lane BVH walk, or the window walk of four lanes a ray,
-    option wf_window)."""
+    >= 1 through the per-lane BVH walk)."""
     h = HASHES["C3"]
     sc = scene_npz(h["scene"])
     st = N.RendererSettings.default(**h["settings"])
-    gpu = N.HipScene(sc, wf_window=window)
+    gpu = N.HipScene(sc)
     got = gpu.render(st)
     assert got.shape == (1080, 1920, 3)
     want = oracle.OracleScene(sc).render(st)
