@@ -133,7 +133,8 @@ class SceneInfo(C.Structure):
                 ("wf_sets", C.c_int32), ("pad0", C.c_int32), ("camera_moves", C.c_int64),
                 ("view_rebuilds", C.c_int64), ("records_written", C.c_int64), ("multi_probe", C.c_int32),
                 ("pad1", C.c_int32), ("multi_probe_ms", C.c_double), ("bins_binnings", C.c_int64),
-                ("bins_reuses", C.c_int64), ("bvh_on_device", C.c_int32), ("bvh_depth", C.c_int32)]
+                ("bins_reuses", C.c_int64), ("bvh_on_device", C.c_int32), ("bvh_depth", C.c_int32),
+                ("light_bin_records", C.c_int64), ("light_bins_ms", C.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -598,6 +598,8 @@ int crt_hip_scene_info(const crt_hip_scene *sc, crt_scene_info *out) {
     out->records_written = sc->records_written;
     out->bins_binnings = sc->bins.binnings;
     out->bins_reuses = sc->bins.reuses;
+    out->light_bin_records = sc->lbins_records;
+    out->light_bins_ms = sc->lbins_ms;
     return CRT_OK;
 }
 
@@ -1073,6 +1075,9 @@ static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
         sc->calib_walk = -1;
     } else if (k == "shadows") {
         sc->shadows = value != 0;
+    } else if (k == "light_bins") {
+        sc->light_bins = value != 0;
+        if (sc->lbins_tried) sc->ds.lbin_n = sc->light_bins ? sc->lbins_n : 0;
     } else if (k == "trace_walk") {
         if (value < 0 || value > 2) return set_error(CRT_E_INVALID, "trace_walk must be 0, 1 or 2 (BVH)");
         sc->trace_walk = value;

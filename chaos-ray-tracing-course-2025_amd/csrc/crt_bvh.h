@@ -670,6 +670,129 @@ CRT_HD int occluded_bvh(const BNode *bnodes, int bn, const DTriGeo *btri, const 
     return 0;
 }
 
+/* Step 1 of a shadow ray towards light P over its light bins (crt_layout.h
+ * DLightBin; lists built by crt_light_bins.cpp, where the bound below is
+ * derived): the first candidate with a hit the reference's triangle test
+ * accepts within the light (fl(t * t) <= r2).  Returns 1 with (tri, t) set,
+ * 0 when no triangle has such a hit, -1 when the bins do not decide this ray
+ * (origin past the hull margins' bound, the line passes the light farther
+ * than e_max, it ends farther than R0 past the light, or NaN) — the BVH
+ * does.  With w = o - L, e the line's distance from L and the ray ending
+ * within R0 of L: every hit point q the ray can reach lies in its
+ * triangle's hull, either within R0 of L (the near list) or on the stretch
+ * before the line's closest approach, where |q - L| <= |w| and the
+ * direction of q - L is within asin(e_max / R0) of w's — in w's cell list,
+ * whose candidates past dmin > |w| cannot hold it. */
+/* One ray's part of the walk: ok = the bins decide it; its cell (-1: its
+ * origin is within R0, the near list holds everything it can hit) and the
+ * squared cut-offs of the near list and of the cell. */
+struct LbinRay {
+    double cut_near, cut_far;
+    int cell;
+    bool ok;
+};
+
+CRT_HD LbinRay lbin_setup(const DLightBin &P, int N, float prune_origin_max, Vec o, Vec d, float lim) {
+    LbinRay r;
+    r.cut_near = r.cut_far = 0.0;
+    r.cell = -1;
+    r.ok = false;
+    if (!P.on) return r;
+    if (!(fabsf(o.x) <= prune_origin_max && fabsf(o.y) <= prune_origin_max && fabsf(o.z) <= prune_origin_max))
+        return r;   /* also NaN */
+    const double dx = d.x, dy = d.y, dz = d.z;
+    const double dd = dx * dx + dy * dy + dz * dz;
+    if (!(dd > 0.0) || !(dd < 1e300)) return r;
+    const double wx = (double)o.x - P.lx, wy = (double)o.y - P.ly, wz = (double)o.z - P.lz;
+    const double cx = wy * dz - wz * dy, cy = wz * dx - wx * dz, cz = wx * dy - wy * dx;
+    const double e2 = (cx * cx + cy * cy + cz * cz) / dd;
+    if (!(e2 <= P.e_sq)) return r;
+    const double l = lim;
+    const double ex = wx + dx * l, ey = wy + dy * l, ez = wz + dz * l;
+    const double end2 = ex * ex + ey * ey + ez * ez;
+    if (!(end2 < 0.98 * P.r0_sq)) return r;
+    const double w2 = wx * wx + wy * wy + wz * wz;
+    r.ok = true;
+    /* near list: points up to the closest approach are within |w|, past it within max(e, |end|) */
+    r.cut_near = fmax(w2, fmax(e2, end2)) * (1.0 + 1e-9);
+    /* a cell's triangles (hull >= R0 away) only before the closest approach, within |w| */
+    r.cut_far = w2 * (1.0 + 1e-9);
+    if (!(w2 >= 0.999 * P.r0_sq)) return r;   /* nearer origins: every point the ray reaches is within R0 */
+    /* w's cell: face by the largest |w| component (ties: the lower axis), u, v = w_j / |w_k| */
+    const double ax = fabs(wx), ay = fabs(wy), az = fabs(wz);
+    int k;
+    double m, a, b;
+    if (ax >= ay && ax >= az) { k = 0; m = ax; a = wy; b = wz; }
+    else if (ay >= az) { k = 1; m = ay; a = wx; b = wz; }
+    else { k = 2; m = az; a = wx; b = wy; }
+    const double wk = k == 0 ? wx : (k == 1 ? wy : wz);
+    const int face = 2 * k + (wk < 0.0 ? 1 : 0);
+    const double h = 0.5 * N;
+    int cu = (int)floor((a / m + 1.0) * h), cv = (int)floor((b / m + 1.0) * h);
+    cu = cu < 0 ? 0 : (cu > N - 1 ? N - 1 : cu);
+    cv = cv < 0 ? 0 : (cv > N - 1 ? N - 1 : cv);
+    r.cell = (face * N + cv) * N + cu;
+    return r;
+}
+
+/* a candidate: a hit the reference's test accepts within the light */
+CRT_HD bool lbin_test(const CamCand &cc, Vec o, Vec d, const PruneRay &pr, float lim, float r2, float &t) {
+    if (!cand_alive(cc, pr, lim)) return false;
+    const uint8_t cull = (uint8_t)((uint32_t)cc.id >> 31);
+    return tri_hit(o, d, cc.g, &cull, t) && !(t * t > r2);
+}
+
+#ifndef CRT_LBINS_CAP
+#define CRT_LBINS_CAP 48   /* candidates a shadow ray walks in its cell at most (more: undecided, the BVH decides) */
+#endif
+
+template <bool COUNT>
+CRT_HD int lbin_first_hit(const CamCand *lb, const int32_t *off, const DLightBin &P, int N, float prune_origin_max,
+                          Vec o, Vec d, float r2, int &tri, float &t_hit, WalkCounts &c) {
+    tri = -1;
+    t_hit = 0.0f;
+    const float lim = sqrtf(r2) * (1.0f + 0x1p-20f);
+    const LbinRay lr = lbin_setup(P, N, prune_origin_max, o, d, lim);
+    if (!lr.ok) return -1;
+    const PruneRay pr = make_prune_ray(o, d, prune_origin_max);
+    for (int phase = 0; phase < 2; ++phase) {
+        if (phase == 1 && lr.cell < 0) break;
+        const int beg = off[P.base + (phase ? 1 + lr.cell : 0)], end = off[P.base + (phase ? 2 + lr.cell : 1)];
+        const double cut = phase ? lr.cut_far : lr.cut_near;
+        for (int k = beg; k < end; ++k) {
+            if (phase == 1 && k - beg >= CRT_LBINS_CAP) return -1;   /* a long walk: the BVH's */
+            const CamCand cc = CRT_LDG(lb, k);
+            if ((double)cc.dmin * (double)cc.dmin > cut) break;
+            if (COUNT) ++c.tris;
+            float t;
+            if (lbin_test(cc, o, d, pr, lim, r2, t)) {
+                tri = cc.id & 0x7fffffff;
+                t_hit = t;
+                return 1;
+            }
+        }
+    }
+    return 0;
+}
+
+/* lbin_first_hit with its hit proved on the reference's tree: 1 occluded,
+ * 0 lit, -1 undecided (the BVH or the exact walk decides). */
+template <bool COUNT>
+CRT_HD int occluded_lbins(const CamCand *lb, const int32_t *off, const DLightBin &P, int N, float prune_origin_max,
+                          const DNode *nodes, const int32_t *slot_tri, const KTopo *ktopo, const KTopo2 *ktopo2,
+                          bool planes_ok, Vec o, Vec d, float r2, WalkCounts &c) {
+    int tri;
+    float t;
+    const int r = lbin_first_hit<COUNT>(lb, off, P, N, prune_origin_max, o, d, r2, tri, t, c);
+    if (r != 1) return r;
+    const RayRcp rr = make_ray_rcp(o, d, planes_ok);
+    const Vec p = vadd(o, vscale(d, t));
+    const int slot = CRT_PROOF_TOPO && ktopo ? verify_topo<COUNT>(ktopo, nodes, slot_tri, tri, o, d, rr, p, c,
+                                                                  CRT_PROOF_TOPO2 ? ktopo2 : nullptr)
+                                             : verify_kd<COUNT>(nodes, slot_tri, tri, o, d, rr, p, c);
+    return slot >= 0 ? 1 : -1;
+}
+
 /* The same answer for a camera ray of cell [beg, end) through the camera bins. */
 template <bool COUNT>
 CRT_HD int trace_bins_exact(const CamCand *cands, int beg, int end, int bit, const DNode *nodes, const PNode *pnodes, int n,

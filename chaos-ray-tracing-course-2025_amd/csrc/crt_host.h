@@ -151,6 +151,18 @@ bool bin_camera_of(const DCamera &c, float prune_origin_max, BinCamera &cam);
 /* Per-triangle static part of the candidate records (hull box, id, geometry). */
 void bin_templates(const HostScene &hs, std::vector<CamCand> &tpl);
 
+/* Light bins (crt_layout.h DLightBin, crt_light_bins.cpp) of every light over
+ * the triangles' templates: N x N cells a cube face, for rays passing their
+ * light within e_max.  False (out empty) when no light takes bins. */
+struct LightBinsHost {
+    int n = 0;
+    std::vector<DLightBin> par;
+    std::vector<int32_t> off;
+    std::vector<CamCand> recs;
+};
+bool build_light_bins(const CamCand *tpl, int nt, const DLight *lights, int nl, double e_max, int N,
+                      LightBinsHost &out);
+
 /* Mesh prep + (build_tree) the exact tree build and its flattening. */
 int prepare_scene(const crt_scene_desc *desc, HostScene &out, bool build_tree = true);
 /* The reference's built scene (vertices + tree) flattened as it is. */

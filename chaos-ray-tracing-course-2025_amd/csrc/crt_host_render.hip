@@ -425,6 +425,47 @@ int ensure_gi_tables(crt_hip_scene *sc) {
     return CRT_OK;
 }
 
+/* Light bins (crt_light_bins.cpp; option "light_bins", off by default: on
+ * C2 the per-lane list walks measured 0.43-0.46 ms a shadow-ray frame against
+ * 0.41-0.43 for the BVH wave walk) for the shadow rays, built at the first
+ * shadow-ray frame with them on, from the camera bins' per-triangle templates (on the
+ * device since the create) and the lights: once per scene, the camera does
+ * not enter them.  Rays passing their light within e_max = max(0.02,
+ * 1.25 |shadow_bias|) of the first frame are decided by them (larger biases
+ * later: the BVH decides).  No templates (no camera bins) or no light taking
+ * bins: the BVH walks as before. */
+#ifndef CRT_LBINS_N
+#define CRT_LBINS_N 64   /* light bins: cells a cube-face side */
+#endif
+int ensure_light_bins(crt_hip_scene *sc, const crt_renderer_settings *st) {
+    if (!sc->light_bins || sc->lbins_tried) {
+        sc->ds.lbin_n = sc->light_bins ? sc->lbins_n : 0;
+        return CRT_OK;
+    }
+    sc->lbins_tried = true;
+    const int nt = sc->bins.nt, nl = sc->ds.light_count;
+    if (!sc->bins.tpl || nt <= 0 || nl <= 0 || !sc->ds.bnodes) return CRT_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<CamCand> tpl((size_t)nt);
+    std::vector<DLight> lights((size_t)nl);
+    HIP_TRY(hipMemcpy(tpl.data(), sc->bins.tpl, tpl.size() * sizeof(CamCand), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(lights.data(), sc->ds.lights, lights.size() * sizeof(DLight), hipMemcpyDeviceToHost));
+    const double bias = std::isfinite(st->shadow_bias) ? std::fabs((double)st->shadow_bias) : 0.0;
+    LightBinsHost L;
+    if (!build_light_bins(tpl.data(), nt, lights.data(), nl, std::max(0.02, 1.25 * bias), CRT_LBINS_N, L)) return CRT_OK;
+    UploadBatch ub;
+    ub.add(L.par, &sc->ds.lbin_par);
+    ub.add(L.off, &sc->ds.lbin_off);
+    ub.add(L.recs, &sc->ds.lbins, 1);   /* + a zero record: the wave walk loads one past a list */
+    const int rc = ub.flush(sc);
+    if (rc != CRT_OK) return rc;
+    sc->lbins_n = L.n;
+    sc->lbins_records = (int64_t)L.recs.size();
+    sc->ds.lbin_n = sc->light_bins ? L.n : 0;
+    sc->lbins_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return CRT_OK;
+}
+
 /* Device copy of sc->ds for the render kernels.  When the host record
  * changed (a new camera, the first GI frame's tables) the next slot of a ring
  * of kRecRing records takes it, written on `stream` by a one-thread kernel
@@ -1107,6 +1148,10 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
     }
     if (sc->has_refractive && sc->info.refractions_on) {
         const int rc = ensure_pow5_table(sc);
+        if (rc != CRT_OK) return rc;
+    }
+    if (sc->shadows) {
+        const int rc = ensure_light_bins(sc, st);
         if (rc != CRT_OK) return rc;
     }
     if (plan.ntiles == 0) return CRT_OK;

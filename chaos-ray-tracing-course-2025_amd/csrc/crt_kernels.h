@@ -24,6 +24,9 @@
 #define CRT_BVH_WINDOW 1     /* split tiles of camera frames on the BVH: one ray per group of lanes (trace_bvh_window) */
 #endif
 #ifndef CRT_BVH_WAVES
+#ifndef CRT_SHADOW_WAVES
+#define CRT_SHADOW_WAVES 3   /* min waves/SIMD asked of the shadow-ray kernels without recursion (1: no bound; 3: 0.41 against 0.52 ms, C2 with shadows) */
+#endif
 #define CRT_BVH_WAVES 1      /* min waves/SIMD asked of the camera BVH-walk (14) kernel (1: no bound) */
 #endif
 #ifndef CRT_PACKET_WAVES

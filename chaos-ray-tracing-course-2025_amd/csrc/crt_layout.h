@@ -130,6 +130,24 @@ struct alignas(16) CamCand {
 };
 static_assert(sizeof(CamCand) == 96, "CamCand must be 96 B");
 
+/* Light bins of one light (crt_light_bins.cpp build_light_bins, crt_bvh.h
+ * lbin_first_hit): a cube map of N x N cells a face around the light, each
+ * cell listing (CamCand records, mask / rest unused) every triangle a shadow
+ * ray whose origin lies in that cell's direction can hit on its way to the
+ * light, sorted by dmin = the distance from the light to the hull, rounded
+ * down; triangles whose hull comes within R0 of the light (and unbounded
+ * hulls) are in a near list every ray tests.  Offsets
+ * off[base] .. off[base + 6 N^2 + 1]: the near list, then the cells in order
+ * (face = 2 axis + (w_axis < 0), row v, column u). */
+struct DLightBin {
+    double lx, ly, lz;      /* the light's position */
+    double r0_sq;           /* R0^2 */
+    double e_sq;            /* rays passing the light farther than e_max (e_sq = e_max^2) are not decided here */
+    int32_t base;           /* first offset of this light */
+    int32_t on;             /* 0: this light's rays take the BVH */
+};
+static_assert(sizeof(DLightBin) == 48, "DLightBin must be 48 B");
+
 struct alignas(16) DTriAttr {
     int32_t i0, i1, i2;
     int32_t mat_flags;   /* material index | (smooth_shading << 31) */
@@ -210,6 +228,13 @@ struct DeviceScene {
     const DVec4 *texels;
     const DLight *lights;
     int32_t light_count;
+    /* light bins (DLightBin; built at the first shadow-ray frame, option
+     * "light_bins"): per light its parameters, the offsets and the records;
+     * lbin_n 0 when not built */
+    const DLightBin *lbin_par;
+    const int32_t *lbin_off;
+    const CamCand *lbins;
+    int32_t lbin_n;
     /* GI angle tables: (cosf, sinf) pairs of pi*u and of 2*pi*u for the 2^23 values of u */
     const float *gi_pi;
     const float *gi_2pi;

@@ -338,7 +338,7 @@ __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSetting
 
 
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW>
-__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(TRAV == 13 ? CRT_WINDOW_WAVES : TRAV == 12 ? CRT_PACKET_WAVES : (TRAV == 14 || TRAV == 15) && !FULL ? CRT_BVH_WAVES : (FULL && MAXF == 4 ? CRT_GI_WAVES : 1)))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
+__global__ CRT_RENDER_BOUNDS __attribute__((amdgpu_waves_per_eu(SHADOW && !FULL ? CRT_SHADOW_WAVES : TRAV == 13 ? CRT_WINDOW_WAVES : TRAV == 12 ? CRT_PACKET_WAVES : (TRAV == 14 || TRAV == 15) && !FULL ? CRT_BVH_WAVES : (FULL && MAXF == 4 ? CRT_GI_WAVES : 1)))) void k_render_tiles(const DeviceScene *__restrict__ scene, DSettings st,
                                                   const Tile *__restrict__ tiles,
                                                       int ntiles, float *__restrict__ out,
                                                       unsigned long long *__restrict__ counters,

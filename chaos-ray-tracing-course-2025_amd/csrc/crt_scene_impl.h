@@ -255,6 +255,11 @@ struct crt_hip_scene {
     bool grid_empty = false;
     int traversal = 8;             /* 7 reference order | 8 pruned (default), see trace<> (env CRT_TRAVERSAL) */
     int shadows = 0;               /* option "shadows": trace the shadow rays (k_render_tiles<..., SHADOW>) */
+    int light_bins = 0;            /* option "light_bins": shadow rays over the light bins (ensure_light_bins; off: the BVH wave walk measured as fast) */
+    bool lbins_tried = false;      /* built (or found not to apply) at the first shadow-ray frame */
+    int lbins_n = 0;               /* their cells a cube-face side (0: none) */
+    int64_t lbins_records = 0;
+    double lbins_ms = 0.0;
     int trace_walk = 1;            /* crt_hip_trace_batch: 0 reference-order walk, 1 pruned per-lane walk */
     float fov_radians = 0.f;       /* the camera's (ds.cam: the rest) */
     int64_t camera_moves = 0;      /* crt_hip_scene_set_camera calls that changed the camera */
@@ -342,6 +347,7 @@ void warm_code_objects(int device, hipStream_t stream);
 void start_host_tables(bool gi, bool pow5);
 int ensure_gi_tables(crt_hip_scene *sc);
 int ensure_pow5_table(crt_hip_scene *sc);
+int ensure_light_bins(crt_hip_scene *sc, const crt_renderer_settings *st);
 /* camera frames of this scene walk the camera bins (walk 15): built, enabled,
  * and the default camera walk selected */
 inline bool bins_active(const crt_hip_scene *sc) { return sc->ds.bins && sc->bins_on && sc->traversal == 14; }

@@ -34,6 +34,13 @@ __device__ __forceinline__ void make_hit(const DeviceScene &s, Vec o, Vec d, flo
  * which is also what the loop computes when it runs, since it intersects the
  * unchanged shadow ray every time (tests/test_shadows.py).  Per-lane pruned
  * walk (called from divergent shading code), closest hit as the reference. */
+#ifndef CRT_SHADOW_DIAG
+#define CRT_SHADOW_DIAG 0   /* diagnostic builds: 1 no shadow walks (frames without recursion) */
+#endif
+#ifndef CRT_LBINS_LANE
+#define CRT_LBINS_LANE 1   /* frames without recursion walk the light bins per lane (0: wave-coherent, 0.65 against 0.45 ms) */
+#endif
+
 template <bool COUNT>
 __device__ __forceinline__ bool shadow_occluded_kd(const DeviceScene &s, Vec o, Vec d, float r2, LaneCounts &c) {
     float t;
@@ -42,7 +49,18 @@ __device__ __forceinline__ bool shadow_occluded_kd(const DeviceScene &s, Vec o, 
 }
 
 template <bool COUNT>
-__device__ __forceinline__ bool shadow_occluded(const DeviceScene &s, Vec o, Vec d, float r2, LaneCounts &c) {
+__device__ __forceinline__ bool shadow_occluded(const DeviceScene &s, int light, Vec o, Vec d, float r2, LaneCounts &c) {
+    if (s.lbin_n) {   /* the light's bins (crt_bvh.h occluded_lbins): first hit within the light, proved */
+        WalkCounts wc = {0u, 0u};
+        const int r = occluded_lbins<COUNT>(s.lbins, s.lbin_off, s.lbin_par[light], s.lbin_n, s.prune_origin_max,
+                                            s.nodes, s.slot_tri, s.ktopo, s.ktopo2, s.planes_ok != 0, o, d, r2, wc);
+        if (COUNT) {
+            c.nodes += wc.nodes;
+            c.tris += wc.tris;
+            if (r >= 0) ++c.traversals;
+        }
+        if (r >= 0) return r == 1;
+    }
     if (s.bnodes) {   /* any hit within the light through the BVH, proved on the reference's tree (crt_bvh.h) */
         WalkCounts wc = {0u, 0u};
         const int r = occluded_bvh<COUNT>(s.bnodes, s.bnode_count, s.btri, s.btri_id, s.nodes, s.slot_tri, s.ktopo,
@@ -71,7 +89,7 @@ __device__ __forceinline__ Vec diffuse_finish(const DeviceScene &s, const DSetti
         const float dn = vdot(ld, n);
         const float cos_law = (0.0f < dn) ? dn : 0.0f;          /* std::max(0.0f, dn) */
         const float area = 4 * kPi * r2;
-        if (SHADOW && shadow_occluded<COUNT>(s, vadd(p, vscale(n, st.shadow_bias)), ld, r2, *c)) continue;
+        if (SHADOW && shadow_occluded<COUNT>(s, l, vadd(p, vscale(n, st.shadow_bias)), ld, r2, *c)) continue;
         acc = vadd(acc, vscale(vdiv(vscale(alb, L.intensity), area), cos_law));
     }
     return vdiv(acc, (float)(st.diffuse_reflection_ray_count + 1));
@@ -347,11 +365,37 @@ __device__ Vec shade_hit_shadowed(const DeviceScene &s, const DSettings &st, boo
         const float cos_law = (0.0f < dn) ? dn : 0.0f;
         const float area = 4 * kPi * r2;
         bool lit = true;
+#if CRT_SHADOW_DIAG == 1
+        if (false) {      /* diagnostic build: no shadow walks (every light lit) */
+#else
         if (s.bnodes) {   /* the wave's shadow rays through the BVH (any hit within the light) */
+#endif
             const Vec so = vadd(h.p, vscale(h.n, st.shadow_bias));
-            const int r = occluded_bvh_wave<COUNT>(s, diffuse, so, ld, r2, cnt);
+            int r = -1;
+            if (s.lbin_n) {   /* the light's bins */
+#if CRT_LBINS_LANE
+                r = 0;
+                if (diffuse) {
+                    WalkCounts wc = {0u, 0u};
+                    r = occluded_lbins<COUNT>(s.lbins, s.lbin_off, s.lbin_par[l], s.lbin_n, s.prune_origin_max, s.nodes,
+                                              s.slot_tri, s.ktopo, s.ktopo2, s.planes_ok != 0, so, ld, r2, wc);
+                    if (COUNT) {
+                        cnt.nodes += wc.nodes;
+                        cnt.tris += wc.tris;
+                        if (r >= 0) ++cnt.traversals;
+                    }
+                }
+#else
+                r = occluded_lbins_wave<COUNT>(s, l, diffuse, so, ld, r2, cnt);
+#endif
+            }
+            if (__ballot(diffuse && r < 0) != 0ull) {   /* rays the bins do not decide */
+                const int rb = occluded_bvh_wave<COUNT>(s, diffuse && r < 0, so, ld, r2, cnt);
+                if (diffuse && r < 0) r = rb;
+            }
+            if (!diffuse) r = 0;
             if (r != 0) lit = r == 1 ? false : !shadow_occluded_kd<COUNT>(s, so, ld, r2, cnt);
-        } else if (__ballot(diffuse) != 0ull) {
+        } else if (!CRT_SHADOW_DIAG && __ballot(diffuse) != 0ull) {
             lit = !shadow_occluded_packet<COUNT>(s, diffuse, vadd(h.p, vscale(h.n, st.shadow_bias)), ld, r2, cnt);
         }
         if (diffuse && lit) acc = vadd(acc, vscale(vdiv(vscale(alb, Lt.intensity), area), cos_law));

@@ -696,6 +696,97 @@ __device__ int occluded_bvh_wave(const DeviceScene &s, bool active, Vec o, Vec d
     return res;
 }
 
+/* The wave's shadow rays towards light `light` over its light bins
+ * (crt_bvh.h lbin_setup / lbin_test, the lists as lbin_first_hit walks
+ * them), wave-coherent: the near list, then one cell at a time — the cell of
+ * the first lane still looking, walked with scalar loads by the lanes whose
+ * ray is in it (a tile's rays share few cells) until each has a hit or is
+ * past its cut-off; then the proofs of every lane that found a hit, side by
+ * side.  1 occluded, 0 lit, -1 not decided here (the BVH decides). */
+template <bool COUNT>
+__device__ int occluded_lbins_wave(const DeviceScene &s, int light, bool active, Vec o, Vec d, float r2,
+                                   LaneCounts &c) {
+    const DLightBin P = load_scalar(s.lbin_par, light);
+    const float lim = sqrtf(r2) * (1.0f + 0x1p-20f);
+    LbinRay lr;
+    lr.ok = false;
+    lr.cell = -1;
+    lr.cut_near = lr.cut_far = 0.0;
+    if (active) lr = lbin_setup(P, s.lbin_n, s.prune_origin_max, o, d, lim);
+    const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
+    int tri = -1;
+    float th = 0.0f;
+    bool look = lr.ok;      /* near list */
+    bool far = lr.ok && lr.cell >= 0;
+    bool capped = false;
+    const int base = P.base;
+    for (int phase = 0; phase < 2; ++phase) {
+        do {
+            int beg, end;
+            double cut;
+            int cell = -1;
+            if (phase == 0) {
+                beg = load_scalar(s.lbin_off, base);
+                end = load_scalar(s.lbin_off, base + 1);
+                cut = lr.cut_near;
+            } else {
+                const uint64_t m = __ballot(far);
+                if (m == 0ull) break;
+                cell = uniform_i(__shfl(lr.cell, (int)__builtin_ctzll(m)));
+                look = far && lr.cell == cell;
+                beg = load_scalar(s.lbin_off, base + 1 + cell);
+                end = load_scalar(s.lbin_off, base + 2 + cell);
+                cut = lr.cut_far;
+            }
+            CamCand nx = load_scalar(s.lbins, beg);   /* (a zero record past the last list) */
+            const int end0 = end;
+            if (phase == 1 && end - beg > CRT_LBINS_CAP) end = beg + CRT_LBINS_CAP;
+            for (int k = beg; k < end; ++k) {
+                if (__ballot(look) == 0ull) break;
+                const CamCand cc = nx;
+                nx = load_scalar(s.lbins, k + 1);
+                if (COUNT) ++c.wave_tris;
+                if (look) {
+                    float t;
+                    if ((double)cc.dmin * (double)cc.dmin > cut) {
+                        look = false;
+                    } else {
+                        if (COUNT) ++c.tris;
+                        if (lbin_test(cc, o, d, pr, lim, r2, t)) {
+                            tri = cc.id & 0x7fffffff;
+                            th = t;
+                            look = false;
+                            far = false;
+                        }
+                    }
+                }
+            }
+            if (phase == 1 && lr.cell == cell) {
+                far = false;
+                if (look && end < end0) capped = true;   /* still looking at the cap: undecided */
+            }
+        } while (phase == 1);
+        look = false;
+    }
+    int res = active && (!lr.ok || capped) ? -1 : 0;
+    if (tri >= 0) {
+        WalkCounts wc = {0u, 0u};
+        const RayRcp rr = make_ray_rcp(o, d, s.planes_ok != 0);
+        const Vec p = vadd(o, vscale(d, th));
+        const int slot = CRT_PROOF_TOPO && s.ktopo
+                             ? verify_topo<COUNT>(s.ktopo, s.nodes, s.slot_tri, tri, o, d, rr, p, wc,
+                                                  CRT_PROOF_TOPO2 ? s.ktopo2 : nullptr)
+                             : verify_kd<COUNT>(s.nodes, s.slot_tri, tri, o, d, rr, p, wc);
+        res = slot >= 0 ? 1 : -1;
+        if (COUNT) {
+            c.nodes += wc.nodes;
+            c.tris += wc.tris;
+        }
+    }
+    if (COUNT && active && res >= 0) ++c.traversals;
+    return res;
+}
+
 /* FAST (walk 12, picked by the host): every camera ray of the frame is in the
  * hoisted-division window (camera_rays_fast), so the out-of-line exact box
  * path is not compiled in — 77 instead of 82 VGPRs, 6 waves/SIMD. */

@@ -158,6 +158,8 @@ typedef struct crt_scene_info {
     int32_t bvh_on_device;     /* 1: the BVH was built on the device (crt_lbvh.hip, > 2^18 triangles; its
                                 * time is in bvh_ms) */
     int32_t bvh_depth;         /* ... its deepest node (root 0), 0 for the host build */
+    int64_t light_bin_records; /* light bins' candidate records (built at the first shadow-ray frame; 0: none) */
+    double  light_bins_ms;     /* wall time of that build and upload */
 } crt_scene_info;
 
 typedef struct crt_render_stats {

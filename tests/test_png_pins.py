@@ -117,7 +117,7 @@ def test_gpu_shadow_rays_match_oracle(oracle, name, w, h, over):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("opts", [{}, {"bins": 0}, {"traversal": 8}, {"bins_reuse": 0}])
+@pytest.mark.parametrize("opts", [{}, {"bins": 0}, {"traversal": 8}, {"bins_reuse": 0}, {"light_bins": 1}])
 def test_gpu_shadow_walks_agree(oracle, opts):
     """Shadow rays through every camera walk: camera bins (the default), the
     BVH walk (bins off), the kd packet walk; each frame's shadow rays go
@@ -136,6 +136,38 @@ def test_gpu_shadow_walks_agree(oracle, opts):
         for f in range(2):
             got = bits(gpu.render(st))
             assert int((got != want).sum()) == 0, f"pose {k} frame {f} {opts}"
+
+
+@pytest.mark.gpu
+def test_gpu_light_bins(oracle):
+    """Shadow rays over the light bins (crt_light_bins.cpp, built at the first
+    shadow-ray frame, kept across camera moves): equal to the oracle with the
+    bins on and off, and with a larger shadow bias than the bins were built
+    for (its rays pass the light farther than e_max: the BVH decides them)."""
+    from crt_amd import native as N
+    from crt_amd.camera import orbit_poses
+    name = "14-01-acceleration-tree__scene1"
+    gpu = N.HipScene(scene_npz(name).set_resolution(480, 270), shadows=1)
+    st = N.RendererSettings.default()
+    for k, (loc, rot) in enumerate(orbit_poses(scene_npz(name).a, 3, yaw_amp=30.0)):
+        sc = scene_npz(name).set_resolution(480, 270).set_camera(location=loc, rotation=rot)
+        want = bits(oracle.OracleScene(sc).set_shadows(True).render(st))
+        gpu.set_camera(location=loc, rotation=rot)
+        for lb in (1, 0, 1):
+            gpu.set_option("light_bins", lb)
+            assert np.array_equal(bits(gpu.render(st)), want), f"pose {k} light_bins {lb}"
+    info = gpu.info()
+    assert info["light_bin_records"] > 0 and info["light_bins_ms"] > 0
+    big = N.RendererSettings.default(shadow_bias=0.08)
+    want = bits(oracle.OracleScene(scene_npz(name).set_resolution(480, 270)).set_shadows(True).render(big))
+    gpu.set_camera(location=scene_npz(name).a["cam_loc"], rotation=scene_npz(name).a["cam_rot"])
+    assert np.array_equal(bits(gpu.render(big)), want)
+    # a scene whose lights sit among its triangles (near lists), GI off
+    name = "11-01-refractive__scene8"
+    sc = scene_npz(name).set_resolution(200, 112)
+    st1 = N.RendererSettings.default(max_ray_depth=1)
+    g2 = N.HipScene(sc, shadows=1, light_bins=1)
+    assert np.array_equal(bits(g2.render(st1)), bits(oracle.OracleScene(sc).set_shadows(True).render(st1)))
 
 
 @pytest.mark.gpu

@@ -131,6 +131,89 @@ int bvh_sim_trace(const crt_scene_desc *desc, const float *rays, int64_t n, int3
     return CRT_OK;
 }
 
+/* Shadow rays over the light bins (crt_light_bins.cpp, crt_bvh.h
+ * occluded_lbins) next to the reference's closest hit: rays[8 i ..] =
+ * {o, d, r2, light}; ref[i] = 1 when the reference's closest hit is within
+ * the light (fl(t * t) <= r2), lb[i] = the bins' answer (1 / 0 / -1
+ * undecided).  info[0..3] = records, lights on, near records of light 0,
+ * candidate tests. */
+int lbins_sim_check(const crt_scene_desc *desc, const float *rays, int64_t n, double e_max, int N, int8_t *ref,
+                    int8_t *lb, int64_t *info) {
+    HostScene hs;
+    int rc = prepare_scene(desc, hs);
+    if (rc != CRT_OK) return rc;
+    if (hs.bnode_count == 0 && ((rc = build_bvh(hs)) != CRT_OK || (rc = build_proof_tables(hs)) != CRT_OK))
+        return rc;
+    std::vector<CamCand> tpl;
+    bin_templates(hs, tpl);
+    LightBinsHost L;
+    build_light_bins(tpl.data(), (int)tpl.size(), hs.lights.data(), (int)hs.lights.size(), e_max, N, L);
+    info[0] = (int64_t)L.recs.size();
+    info[1] = 0;
+    for (const DLightBin &p : L.par) info[1] += p.on;
+    info[2] = L.par.empty() ? 0 : L.off[1] - L.off[0];
+    WalkCounts c = {0u, 0u};
+    uint64_t rn = 0, rt = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const float *r = rays + 8 * i;
+        const Vec o = vec(r[0], r[1], r[2]), d = vec(r[3], r[4], r[5]);
+        const float r2 = r[6];
+        const int l = (int)r[7];
+        float t = 0.f;
+        const int rs = walk_reference(hs, o, d, t, rn, rt);
+        ref[i] = (int8_t)(rs >= 0 && !(t * t > r2));
+        lb[i] = L.par.empty() ? (int8_t)-1
+                              : (int8_t)occluded_lbins<true>(L.recs.data(), L.off.data(), L.par[(size_t)l], L.n,
+                                                             hs.prune_origin_max, hs.nodes.data(), hs.slot_tri.data(),
+                                                             hs.ktopo.empty() ? nullptr : hs.ktopo.data(),
+                                                             hs.ktopo2.empty() ? nullptr : hs.ktopo2.data(), false, o, d,
+                                                             r2, c);
+    }
+    info[3] = (int64_t)c.tris;
+    return CRT_OK;
+}
+
+/* Per shadow ray of the light bins: its cell (-1 near only, -2 undecided) and
+ * the candidates its walk visits (near + cell), for wave-cost analysis
+ * (scripts/lbins_wave_cost.py). */
+int lbins_sim_steps(const crt_scene_desc *desc, const float *rays, int64_t n, double e_max, int N, int32_t *cell,
+                    int32_t *steps) {
+    HostScene hs;
+    int rc = prepare_scene(desc, hs);
+    if (rc != CRT_OK) return rc;
+    std::vector<CamCand> tpl;
+    bin_templates(hs, tpl);
+    LightBinsHost L;
+    if (!build_light_bins(tpl.data(), (int)tpl.size(), hs.lights.data(), (int)hs.lights.size(), e_max, N, L)) return -1;
+    for (int64_t i = 0; i < n; ++i) {
+        const float *r = rays + 8 * i;
+        const Vec o = vec(r[0], r[1], r[2]), d = vec(r[3], r[4], r[5]);
+        const float r2 = r[6];
+        const DLightBin &P = L.par[(size_t)r[7]];
+        const float lim = sqrtf(r2) * (1.0f + 0x1p-20f);
+        const LbinRay lr = lbin_setup(P, L.n, hs.prune_origin_max, o, d, lim);
+        cell[i] = lr.ok ? lr.cell : -2;
+        steps[i] = 0;
+        if (!lr.ok) continue;
+        const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
+        bool done = false;
+        for (int phase = 0; phase < 2 && !done; ++phase) {
+            if (phase == 1 && lr.cell < 0) break;
+            const int beg = L.off[(size_t)P.base + (phase ? 1 + lr.cell : 0)];
+            const int end = L.off[(size_t)P.base + (phase ? 2 + lr.cell : 1)];
+            const double cut = phase ? lr.cut_far : lr.cut_near;
+            for (int k = beg; k < end && !done; ++k) {
+                const CamCand &cc = L.recs[(size_t)k];
+                ++steps[i];
+                if ((double)cc.dmin * (double)cc.dmin > cut) break;
+                float t;
+                if (lbin_test(cc, o, d, pr, lim, r2, t)) done = true;
+            }
+        }
+    }
+    return CRT_OK;
+}
+
 /* Per-ray work of trace_bvh_exact (for wave-cost analysis, scripts/bvh_wave_cost.py):
  * out[4 i ..] = {BVH walk nodes, BVH walk triangles, proof/fallback nodes +
  * triangles, fallback taken}. */
