@@ -619,6 +619,8 @@ void crt_hip_scene_destroy(crt_hip_scene *sc) {
     for (hipEvent_t e : sc->copy_band_ev)
         if (e) (void)hipEventDestroy(e);
     if (sc->gi_frames) (void)hipFree(sc->gi_frames);
+    if (sc->sh_buf) (void)hipFree(sc->sh_buf);
+    if (sc->sh_done) (void)hipEventDestroy(sc->sh_done);
     wf_free(sc->wf);
     for (auto &kv : sc->unpack_plans) (void)hipFree(kv.second.first);
     for (auto &kv : sc->compact_unpack) (void)hipFree(kv.second.first);
@@ -1075,6 +1077,8 @@ static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
         sc->calib_walk = -1;
     } else if (k == "shadows") {
         sc->shadows = value != 0;
+    } else if (k == "shadow_defer") {
+        sc->shadow_defer = value != 0;
     } else if (k == "light_bins") {
         sc->light_bins = value != 0;
         if (sc->lbins_tried) sc->ds.lbin_n = sc->light_bins ? sc->lbins_n : 0;

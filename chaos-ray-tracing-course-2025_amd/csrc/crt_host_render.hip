@@ -466,6 +466,55 @@ int ensure_light_bins(crt_hip_scene *sc, const crt_renderer_settings *st) {
     return CRT_OK;
 }
 
+/* Deferred shadow rays of a frame without recursion (option "shadow_defer"):
+ * the render kernel writes a group of records per diffuse hit (crt_shade.h
+ * shade_hit_shadowed), k_shadow_vis traces one ray a lane over the whole
+ * chip, k_shadow_compose writes the diffuse pixels.  Inline, a wave traced its
+ * tile's rays light after light and the frame ended with its slowest waves
+ * (C2: ~90 % of the SIMD slots idle).  The buffers hold a group per pixel;
+ * frames on another stream wait for the previous deferred frame's compose. */
+int shadow_defer_begin(crt_hip_scene *sc, DSettings &ds, hipStream_t stream) {
+    const int nl = sc->ds.light_count;
+    const int64_t cap = ((int64_t)sc->info.width * sc->info.height + 63) & ~int64_t(63);   /* whole chunks of 64 groups */
+    const int64_t bytes = cap * nl * (int64_t)(sizeof(ShRay) + sizeof(ShCon));
+    if (nl <= 0 || cap <= 0 || cap > INT32_MAX || bytes > (int64_t(4) << 30)) return CRT_OK;   /* inline */
+    if (!sc->sh_count) {
+        HIP_TRY(hipMalloc(&sc->sh_count, 256));
+        HIP_TRY(hipEventCreateWithFlags(&sc->sh_done, hipEventDisableTiming));
+    }
+    if (bytes > sc->sh_bytes) {
+        HIP_TRY(hipDeviceSynchronize());
+        if (sc->sh_buf) (void)hipFree(sc->sh_buf);
+        sc->sh_buf = nullptr;
+        sc->sh_bytes = 0;
+        HIP_TRY(hipMalloc(&sc->sh_buf, (size_t)bytes));
+        sc->sh_bytes = bytes;
+        sc->sh_stream = nullptr;
+    }
+    if (sc->sh_stream && sc->sh_stream != stream) HIP_TRY(hipStreamWaitEvent(stream, sc->sh_done, 0));
+    HIP_TRY(hipMemsetAsync(sc->sh_count, 0, sizeof(int32_t), stream));
+    ds.sh_rays = static_cast<ShRay *>(sc->sh_buf);
+    ds.sh_con = reinterpret_cast<ShCon *>(static_cast<char *>(sc->sh_buf) + cap * nl * (int64_t)sizeof(ShRay));
+    ds.sh_count = sc->sh_count;
+    ds.sh_cap = (int32_t)cap;
+    return CRT_OK;
+}
+
+int shadow_defer_end(crt_hip_scene *sc, const DeviceScene *d_scene, const DSettings &ds, float *d_out,
+                     hipStream_t stream) {
+    if (!ds.sh_rays) return CRT_OK;
+    hipLaunchKernelGGL(k_shadow_vis, dim3(2048), dim3(256), 0, stream, d_scene, ds.sh_rays, ds.sh_con, ds.sh_count,
+                       ds.sh_cap);
+    HIP_TRY(hipGetLastError());
+    const unsigned cb = (unsigned)std::min<int64_t>(4096, ((int64_t)ds.sh_cap + 255) / 256);
+    hipLaunchKernelGGL(k_shadow_compose, dim3(cb), dim3(256), 0, stream, d_scene, ds, ds.sh_rays, ds.sh_con,
+                       ds.sh_count, ds.sh_cap, d_out);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(sc->sh_done, stream));
+    sc->sh_stream = stream;
+    return CRT_OK;
+}
+
 /* Device copy of sc->ds for the render kernels.  When the host record
  * changed (a new camera, the first GI frame's tables) the next slot of a ring
  * of kRecRing records takes it, written on `stream` by a one-thread kernel
@@ -670,6 +719,10 @@ DSettings to_dsettings(const crt_renderer_settings *st) {
     d.reflection_bias = st->reflection_bias;
     d.diffuse_reflection_bias = st->diffuse_reflection_bias;
     d.refraction_bias = st->refraction_bias;
+    d.sh_rays = nullptr;   /* shadow rays inline unless a frame defers them (shadow_defer_begin) */
+    d.sh_con = nullptr;
+    d.sh_count = nullptr;
+    d.sh_cap = 0;
     return d;
 }
 
@@ -1170,7 +1223,8 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         const int rc = sync_device_record(sc, &d_scene, stream);
         if (rc != CRT_OK) return rc;
     }
-    const DSettings ds = to_dsettings(st);
+    DSettings ds = to_dsettings(st);
+    const bool sh_defer = sc->shadows && sc->shadow_defer && !full && !count && !stamps;
     /* Walks: camera rays take the packet walk (traversal 7, or 8 pruned).
      * Secondary rays scatter and take the cooperative walk: pruned (10) for
      * reflect/refract levels (C3), reference order (4) for GI fan-out — the
@@ -1193,6 +1247,10 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
         if (!full) {   /* no recursion: the frame's camera walk, packet walks for shadow rays (shade_hit_shadowed) */
             int tr = camera_walk(sc, sc->traversal);
             if (tr == 13 && !plan.has_small) tr = 12;
+            if (sh_defer) {
+                const int rc = shadow_defer_begin(sc, ds, stream);
+                if (rc != CRT_OK) return rc;
+            }
 #define CRT_LAUNCH_SH(TR, COUNT)                                                                            \
     hipLaunchKernelGGL((k_render_tiles<false, 0, TR, TR, COUNT, true>), dim3(nb), dim3(256), 0, stream, d_scene, ds, \
                        plan.d_tiles, plan.ntiles, d_out, cn, nullptr, BinsPlan{})
@@ -1207,7 +1265,7 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
             }
 #undef CRT_LAUNCH_SH
             HIP_TRY(hipGetLastError());
-            return CRT_OK;
+            return shadow_defer_end(sc, d_scene, ds, d_out, stream);
         }
 #define CRT_LAUNCH_S(MAXF, COUNT)                                                                           \
     hipLaunchKernelGGL((k_render_tiles<true, MAXF, 10, 10, COUNT, true>), dim3(nb), dim3(256), 0, stream,      \
@@ -1261,8 +1319,15 @@ int launch_render(crt_hip_scene *sc, const crt_renderer_settings *st, const Shar
 #define CRT_LAUNCH_B(COUNT, SH)                                                                             \
     hipLaunchKernelGGL((k_render_tiles<false, 0, 15, 15, COUNT, SH>), dim3(bb), dim3(256), 0, stream, d_scene, ds, \
                        plan.d_tiles, plan.waves, d_out, cnt, stamps, bp)
-        if (sc->shadows) {   /* the course's earlier renderer: shadow rays per lane (crt_shade.h shadow_occluded) */
+        if (sc->shadows) {   /* the course's earlier renderer: shadow rays (crt_shade.h shade_hit_shadowed) */
+            if (sh_defer) {
+                const int rc = shadow_defer_begin(sc, ds, stream);
+                if (rc != CRT_OK) return rc;
+            }
             if (count) CRT_LAUNCH_B(true, true); else CRT_LAUNCH_B(false, true);
+            HIP_TRY(hipGetLastError());
+            const int rc = shadow_defer_end(sc, d_scene, ds, d_out, stream);
+            if (rc != CRT_OK) return rc;
         } else {
             if (count) CRT_LAUNCH_B(true, false); else CRT_LAUNCH_B(false, false);
         }

@@ -136,6 +136,13 @@ __global__ void k_row_spans(const float *__restrict__ img, int width, Rgb<uint32
 __global__ void k_rows_to_host(const float *__restrict__ img, int width, int height, int y0,
                                const int2 *__restrict__ spans, float *__restrict__ host);
 __global__ void k_warm_render();
+/* deferred shadow rays (crt_layout.h ShRay / ShCon): visibility of every
+ * record, then each group's pixel (crt_render.hip) */
+__global__ void k_shadow_vis(const DeviceScene *__restrict__ scene, const ShRay *__restrict__ rays,
+                             ShCon *__restrict__ con, const int32_t *__restrict__ count, int cap);
+__global__ void k_shadow_compose(const DeviceScene *__restrict__ scene, DSettings st, const ShRay *__restrict__ rays,
+                                 const ShCon *__restrict__ con, const int32_t *__restrict__ count, int cap,
+                                 float *__restrict__ out);
 __global__ void k_warm_gi();
 __global__ void k_warm_wf();
 __global__ void k_warm_side();

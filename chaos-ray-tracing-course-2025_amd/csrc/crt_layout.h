@@ -251,6 +251,27 @@ struct DeviceScene {
 };
 
 /* Renderer settings as the kernels see them (crt_renderer.h:18-25). */
+/* Deferred shadow rays of a frame without recursion (crt_shade.h
+ * shade_hit_shadowed, k_shadow_vis, k_shadow_compose): per diffuse hit g a
+ * group of light_count records, light-major in chunks of 64 groups
+ * (sh_index): a wave of k_shadow_vis takes 64 neighbouring pixels' rays
+ * towards one light, whose walks read the same lists. */
+#if defined(__HIPCC__)
+__host__ __device__ inline
+#else
+inline
+#endif
+int64_t sh_index(int64_t g, int l, int nl) { return ((g >> 6) * nl + l) * 64 + (g & 63); }
+struct alignas(16) ShRay {
+    float ox, oy, oz, r2;   /* origin p + n bias, |light - p|^2 */
+    float dx, dy, dz;       /* normalised direction to the light */
+    int32_t pix;            /* the pixel's index in the output image (3 floats a pixel); -1: no ray */
+};
+struct alignas(16) ShCon {
+    float x, y, z;          /* the light's term (crt_renderer.cpp:90-95), added when the light is visible */
+    uint32_t vis;           /* written by k_shadow_vis */
+};
+
 struct DSettings {
     uint32_t max_ray_depth;
     uint32_t diffuse_reflection_ray_count;
@@ -258,6 +279,11 @@ struct DSettings {
     float reflection_bias;
     float diffuse_reflection_bias;
     float refraction_bias;
+    /* deferred shadow rays (null: traced inline) */
+    ShRay *sh_rays;
+    ShCon *sh_con;
+    int32_t *sh_count;      /* groups taken this frame */
+    int32_t sh_cap;         /* groups the buffers hold */
 };
 
 /* A bucket of the reference grid (crt_renderer.cpp:160-174). */

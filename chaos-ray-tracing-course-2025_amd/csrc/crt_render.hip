@@ -158,7 +158,9 @@ __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSetting
             const int slot = R == 4 ? trace_window<COUNT, 4>(s, r, sl, act, o, d, t, cw)
                                     : trace_window<COUNT, 16>(s, r, sl, act, o, d, t, cw);
             Vec c;
-            if constexpr (SHADOW) c = shade_hit_shadowed<COUNT>(s, st, act && sl == 0, o, d, slot, t, cw);   /* wave-wide */
+            if constexpr (SHADOW)   /* wave-wide */
+                c = shade_hit_shadowed<COUNT>(s, st, act && sl == 0, o, d, slot, t, cw,
+                                              tl.out_base + (int64_t)py * tl.out_stride + px);
             if (act && sl == 0) {
                 if constexpr (!SHADOW) c = shade_primary(s, st, o, d, slot, t);   /* (SHADOW: wave-wide above) */
                 float *pxo = out + 3 * (tl.out_base + (int64_t)py * tl.out_stride + px);
@@ -211,7 +213,9 @@ __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSetting
                 CamCand *stw = stage + (threadIdx.x >> 6) * kBinChunk;
                 const int slot = trace_bins_lanes<COUNT, 4>(s, stw, beg, end, bit, sl, act, o, d, t, cw);
                 Vec c;
-                if constexpr (SHADOW) c = shade_hit_shadowed<COUNT>(s, st, act && sl == 0, o, d, slot, t, cw);   /* wave-wide */
+                if constexpr (SHADOW)   /* wave-wide */
+                    c = shade_hit_shadowed<COUNT>(s, st, act && sl == 0, o, d, slot, t, cw,
+                                                  tl.out_base + (int64_t)ly * tl.out_stride + lx);
                 if (act && sl == 0) {
                     if constexpr (!SHADOW) c = shade_primary(s, st, o, d, slot, t);
                     float *pxo = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
@@ -239,7 +243,8 @@ __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSetting
             const int slot = trace_bins_wave<COUNT>(s, stage + (threadIdx.x >> 6) * kBinChunk, beg, end, bit, act, o,
                                                     d, t, cw, stamps ? &stamps[2 * wave] : nullptr);
             Vec c;
-            if constexpr (SHADOW) c = shade_hit_shadowed<COUNT>(s, st, act, o, d, slot, t, cw);   /* wave-wide */
+            if constexpr (SHADOW)   /* wave-wide */
+                c = shade_hit_shadowed<COUNT>(s, st, act, o, d, slot, t, cw, tl.out_base + (int64_t)ly * tl.out_stride + lx);
             if (act) {
                 if constexpr (!SHADOW) c = shade_primary(s, st, o, d, slot, t);
                 float *pxo = out + 3 * (tl.out_base + (int64_t)ly * tl.out_stride + lx);
@@ -276,7 +281,9 @@ __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSetting
             const int slot = K == 16 ? trace_bvh_window<COUNT, 16>(s, sl, act, o, d, t, cw)
                                      : trace_bvh_window<COUNT, 4>(s, sl, act, o, d, t, cw);
             Vec c;
-            if constexpr (SHADOW) c = shade_hit_shadowed<COUNT>(s, st, act && sl == 0, o, d, slot, t, cw);   /* wave-wide */
+            if constexpr (SHADOW)   /* wave-wide */
+                c = shade_hit_shadowed<COUNT>(s, st, act && sl == 0, o, d, slot, t, cw,
+                                              tl.out_base + (int64_t)py * tl.out_stride + px);
             if (act && sl == 0) {
                 if constexpr (!SHADOW) c = shade_primary(s, st, o, d, slot, t);
                 float *pxo = out + 3 * (tl.out_base + (int64_t)py * tl.out_stride + px);
@@ -308,7 +315,8 @@ __device__ __forceinline__ void render_tile(const DeviceScene &s, const DSetting
     Vec c;
     if constexpr (SHADOW && !FULL)
         c = shade_shadowed<(TRAV == 15 ? 14 : TRAV), COUNT>(s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0),
-                                                            cnt, &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px);
+                                                            cnt, &coop[kCoop ? (threadIdx.x >> 6) : 0], has_px,
+                                                            tl.out_base + (int64_t)ly * tl.out_stride + lx);
     else
         c = shade_pixel<FULL, MAXF, (TRAV == 15 ? 14 : TRAV), (SEC == 15 ? 14 : SEC), COUNT, SHADOW>(
             s, st, tl.x + (has_px ? lx : 0), tl.y + (has_px ? ly : 0), cnt, &coop[kCoop ? (threadIdx.x >> 6) : 0],
@@ -417,6 +425,73 @@ __global__ __launch_bounds__(256) void k_probe_tiles(const DeviceScene *__restri
 #define CRT_INST_PROBE(T) template __global__ CRT_PROBE_SIG(T)
 CRT_TILES_INSTANCES(CRT_INST_TILES)
 CRT_PROBE_INSTANCES(CRT_INST_PROBE)
+
+/* Deferred shadow rays, one record a lane (a group's lights side by side,
+ * groups of neighbouring pixels after one another): the light's bins per
+ * lane where the scene has them, the rays they leave undecided through the
+ * wave's BVH walk, a failed proof through the exact kd walk — the answer of
+ * shadow_occluded.  A persistent grid walks the records a wave at a time
+ * (the walks' ballots need whole waves). */
+__global__ __launch_bounds__(256) void k_shadow_vis(const DeviceScene *__restrict__ scene,
+                                                    const ShRay *__restrict__ rays, ShCon *__restrict__ con,
+                                                    const int32_t *__restrict__ count, int cap) {
+    const DeviceScene &s = *scene;
+    const int nl = s.light_count;
+    const int ng = min(*count, cap);
+    const int64_t n = (int64_t)((ng + 63) >> 6) * nl * 64;   /* whole chunks (sh_index) */
+    const int lane = (int)(threadIdx.x & 63);
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    LaneCounts cnt = {};
+    for (int64_t base = (int64_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; base < n; base += nw * 64) {
+        const int64_t i = base + lane;
+        const int64_t g = ((i >> 6) / nl) * 64 + (i & 63);   /* the record's group and light (sh_index) */
+        ShRay r;
+        r.pix = -1;
+        if (i < n && g < ng) r = rays[i];
+        const bool act = r.pix >= 0;
+        const int l = (int)((i >> 6) % nl);
+        const Vec o = vec(r.ox, r.oy, r.oz), d = vec(r.dx, r.dy, r.dz);
+        int res = 0;
+        if (act) {
+            res = -1;
+            if (s.lbin_n) {
+                WalkCounts wc = {0u, 0u};
+                res = occluded_lbins<false>(s.lbins, s.lbin_off, s.lbin_par[l], s.lbin_n, s.prune_origin_max, s.nodes,
+                                            s.slot_tri, s.ktopo, s.ktopo2, s.planes_ok != 0, o, d, r.r2, wc);
+            }
+        }
+        if (s.bnodes && __ballot(act && res < 0) != 0ull) {
+            const int rb = occluded_bvh_wave<false>(s, act && res < 0, o, d, r.r2, cnt);
+            if (act && res < 0) res = rb;
+        }
+        if (act && res < 0) res = shadow_occluded_kd<false>(s, o, d, r.r2, cnt) ? 1 : 0;
+        if (act) con[i].vis = res == 1 ? 0u : 1u;
+    }
+}
+
+/* Each group's pixel: its visible lights' terms summed in light order, over
+ * diffuse_reflection_ray_count + 1 (shade_hit_shadowed's operations). */
+__global__ __launch_bounds__(256) void k_shadow_compose(const DeviceScene *__restrict__ scene, DSettings st,
+                                                        const ShRay *__restrict__ rays, const ShCon *__restrict__ con,
+                                                        const int32_t *__restrict__ count, int cap,
+                                                        float *__restrict__ out) {
+    const int nl = scene->light_count;
+    const int n = min(*count, cap);
+    for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < n; g += gridDim.x * blockDim.x) {
+        const int32_t pix = rays[sh_index(g, 0, nl)].pix;
+        if (pix < 0) continue;
+        Vec acc = vec(0.f, 0.f, 0.f);
+        for (int l = 0; l < nl; ++l) {
+            const ShCon c = con[sh_index(g, l, nl)];
+            if (c.vis) acc = vadd(acc, vec(c.x, c.y, c.z));
+        }
+        const Vec col = vdiv(acc, (float)(st.diffuse_reflection_ray_count + 1));
+        float *po = out + 3 * (int64_t)pix;
+        po[0] = col.x;
+        po[1] = col.y;
+        po[2] = col.z;
+    }
+}
 
 /* empty kernel: its launch at scene creation loads this TU's code object
  * (warm_code_objects) */

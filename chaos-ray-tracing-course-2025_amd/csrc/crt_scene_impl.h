@@ -249,6 +249,14 @@ struct crt_hip_scene {
     int gi_machine = 1;                /* ... as per-lane state machines (k_render_gi; option "gi_machine") */
     int rec_machine = 0;               /* recursion without GI through the same state machine (option "rec_machine") */
     int gi_blocks = 1024;              /* blocks of the k_render_gi grid (resident blocks per CU x CUs) */
+    /* deferred shadow rays (option "shadow_defer", crt_host_render.hip
+     * launch_shadow_frame): records of the frame's groups, its counter */
+    int shadow_defer = 0;   /* (0: traced inline — deferred measured 0.50-0.60 against 0.44 ms, group-major records) */
+    void *sh_buf = nullptr;
+    int64_t sh_bytes = 0;
+    int32_t *sh_count = nullptr;
+    hipEvent_t sh_done = nullptr;      /* after the last deferred frame's compose */
+    hipStream_t sh_stream = nullptr;   /* ... on this stream */
     void *gi_frames = nullptr;         /* k_render_gi: frames below the LDS ones (grown on demand) */
     int64_t gi_frames_bytes = 0;
     int refill_waves = 5120;           /* waves of the refill grid: CUs x 4 SIMDs x CRT_GI_WAVES */

@@ -340,7 +340,7 @@ __device__ __forceinline__ bool shadow_occluded_packet(const DeviceScene &s, boo
  * instead of one per-lane walk per lane. */
 template <bool COUNT>
 __device__ Vec shade_hit_shadowed(const DeviceScene &s, const DSettings &st, bool has_px, Vec o, Vec d, int slot,
-                                  float t, LaneCounts &cnt) {
+                                  float t, LaneCounts &cnt, int64_t pix) {
     Vec col = vec(s.background[0], s.background[1], s.background[2]);
     bool diffuse = false;
     HitRec h;
@@ -356,6 +356,48 @@ __device__ Vec shade_hit_shadowed(const DeviceScene &s, const DSettings &st, boo
     }
     Vec acc = vec(0.f, 0.f, 0.f);
     const int nl = s.light_count;
+    if (!COUNT && st.sh_rays && nl > 0) {
+        /* deferred: each diffuse hit takes a group of nl records (its rays and
+         * its lights' terms); k_shadow_vis traces them, k_shadow_compose sums
+         * the visible terms in light order and writes the pixel — the same
+         * operations as below */
+        const uint64_t dm = __ballot(diffuse);
+        int g = 0;
+        if (dm != 0ull) {
+            const int lane = (int)(threadIdx.x & 63);
+            const int leader = __ffsll((long long)dm) - 1;
+            int b = 0;
+            if (lane == leader) b = atomicAdd(st.sh_count, __popcll(dm));
+            b = __shfl(b, leader);
+            g = b + __popcll(dm & ((1ull << lane) - 1ull));
+        }
+        if (__ballot(diffuse && g >= st.sh_cap) == 0ull) {
+            if (diffuse) {
+                for (int l = 0; l < nl; ++l) {
+                    const DLight Lt = s.lights[l];
+                    Vec ld = vsub(vec(Lt.px, Lt.py, Lt.pz), h.p);
+                    const float r2 = vlen_sq(ld);
+                    ld = vnormalize(ld);
+                    const float dn = vdot(ld, h.n);
+                    const float cos_law = (0.0f < dn) ? dn : 0.0f;
+                    const float area = 4 * kPi * r2;
+                    const Vec so = vadd(h.p, vscale(h.n, st.shadow_bias));
+                    const Vec term = vscale(vdiv(vscale(alb, Lt.intensity), area), cos_law);
+                    ShRay r;
+                    r.ox = so.x; r.oy = so.y; r.oz = so.z; r.r2 = r2;
+                    r.dx = ld.x; r.dy = ld.y; r.dz = ld.z;
+                    r.pix = (int32_t)pix;
+                    ShCon cn;
+                    cn.x = term.x; cn.y = term.y; cn.z = term.z; cn.vis = 0u;
+                    st.sh_rays[sh_index(g, l, nl)] = r;
+                    st.sh_con[sh_index(g, l, nl)] = cn;
+                }
+            }
+            return col;   /* (a diffuse pixel's colour: written by k_shadow_compose) */
+        }
+        if (diffuse && g < st.sh_cap)   /* past the buffers (not sized for this frame): traced inline below */
+            for (int l = 0; l < nl; ++l) st.sh_rays[sh_index(g, l, nl)].pix = -1;
+    }
     for (int l = 0; l < nl; ++l) {                                    /* :81-96 */
         const DLight Lt = s.lights[l];
         Vec ld = vsub(vec(Lt.px, Lt.py, Lt.pz), h.p);
@@ -406,12 +448,12 @@ __device__ Vec shade_hit_shadowed(const DeviceScene &s, const DSettings &st, boo
 
 template <int TRAV, bool COUNT>
 __device__ Vec shade_shadowed(const DeviceScene &s, const DSettings &st, int x, int y, LaneCounts &cnt, CoopLds *L,
-                              bool has_px) {
+                              bool has_px, int64_t pix) {
     Vec o, d;
     camera_ray(s.cam, x, y, o, d);
     float t;
     const int slot = trace<TRAV, COUNT>(s, L, has_px, o, d, t, cnt);
-    return shade_hit_shadowed<COUNT>(s, st, has_px, o, d, slot, t, cnt);
+    return shade_hit_shadowed<COUNT>(s, st, has_px, o, d, slot, t, cnt, pix);
 }
 
 template <bool FULL, int MAXF, int TRAV, int SEC, bool COUNT, bool SHADOW = false>
