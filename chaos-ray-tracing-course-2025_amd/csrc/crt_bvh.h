@@ -736,8 +736,7 @@ CRT_HD LbinRay lbin_setup(const DLightBin &P, int N, float prune_origin_max, Vec
 }
 
 /* a candidate: a hit the reference's test accepts within the light */
-CRT_HD bool lbin_test(const CamCand &cc, Vec o, Vec d, const PruneRay &pr, float lim, float r2, float &t) {
-    if (!cand_alive(cc, pr, lim)) return false;
+CRT_HD bool lbin_test(const LightCand &cc, Vec o, Vec d, float r2, float &t) {
     const uint8_t cull = (uint8_t)((uint32_t)cc.id >> 31);
     return tri_hit(o, d, cc.g, &cull, t) && !(t * t > r2);
 }
@@ -747,25 +746,24 @@ CRT_HD bool lbin_test(const CamCand &cc, Vec o, Vec d, const PruneRay &pr, float
 #endif
 
 template <bool COUNT>
-CRT_HD int lbin_first_hit(const CamCand *lb, const int32_t *off, const DLightBin &P, int N, float prune_origin_max,
+CRT_HD int lbin_first_hit(const LightCand *lb, const int32_t *off, const DLightBin &P, int N, float prune_origin_max,
                           Vec o, Vec d, float r2, int &tri, float &t_hit, WalkCounts &c) {
     tri = -1;
     t_hit = 0.0f;
     const float lim = sqrtf(r2) * (1.0f + 0x1p-20f);
     const LbinRay lr = lbin_setup(P, N, prune_origin_max, o, d, lim);
     if (!lr.ok) return -1;
-    const PruneRay pr = make_prune_ray(o, d, prune_origin_max);
     for (int phase = 0; phase < 2; ++phase) {
         if (phase == 1 && lr.cell < 0) break;
         const int beg = off[P.base + (phase ? 1 + lr.cell : 0)], end = off[P.base + (phase ? 2 + lr.cell : 1)];
         const double cut = phase ? lr.cut_far : lr.cut_near;
         for (int k = beg; k < end; ++k) {
             if (phase == 1 && k - beg >= CRT_LBINS_CAP) return -1;   /* a long walk: the BVH's */
-            const CamCand cc = CRT_LDG(lb, k);
+            const LightCand cc = CRT_LDG(lb, k);
             if ((double)cc.dmin * (double)cc.dmin > cut) break;
             if (COUNT) ++c.tris;
             float t;
-            if (lbin_test(cc, o, d, pr, lim, r2, t)) {
+            if (lbin_test(cc, o, d, r2, t)) {
                 tri = cc.id & 0x7fffffff;
                 t_hit = t;
                 return 1;
@@ -778,7 +776,7 @@ CRT_HD int lbin_first_hit(const CamCand *lb, const int32_t *off, const DLightBin
 /* lbin_first_hit with its hit proved on the reference's tree: 1 occluded,
  * 0 lit, -1 undecided (the BVH or the exact walk decides). */
 template <bool COUNT>
-CRT_HD int occluded_lbins(const CamCand *lb, const int32_t *off, const DLightBin &P, int N, float prune_origin_max,
+CRT_HD int occluded_lbins(const LightCand *lb, const int32_t *off, const DLightBin &P, int N, float prune_origin_max,
                           const DNode *nodes, const int32_t *slot_tri, const KTopo *ktopo, const KTopo2 *ktopo2,
                           bool planes_ok, Vec o, Vec d, float r2, WalkCounts &c) {
     int tri;

@@ -158,7 +158,7 @@ struct LightBinsHost {
     int n = 0;
     std::vector<DLightBin> par;
     std::vector<int32_t> off;
-    std::vector<CamCand> recs;
+    std::vector<LightCand> recs;
 };
 bool build_light_bins(const CamCand *tpl, int nt, const DLight *lights, int nl, double e_max, int N,
                       LightBinsHost &out);

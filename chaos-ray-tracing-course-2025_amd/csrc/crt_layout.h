@@ -132,13 +132,23 @@ static_assert(sizeof(CamCand) == 96, "CamCand must be 96 B");
 
 /* Light bins of one light (crt_light_bins.cpp build_light_bins, crt_bvh.h
  * lbin_first_hit): a cube map of N x N cells a face around the light, each
- * cell listing (CamCand records, mask / rest unused) every triangle a shadow
+ * cell listing (LightCand records) every triangle a shadow
  * ray whose origin lies in that cell's direction can hit on its way to the
  * light, sorted by dmin = the distance from the light to the hull, rounded
  * down; triangles whose hull comes within R0 of the light (and unbounded
  * hulls) are in a near list every ray tests.  Offsets
  * off[base] .. off[base + 6 N^2 + 1]: the near list, then the cells in order
  * (face = 2 axis + (w_axis < 0), row v, column u). */
+/* A light-bin candidate (one 64-B line): dmin = the distance from the light
+ * to the triangle's hull, rounded down; the triangle as the BVH holds it. */
+struct alignas(16) LightCand {
+    float dmin;
+    int32_t id;      /* triangle id | back_face_culling << 31 */
+    int32_t pad0, pad1;
+    DTriGeo g;
+};
+static_assert(sizeof(LightCand) == 64, "LightCand must be 64 B");
+
 struct DLightBin {
     double lx, ly, lz;      /* the light's position */
     double r0_sq;           /* R0^2 */
@@ -233,7 +243,7 @@ struct DeviceScene {
      * lbin_n 0 when not built */
     const DLightBin *lbin_par;
     const int32_t *lbin_off;
-    const CamCand *lbins;
+    const LightCand *lbins;
     int32_t lbin_n;
     /* GI angle tables: (cosf, sinf) pairs of pi*u and of 2*pi*u for the 2^23 values of u */
     const float *gi_pi;

@@ -92,7 +92,7 @@ void hull_cells(const double lo[3], const double hi[3], const double L[3], doubl
 struct OneLight {
     DLightBin par{};
     std::vector<int32_t> off;     /* 6 N^2 + 2, relative to recs */
-    std::vector<CamCand> recs;
+    std::vector<LightCand> recs;
 };
 
 void build_one(const CamCand *tpl, int nt, const DLight &lt, double e_max, int N, OneLight &out) {
@@ -161,9 +161,10 @@ void build_one(const CamCand *tpl, int nt, const DLight &lt, double e_max, int N
     out.recs.resize((size_t)(near_n + total));
     std::vector<int32_t> fill(out.off.begin(), out.off.end() - 1);
     auto rec = [&](int t) {
-        CamCand r = tpl[t];
+        LightCand r{};
         r.dmin = dist[(size_t)t] < 0.0 ? 0.0f : round_down(dist[(size_t)t]);
-        r.mask = r.rest = 0ull;
+        r.id = tpl[t].id;
+        r.g = tpl[t].g;
         return r;
     };
     for (int t = 0; t < nt; ++t) {
@@ -174,7 +175,7 @@ void build_one(const CamCand *tpl, int nt, const DLight &lt, double e_max, int N
         const CamCand &c = tpl[t];
         const double lo[3] = {c.lo_x, c.lo_y, c.lo_z}, hi[3] = {c.hi_x, c.hi_y, c.hi_z};
         hull_cells(lo, hi, L, dist[(size_t)t], margin_of(dist[(size_t)t]), N, rects);
-        const CamCand r = rec(t);
+        const LightCand r = rec(t);
         for (const Rect &q : rects)
             for (int v = q.v0; v <= q.v1; ++v)
                 for (int u = q.u0; u <= q.u1; ++u) out.recs[(size_t)fill[(size_t)1 + (q.face * N + v) * N + u]++] = r;
@@ -182,7 +183,7 @@ void build_one(const CamCand *tpl, int nt, const DLight &lt, double e_max, int N
     /* each list by (dmin, triangle id) */
     for (size_t c = 0; c + 1 < out.off.size(); ++c)
         std::sort(out.recs.begin() + out.off[c], out.recs.begin() + out.off[c + 1],
-                  [](const CamCand &a, const CamCand &b) {
+                  [](const LightCand &a, const LightCand &b) {
                       return a.dmin < b.dmin || (a.dmin == b.dmin && (a.id & 0x7fffffff) < (b.id & 0x7fffffff));
                   });
     out.par.r0_sq = R0 * R0;

@@ -713,7 +713,6 @@ __device__ int occluded_lbins_wave(const DeviceScene &s, int light, bool active,
     lr.cell = -1;
     lr.cut_near = lr.cut_far = 0.0;
     if (active) lr = lbin_setup(P, s.lbin_n, s.prune_origin_max, o, d, lim);
-    const PruneRay pr = make_prune_ray(o, d, s.prune_origin_max);
     int tri = -1;
     float th = 0.0f;
     bool look = lr.ok;      /* near list */
@@ -738,12 +737,12 @@ __device__ int occluded_lbins_wave(const DeviceScene &s, int light, bool active,
                 end = load_scalar(s.lbin_off, base + 2 + cell);
                 cut = lr.cut_far;
             }
-            CamCand nx = load_scalar(s.lbins, beg);   /* (a zero record past the last list) */
+            LightCand nx = load_scalar(s.lbins, beg);   /* (a zero record past the last list) */
             const int end0 = end;
             if (phase == 1 && end - beg > CRT_LBINS_CAP) end = beg + CRT_LBINS_CAP;
             for (int k = beg; k < end; ++k) {
                 if (__ballot(look) == 0ull) break;
-                const CamCand cc = nx;
+                const LightCand cc = nx;
                 nx = load_scalar(s.lbins, k + 1);
                 if (COUNT) ++c.wave_tris;
                 if (look) {
@@ -752,7 +751,7 @@ __device__ int occluded_lbins_wave(const DeviceScene &s, int light, bool active,
                         look = false;
                     } else {
                         if (COUNT) ++c.tris;
-                        if (lbin_test(cc, o, d, pr, lim, r2, t)) {
+                        if (lbin_test(cc, o, d, r2, t)) {
                             tri = cc.id & 0x7fffffff;
                             th = t;
                             look = false;

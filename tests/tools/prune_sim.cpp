@@ -195,7 +195,6 @@ int lbins_sim_steps(const crt_scene_desc *desc, const float *rays, int64_t n, do
         cell[i] = lr.ok ? lr.cell : -2;
         steps[i] = 0;
         if (!lr.ok) continue;
-        const PruneRay pr = make_prune_ray(o, d, hs.prune_origin_max);
         bool done = false;
         for (int phase = 0; phase < 2 && !done; ++phase) {
             if (phase == 1 && lr.cell < 0) break;
@@ -203,11 +202,11 @@ int lbins_sim_steps(const crt_scene_desc *desc, const float *rays, int64_t n, do
             const int end = L.off[(size_t)P.base + (phase ? 2 + lr.cell : 1)];
             const double cut = phase ? lr.cut_far : lr.cut_near;
             for (int k = beg; k < end && !done; ++k) {
-                const CamCand &cc = L.recs[(size_t)k];
+                const LightCand &cc = L.recs[(size_t)k];
                 ++steps[i];
                 if ((double)cc.dmin * (double)cc.dmin > cut) break;
                 float t;
-                if (lbin_test(cc, o, d, pr, lim, r2, t)) done = true;
+                if (lbin_test(cc, o, d, r2, t)) done = true;
             }
         }
     }
