@@ -849,8 +849,10 @@ def main():
                      "vs_reference_published_s": round(0.066962 / (s_ms * 1e-3), 1),
                      "note": "the course's earlier renderer (option shadows; the reference's published KD-tree time, "
                              "0.066962 s at src/README.md:11, was taken at tag 14-01, which traced shadow rays): camera "
-                             "bins for the camera rays, one shadow ray per (diffuse hit, light) through the BVH to "
-                             "its first hit within the light (crt_bvh.h occluded_bvh); not HEAD parity"}
+                             "bins for the camera rays; one shadow ray per (diffuse hit, light), deferred: written by "
+                             "the render kernel, traced one per lane by k_shadow_vis over the light's bins to its "
+                             "first hit within the light (crt_bvh.h lbin_first_hit; the BVH where they do not "
+                             "decide), the visible terms summed by k_shadow_compose; not HEAD parity"}
         del gs
         if s_check == "DIFFERS":
             print("check: shadow-ray frame DIFFERS from the blocking render", flush=True)

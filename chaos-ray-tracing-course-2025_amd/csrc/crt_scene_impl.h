@@ -251,7 +251,7 @@ struct crt_hip_scene {
     int gi_blocks = 1024;              /* blocks of the k_render_gi grid (resident blocks per CU x CUs) */
     /* deferred shadow rays (option "shadow_defer", crt_host_render.hip
      * launch_shadow_frame): records of the frame's groups, its counter */
-    int shadow_defer = 0;   /* (0: traced inline — deferred measured 0.50-0.60 against 0.44 ms, group-major records) */
+    int shadow_defer = 1;   /* (C2 with shadows: 0.396 ms deferred with light bins, 0.416 inline BVH walks, 0.427 inline light bins) */
     void *sh_buf = nullptr;
     int64_t sh_bytes = 0;
     int32_t *sh_count = nullptr;
@@ -263,7 +263,7 @@ struct crt_hip_scene {
     bool grid_empty = false;
     int traversal = 8;             /* 7 reference order | 8 pruned (default), see trace<> (env CRT_TRAVERSAL) */
     int shadows = 0;               /* option "shadows": trace the shadow rays (k_render_tiles<..., SHADOW>) */
-    int light_bins = 0;            /* option "light_bins": shadow rays over the light bins (ensure_light_bins; off: the BVH wave walk measured as fast) */
+    int light_bins = 1;            /* option "light_bins": shadow rays over the light bins (ensure_light_bins) */
     bool lbins_tried = false;      /* built (or found not to apply) at the first shadow-ray frame */
     int lbins_n = 0;               /* their cells a cube-face side (0: none) */
     int64_t lbins_records = 0;

@@ -13,7 +13,7 @@ for c in ${CFGS:-c2 c3 c4 c5}; do
   case $c in
     c2) CFG=c2 KERNEL=k_render_tiles SIZE="1920 1080" LAST=2 FRAME_END= \
           CMD="$RL --scene 14-01-acceleration-tree__scene1 --frames 2 --opt calibrate=1" bash scripts/gpu_pmc.sh || exit 1 ;;
-    c2s) CFG=c2s KERNEL=k_render_tiles SIZE="1920 1080" LAST=2 FRAME_END= \
+    c2s) CFG=c2s KERNEL="k_render_tiles|k_shadow_vis|k_shadow_compose" SIZE="1920 1080" LAST=2 FRAME_END=k_shadow_compose \
           CMD="$RL --scene 14-01-acceleration-tree__scene1 --frames 3 --opt calibrate=1 --set shadows=1" bash scripts/gpu_pmc.sh || exit 1 ;;
     c3) CFG=c3 KERNEL=k_wf_ SIZE="1920 1080" LAST=2 FRAME_END=k_wf_pixels \
           CMD="$RL --scene 11-01-refractive__scene8 --depth 8 --frames 3 --opt calibrate=1" bash scripts/gpu_pmc.sh || exit 1 ;;

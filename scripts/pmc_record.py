@@ -48,7 +48,7 @@ def averages(root: Path, kernel: str, last: int = 0, frame_end: str = "") -> tup
         per = collections.defaultdict(lambda: collections.defaultdict(float))
         names = {}
         for r in csv.DictReader(open(f)):
-            if kernel not in r["Kernel_Name"]:
+            if not any(k in r["Kernel_Name"] for k in kernel.split("|")):   # "a|b": any of them
                 continue
             per[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
             names[int(r["Dispatch_Id"])] = r["Kernel_Name"]

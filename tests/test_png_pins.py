@@ -117,8 +117,8 @@ def test_gpu_shadow_rays_match_oracle(oracle, name, w, h, over):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("opts", [{}, {"bins": 0}, {"traversal": 8}, {"bins_reuse": 0}, {"light_bins": 1}, {"shadow_defer": 1},
-                                  {"shadow_defer": 1, "light_bins": 1}, {"shadow_defer": 1, "bins": 0}])
+@pytest.mark.parametrize("opts", [{}, {"bins": 0}, {"traversal": 8}, {"bins_reuse": 0}, {"light_bins": 0},
+                                  {"shadow_defer": 0}, {"shadow_defer": 0, "light_bins": 0}, {"bins": 0, "light_bins": 0}])
 def test_gpu_shadow_walks_agree(oracle, opts):
     """Shadow rays through every camera walk: camera bins (the default), the
     BVH walk (bins off), the kd packet walk; each frame's shadow rays go
