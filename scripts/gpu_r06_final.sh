@@ -31,11 +31,10 @@ if [[ $STEPS == *pmc* ]]; then
   mkdir -p profiles/r06 && for c in c2 c2s c3 c4 c5; do cp "gpurun_out/$TAG/pmc/$c/pmc_$c.json" "profiles/r06/pmc_$c.json" || exit 1; done
   grep -h "\"build_id\"" profiles/r06/pmc_c*.json | cut -c1-120 | head -5
 fi
-if [[ $STEPS == *bench* ]]; then
-  run bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5
-  run bench_c3 600 python bench.py --config c3 --steps 100 --warmup 10
-  run bench_c4 1100 python bench.py --config c4 --steps 8 --warmup 2
-  run bench_c5 900 python bench.py --config c5 --steps 10 --warmup 2
-fi
+# bench: every line; bench_driver / bench_c3 / bench_c4 / bench_c5: one each
+[[ $STEPS == *bench* && ( $STEPS != *bench_* || $STEPS == *bench_driver* ) ]] && run bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5
+[[ $STEPS == *bench* && ( $STEPS != *bench_* || $STEPS == *bench_c3* ) ]] && run bench_c3 600 python bench.py --config c3 --steps 100 --warmup 10
+[[ $STEPS == *bench* && ( $STEPS != *bench_* || $STEPS == *bench_c4* ) ]] && run bench_c4 1100 python bench.py --config c4 --steps 8 --warmup 2
+[[ $STEPS == *bench* && ( $STEPS != *bench_* || $STEPS == *bench_c5* ) ]] && run bench_c5 900 python bench.py --config c5 --steps 10 --warmup 2
 [[ $STEPS == *trace* ]] && run trace_driver 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_driver" -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-e2e
 exit 0
