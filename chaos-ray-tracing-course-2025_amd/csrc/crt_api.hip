@@ -1059,6 +1059,7 @@ static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
         if (value < 0 || value > 2) return set_error(CRT_E_INVALID, "calibrate must be 0 (estimate plan), 1 (tuned) or 2 (fixed k)");
         sc->calib_defer = false;   /* an explicit plan request: calibrate on the first frame */
         if (value != sc->calibrate) sc->calib_walk = sc->calibrate ? -1 : sc->calib_walk;   /* re-plan on next use */
+        sc->calib_tuned = false;   /* calibrate 1: tune k again */
         sc->calibrate = value;
         if (!sc->calibrate && !sc->calib.empty()) {   /* back to the estimate plan */
             HIP_TRY(hipDeviceSynchronize());
@@ -1075,6 +1076,7 @@ static int set_option_one(crt_hip_scene *sc, const char *name, int value) {
         sc->calib_defer = false;   /* an explicit plan request: calibrate on the first frame */
         sc->calib_min = value;
         sc->calib_walk = -1;
+        sc->calib_tuned = false;
     } else if (k == "shadows") {
         sc->shadows = value != 0;
     } else if (k == "shadow_defer") {
@@ -1109,6 +1111,7 @@ int rebuild_view(crt_hip_scene *sc, const DCamera &c, bool resized, bool bins_ok
         sc->calib.clear();   /* per 8x8 tile of the old frame */
         sc->calib_walk = -1;
         sc->calib_deferred_walk = -1;
+        sc->calib_tuned = false;
         if (!sc->ref_children.empty())
             sc->tile_work = tile_work_estimate_of(c, sc->ref_bounds, sc->ref_children, sc->ref_leaf_off,
                                                   (c.width + 7) / 8, (c.height + 7) / 8);

@@ -659,7 +659,7 @@ int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t
     HIP_TRY(hipDeviceSynchronize());   /* earlier frames may still read the old tile lists */
     int64_t px = 0;
     const std::vector<DBucket> all = shard_buckets(sc->info.width, sc->info.height, sc->info.bucket_size, 0, 1, &px);
-    if (sc->calibrate == 2) {
+    if (sc->calibrate == 2 || sc->calib_tuned) {
         if ((rc = calibrate_plan(sc, d_scene, walk, stream)) != CRT_OK) return rc;
         free_plans(sc);
         return make_tile_plan(sc, all, true, sc->full);
@@ -705,6 +705,7 @@ int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t
     (void)hipFree(scratch);
     if (rc != CRT_OK) return rc;
     sc->calib_k = best_k;
+    sc->calib_tuned = true;
     sc->calib.swap(best_cal);
     sc->calib_walk = walk;
     free_plans(sc);

@@ -297,6 +297,8 @@ struct crt_hip_scene {
     float calib_k = 2.25f;         /* split a wave whose cost exceeds k x (total cost / wave slots); 2.25 = C2's
                                     * tuned k (profiles/r02/gab, shard_kscan) */
     int calib_min = 2;             /* smallest sub-tile side */
+    bool calib_tuned = false;      /* calibrate 1: k was tuned (once per scene and resolution; a later walk — a
+                                    * camera move between fast and slow poses — calibrates with it, no trial frames) */
     bool calib_defer = true;       /* calibrate 2 (one-shot default): a walk's first frame renders with the
                                     * current plan and the calibration runs on its second frame (off once the
                                     * caller sets calibrate / calib_k_milli / calib_min) */
