@@ -644,7 +644,10 @@ static const float kCalibK[] = {1.5f, 1.75f, 2.0f, 2.25f, 2.5f, 2.75f, 3.0f, 3.5
 int ensure_plans(crt_hip_scene *sc, const crt_renderer_settings *st, hipStream_t stream, bool render) {
     if (!sc->calibrate || sc->grid_empty) return CRT_OK;
     const int walk = plan_walk(sc, st);
-    if (walk < 0 || walk == sc->calib_walk) return CRT_OK;
+    /* the packet walk's camera-fast forms (12, 13: chosen per camera pose) share
+     * one plan with it: a moving camera does not calibrate again */
+    auto family = [](int w) { return w == 12 || w == 13 ? 8 : w; };
+    if (walk < 0 || family(walk) == family(sc->calib_walk)) return CRT_OK;
     /* a one-shot caller's frame (calibrate 2, render entry points): the first
      * frame of this walk renders with the plan at hand (the scene's estimate
      * plan: C2 0.135 vs 0.108 ms) instead of paying the probes (~2.5 ms,
