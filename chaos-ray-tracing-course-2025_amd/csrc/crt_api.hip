@@ -519,6 +519,10 @@ int scene_upload(const HostScene &hs, int device, bool primary, crt_hip_scene **
             HIP_TRY(hipMemcpyAsync(sc->h_stage, sc->d_out, bytes, hipMemcpyDeviceToHost, sc->stream));
             HIP_TRY(hipStreamSynchronize(sc->stream));
             if ((rc = ensure_copy_rows(sc.get())) != CRT_OK) return rc;   /* the compact copy's row records */
+            {   /* the copy's host threads started here, not inside the first render call */
+                HostPool &pool = HostPool::get();
+                pool.run(pool.threads(), [](void *, int) {}, nullptr);
+            }
             CRT_CREATE_STAMP("first_dma");
         }
         unsigned long long probe[16];
