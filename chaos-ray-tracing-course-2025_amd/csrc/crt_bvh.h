@@ -742,7 +742,7 @@ CRT_HD bool lbin_test(const LightCand &cc, Vec o, Vec d, float r2, float &t) {
 }
 
 #ifndef CRT_LBINS_CAP
-#define CRT_LBINS_CAP 48   /* candidates a shadow ray walks in its cell at most (more: undecided, the BVH decides) */
+#define CRT_LBINS_CAP 96   /* candidates a shadow ray walks in its cell at most (more: undecided, the BVH decides; C2 with shadows: 24 0.42, 48 0.40, 96 0.37 ms) */
 #endif
 
 template <bool COUNT>

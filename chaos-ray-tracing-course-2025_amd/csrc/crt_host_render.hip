@@ -435,7 +435,7 @@ int ensure_gi_tables(crt_hip_scene *sc) {
  * later: the BVH decides).  No templates (no camera bins) or no light taking
  * bins: the BVH walks as before. */
 #ifndef CRT_LBINS_N
-#define CRT_LBINS_N 64   /* light bins: cells a cube-face side */
+#define CRT_LBINS_N 128   /* light bins: cells a cube-face side (C2 with shadows: 64 0.400, 128 0.366-0.377 ms) */
 #endif
 int ensure_light_bins(crt_hip_scene *sc, const crt_renderer_settings *st) {
     if (!sc->light_bins || sc->lbins_tried) {
